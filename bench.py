@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark: forward+backward Mpix/s of the MI355X Gaussian-splat rasterizer at 1080p, 1M Gaussians,
+SH degree 3 (BASELINE.json configs[1]), one training view per GPU.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one view rendered through the public GaussianRasterizer API (forward, including its
+num_rendered host sync), loss = <dL/dcolor, color> + <dL/dinvdepth, invdepth> with fixed synthetic
+upstream gradients, full backward, and -- for N > 1 -- the RCCL all-reduce of every Gaussian gradient
+(view-data parallel, weak scaling: each rank renders its own view of its own 1M-Gaussian replica).
+Inputs are synthetic (seeded), resident in HBM before timing starts.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "hierarchical-lod-gaussians_amd")
+sys.path[:0] = [ROOT, PKG]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(stage, P, V, R, N, T, M, D):
+    """Per-launch algorithmic HBM bytes of each stage."""
+    return {
+        "preprocess": P * (44 + 12 * M) + 83 * P,
+        "scan": 8 * P,
+        "scatter": 28 * V + 12 * R,
+        "tile_sort": 24 * R,
+        "tile_ranges": 8 * R + 8 * T,
+        "blend_fwd": 8 * T + R * (40 + 4 * D) + N * (20 + 4 * D),
+        "blend_bwd": 8 * T + R * (40 + 4 * D) + N * (20 + 4 * D) + V * (36 + 4 * D),
+        "gauss_bwd": V * (60 + 4 * D) + 40 * V + V * (107 + 12 * M) + V * (40 + 12 * M),
+    }[stage]
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(P, deg, W, H):
+    """The oracle (C restatement of the reference algorithm, 1 thread) on one full frame: fwd + bwd."""
+    from oracle import oracle as O
+    from hlgs_core import synthetic as S
+    cam = S.make_camera(W, H)
+    sc = S.make_gaussians(P, deg, cam, seed=0)
+    g, gd = S.upstream_grads(W, H)
+    O.build()
+    t0 = time.perf_counter()
+    fr = O.forward(sc, S.cam_numpy(cam), do_depth=True)
+    O.backward(fr, sc, g, gd)
+    dt = time.perf_counter() - t0
+    return dict(value=round(W * H / dt / 1e6, 4), unit="Mpix/s", cores=1, kind="port",
+                sample=f"one full frame: {P} Gaussians, SH deg {deg}, {W}x{H}, forward+backward, "
+                       f"{dt:.2f} s on 1 thread of {cpu_model()} (os.cpu_count()={os.cpu_count()})")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--sh-degree", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stage-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from hlgs_core import _lib as L
+    from hlgs_core import synthetic as S
+    from hlgs_core.dp import FlatGradExchange
+
+    W, H, P, deg = args.W, args.H, args.P, args.sh_degree
+    # every rank: the same scene replica, its own view (ring of cameras); rank 0 = configs[1] camera
+    cam = S.make_camera(W, H) if world == 1 else S.ring_camera(W, H, rank, world)
+    host = S.make_gaussians(P, deg, S.make_camera(W, H), seed=0)
+    to = lambda a: torch.tensor(a, device=dev, requires_grad=True)  # noqa: E731
+    means3D, scales, rots, opac, shs = (to(host["means3D"]), to(host["scales"]), to(host["rotations"]),
+                                        to(host["opacities"]), to(host["shs"]))
+    g_np, gd_np = S.upstream_grads(W, H, seed=1 + rank)
+    g_col, g_inv = torch.tensor(g_np, device=dev), torch.tensor(gd_np, device=dev)
+    e_i = torch.empty(0, dtype=torch.int32, device=dev)
+    e_f = torch.empty(0, dtype=torch.float32, device=dev)
+    rs = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam["viewmatrix"].to(dev),
+        projmatrix=cam["projmatrix"].to(dev), sh_degree=deg, campos=cam["campos"].to(dev), prefiltered=False,
+        debug=False, render_indices=e_i, parent_indices=e_i, interpolation_weights=e_f, num_node_kids=e_i,
+        do_depth=True)
+    rast = GaussianRasterizer(rs)
+    params = [means3D, scales, rots, opac, shs]
+    exchange = FlatGradExchange(params) if world > 1 else None
+    stats = {}
+
+    def step():
+        for p in params:
+            p.grad = None
+        means2D = torch.zeros_like(means3D, requires_grad=True)
+        color, radii, invd = rast(means3D=means3D, means2D=means2D, opacities=opac, shs=shs, scales=scales,
+                                  rotations=rots)
+        loss = (color * g_col).sum() + (invd * g_inv).sum()
+        loss.backward()
+        if exchange is not None:
+            exchange.allreduce()
+        return radii
+
+    for _ in range(args.warmup):
+        radii = step()
+    torch.cuda.synchronize()
+    # frame statistics for the algorithmic-byte model
+    with torch.no_grad():
+        V = int((radii > 0).sum().item())
+    from diff_gaussian_rasterization import _C as DC
+    nr = DC.rasterize_gaussians(rs.bg, e_i, e_i, e_f, e_i, means3D.detach(), e_f, opac.detach(), scales.detach(),
+                                rots.detach(), 1.0, e_f, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, H, W,
+                                shs.detach(), deg, rs.campos, False, False, True)[0]
+    if not args.no_stage_timing:
+        L.set_stage_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if not args.no_stage_timing:
+        stats = L.stage_stats()
+        L.set_stage_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * W * H * args.steps / elapsed / 1e6
+    T = math.ceil(W / 16) * math.ceil(H / 16)
+    M = (deg + 1) ** 2
+    roofline = None
+    stage_report = {}
+    if stats:
+        for name, (ms, calls) in stats.items():
+            if calls <= 0 or ms <= 0:
+                continue
+            b = algorithmic_bytes(name, P, V, nr, W * H, T, M, 1)
+            stage_report[name] = dict(ms=round(ms, 4), calls=calls, alg_GBs=round(b / (ms * 1e-3) / 1e9, 1))
+        dom = max(stage_report, key=lambda k: stage_report[k]["ms"])
+        ach = stage_report[dom]["alg_GBs"]
+        roofline = dict(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
+                        traffic=None, kernel=dom)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(P, deg, W, H)
+    if rank == 0:
+        line = {
+            "metric": "forward+backward Mpix/s at 1080p (1M Gaussians)", "value": round(value, 3), "unit": "Mpix/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded PCG64 scene and upstream gradients; no dataset)",
+            "config": {"workload": f"configs[1]: {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd with depth, "
+                                   f"one view per GPU" + (", RCCL grad all-reduce" if world > 1 else ""),
+                       "num_rendered": nr, "visible": V, "tiles": T,
+                       "parallelism": f"view-dp{world}"},
+            "roofline": roofline, "cpu_baseline": cpu, "stages": stage_report,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

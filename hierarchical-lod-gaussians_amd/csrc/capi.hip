@@ -1,0 +1,578 @@
+// capi.hip -- the C ABI of libhlgs.so (declared in include/hlgs.h) and the host orchestration of the
+// rasterizer stages.  Mirrors CudaRasterizer::Rasterizer::forward/backward
+// (submodules/hierarchy-rasterizer/cuda_rasterizer/rasterizer_impl.cu:203-517) and the LOD entry
+// points of gaussianhierarchy/runtime_switching.cu, re-planned for gfx950.
+//
+// Re-entrancy: no device memory is allocated here and no scratch is static; every buffer is passed
+// in.  The only process-wide state is the opt-in stage-timing instrumentation used by bench.py.
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "hlgs_internal.h"
+
+namespace hlgs {
+void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
+                       hipStream_t s);
+void launch_tile_ranges(const Img& im, int T, hipStream_t s);
+void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
+                    int gy, uint32_t max_count, hipStream_t s, bool timing);
+void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, int gx, int gy,
+                      float* out_color, float* out_invdepth, int* seen, hipStream_t s);
+void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, const BwdScratch& rs,
+                      int gx, int gy, const float* dL_dpix, const float* dL_dinv, hipStream_t s);
+void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
+                      const hlgs_grads& o, bool has_depth, hipStream_t s);
+void launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t s);
+void launch_relocation(int P, const float* oo, const float* so, const int* N, const float* binoms, int n_max,
+                       float* on, float* sn, hipStream_t s);
+void launch_expand_dynamic(int N, float target, const int* nodes, const float* pos, const float* scales,
+                           const float* vp, const float* vd, int* ri, int* pi, int* ni, uint32_t* counts,
+                           uint32_t* incl, uint32_t* tmp, hipStream_t s);
+void launch_weights_dynamic(int n, const int* idx, float target, const int* nodes, const float* pos,
+                            const float* scales, const float* vp, float* ts, int* kids, hipStream_t s);
+void launch_expand_static(int N, float target, const int* nodes, const float* boxes, const float* vp, int* ri,
+                          int* pi, int* ni, uint32_t* counts, uint32_t* incl, uint32_t* tmp, hipStream_t s);
+void launch_weights_static(int n, const int* idx, float target, const int* nodes, const float* boxes,
+                           const float* vp, float* ts, int* kids, hipStream_t s);
+void launch_spt_prepare(int s_, const int* starts, const float* smax, const int* sidx, const float* sdist,
+                        uint32_t* sizes, uint32_t* incl, uint32_t* tmp, hipStream_t s);
+void launch_spt_finish(int s_, int E, int n, const int* gidx, const int* starts, const float* smin, const int* sidx,
+                       const float* sdist, int compat, const uint32_t* sizes, const uint32_t* incl, uint32_t* counts,
+                       uint32_t* counts_incl, uint32_t* tmp_s, int* result, uint32_t* keep, uint32_t* keep_incl,
+                       uint32_t* tmp_n, int* cut, int* counts_prefix, hipStream_t s);
+void launch_lod_interp_fwd(int S, int n, int M3, const int* ridx, const int* pidx, const float* w, const float* means,
+                           const float* scales, const float* rots, const float* opac, const float* shs, float* om,
+                           float* osc, float* orot, float* oop, float* osh, hipStream_t s);
+void launch_lod_interp_bwd(int S, int n, int M3, const int* ridx, const int* pidx, const float* w, const float* rots,
+                           const float* gm, const float* gsc, const float* grot, const float* gop, const float* gsh,
+                           float* dm, float* dsc, float* drot, float* dop, float* dsh, hipStream_t s);
+
+// ---------------------------------------------------------------- buffer carving
+template <typename T>
+static T* take(char*& p, size_t count)
+{
+    T* r = reinterpret_cast<T*>(p);
+    p += align_up(count * sizeof(T));
+    return r;
+}
+
+Geom carve_geom(void* base, int P, size_t* total)
+{
+    char* p = static_cast<char*>(base);
+    Geom g;
+    g.depths = take<float>(p, P);
+    g.clamped = take<uint32_t>(p, P);
+    g.means2D = take<float2>(p, P);
+    g.cov3D = take<float>(p, 6 * (size_t)P);
+    g.conic_opacity = take<float4>(p, P);
+    g.rgb = take<float>(p, 3 * (size_t)P);
+    g.tiles_touched = take<uint32_t>(p, P);
+    g.point_offsets = take<uint32_t>(p, P);
+    g.rects = take<int2>(p, P);
+    g.scan_tmp = take<uint32_t>(p, scan_scratch_elems(P));
+    if (total) *total = (size_t)(p - static_cast<char*>(base));
+    return g;
+}
+
+Img carve_img(void* base, int W, int H, size_t* total)
+{
+    const size_t N = (size_t)W * H;
+    const int T = ((W + 15) / 16) * ((H + 15) / 16);
+    char* p = static_cast<char*>(base);
+    Img im;
+    im.final_T = take<float>(p, N);
+    im.n_contrib = take<uint32_t>(p, N);
+    im.ranges = take<uint2>(p, T);
+    im.tile_count = take<uint32_t>(p, T);
+    im.tile_cursor = take<uint32_t>(p, T);
+    im.misc = take<uint32_t>(p, 16);
+    im.scan_tmp = take<uint32_t>(p, scan_scratch_elems(T));
+    if (total) *total = (size_t)(p - static_cast<char*>(base));
+    return im;
+}
+
+Bin carve_bin(void* base, int R, size_t* total)
+{
+    char* p = static_cast<char*>(base);
+    Bin b;
+    b.keys = take<uint64_t>(p, R);
+    b.keys2 = take<uint64_t>(p, R);
+    b.point_list = take<uint32_t>(p, R);
+    if (total) *total = (size_t)(p - static_cast<char*>(base));
+    return b;
+}
+
+BwdScratch carve_bwd(void* base, int P, int R, size_t* total)
+{
+    char* p = static_cast<char*>(base);
+    BwdScratch r;
+    r.recA = take<float4>(p, R);
+    r.recB = take<float4>(p, R);
+    r.recC = take<float2>(p, R);
+    r.parent_dmean = take<float>(p, 3 * (size_t)P);
+    if (total) *total = (size_t)(p - static_cast<char*>(base));
+    return r;
+}
+
+// ---------------------------------------------------------------- errors & timing
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HLGS_TRY_HIP(expr)                                                                            \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) return fail(HLGS_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// After a group of launches: always surface launch errors; under `debug` also synchronise, as the
+// reference's CHECK_CUDA does (auxiliary.h:23-30).
+static int check_stage(hipStream_t s, bool debug, const char* stage)
+{
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && debug) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(HLGS_ERR_DEVICE, std::string("[HIP ERROR] in ") + stage + ": " + hipGetErrorString(e));
+    return HLGS_OK;
+}
+
+enum Stage { ST_PRE = 0, ST_SCAN, ST_RANGES, ST_SCATTER, ST_SORT, ST_BLEND_FWD, ST_BLEND_BWD, ST_GAUSS_BWD, ST_COUNT };
+static const char* kStageNames[ST_COUNT] = {"preprocess", "scan", "tile_ranges", "scatter", "tile_sort",
+                                            "blend_fwd", "blend_bwd", "gauss_bwd"};
+static bool g_timing = false;
+// event pool per stage: launch i of a stage uses pair i (grown on demand, reused after a reset)
+static std::vector<hipEvent_t> g_ev[ST_COUNT][2];
+static int g_calls[ST_COUNT];
+
+void stage_mark(hipStream_t s, int stage, bool begin)
+{
+    if (!g_timing) return;
+    const size_t i = (size_t)g_calls[stage];
+    auto& pool = g_ev[stage][begin ? 0 : 1];
+    if (pool.size() <= i) {
+        hipEvent_t e;
+        hipEventCreate(&e);
+        pool.push_back(e);
+    }
+    hipEventRecord(pool[i], s);
+    if (!begin) g_calls[stage]++;
+}
+
+static int validate(const hlgs_raster_args* a)
+{
+    if (!a) return fail(HLGS_ERR_ARG, "null args");
+    if (a->P < 0 || a->W <= 0 || a->H <= 0) return fail(HLGS_ERR_ARG, "invalid P/W/H");
+    if (a->P == 0) return HLGS_OK;
+    if (!a->means3D || !a->opacities || !a->viewmatrix || !a->projmatrix || !a->bg || !a->campos)
+        return fail(HLGS_ERR_ARG, "missing required tensor (means3D/opacities/viewmatrix/projmatrix/bg/campos)");
+    if (!a->shs && !a->colors_precomp)
+        return fail(HLGS_ERR_ARG, "For non-RGB, provide precomputed Gaussian colors!");
+    if (a->shs && a->M <= 0) return fail(HLGS_ERR_ARG, "shs given but M == 0");
+    if (!a->cov3D_precomp && (!a->scales || !a->rotations))
+        return fail(HLGS_ERR_ARG, "provide scales+rotations or cov3D_precomp");
+    if (a->D < 0 || a->D > 3) return fail(HLGS_ERR_ARG, "sh_degree must be in [0,3]");
+    if (a->shs && (a->D + 1) * (a->D + 1) > a->M) return fail(HLGS_ERR_ARG, "sh_degree needs more SH coefficients than given");
+    const bool h0 = a->indices != nullptr, h1 = a->parent_indices != nullptr;
+    if (h0 != h1) return fail(HLGS_ERR_ARG, "render_indices and parent_indices must be given together");
+    if ((a->ts != nullptr) != (a->kids != nullptr))
+        return fail(HLGS_ERR_ARG, "interpolation_weights and num_node_kids must be given together");
+    if (h1 && !a->ts) return fail(HLGS_ERR_ARG, "parent_indices requires interpolation_weights");
+    if (!h0 && a->P != a->P_full) return fail(HLGS_ERR_ARG, "P must equal P_full without render_indices");
+    return HLGS_OK;
+}
+
+}  // namespace hlgs
+
+using namespace hlgs;
+
+extern "C" {
+
+const char* hlgs_last_error(void) { return g_err.c_str(); }
+const char* hlgs_version(void) { return "hlgs 0.1 gfx950"; }
+
+size_t hlgs_geom_buffer_size(int P)
+{
+    size_t t = 0;
+    carve_geom(nullptr, P < 0 ? 0 : P, &t);
+    return t + kAlign;
+}
+size_t hlgs_image_buffer_size(int W, int H)
+{
+    size_t t = 0;
+    carve_img(nullptr, W, H, &t);
+    return t + kAlign;
+}
+size_t hlgs_binning_buffer_size(int R)
+{
+    size_t t = 0;
+    carve_bin(nullptr, R < 0 ? 0 : R, &t);
+    return t + kAlign;
+}
+size_t hlgs_backward_scratch_size(int P, int R)
+{
+    size_t t = 0;
+    carve_bwd(nullptr, P, R < 0 ? 0 : R, &t);
+    return t + kAlign;
+}
+
+static void* aligned(const void* p) { return (void*)align_up((size_t)p); }
+
+int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* img, int* radii,
+                                   hlgs_frame_info* info, void* stream)
+{
+    int rc = validate(a);
+    if (rc) return rc;
+    info->num_rendered = 0;
+    info->max_tile_count = 0;
+    if (a->P == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16, T = gx * gy;
+    Geom g = carve_geom(aligned(geom), a->P, nullptr);
+    Img im = carve_img(aligned(img), a->W, a->H, nullptr);
+    hipGetLastError();
+    HLGS_TRY_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
+    HLGS_TRY_HIP(hipMemsetAsync(im.misc, 0, sizeof(uint32_t) * 16, s));
+    stage_mark(s, ST_PRE, true);
+    launch_preprocess(*a, g, radii, im.tile_count, gx, gy, s);
+    stage_mark(s, ST_PRE, false);
+    if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
+    stage_mark(s, ST_SCAN, true);
+    scan_inclusive_u32(g.tiles_touched, g.point_offsets, (size_t)a->P, g.scan_tmp, s);
+    stage_mark(s, ST_SCAN, false);
+    stage_mark(s, ST_RANGES, true);
+    scan_inclusive_u32(im.tile_count, im.tile_cursor, (size_t)T, im.scan_tmp, s);
+    launch_tile_ranges(im, T, s);
+    stage_mark(s, ST_RANGES, false);
+    if ((rc = check_stage(s, a->debug, "scan"))) return rc;
+    uint32_t misc[2];
+    HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
+    HLGS_TRY_HIP(hipStreamSynchronize(s));
+    info->num_rendered = (int)misc[0];
+    info->max_tile_count = (int)misc[1];
+    return HLGS_OK;
+}
+
+int hlgs_rasterize_forward_render(const hlgs_raster_args* a, const int* radii, void* geom, void* img, void* binning,
+                                  const hlgs_frame_info* info, float* out_color, float* out_invdepth, int* seen,
+                                  void* stream)
+{
+    int rc = validate(a);
+    if (rc) return rc;
+    const int R = info->num_rendered;
+    if (a->P == 0 || R == 0) return HLGS_OK;  // rasterizer_impl.cu:332-333: output stays 0
+    hipStream_t s = (hipStream_t)stream;
+    const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16;
+    Geom g = carve_geom(aligned(geom), a->P, nullptr);
+    Img im = carve_img(aligned(img), a->W, a->H, nullptr);
+    Bin b = carve_bin(aligned(binning), R, nullptr);
+    hipGetLastError();
+    launch_binning(*a, radii, g, im, b, gx, gy, (uint32_t)info->max_tile_count, s, g_timing);
+    if ((rc = check_stage(s, a->debug, "binning"))) return rc;
+    stage_mark(s, ST_BLEND_FWD, true);
+    launch_blend_fwd(*a, g, im, b, gx, gy, out_color, out_invdepth, seen, s);
+    stage_mark(s, ST_BLEND_FWD, false);
+    return check_stage(s, a->debug, "blend_fwd");
+}
+
+int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,
+                            const void* binning, int R, void* scratch, const float* dL_dcolor,
+                            const float* dL_dinvdepth, const hlgs_grads* out, void* stream)
+{
+    int rc = validate(a);
+    if (rc) return rc;
+    if (!out || !out->dmean2D || !out->dcolor || !out->dopacity || !out->dmean3D || !out->dcov3D || !out->dscale ||
+        !out->drot || (a->M > 0 && !out->dsh))
+        return fail(HLGS_ERR_ARG, "missing gradient output");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    const size_t Pf = (size_t)a->P_full;
+    if (a->indices || a->P == 0) {
+        // hierarchy mode writes only the rendered rows: clear everything first (rasterize_points.cu:182-190)
+        HLGS_TRY_HIP(hipMemsetAsync(out->dmean2D, 0, 12 * Pf, s));
+        HLGS_TRY_HIP(hipMemsetAsync(out->dcolor, 0, 12 * Pf, s));
+        HLGS_TRY_HIP(hipMemsetAsync(out->dopacity, 0, 4 * Pf, s));
+        HLGS_TRY_HIP(hipMemsetAsync(out->dmean3D, 0, 12 * Pf, s));
+        HLGS_TRY_HIP(hipMemsetAsync(out->dcov3D, 0, 24 * Pf, s));
+        if (out->dsh && a->M > 0) HLGS_TRY_HIP(hipMemsetAsync(out->dsh, 0, 12 * (size_t)a->M * Pf, s));
+        HLGS_TRY_HIP(hipMemsetAsync(out->dscale, 0, 12 * Pf, s));
+        HLGS_TRY_HIP(hipMemsetAsync(out->drot, 0, 16 * Pf, s));
+    }
+    if (a->P == 0) return check_stage(s, a->debug, "backward");
+    const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16;
+    Geom g = carve_geom(aligned(geom), a->P, nullptr);
+    Img im = carve_img(aligned(img), a->W, a->H, nullptr);
+    BwdScratch rs = carve_bwd(aligned(scratch), a->P, R, nullptr);
+    if (R > 0) {
+        Bin b = carve_bin(aligned(binning), R, nullptr);
+        stage_mark(s, ST_BLEND_BWD, true);
+        launch_blend_bwd(*a, g, im, b, rs, gx, gy, dL_dcolor, dL_dinvdepth, s);
+        stage_mark(s, ST_BLEND_BWD, false);
+        if ((rc = check_stage(s, a->debug, "blend_bwd"))) return rc;
+    }
+    stage_mark(s, ST_GAUSS_BWD, true);
+    launch_gauss_bwd(*a, radii, g, rs, *out, dL_dinvdepth != nullptr, s);
+    stage_mark(s, ST_GAUSS_BWD, false);
+    return check_stage(s, a->debug, "gauss_bwd");
+}
+
+int hlgs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                      uint8_t* present, void* stream)
+{
+    (void)projmatrix;
+    if (P < 0) return fail(HLGS_ERR_ARG, "P < 0");
+    if (P == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_mark_visible(P, means3D, viewmatrix, present, s);
+    return check_stage(s, false, "mark_visible");
+}
+
+int hlgs_compute_relocation(int P, const float* opacity_old, const float* scale_old, const int* N,
+                            const float* binoms, int n_max, float* opacity_new, float* scale_new, void* stream)
+{
+    if (P < 0) return fail(HLGS_ERR_ARG, "P < 0");
+    if (P == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_relocation(P, opacity_old, scale_old, N, binoms, n_max, opacity_new, scale_new, s);
+    return check_stage(s, false, "compute_relocation");
+}
+
+// ---------------------------------------------------------------- LOD
+size_t hlgs_lod_scratch_size(int N)
+{
+    const size_t n = N < 0 ? 0 : (size_t)N;
+    return align_up(4 * n) * 2 + align_up(4 * scan_scratch_elems(n)) + kAlign;
+}
+
+struct LodScratch {
+    uint32_t *counts, *incl, *tmp;
+};
+static LodScratch carve_lod(void* base, int N)
+{
+    char* p = static_cast<char*>(aligned(base));
+    LodScratch l;
+    l.counts = take<uint32_t>(p, N);
+    l.incl = take<uint32_t>(p, N);
+    l.tmp = take<uint32_t>(p, scan_scratch_elems(N));
+    return l;
+}
+
+static int read_count(const uint32_t* dev, int* count, hipStream_t s)
+{
+    uint32_t c = 0;
+    HLGS_TRY_HIP(hipMemcpyAsync(&c, dev, sizeof(c), hipMemcpyDeviceToHost, s));
+    HLGS_TRY_HIP(hipStreamSynchronize(s));
+    *count = (int)c;
+    return HLGS_OK;
+}
+
+int hlgs_expand_to_size_dynamic(int N, float target_size, const int* nodes, const float* positions,
+                                const float* scales, const float* viewpoint, const float* viewdir_host,
+                                int* render_indices, int* parent_indices, int* nodes_for_render_indices,
+                                void* scratch, int* count, void* stream)
+{
+    *count = 0;
+    if (N < 0) return fail(HLGS_ERR_ARG, "N < 0");
+    if (N == 0) return HLGS_OK;
+    if (!render_indices || !parent_indices || !nodes_for_render_indices || !viewdir_host)
+        return fail(HLGS_ERR_ARG, "missing output buffer");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    LodScratch l = carve_lod(scratch, N);
+    launch_expand_dynamic(N, target_size, nodes, positions, scales, viewpoint, viewdir_host, render_indices,
+                          parent_indices, nodes_for_render_indices, l.counts, l.incl, l.tmp, s);
+    int rc = check_stage(s, false, "expand_to_size_dynamic");
+    if (rc) return rc;
+    return read_count(l.incl + (N - 1), count, s);
+}
+
+int hlgs_get_interpolation_weights_dynamic(int n, const int* node_indices, float target_size, const int* nodes,
+                                           const float* positions, const float* scales,
+                                           const float* viewpoint_host, const float* viewdir_host, float* ts,
+                                           int* kids, void* stream)
+{
+    (void)viewdir_host;
+    if (n < 0) return fail(HLGS_ERR_ARG, "n < 0");
+    if (n == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_weights_dynamic(n, node_indices, target_size, nodes, positions, scales, viewpoint_host, ts, kids, s);
+    return check_stage(s, false, "get_interpolation_weights_dynamic");
+}
+
+int hlgs_expand_to_size(int N, float target_size, const int* nodes, const float* boxes, const float* viewpoint,
+                        const float* viewdir_host, int* render_indices, int* parent_indices,
+                        int* nodes_for_render_indices, void* scratch, int* count, void* stream)
+{
+    (void)viewdir_host;
+    *count = 0;
+    if (N < 0) return fail(HLGS_ERR_ARG, "N < 0");
+    if (N == 0) return HLGS_OK;
+    if (!render_indices) return fail(HLGS_ERR_ARG, "missing output buffer");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    LodScratch l = carve_lod(scratch, N);
+    launch_expand_static(N, target_size, nodes, boxes, viewpoint, render_indices, parent_indices,
+                         nodes_for_render_indices, l.counts, l.incl, l.tmp, s);
+    int rc = check_stage(s, false, "expand_to_size");
+    if (rc) return rc;
+    return read_count(l.incl + (N - 1), count, s);
+}
+
+int hlgs_get_interpolation_weights(int n, const int* node_indices, float target_size, const int* nodes,
+                                   const float* boxes, const float* viewpoint_host, const float* viewdir_host,
+                                   float* ts, int* kids, void* stream)
+{
+    (void)viewdir_host;
+    if (n < 0) return fail(HLGS_ERR_ARG, "n < 0");
+    if (n == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_weights_static(n, node_indices, target_size, nodes, boxes, viewpoint_host, ts, kids, s);
+    return check_stage(s, false, "get_interpolation_weights");
+}
+
+// ---------------------------------------------------------------- SPT cut
+struct SptScratch {
+    uint32_t *sizes, *incl, *counts, *counts_incl, *tmp;
+};
+static SptScratch carve_spt(void* base, int s_, size_t* total)
+{
+    char* p = static_cast<char*>(aligned(base));
+    char* p0 = p;
+    SptScratch r;
+    r.sizes = take<uint32_t>(p, s_);
+    r.incl = take<uint32_t>(p, s_);
+    r.counts = take<uint32_t>(p, s_);
+    r.counts_incl = take<uint32_t>(p, s_);
+    r.tmp = take<uint32_t>(p, scan_scratch_elems(s_));
+    if (total) *total = (size_t)(p - p0);
+    return r;
+}
+struct SptWork {
+    int* result;
+    uint32_t *keep, *keep_incl, *tmp;
+};
+static SptWork carve_spt_work(void* base, int n, size_t* total)
+{
+    char* p = static_cast<char*>(aligned(base));
+    char* p0 = p;
+    SptWork w;
+    w.result = take<int>(p, n);
+    w.keep = take<uint32_t>(p, n);
+    w.keep_incl = take<uint32_t>(p, n);
+    w.tmp = take<uint32_t>(p, scan_scratch_elems(n));
+    if (total) *total = (size_t)(p - p0);
+    return w;
+}
+
+size_t hlgs_spt_scratch_size(int s_)
+{
+    size_t t = 0;
+    carve_spt(nullptr, s_ < 0 ? 0 : s_, &t);
+    return t + kAlign;
+}
+size_t hlgs_spt_work_size(int n)
+{
+    size_t t = 0;
+    carve_spt_work(nullptr, n < 0 ? 0 : n, &t);
+    return t + kAlign;
+}
+
+int hlgs_spt_cut_prepare(int s_, const int* SPT_starts, const float* SPT_max, const int* SPT_indices,
+                         const float* SPT_distances, void* scratch, int* n_candidates, void* stream)
+{
+    *n_candidates = 0;
+    if (s_ < 0) return fail(HLGS_ERR_ARG, "number_of_SPTs < 0");
+    if (s_ == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    SptScratch r = carve_spt(scratch, s_, nullptr);
+    launch_spt_prepare(s_, SPT_starts, SPT_max, SPT_indices, SPT_distances, r.sizes, r.incl, r.tmp, s);
+    int rc = check_stage(s, false, "spt_cut_prepare");
+    if (rc) return rc;
+    return read_count(r.incl + (s_ - 1), n_candidates, s);
+}
+
+int hlgs_spt_cut_finish(int s_, int E, int n_candidates, const int* gaussian_indices, const int* SPT_starts,
+                        const float* SPT_min, const int* SPT_indices, const float* SPT_distances, int compat,
+                        void* scratch, void* work, int* cut, int* counts_prefix, int* count, void* stream)
+{
+    *count = 0;
+    if (s_ <= 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    SptScratch r = carve_spt(scratch, s_, nullptr);
+    SptWork w = carve_spt_work(work, n_candidates, nullptr);
+    launch_spt_finish(s_, E, n_candidates, gaussian_indices, SPT_starts, SPT_min, SPT_indices, SPT_distances, compat,
+                      r.sizes, r.incl, r.counts, r.counts_incl, r.tmp, w.result, w.keep, w.keep_incl, w.tmp, cut,
+                      counts_prefix, s);
+    int rc = check_stage(s, false, "spt_cut_finish");
+    if (rc) return rc;
+    if (n_candidates == 0) return HLGS_OK;
+    return read_count(w.keep_incl + (n_candidates - 1), count, s);
+}
+
+int hlgs_lod_interp_forward(int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
+                            const float* means, const float* scales, const float* rots, const float* opac,
+                            const float* shs, float* o_means, float* o_scales, float* o_rots, float* o_opac,
+                            float* o_shs, void* stream)
+{
+    if (S < 0 || n < 0 || M3 < 0) return fail(HLGS_ERR_ARG, "negative size");
+    if (S + n == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_lod_interp_fwd(S, n, M3, ridx, pidx, w, means, scales, rots, opac, M3 ? shs : nullptr, o_means, o_scales,
+                          o_rots, o_opac, M3 ? o_shs : nullptr, s);
+    return check_stage(s, false, "lod_interp_forward");
+}
+
+int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
+                             const float* rots, const float* g_means, const float* g_scales, const float* g_rots,
+                             const float* g_opac, const float* g_shs, float* d_means, float* d_scales,
+                             float* d_rots, float* d_opac, float* d_shs, void* stream)
+{
+    if (S < 0 || n < 0 || M3 < 0) return fail(HLGS_ERR_ARG, "negative size");
+    if (S + n == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_lod_interp_bwd(S, n, M3, ridx, pidx, w, rots, g_means, g_scales, g_rots, g_opac, M3 ? g_shs : nullptr,
+                          d_means, d_scales, d_rots, d_opac, M3 ? d_shs : nullptr, s);
+    return check_stage(s, false, "lod_interp_backward");
+}
+
+// ---------------------------------------------------------------- timing hooks
+void hlgs_set_stage_timing(int enable)
+{
+    g_timing = enable != 0;
+    for (int i = 0; i < ST_COUNT; i++) g_calls[i] = 0;
+}
+int hlgs_stage_count(void) { return ST_COUNT; }
+const char* hlgs_stage_name(int i) { return (i >= 0 && i < ST_COUNT) ? kStageNames[i] : ""; }
+int hlgs_stage_stats(float* mean_ms, int* calls, int max)
+{
+    const int n = max < ST_COUNT ? max : ST_COUNT;
+    for (int i = 0; i < n; i++) {
+        double tot = 0.0;
+        int k = 0;
+        for (int c = 0; c < g_calls[i]; c++) {
+            float t = 0.f;
+            if (hipEventSynchronize(g_ev[i][1][c]) != hipSuccess) continue;
+            if (hipEventElapsedTime(&t, g_ev[i][0][c], g_ev[i][1][c]) != hipSuccess) continue;
+            tot += t;
+            k++;
+        }
+        mean_ms[i] = k ? (float)(tot / k) : -1.f;
+        calls[i] = k;
+    }
+    return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// hlgs_internal.h -- buffer layouts and kernel launchers shared by the translation units of libhlgs.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/hlgs.h"
+
+namespace hlgs {
+
+constexpr int kScanItems = 2048;    // elements per scan block (256 threads x 8)
+constexpr int kSortCap = 4096;      // largest per-tile list sorted in one LDS pass
+constexpr size_t kAlign = 256;
+
+inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+size_t scan_scratch_elems(size_t n);
+
+// Per-Gaussian state written by the forward preprocess and read by the backward
+// (the reference's GeometryState, rasterizer_impl.h:29-45).
+struct Geom {
+    float* depths;            // P
+    uint32_t* clamped;        // P, bit c = colour channel c clamped at 0
+    float2* means2D;          // P, pixel-space centre
+    float* cov3D;             // P x 6
+    float4* conic_opacity;    // P
+    float* rgb;               // P x 3
+    uint32_t* tiles_touched;  // P
+    uint32_t* point_offsets;  // P, inclusive scan of tiles_touched
+    int2* rects;              // P, per-axis 3-sigma extent in pixels
+    uint32_t* scan_tmp;
+};
+Geom carve_geom(void* base, int P, size_t* total);
+
+// Per-pixel / per-tile state (ImageState, rasterizer_impl.h:47-54) plus binning counters.
+struct Img {
+    float* final_T;        // N
+    uint32_t* n_contrib;   // N
+    uint2* ranges;         // T: [start, end) into point_list
+    uint32_t* tile_count;  // T
+    uint32_t* tile_cursor; // T
+    uint32_t* misc;        // 16: [0] = R, [1] = max per-tile count
+    uint32_t* scan_tmp;
+};
+Img carve_img(void* base, int W, int H, size_t* total);
+
+// Per-instance state (BinningState).  keys = depth_bits << 32 | gaussian index, grouped by tile.
+struct Bin {
+    uint64_t* keys;
+    uint64_t* keys2;
+    uint32_t* point_list;  // R, tile-major then front-to-back
+};
+Bin carve_bin(void* base, int R, size_t* total);
+
+// Backward scratch: one gradient record per (tile, Gaussian) instance, stored Gaussian-major at the
+// Gaussian's point_offsets slot so the per-Gaussian reduction reads contiguous rows.
+struct BwdScratch {
+    float4* recA;   // dmean2D.x, dmean2D.y, dconic.x, dconic.y
+    float4* recB;   // dconic.w, dopacity, dcolor.r, dcolor.g
+    float2* recC;   // dcolor.b, dinvdepth
+    float* parent_dmean;  // P x 3 (hierarchy mode only)
+};
+BwdScratch carve_bwd(void* base, int P, int R, size_t* total);
+
+// scan.hip
+void scan_inclusive_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp, hipStream_t s);
+
+// stage timing (capi.cpp)
+void stage_mark(hipStream_t s, int stage, bool begin);
+
+}  // namespace hlgs

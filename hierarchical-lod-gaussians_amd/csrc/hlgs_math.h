@@ -1,0 +1,201 @@
+// hlgs_math.h -- per-Gaussian projection / covariance / SH math shared by the gfx950 kernels.
+//
+// Semantics follow the reference rasterizer (paths relative to
+// submodules/hierarchy-rasterizer/cuda_rasterizer): forward.cu:25-215 and
+// auxiliary.h:53-142.  glm's column-major mat3 and its summation order are
+// reproduced (m[c][r] = column c, row r) so results agree with the reference to
+// the last few ulps; FMA contraction is left to the compiler, as nvcc does.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HLGS_TILE 16
+#define HLGS_TILE_PIX 256
+
+namespace hlgs {
+
+constexpr float kSH_C0 = 0.28209479177387814f;
+constexpr float kSH_C1 = 0.4886025119029199f;
+constexpr float kSH_C2[5] = {1.0925484305920792f, -1.0925484305920792f,
+                                                       0.31539156525252005f, -1.0925484305920792f,
+                                                       0.5462742152960396f};
+constexpr float kSH_C3[7] = {-0.5900435899266435f, 2.890611442640554f,
+                                                       -0.4570457994644658f, 0.3731763325901154f,
+                                                       -0.4570457994644658f, 1.445305721320277f,
+                                                       -0.5900435899266435f};
+
+struct f3 { float x, y, z; };
+struct m3 { float m[3][3]; };
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 scl(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+__device__ __forceinline__ m3 mcols(float a0, float a1, float a2, float a3, float a4, float a5, float a6,
+                                    float a7, float a8)
+{
+    m3 r;
+    r.m[0][0] = a0; r.m[0][1] = a1; r.m[0][2] = a2;
+    r.m[1][0] = a3; r.m[1][1] = a4; r.m[1][2] = a5;
+    r.m[2][0] = a6; r.m[2][1] = a7; r.m[2][2] = a8;
+    return r;
+}
+__device__ __forceinline__ m3 mmul(const m3& a, const m3& b)
+{
+    m3 r;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int row = 0; row < 3; row++)
+            r.m[c][row] = a.m[0][row] * b.m[c][0] + a.m[1][row] * b.m[c][1] + a.m[2][row] * b.m[c][2];
+    return r;
+}
+__device__ __forceinline__ m3 mtrans(const m3& a)
+{
+    m3 r;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int row = 0; row < 3; row++) r.m[c][row] = a.m[row][c];
+    return r;
+}
+
+// auxiliary.h:53-56, evaluated in double exactly as the reference does
+__device__ __forceinline__ float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+__device__ __forceinline__ f3 xform43(f3 p, const float* m)
+{
+    return mk(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+              m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+__device__ __forceinline__ float xform44w(f3 p, const float* m) { return m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]; }
+
+// auxiliary.h:70-80 (the torch path always passes per-axis rect extents)
+__device__ __forceinline__ void tile_rect(float px, float py, int ex, int ey, int gx, int gy, int& x0, int& y0,
+                                          int& x1, int& y1)
+{
+    x0 = min(gx, max(0, (int)((px - ex) / HLGS_TILE)));
+    y0 = min(gy, max(0, (int)((py - ey) / HLGS_TILE)));
+    x1 = min(gx, max(0, (int)((px + ex + HLGS_TILE - 1) / HLGS_TILE)));
+    y1 = min(gy, max(0, (int)((py + ey + HLGS_TILE - 1) / HLGS_TILE)));
+}
+
+// forward.cu:25-76; `sh` points at M*3 floats of one Gaussian (possibly a lerped copy)
+template <typename SHLoad>
+__device__ __forceinline__ f3 sh_to_rgb(int deg, SHLoad shv, f3 pos, f3 campos, uint32_t& clamp_bits)
+{
+    f3 dir = sub(pos, campos);
+    float len = sqrtf(dot(dir, dir));
+    dir = mk(dir.x / len, dir.y / len, dir.z / len);
+    f3 res = scl(kSH_C0, shv(0));
+    if (deg > 0) {
+        float x = dir.x, y = dir.y, z = dir.z;
+        res = sub(add(sub(res, scl(kSH_C1 * y, shv(1))), scl(kSH_C1 * z, shv(2))), scl(kSH_C1 * x, shv(3)));
+        if (deg > 1) {
+            float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            res = add(res, scl(kSH_C2[0] * xy, shv(4)));
+            res = add(res, scl(kSH_C2[1] * yz, shv(5)));
+            res = add(res, scl(kSH_C2[2] * (2.0f * zz - xx - yy), shv(6)));
+            res = add(res, scl(kSH_C2[3] * xz, shv(7)));
+            res = add(res, scl(kSH_C2[4] * (xx - yy), shv(8)));
+            if (deg > 2) {
+                res = add(res, scl(kSH_C3[0] * y * (3.0f * xx - yy), shv(9)));
+                res = add(res, scl(kSH_C3[1] * xy * z, shv(10)));
+                res = add(res, scl(kSH_C3[2] * y * (4.0f * zz - xx - yy), shv(11)));
+                res = add(res, scl(kSH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy), shv(12)));
+                res = add(res, scl(kSH_C3[4] * x * (4.0f * zz - xx - yy), shv(13)));
+                res = add(res, scl(kSH_C3[5] * z * (xx - yy), shv(14)));
+                res = add(res, scl(kSH_C3[6] * x * (xx - 3.0f * yy), shv(15)));
+            }
+        }
+    }
+    res = mk(res.x + 0.5f, res.y + 0.5f, res.z + 0.5f);
+    clamp_bits = (res.x < 0 ? 1u : 0u) | (res.y < 0 ? 2u : 0u) | (res.z < 0 ? 4u : 0u);
+    return mk(fmaxf(res.x, 0.0f), fmaxf(res.y, 0.0f), fmaxf(res.z, 0.0f));
+}
+
+__device__ __forceinline__ m3 quat_rot(const float q[4])
+{
+    float r = q[0], x = q[1], y = q[2], z = q[3];
+    return mcols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                 2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                 2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+}
+
+// forward.cu:181-215 (quaternion used as given, no normalisation)
+__device__ __forceinline__ void cov3d_fwd(f3 scale, float mod, const float q[4], float out[6])
+{
+    m3 S = mcols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    S.m[0][0] = mod * scale.x;
+    S.m[1][1] = mod * scale.y;
+    S.m[2][2] = mod * scale.z;
+    m3 M = mmul(S, quat_rot(q));
+    m3 Sig = mmul(mtrans(M), M);
+    out[0] = Sig.m[0][0]; out[1] = Sig.m[0][1]; out[2] = Sig.m[0][2];
+    out[3] = Sig.m[1][1]; out[4] = Sig.m[1][2]; out[5] = Sig.m[2][2];
+}
+
+// forward.cu:141-176 / backward.cu:176-204: EWA Jacobian and projected covariance
+struct Cov2D {
+    f3 t;
+    float txtz, tytz, limx, limy;
+    m3 W, T, Vrk, cov;
+};
+__device__ __forceinline__ void cov2d_eval(f3 mean, float fx, float fy, float tanx, float tany, const float* c3,
+                                           const float* view, Cov2D& k)
+{
+    f3 t = xform43(mean, view);
+    k.limx = 1.3f * tanx;
+    k.limy = 1.3f * tany;
+    k.txtz = t.x / t.z;
+    k.tytz = t.y / t.z;
+    t.x = fminf(k.limx, fmaxf(-k.limx, k.txtz)) * t.z;
+    t.y = fminf(k.limy, fmaxf(-k.limy, k.tytz)) * t.z;
+    k.t = t;
+    m3 J = mcols(fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z, -(fy * t.y) / (t.z * t.z), 0, 0, 0);
+    k.W = mcols(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6], view[10]);
+    k.T = mmul(k.W, J);
+    k.Vrk = mcols(c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]);
+    k.cov = mmul(mmul(mtrans(k.T), mtrans(k.Vrk)), k.T);
+}
+
+// auxiliary.h:132-142
+__device__ __forceinline__ f3 dnormvdv(f3 v, f3 dv)
+{
+    float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    f3 r;
+    r.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
+    r.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
+    r.z = (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32;
+    return r;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md section 5): consecutive logical blocks
+// land on the same XCD so neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg)
+{
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+// Full-wave (64-lane) sum with DPP; the total lands in lane 63.
+template <int CTRL, int ROW, bool BC>
+__device__ __forceinline__ float dpp(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW, 0xF, BC));
+}
+__device__ __forceinline__ float wave_sum_to_lane63(float v)
+{
+    v += dpp<0xB1, 0xF, true>(v);   // quad_perm [1,0,3,2]
+    v += dpp<0x4E, 0xF, true>(v);   // quad_perm [2,3,0,1]
+    v += dpp<0x124, 0xF, true>(v);  // row_ror:4
+    v += dpp<0x128, 0xF, true>(v);  // row_ror:8 -> every lane holds its row sum
+    v += dpp<0x142, 0xA, false>(v); // row_bcast:15 into rows 1,3
+    v += dpp<0x143, 0xC, false>(v); // row_bcast:31 into rows 2,3
+    return v;
+}
+
+}  // namespace hlgs

@@ -1,0 +1,412 @@
+// lod.hip -- hierarchical level-of-detail selection and child/parent interpolation for gfx950.
+//
+// Reference semantics (submodules/gaussianhierarchy/runtime_switching.cu):
+//   k_mark_dynamic / k_put_dynamic   <- markNodesForSizeDynamic :533-582, putRenderIndicesDynamic :95-108
+//   k_weights_dynamic                <- computeTsIndexedDynamic :637-684
+//   k_mark_static / k_put_static     <- markNodesForSize :495-529, putRenderIndices :68-93
+//   k_weights_static                 <- computeTsIndexed :588-634
+//   k_spt_bsearch / k_spt_populate   <- binary_search_SPTs :784-810, populate_SPT :812-856,
+//                                       DeviceSelect::If :944-950, ExclusiveSum :973-986
+//   k_lod_interp_fwd / _bwd          <- gaussian_renderer/__init__.py:304-339 (render_post lerp) and its autograd
+#include <float.h>
+
+#include "hlgs_internal.h"
+#include "hlgs_math.h"
+
+namespace hlgs {
+
+// ---- dynamic hierarchy: HierarchyNode {depth, parent, child_count, first_child, next_sibling, max_side_length}
+__device__ __forceinline__ float gauss_dist(const float* p, float vx, float vy, float vz)
+{
+    const float d0 = vx - p[0], d1 = vy - p[1], d2 = vz - p[2];
+    return sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+}
+__device__ __forceinline__ bool in_cone(const float* p, float vx, float vy, float vz, float zx, float zy, float zz)
+{
+    const float d0 = vx - p[0], d1 = vy - p[1], d2 = vz - p[2];
+    const float n = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+    const float c = d0 / n * zx + d1 / n * zy + d2 / n * zz;
+    return c < -0.5f;
+}
+__device__ __forceinline__ float size_dyn(const float* p, const float* s, float vx, float vy, float vz)
+{
+    const float md = gauss_dist(p, vx, vy, vz);
+    if (md < 0.0f) return 0;
+    return fmaxf(s[0], fmaxf(s[1], s[2])) / md;
+}
+
+__global__ void __launch_bounds__(256) k_mark_dynamic(int N, const int* __restrict__ nodes, const float* __restrict__ pos,
+                                                      const float* __restrict__ scales, const float* __restrict__ vp,
+                                                      float zx, float zy, float zz, float target,
+                                                      uint32_t* __restrict__ counts)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const float vx = vp[0], vy = vp[1], vz = vp[2];
+    const int* nd = nodes + 6 * i;
+    uint32_t c = 0;
+    if (in_cone(pos + 3 * i, vx, vy, vz, zx, zy, zz)) {
+        const float size = size_dyn(pos + 3 * i, scales + 3 * i, vx, vy, vz);
+        const int depth = nd[0], parent = nd[1], nchild = nd[2];
+        if (depth < 0) c = 0;
+        else if (size >= target && nchild == 0) c = 1;
+        else if (parent >= 0) {
+            const float ps = size_dyn(pos + 3 * parent, scales + 3 * parent, vx, vy, vz);
+            if (ps >= target && size < target) c = 1;
+        }
+    }
+    counts[i] = c;
+}
+
+__global__ void __launch_bounds__(256) k_put_dynamic(int N, const int* __restrict__ nodes, const uint32_t* __restrict__ counts,
+                                                     const uint32_t* __restrict__ incl, int* __restrict__ render_indices,
+                                                     int* __restrict__ parent_indices, int* __restrict__ nodes_for)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N || counts[i] == 0) return;
+    const uint32_t off = incl[i] - 1;
+    render_indices[off] = i;
+    nodes_for[off] = i;
+    const int parent = nodes[6 * i + 1];
+    if (parent != -1) parent_indices[off] = parent;
+}
+
+__global__ void __launch_bounds__(256) k_weights_dynamic(int n, const int* __restrict__ idx, const int* __restrict__ nodes,
+                                                         const float* __restrict__ pos, const float* __restrict__ scales,
+                                                         float vx, float vy, float vz, float target,
+                                                         float* __restrict__ ts, int* __restrict__ kids)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int id = idx[i];
+    const int parent = nodes[6 * id + 1];
+    float t;
+    if (parent < 0) t = 1.0f;
+    else {
+        const float ps = size_dyn(pos + 3 * parent, scales + 3 * parent, vx, vy, vz);
+        if (ps > 2.0f * target) t = 1.0f;
+        else {
+            const float s = size_dyn(pos + 3 * id, scales + 3 * id, vx, vy, vz);
+            const float start = fmaxf(0.5f * ps, s);
+            const float diff = ps - start;
+            if (diff <= 0) t = 1.0f;
+            else {
+                const float td = fmaxf(0.0f, target - start);
+                t = fmaxf(1.0f - (td / diff), 0.0f);
+            }
+        }
+    }
+    ts[i] = t;
+    kids[i] = parent < 0 ? 1 : nodes[6 * parent + 2];
+}
+
+// ---- static (.hier) hierarchy: Node {depth, parent, start, count_leafs, count_merged, start_children,
+// count_children}, Box {minn xyzw, maxx xyzw}
+__device__ __forceinline__ float size_box(const float* b, float vx, float vy, float vz)
+{
+    const bool inside = vx >= b[0] && vx <= b[4] && vy >= b[1] && vy <= b[5] && vz >= b[2] && vz <= b[6];
+    if (inside) return FLT_MAX;
+    const float c0 = fmaxf(b[0], fminf(b[4], vx)), c1 = fmaxf(b[1], fminf(b[5], vy)), c2 = fmaxf(b[2], fminf(b[6], vz));
+    const float d0 = vx - c0, d1 = vy - c1, d2 = vz - c2;
+    return b[3] / sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+}
+
+__global__ void __launch_bounds__(256) k_mark_static(int N, const int* __restrict__ nodes, const float* __restrict__ boxes,
+                                                     const float* __restrict__ vp, float target,
+                                                     uint32_t* __restrict__ counts)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const float vx = vp[0], vy = vp[1], vz = vp[2];
+    const int* nd = nodes + 7 * i;
+    const float size = size_box(boxes + 8 * i, vx, vy, vz);
+    int c = 0;
+    if (size >= target) c = nd[3];
+    else if (nd[1] != -1) {
+        const float ps = size_box(boxes + 8 * nd[1], vx, vy, vz);
+        if (ps >= target) {
+            c = nd[3];
+            if (nd[0] != 0) c += nd[4];
+        }
+    }
+    counts[i] = (uint32_t)c;
+}
+
+__global__ void __launch_bounds__(256) k_put_static(int N, const int* __restrict__ nodes, const uint32_t* __restrict__ counts,
+                                                    const uint32_t* __restrict__ incl, int* __restrict__ render_indices,
+                                                    int* __restrict__ parent_indices, int* __restrict__ nodes_for)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const uint32_t c = counts[i];
+    if (c == 0) return;
+    const uint32_t off = incl[i] - c;
+    const int* nd = nodes + 7 * i;
+    const int pg = nd[1] != -1 ? nodes[7 * nd[1] + 2] : -1;
+    for (uint32_t k = 0; k < c; k++) {
+        render_indices[off + k] = nd[2] + (int)k;
+        if (parent_indices) parent_indices[off + k] = pg;
+        if (nodes_for) nodes_for[off + k] = i;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_weights_static(int n, const int* __restrict__ idx, const int* __restrict__ nodes,
+                                                        const float* __restrict__ boxes, float vx, float vy, float vz,
+                                                        float target, float* __restrict__ ts, int* __restrict__ kids)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int id = idx[i];
+    const int parent = nodes[7 * id + 1];
+    float t;
+    if (parent == -1) t = 1.0f;
+    else {
+        const float ps = size_box(boxes + 8 * parent, vx, vy, vz);
+        if (ps > 2.0f * target) t = 1.0f;
+        else {
+            const float s = size_box(boxes + 8 * id, vx, vy, vz);
+            const float start = fmaxf(0.5f * ps, s);
+            const float diff = ps - start;
+            if (diff <= 0) t = 1.0f;
+            else {
+                const float td = fmaxf(0.0f, target - start);
+                t = fmaxf(1.0f - (td / diff), 0.0f);
+            }
+        }
+    }
+    ts[i] = t;
+    kids[i] = parent == -1 ? 1 : nodes[7 * parent + 6];
+}
+
+// ---- SPT cut
+__global__ void __launch_bounds__(256) k_spt_bsearch(int s, const int* __restrict__ starts, const float* __restrict__ smax,
+                                                     const int* __restrict__ sidx, const float* __restrict__ sdist,
+                                                     uint32_t* __restrict__ sizes)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= s) return;
+    const int index = sidx[k];
+    const float d = sdist[k];
+    int low = starts[index], high = starts[index + 1];
+    int pivot = (low + high) / 2;
+    while (high - low > 1) {
+        if (smax[pivot] > d) low = pivot;
+        else high = pivot;
+        pivot = (low + high) / 2;
+    }
+    sizes[k] = (uint32_t)(high - starts[index]);
+}
+
+__global__ void __launch_bounds__(256) k_spt_populate(int s, int E, int n, const int* __restrict__ gidx,
+                                                      const int* __restrict__ starts, const float* __restrict__ smin,
+                                                      const int* __restrict__ sidx, const float* __restrict__ sdist,
+                                                      const uint32_t* __restrict__ sizes, const uint32_t* __restrict__ incl,
+                                                      int compat, int* __restrict__ result, uint32_t* __restrict__ keep,
+                                                      uint32_t* __restrict__ counts)
+{
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n) return;
+    auto prefix = [&](int k) { return (int)(incl[k] - sizes[k]); };
+    int ii;
+    if (compat) {  // populate_SPT's search, including its `>=` boundary attribution (App. A-10)
+        int low = 0, high = s;
+        ii = s / 2;
+        while (high - low > 1) {
+            if (prefix(ii) >= idx) high = ii;
+            else low = ii;
+            ii = (high + low) / 2;
+        }
+    } else {  // intended semantics (scene/gaussian_model.py:163-181): largest k with prefix[k] <= idx
+        int low = 0, high = s;
+        while (high - low > 1) {
+            const int mid = (low + high) / 2;
+            if (prefix(mid) <= idx) low = mid; else high = mid;
+        }
+        ii = low;
+    }
+    const int g = starts[sidx[ii]] + (idx - prefix(ii));
+    uint32_t kp = 0;
+    int v = 0;
+    if (g < E && smin[g] < sdist[ii]) {
+        atomicAdd(&counts[ii], 1u);
+        v = gidx[g];
+        kp = (!compat || v != 0) ? 1u : 0u;
+    }
+    result[idx] = v;
+    keep[idx] = kp;
+}
+
+__global__ void __launch_bounds__(256) k_compact(int n, const int* __restrict__ result, const uint32_t* __restrict__ keep,
+                                                 const uint32_t* __restrict__ incl, int* __restrict__ cut)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n || !keep[i]) return;
+    cut[incl[i] - 1] = result[i];
+}
+
+__global__ void __launch_bounds__(256) k_excl_from_incl(int s, const uint32_t* __restrict__ counts,
+                                                        const uint32_t* __restrict__ incl, int* __restrict__ out)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k < s) out[k] = (int)(incl[k] - counts[k]);
+}
+
+// ---- render_post lerp: one thread per output row
+__global__ void __launch_bounds__(256) k_lod_interp_fwd(int S, int n, int M3, const int* __restrict__ ridx,
+                                                        const int* __restrict__ pidx, const float* __restrict__ w,
+                                                        const float* __restrict__ means, const float* __restrict__ scales,
+                                                        const float* __restrict__ rots, const float* __restrict__ opac,
+                                                        const float* __restrict__ shs, float* __restrict__ om,
+                                                        float* __restrict__ osc, float* __restrict__ orot,
+                                                        float* __restrict__ oop, float* __restrict__ osh)
+{
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    if (o >= S + n) return;
+    if (o < S) {
+        for (int k = 0; k < 3; k++) { om[3 * o + k] = means[3 * o + k]; osc[3 * o + k] = scales[3 * o + k]; }
+        reinterpret_cast<float4*>(orot)[o] = reinterpret_cast<const float4*>(rots)[o];
+        oop[o] = opac[o];
+        if (shs)
+            for (int k = 0; k < M3; k++) osh[(size_t)M3 * o + k] = shs[(size_t)M3 * o + k];
+        return;
+    }
+    const int i = o - S, c = ridx[i], p = pidx[i];
+    const float t = w[i], u = 1 - w[i];
+    for (int k = 0; k < 3; k++) om[3 * o + k] = t * means[3 * c + k] + u * means[3 * p + k];
+    for (int k = 0; k < 3; k++) osc[3 * o + k] = t * scales[3 * c + k] + u * scales[3 * p + k];
+    if (shs)
+        for (int k = 0; k < M3; k++) osh[(size_t)M3 * o + k] = t * shs[(size_t)M3 * c + k] + u * shs[(size_t)M3 * p + k];
+    const float4 rc = reinterpret_cast<const float4*>(rots)[c];
+    float4 rp = reinterpret_cast<const float4*>(rots)[p];
+    float dotv = 0.f;
+    dotv += rc.x * rp.x;
+    dotv += rc.y * rp.y;
+    dotv += rc.z * rp.z;
+    dotv += rc.w * rp.w;
+    if (dotv < 0) { rp.x = -rp.x; rp.y = -rp.y; rp.z = -rp.z; rp.w = -rp.w; }
+    reinterpret_cast<float4*>(orot)[o] =
+        make_float4(t * rc.x + u * rp.x, t * rc.y + u * rp.y, t * rc.z + u * rp.z, t * rc.w + u * rp.w);
+    oop[o] = t * opac[c] + u * opac[p];
+}
+
+__global__ void __launch_bounds__(256) k_lod_interp_bwd(int S, int n, int M3, const int* __restrict__ ridx,
+                                                        const int* __restrict__ pidx, const float* __restrict__ w,
+                                                        const float* __restrict__ rots, const float* __restrict__ gm,
+                                                        const float* __restrict__ gsc, const float* __restrict__ grot,
+                                                        const float* __restrict__ gop, const float* __restrict__ gsh,
+                                                        float* dm, float* dsc, float* drot, float* dop, float* dsh)
+{
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    if (o >= S + n) return;
+    if (o < S) {
+        for (int k = 0; k < 3; k++) { atomicAdd(&dm[3 * o + k], gm[3 * o + k]); atomicAdd(&dsc[3 * o + k], gsc[3 * o + k]); }
+        for (int k = 0; k < 4; k++) atomicAdd(&drot[4 * o + k], grot[4 * o + k]);
+        atomicAdd(&dop[o], gop[o]);
+        if (gsh)
+            for (int k = 0; k < M3; k++) atomicAdd(&dsh[(size_t)M3 * o + k], gsh[(size_t)M3 * o + k]);
+        return;
+    }
+    const int i = o - S, c = ridx[i], p = pidx[i];
+    const float t = w[i], u = 1 - w[i];
+    for (int k = 0; k < 3; k++) {
+        atomicAdd(&dm[3 * c + k], t * gm[3 * o + k]);
+        atomicAdd(&dm[3 * p + k], u * gm[3 * o + k]);
+        atomicAdd(&dsc[3 * c + k], t * gsc[3 * o + k]);
+        atomicAdd(&dsc[3 * p + k], u * gsc[3 * o + k]);
+    }
+    const float4 rc = reinterpret_cast<const float4*>(rots)[c];
+    const float4 rp = reinterpret_cast<const float4*>(rots)[p];
+    float dotv = 0.f;
+    dotv += rc.x * rp.x;
+    dotv += rc.y * rp.y;
+    dotv += rc.z * rp.z;
+    dotv += rc.w * rp.w;
+    const float sg = dotv < 0 ? -1.0f : 1.0f;
+    for (int k = 0; k < 4; k++) {
+        atomicAdd(&drot[4 * c + k], t * grot[4 * o + k]);
+        atomicAdd(&drot[4 * p + k], sg * (u * grot[4 * o + k]));
+    }
+    atomicAdd(&dop[c], t * gop[o]);
+    atomicAdd(&dop[p], u * gop[o]);
+    if (gsh)
+        for (int k = 0; k < M3; k++) {
+            atomicAdd(&dsh[(size_t)M3 * c + k], t * gsh[(size_t)M3 * o + k]);
+            atomicAdd(&dsh[(size_t)M3 * p + k], u * gsh[(size_t)M3 * o + k]);
+        }
+}
+
+// ---- host launchers
+static inline dim3 g256(long n) { return dim3((unsigned)((n + 255) / 256)); }
+
+void launch_expand_dynamic(int N, float target, const int* nodes, const float* pos, const float* scales, const float* vp,
+                           const float* vd, int* ri, int* pi, int* ni, uint32_t* counts, uint32_t* incl, uint32_t* tmp,
+                           hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mark_dynamic, g256(N), dim3(256), 0, s, N, nodes, pos, scales, vp, vd[0], vd[1], vd[2], target,
+                       counts);
+    scan_inclusive_u32(counts, incl, (size_t)N, tmp, s);
+    hipLaunchKernelGGL(k_put_dynamic, g256(N), dim3(256), 0, s, N, nodes, counts, incl, ri, pi, ni);
+}
+
+void launch_weights_dynamic(int n, const int* idx, float target, const int* nodes, const float* pos,
+                            const float* scales, const float* vp, float* ts, int* kids, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_weights_dynamic, g256(n), dim3(256), 0, s, n, idx, nodes, pos, scales, vp[0], vp[1], vp[2],
+                       target, ts, kids);
+}
+
+void launch_expand_static(int N, float target, const int* nodes, const float* boxes, const float* vp, int* ri, int* pi,
+                          int* ni, uint32_t* counts, uint32_t* incl, uint32_t* tmp, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mark_static, g256(N), dim3(256), 0, s, N, nodes, boxes, vp, target, counts);
+    scan_inclusive_u32(counts, incl, (size_t)N, tmp, s);
+    hipLaunchKernelGGL(k_put_static, g256(N), dim3(256), 0, s, N, nodes, counts, incl, ri, pi, ni);
+}
+
+void launch_weights_static(int n, const int* idx, float target, const int* nodes, const float* boxes, const float* vp,
+                           float* ts, int* kids, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_weights_static, g256(n), dim3(256), 0, s, n, idx, nodes, boxes, vp[0], vp[1], vp[2], target,
+                       ts, kids);
+}
+
+void launch_spt_prepare(int s_, const int* starts, const float* smax, const int* sidx, const float* sdist,
+                        uint32_t* sizes, uint32_t* incl, uint32_t* tmp, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_spt_bsearch, g256(s_), dim3(256), 0, s, s_, starts, smax, sidx, sdist, sizes);
+    scan_inclusive_u32(sizes, incl, (size_t)s_, tmp, s);
+}
+
+void launch_spt_finish(int s_, int E, int n, const int* gidx, const int* starts, const float* smin, const int* sidx,
+                       const float* sdist, int compat, const uint32_t* sizes, const uint32_t* incl, uint32_t* counts,
+                       uint32_t* counts_incl, uint32_t* tmp_s, int* result, uint32_t* keep, uint32_t* keep_incl,
+                       uint32_t* tmp_n, int* cut, int* counts_prefix, hipStream_t s)
+{
+    hipMemsetAsync(counts, 0, sizeof(uint32_t) * (size_t)s_, s);
+    if (n > 0) {
+        hipLaunchKernelGGL(k_spt_populate, g256(n), dim3(256), 0, s, s_, E, n, gidx, starts, smin, sidx, sdist, sizes,
+                           incl, compat, result, keep, counts);
+        scan_inclusive_u32(keep, keep_incl, (size_t)n, tmp_n, s);
+        hipLaunchKernelGGL(k_compact, g256(n), dim3(256), 0, s, n, result, keep, keep_incl, cut);
+    }
+    scan_inclusive_u32(counts, counts_incl, (size_t)s_, tmp_s, s);
+    hipLaunchKernelGGL(k_excl_from_incl, g256(s_), dim3(256), 0, s, s_, counts, counts_incl, counts_prefix);
+}
+
+void launch_lod_interp_fwd(int S, int n, int M3, const int* ridx, const int* pidx, const float* w, const float* means,
+                           const float* scales, const float* rots, const float* opac, const float* shs, float* om,
+                           float* osc, float* orot, float* oop, float* osh, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_lod_interp_fwd, g256((long)S + n), dim3(256), 0, s, S, n, M3, ridx, pidx, w, means, scales,
+                       rots, opac, shs, om, osc, orot, oop, osh);
+}
+
+void launch_lod_interp_bwd(int S, int n, int M3, const int* ridx, const int* pidx, const float* w, const float* rots,
+                           const float* gm, const float* gsc, const float* grot, const float* gop, const float* gsh,
+                           float* dm, float* dsc, float* drot, float* dop, float* dsh, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_lod_interp_bwd, g256((long)S + n), dim3(256), 0, s, S, n, M3, ridx, pidx, w, rots, gm, gsc, grot,
+                       gop, gsh, dm, dsc, drot, dop, dsh);
+}
+
+}  // namespace hlgs

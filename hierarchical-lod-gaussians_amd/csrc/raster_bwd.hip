@@ -1,0 +1,495 @@
+// raster_bwd.hip -- backward rasterizer kernels for gfx950.
+//
+// Reference semantics (submodules/hierarchy-rasterizer/cuda_rasterizer):
+//   k_blend_bwd  <- renderCUDA<3> backward      backward.cu:498-721
+//   k_gauss_bwd  <- computeCov2DCUDA            backward.cu:147-326
+//                 + preprocessCUDA<3> backward  backward.cu:398-495 (SH :23-142, cov3D :330-393)
+//
+// The reference issues one global float atomic per (pixel, Gaussian, gradient component)
+// (backward.cu:669-718).  Here each wave owns one tile: every lane folds its four pixels, a DPP
+// wave reduction folds the 64 lanes, and the per-(tile, Gaussian) partial is stored once -- with
+// a plain store -- into a Gaussian-major record slot (the Gaussian's point_offsets range, indexed by
+// the tile's position inside its rect).  k_gauss_bwd then sums each Gaussian's contiguous records
+// in a fixed order, so the backward has no float atomics and is bitwise reproducible.
+#include "hlgs_internal.h"
+#include "hlgs_math.h"
+
+namespace hlgs {
+
+template <bool INTERP, bool DEPTH>
+__global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
+                                                  int W, int H, int gx, int gy, int T, Geom g,
+                                                  const float* __restrict__ colors, const float* __restrict__ final_Ts,
+                                                  const uint32_t* __restrict__ n_contrib, const float* __restrict__ bg,
+                                                  const float* __restrict__ dL_dpixels,
+                                                  const float* __restrict__ dL_dinvdepths, const float* __restrict__ ts,
+                                                  const int* __restrict__ kids, BwdScratch rec)
+{
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, t
+    __shared__ float4 s_co[64];
+    __shared__ float4 s_col[64];  // r, g, b, 1/kids
+    __shared__ float4 s_ra[64];
+    __shared__ float4 s_rb[64];
+    __shared__ float2 s_rc[64];
+    const int tile = xcd_remap(blockIdx.x, T);
+    const int lane = threadIdx.x;
+    const int tx = tile % gx, ty = tile / gx;
+    const int px = tx * HLGS_TILE + (lane & 15);
+    const int py0 = ty * HLGS_TILE + (lane >> 4);
+    const float pxf = (float)px;
+    const uint2 range = ranges[tile];
+    const uint32_t cnt = range.y - range.x;
+    if (cnt == 0) return;
+    const size_t HW = (size_t)H * W;
+    const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+
+    float Tcur[4], Tfin[4], ar[4], ag[4], ab[4], la[4], lr[4], lg[4], lb[4], dr[4], dgc[4], db[4], bgd[4];
+    float dinv[4], ainv[4], linv[4];
+    uint32_t lastc[4];
+    uint32_t maxlast = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int py = py0 + 4 * k;
+        const bool inside = px < W && py < H;
+        const size_t pid = (size_t)W * py + px;
+        Tfin[k] = inside ? final_Ts[pid] : 0.f;
+        Tcur[k] = Tfin[k];
+        lastc[k] = inside ? n_contrib[pid] : 0u;
+        maxlast = max(maxlast, lastc[k]);
+        ar[k] = ag[k] = ab[k] = la[k] = lr[k] = lg[k] = lb[k] = 0.f;
+        dr[k] = inside ? dL_dpixels[pid] : 0.f;
+        dgc[k] = inside ? dL_dpixels[HW + pid] : 0.f;
+        db[k] = inside ? dL_dpixels[2 * HW + pid] : 0.f;
+        bgd[k] = 0.f;
+        bgd[k] += bg[0] * dr[k];
+        bgd[k] += bg[1] * dgc[k];
+        bgd[k] += bg[2] * db[k];
+        dinv[k] = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
+        ainv[k] = linv[k] = 0.f;
+    }
+    // wave-uniform: the furthest-back position any pixel of this tile still needs
+    for (int off = 32; off > 0; off >>= 1) maxlast = max(maxlast, (uint32_t)__shfl_xor((int)maxlast, off, 64));
+
+    for (uint32_t b0 = 0; b0 < cnt; b0 += 64) {
+        // batch covers local positions cnt-1-b0 down to cnt-1-b0-(n-1)
+        const int n = (int)min(64u, cnt - b0);
+        const uint32_t li_top = cnt - 1 - b0;
+        const bool lane_valid = lane < n;
+        uint32_t slot = 0;
+        if (lane_valid) {
+            const uint32_t pos = range.x + li_top - lane;
+            const uint32_t id = point_list[pos];
+            const float2 xy = g.means2D[id];
+            s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1.f / g.depths[id] : 0.f, INTERP ? ts[id] : 0.f);
+            s_co[lane] = g.conic_opacity[id];
+            s_col[lane] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2],
+                                      INTERP ? 1.0f / (float)kids[id] : 0.f);
+            const int2 ext = g.rects[id];
+            int x0, y0, x1, y1;
+            tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
+            slot = g.point_offsets[id] - g.tiles_touched[id] + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
+            s_ra[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_rb[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_rc[lane] = make_float2(0.f, 0.f);
+        }
+        __syncthreads();
+        // every splat of this batch lies behind all contributors of every pixel: records stay zero
+        const uint32_t li_bot = li_top - (uint32_t)(n - 1);
+        if (li_bot < maxlast) {
+            for (int j = 0; j < n; j++) {
+                const uint32_t li = li_top - (uint32_t)j;
+                if (li >= maxlast) continue;
+                const float4 xy = s_xy[j];
+                const float4 co = s_co[j];
+                const float4 col = s_col[j];
+                float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
+                bool any = false;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (li >= lastc[k]) continue;
+                    const float dx = xy.x - pxf, dy = xy.y - (float)(py0 + 4 * k);
+                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    if (power > 0.0f) continue;
+                    const float G = __expf(power);
+                    const float test_alpha = co.w * G;
+                    const bool nullalpha = test_alpha > 0.99f;
+                    const float my_alpha = fminf(0.99f, test_alpha);
+                    float alpha = my_alpha;
+                    if (INTERP) alpha = xy.w * my_alpha + (1.0f - xy.w) * (1.0f - powf(1.0f - my_alpha, col.w));
+                    if (alpha < 1.0f / 255.0f) continue;
+                    any = true;
+                    Tcur[k] = Tcur[k] / (1.f - alpha);
+                    const float weight = alpha * Tcur[k];
+                    float dL_dalpha = 0.0f;
+                    ar[k] = la[k] * lr[k] + (1.f - la[k]) * ar[k];
+                    lr[k] = col.x;
+                    dL_dalpha += (col.x - ar[k]) * dr[k];
+                    g6 += weight * dr[k];
+                    ag[k] = la[k] * lg[k] + (1.f - la[k]) * ag[k];
+                    lg[k] = col.y;
+                    dL_dalpha += (col.y - ag[k]) * dgc[k];
+                    g7 += weight * dgc[k];
+                    ab[k] = la[k] * lb[k] + (1.f - la[k]) * ab[k];
+                    lb[k] = col.z;
+                    dL_dalpha += (col.z - ab[k]) * db[k];
+                    g8 += weight * db[k];
+                    if (DEPTH) {
+                        ainv[k] = la[k] * linv[k] + (1.f - la[k]) * ainv[k];
+                        linv[k] = xy.z;
+                        dL_dalpha += (xy.z - ainv[k]) * dinv[k];
+                        g9 += weight * dinv[k];
+                    }
+                    dL_dalpha *= Tcur[k];
+                    la[k] = alpha;
+                    dL_dalpha += (-Tfin[k] / (1.f - alpha)) * bgd[k];
+                    dL_dalpha = nullalpha ? 0.f : dL_dalpha;
+                    const float dL_dG = co.w * dL_dalpha;
+                    const float gdx = G * dx, gdy = G * dy;
+                    const float dG_ddelx = -gdx * co.x - gdy * co.y;
+                    const float dG_ddely = -gdy * co.z - gdx * co.y;
+                    g0 += dL_dG * dG_ddelx * ddelx_dx;
+                    g1 += dL_dG * dG_ddely * ddely_dy;
+                    g2 += -0.5f * gdx * dx * dL_dG;
+                    g3 += -0.5f * gdx * dy * dL_dG;
+                    g4 += -0.5f * gdy * dy * dL_dG;
+                    float mult = 1.0f;
+                    if (INTERP) mult = xy.w - powf(1.0f - my_alpha, col.w - 1.0f) * (xy.w - 1.0f) * col.w;
+                    g5 += mult * G * dL_dalpha;
+                }
+                if (__ballot(any)) {
+                    g0 = wave_sum_to_lane63(g0);
+                    g1 = wave_sum_to_lane63(g1);
+                    g2 = wave_sum_to_lane63(g2);
+                    g3 = wave_sum_to_lane63(g3);
+                    g4 = wave_sum_to_lane63(g4);
+                    g5 = wave_sum_to_lane63(g5);
+                    g6 = wave_sum_to_lane63(g6);
+                    g7 = wave_sum_to_lane63(g7);
+                    g8 = wave_sum_to_lane63(g8);
+                    if (DEPTH) g9 = wave_sum_to_lane63(g9);
+                    if (lane == 63) {
+                        s_ra[j] = make_float4(g0, g1, g2, g3);
+                        s_rb[j] = make_float4(g4, g5, g6, g7);
+                        s_rc[j] = make_float2(g8, g9);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (lane_valid) {
+            rec.recA[slot] = s_ra[lane];
+            rec.recB[slot] = s_rb[lane];
+            rec.recC[slot] = s_rc[lane];
+        }
+        __syncthreads();
+    }
+}
+
+// One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
+// backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
+template <bool HIER>
+__global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
+                                                   BwdScratch rec, hlgs_grads o, float fx, float fy, int has_depth)
+{
+    const int t_idx = blockIdx.x * 256 + threadIdx.x;
+    if (t_idx >= a.P) return;
+    const int idx = HIER ? a.indices[t_idx] : t_idx;
+    const int M3 = a.M * 3;
+    if (!(radii[t_idx] > 0)) {
+        if (!HIER) {
+            o.dmean2D[3 * idx] = 0.f; o.dmean2D[3 * idx + 1] = 0.f; o.dmean2D[3 * idx + 2] = 0.f;
+            o.dcolor[3 * idx] = 0.f; o.dcolor[3 * idx + 1] = 0.f; o.dcolor[3 * idx + 2] = 0.f;
+            o.dopacity[idx] = 0.f;
+            o.dmean3D[3 * idx] = 0.f; o.dmean3D[3 * idx + 1] = 0.f; o.dmean3D[3 * idx + 2] = 0.f;
+            for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = 0.f;
+            if (o.dsh)
+                for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+            o.dscale[3 * idx] = 0.f; o.dscale[3 * idx + 1] = 0.f; o.dscale[3 * idx + 2] = 0.f;
+            reinterpret_cast<float4*>(o.drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        return;
+    }
+    // ---- per-Gaussian sum of the blend records (fixed order => deterministic)
+    const uint32_t end = g.point_offsets[t_idx], start = end - g.tiles_touched[t_idx];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f, s8 = 0.f, s9 = 0.f;
+    for (uint32_t r = start; r < end; r++) {
+        const float4 A = rec.recA[r];
+        const float4 B = rec.recB[r];
+        const float2 Cc = rec.recC[r];
+        s0 += A.x; s1 += A.y; s2 += A.z; s3 += A.w;
+        s4 += B.x; s5 += B.y; s6 += B.z; s7 += B.w;
+        s8 += Cc.x; s9 += Cc.y;
+    }
+    o.dmean2D[3 * idx] = s0;
+    o.dmean2D[3 * idx + 1] = s1;
+    o.dmean2D[3 * idx + 2] = 0.f;
+    o.dcolor[3 * idx] = s6;
+    o.dcolor[3 * idx + 1] = s7;
+    o.dcolor[3 * idx + 2] = s8;
+
+    // ---- computeCov2DCUDA (backward.cu:147-326)
+    const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
+    float c3[6];
+    for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
+    const f3 mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    Cov2D k;
+    cov2d_eval(mean, fx, fy, a.tanfovx, a.tanfovy, c3, a.viewmatrix, k);
+    const float xg = k.txtz < -k.limx || k.txtz > k.limx ? 0.f : 1.f;
+    const float yg = k.tytz < -k.limy || k.tytz > k.limy ? 0.f : 1.f;
+    float c_xx = k.cov.m[0][0], c_xy = k.cov.m[0][1], c_yy = k.cov.m[1][1];
+    const float h_var = 0.3f;
+    const float det_cov = c_xx * c_yy - c_xy * c_xy;
+    c_xx += h_var;
+    c_yy += h_var;
+    const float det_h = c_xx * c_yy - c_xy * c_xy;
+    const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    const float d_hs = s5 * a.opacities[idx];
+    const float dop = s5 * hs;
+    const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
+    float dxx, dxy, dyy;
+    {
+        const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
+        const float sqv = w * w + w * (x + y) + x * y - z * z;
+        const float denom_f = d_inside / (sqv * sqv);
+        dxx = w * (w * y + y * y + z * z) * denom_f;
+        dyy = w * (w * x + x * x + z * z) * denom_f;
+        dxy = -2.f * w * z * (w + x + y) * denom_f;
+    }
+    const float dcx = s2, dcy = s3, dcz = s4;
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const m3& Tm = k.T;
+    const m3& V = k.Vrk;
+    float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#define TT(c, r) Tm.m[c][r]
+#define VK(c, r) V.m[c][r]
+    if (denom2inv != 0) {
+        dxx += denom2inv * (-c_yy * c_yy * dcx + 2 * c_xy * c_yy * dcy + (denom - c_xx * c_yy) * dcz);
+        dyy += denom2inv * (-c_xx * c_xx * dcz + 2 * c_xx * c_xy * dcy + (denom - c_xx * c_yy) * dcx);
+        dxy += denom2inv * 2 * (c_xy * c_yy * dcx - (denom + 2 * c_xy * c_xy) * dcy + c_xx * c_xy * dcz);
+        dc[0] = (TT(0, 0) * TT(0, 0) * dxx + TT(0, 0) * TT(1, 0) * dxy + TT(1, 0) * TT(1, 0) * dyy);
+        dc[3] = (TT(0, 1) * TT(0, 1) * dxx + TT(0, 1) * TT(1, 1) * dxy + TT(1, 1) * TT(1, 1) * dyy);
+        dc[5] = (TT(0, 2) * TT(0, 2) * dxx + TT(0, 2) * TT(1, 2) * dxy + TT(1, 2) * TT(1, 2) * dyy);
+        dc[1] = 2 * TT(0, 0) * TT(0, 1) * dxx + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dxy + 2 * TT(1, 0) * TT(1, 1) * dyy;
+        dc[2] = 2 * TT(0, 0) * TT(0, 2) * dxx + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dxy + 2 * TT(1, 0) * TT(1, 2) * dyy;
+        dc[4] = 2 * TT(0, 2) * TT(0, 1) * dxx + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dxy + 2 * TT(1, 1) * TT(1, 2) * dyy;
+    }
+    const float dT00 = 2 * (TT(0, 0) * VK(0, 0) + TT(0, 1) * VK(0, 1) + TT(0, 2) * VK(0, 2)) * dxx + (TT(1, 0) * VK(0, 0) + TT(1, 1) * VK(0, 1) + TT(1, 2) * VK(0, 2)) * dxy;
+    const float dT01 = 2 * (TT(0, 0) * VK(1, 0) + TT(0, 1) * VK(1, 1) + TT(0, 2) * VK(1, 2)) * dxx + (TT(1, 0) * VK(1, 0) + TT(1, 1) * VK(1, 1) + TT(1, 2) * VK(1, 2)) * dxy;
+    const float dT02 = 2 * (TT(0, 0) * VK(2, 0) + TT(0, 1) * VK(2, 1) + TT(0, 2) * VK(2, 2)) * dxx + (TT(1, 0) * VK(2, 0) + TT(1, 1) * VK(2, 1) + TT(1, 2) * VK(2, 2)) * dxy;
+    const float dT10 = 2 * (TT(1, 0) * VK(0, 0) + TT(1, 1) * VK(0, 1) + TT(1, 2) * VK(0, 2)) * dyy + (TT(0, 0) * VK(0, 0) + TT(0, 1) * VK(0, 1) + TT(0, 2) * VK(0, 2)) * dxy;
+    const float dT11 = 2 * (TT(1, 0) * VK(1, 0) + TT(1, 1) * VK(1, 1) + TT(1, 2) * VK(1, 2)) * dyy + (TT(0, 0) * VK(1, 0) + TT(0, 1) * VK(1, 1) + TT(0, 2) * VK(1, 2)) * dxy;
+    const float dT12 = 2 * (TT(1, 0) * VK(2, 0) + TT(1, 1) * VK(2, 1) + TT(1, 2) * VK(2, 2)) * dyy + (TT(0, 0) * VK(2, 0) + TT(0, 1) * VK(2, 1) + TT(0, 2) * VK(2, 2)) * dxy;
+#undef VK
+#undef TT
+    const m3& Wm = k.W;
+    const float dJ00 = Wm.m[0][0] * dT00 + Wm.m[0][1] * dT01 + Wm.m[0][2] * dT02;
+    const float dJ02 = Wm.m[2][0] * dT00 + Wm.m[2][1] * dT01 + Wm.m[2][2] * dT02;
+    const float dJ11 = Wm.m[1][0] * dT10 + Wm.m[1][1] * dT11 + Wm.m[1][2] * dT12;
+    const float dJ12 = Wm.m[2][0] * dT10 + Wm.m[2][1] * dT11 + Wm.m[2][2] * dT12;
+    const f3 t = k.t;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = xg * -fx * tz2 * dJ02;
+    const float dty = yg * -fy * tz2 * dJ12;
+    float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * t.x) * tz3 * dJ02 + (2 * fy * t.y) * tz3 * dJ12;
+    if (has_depth) dtz -= s9 / (t.z * t.z);
+    const float* vm = a.viewmatrix;
+    f3 dmean = mk(vm[0] * dtx + vm[1] * dty + vm[2] * dtz, vm[4] * dtx + vm[5] * dty + vm[6] * dtz,
+                  vm[8] * dtx + vm[9] * dty + vm[10] * dtz);
+
+    // ---- preprocessCUDA backward (backward.cu:398-495): screen-space mean -> world mean
+    const float* proj = a.projmatrix;
+    const f3 m = mean;
+    const float m_w = 1.0f / (xform44w(m, proj) + 0.0000001f);
+    const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+    const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+    f3 d2;
+    d2.x = (proj[0] * m_w - proj[3] * mul1) * s0 + (proj[1] * m_w - proj[3] * mul2) * s1;
+    d2.y = (proj[4] * m_w - proj[7] * mul1) * s0 + (proj[5] * m_w - proj[7] * mul2) * s1;
+    d2.z = (proj[8] * m_w - proj[11] * mul1) * s0 + (proj[9] * m_w - proj[11] * mul2) * s1;
+    dmean = add(dmean, d2);
+
+    // ---- SH backward (backward.cu:23-142)
+    if (a.shs) {
+        const int deg = a.D;
+        const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+        const f3 dir_orig = sub(m, campos);
+        const float len = sqrtf(dot(dir_orig, dir_orig));
+        const f3 dir = mk(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+        const float* sh = a.shs + (size_t)idx * M3;
+        auto SHV = [&](int c) { return mk(sh[3 * c], sh[3 * c + 1], sh[3 * c + 2]); };
+        const uint32_t cl = g.clamped[t_idx];
+        f3 dRGB = mk(s6, s7, s8);
+        dRGB.x *= (cl & 1u) ? 0 : 1;
+        dRGB.y *= (cl & 2u) ? 0 : 1;
+        dRGB.z *= (cl & 4u) ? 0 : 1;
+        f3 ddx = mk(0, 0, 0), ddy = mk(0, 0, 0), ddz = mk(0, 0, 0);
+        const float x = dir.x, y = dir.y, z = dir.z;
+        float* dsh = o.dsh + (size_t)idx * M3;
+        int written = 1;
+        auto PUT = [&](int c, float s) {
+            const f3 v = scl(s, dRGB);
+            dsh[3 * c] = v.x; dsh[3 * c + 1] = v.y; dsh[3 * c + 2] = v.z;
+        };
+        PUT(0, kSH_C0);
+        if (deg > 0) {
+            PUT(1, -kSH_C1 * y);
+            PUT(2, kSH_C1 * z);
+            PUT(3, -kSH_C1 * x);
+            written = 4;
+            ddx = scl(-kSH_C1, SHV(3));
+            ddy = scl(-kSH_C1, SHV(1));
+            ddz = scl(kSH_C1, SHV(2));
+            if (deg > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                PUT(4, kSH_C2[0] * xy);
+                PUT(5, kSH_C2[1] * yz);
+                PUT(6, kSH_C2[2] * (2.f * zz - xx - yy));
+                PUT(7, kSH_C2[3] * xz);
+                PUT(8, kSH_C2[4] * (xx - yy));
+                written = 9;
+                ddx = add(ddx, add(add(add(scl(kSH_C2[0] * y, SHV(4)), scl(kSH_C2[2] * 2.f * -x, SHV(6))),
+                                       scl(kSH_C2[3] * z, SHV(7))), scl(kSH_C2[4] * 2.f * x, SHV(8))));
+                ddy = add(ddy, add(add(add(scl(kSH_C2[0] * x, SHV(4)), scl(kSH_C2[1] * z, SHV(5))),
+                                       scl(kSH_C2[2] * 2.f * -y, SHV(6))), scl(kSH_C2[4] * 2.f * -y, SHV(8))));
+                ddz = add(ddz, add(add(scl(kSH_C2[1] * y, SHV(5)), scl(kSH_C2[2] * 2.f * 2.f * z, SHV(6))),
+                                   scl(kSH_C2[3] * x, SHV(7))));
+                if (deg > 2) {
+                    PUT(9, kSH_C3[0] * y * (3.f * xx - yy));
+                    PUT(10, kSH_C3[1] * xy * z);
+                    PUT(11, kSH_C3[2] * y * (4.f * zz - xx - yy));
+                    PUT(12, kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy));
+                    PUT(13, kSH_C3[4] * x * (4.f * zz - xx - yy));
+                    PUT(14, kSH_C3[5] * z * (xx - yy));
+                    PUT(15, kSH_C3[6] * x * (xx - 3.f * yy));
+                    written = 16;
+                    f3 sx = scl(2.f * xy, scl(3.f, scl(kSH_C3[0], SHV(9))));
+                    sx = add(sx, scl(yz, scl(kSH_C3[1], SHV(10))));
+                    sx = add(sx, scl(xy, scl(-2.f, scl(kSH_C3[2], SHV(11)))));
+                    sx = add(sx, scl(2.f * xz, scl(-3.f, scl(kSH_C3[3], SHV(12)))));
+                    sx = add(sx, scl(-3.f * xx + 4.f * zz - yy, scl(kSH_C3[4], SHV(13))));
+                    sx = add(sx, scl(xz, scl(2.f, scl(kSH_C3[5], SHV(14)))));
+                    sx = add(sx, scl(xx - yy, scl(3.f, scl(kSH_C3[6], SHV(15)))));
+                    ddx = add(ddx, sx);
+                    f3 sy = scl(xx - yy, scl(3.f, scl(kSH_C3[0], SHV(9))));
+                    sy = add(sy, scl(xz, scl(kSH_C3[1], SHV(10))));
+                    sy = add(sy, scl(-3.f * yy + 4.f * zz - xx, scl(kSH_C3[2], SHV(11))));
+                    sy = add(sy, scl(2.f * yz, scl(-3.f, scl(kSH_C3[3], SHV(12)))));
+                    sy = add(sy, scl(xy, scl(-2.f, scl(kSH_C3[4], SHV(13)))));
+                    sy = add(sy, scl(yz, scl(-2.f, scl(kSH_C3[5], SHV(14)))));
+                    sy = add(sy, scl(2.f * xy, scl(-3.f, scl(kSH_C3[6], SHV(15)))));
+                    ddy = add(ddy, sy);
+                    f3 sz = scl(xy, scl(kSH_C3[1], SHV(10)));
+                    sz = add(sz, scl(2.f * yz, scl(4.f, scl(kSH_C3[2], SHV(11)))));
+                    sz = add(sz, scl(2.f * zz - xx - yy, scl(3.f, scl(kSH_C3[3], SHV(12)))));
+                    sz = add(sz, scl(2.f * xz, scl(4.f, scl(kSH_C3[4], SHV(13)))));
+                    sz = add(sz, scl(xx - yy, scl(kSH_C3[5], SHV(14))));
+                    ddz = add(ddz, sz);
+                }
+            }
+        }
+        for (int i = 3 * written; i < M3; i++) dsh[i] = 0.f;
+        const f3 dL_ddir = mk(dot(ddx, dRGB), dot(ddy, dRGB), dot(ddz, dRGB));
+        dmean = add(dmean, dnormvdv(dir_orig, dL_ddir));
+    } else if (o.dsh) {
+        for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+    }
+
+    // ---- cov3D backward (backward.cu:330-393)
+    float dscale[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.scales) {
+        const float4 q4 = reinterpret_cast<const float4*>(a.rotations)[idx];
+        const float qq[4] = {q4.x, q4.y, q4.z, q4.w};
+        const float r = qq[0], x = qq[1], y = qq[2], z = qq[3];
+        const m3 R = quat_rot(qq);
+        m3 S = mcols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        const f3 s = scl(a.scale_modifier, mk(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]));
+        S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
+        const m3 Mm = mmul(S, R);
+        const m3 dS = mcols(dc[0], 0.5f * dc[1], 0.5f * dc[2], 0.5f * dc[1], dc[3], 0.5f * dc[4], 0.5f * dc[2],
+                            0.5f * dc[4], dc[5]);
+        m3 M2 = Mm;
+        for (int c = 0; c < 3; c++)
+            for (int rr = 0; rr < 3; rr++) M2.m[c][rr] = 2.0f * Mm.m[c][rr];
+        const m3 dM = mmul(M2, dS);
+        const m3 Rt = mtrans(R);
+        m3 dMt = mtrans(dM);
+        for (int i = 0; i < 3; i++)
+            dscale[i] = Rt.m[i][0] * dMt.m[i][0] + Rt.m[i][1] * dMt.m[i][1] + Rt.m[i][2] * dMt.m[i][2];
+        for (int rr = 0; rr < 3; rr++) { dMt.m[0][rr] *= s.x; dMt.m[1][rr] *= s.y; dMt.m[2][rr] *= s.z; }
+        dq[0] = 2 * z * (dMt.m[0][1] - dMt.m[1][0]) + 2 * y * (dMt.m[2][0] - dMt.m[0][2]) + 2 * x * (dMt.m[1][2] - dMt.m[2][1]);
+        dq[1] = 2 * y * (dMt.m[1][0] + dMt.m[0][1]) + 2 * z * (dMt.m[2][0] + dMt.m[0][2]) + 2 * r * (dMt.m[1][2] - dMt.m[2][1]) - 4 * x * (dMt.m[2][2] + dMt.m[1][1]);
+        dq[2] = 2 * x * (dMt.m[1][0] + dMt.m[0][1]) + 2 * r * (dMt.m[2][0] - dMt.m[0][2]) + 2 * z * (dMt.m[1][2] + dMt.m[2][1]) - 4 * y * (dMt.m[2][2] + dMt.m[0][0]);
+        dq[3] = 2 * r * (dMt.m[0][1] - dMt.m[1][0]) + 2 * x * (dMt.m[2][0] + dMt.m[0][2]) + 2 * y * (dMt.m[1][2] + dMt.m[2][1]) - 4 * z * (dMt.m[1][1] + dMt.m[0][0]);
+    }
+    float dop_out = dop;
+    if (HIER) {
+        // backward.cu:458-494: the child's opacity/scale/rotation/SH gradients are dropped and
+        // (1 - t) of its mean gradient moves to the parent (added by k_parent_mean_add).
+        const int parent = a.parent_indices[t_idx];
+        if (parent != -1) {
+            const float tt = a.ts[t_idx];
+            dop_out = 0.f;
+            for (int i = 0; i < 3; i++) dscale[i] = 0.f;
+            for (int i = 0; i < 4; i++) dq[i] = 0.f;
+            rec.parent_dmean[3 * t_idx] = (1.0f - tt) * dmean.x;
+            rec.parent_dmean[3 * t_idx + 1] = (1.0f - tt) * dmean.y;
+            rec.parent_dmean[3 * t_idx + 2] = (1.0f - tt) * dmean.z;
+            dmean = mk(0.f, 0.f, 0.f);
+            if (o.dsh)
+                for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+        }
+    }
+    o.dopacity[idx] = dop_out;
+    for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = dc[i];
+    o.dmean3D[3 * idx] = dmean.x;
+    o.dmean3D[3 * idx + 1] = dmean.y;
+    o.dmean3D[3 * idx + 2] = dmean.z;
+    o.dscale[3 * idx] = dscale[0];
+    o.dscale[3 * idx + 1] = dscale[1];
+    o.dscale[3 * idx + 2] = dscale[2];
+    reinterpret_cast<float4*>(o.drot)[idx] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+}
+
+__global__ void __launch_bounds__(256) k_parent_mean_add(int P, const int* __restrict__ radii,
+                                                         const int* __restrict__ parent_indices,
+                                                         const float* __restrict__ pd, float* __restrict__ dmean3D)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= P || !(radii[t] > 0)) return;
+    const int p = parent_indices[t];
+    if (p == -1) return;
+    for (int i = 0; i < 3; i++) atomicAdd(&dmean3D[3 * p + i], pd[3 * t + i]);
+}
+
+void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, const BwdScratch& rs,
+                      int gx, int gy, const float* dL_dpix, const float* dL_dinv, hipStream_t s)
+{
+    const int T = gx * gy;
+    const float* colors = a.colors_precomp ? a.colors_precomp : g.rgb;
+    const bool interp = a.ts != nullptr && a.kids != nullptr;
+#define HLGS_BB(I, Dp)                                                                                              \
+    hipLaunchKernelGGL((k_blend_bwd<I, Dp>), dim3(T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, \
+                       colors, im.final_T, im.n_contrib, a.bg, dL_dpix, dL_dinv, a.ts, a.kids, rs)
+    if (interp) { if (dL_dinv) HLGS_BB(true, true); else HLGS_BB(true, false); }
+    else { if (dL_dinv) HLGS_BB(false, true); else HLGS_BB(false, false); }
+#undef HLGS_BB
+}
+
+void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
+                      const hlgs_grads& o, bool has_depth, hipStream_t s)
+{
+    const float fy = a.H / (2.0f * a.tanfovy);
+    const float fx = a.W / (2.0f * a.tanfovx);
+    const dim3 grid((a.P + 255) / 256);
+    if (a.indices) {
+        hipLaunchKernelGGL(k_gauss_bwd<true>, grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
+        if (a.parent_indices)
+            hipLaunchKernelGGL(k_parent_mean_add, grid, dim3(256), 0, s, a.P, radii, a.parent_indices,
+                               rs.parent_dmean, o.dmean3D);
+    } else {
+        hipLaunchKernelGGL(k_gauss_bwd<false>, grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
+    }
+}
+
+}  // namespace hlgs

@@ -1,0 +1,447 @@
+// raster_fwd.hip -- forward rasterizer kernels for gfx950.
+//
+// Reference semantics (submodules/hierarchy-rasterizer/cuda_rasterizer):
+//   k_preprocess      <- preprocessCUDA<3>   forward.cu:218-445   (+ per-tile instance counting)
+//   k_tile_ranges     <- identifyTileRanges  rasterizer_impl.cu:120-142 (from the tile-count scan)
+//   k_scatter_keys    <- duplicateWithKeys   rasterizer_impl.cu:70-115
+//   k_tile_sort / k_merge_runs <- cub::DeviceRadixSort::SortPairs rasterizer_impl.cu:355-363
+//   k_blend_fwd       <- renderCUDA<3>       forward.cu:450-596
+//
+// Binning is re-designed for MI355X: instead of one 45-bit global LSD radix sort (6+ passes over R
+// 12-byte pairs) instances are counted per tile in the preprocess, scattered once into their tile's
+// segment, and each segment is sorted in LDS by the total order (depth bits, Gaussian index).  That
+// is exactly the order CUB's stable sort of (tile | depth) produces from the reference's
+// Gaussian-ordered duplicate list, so point_list is identical.
+#include "hlgs_internal.h"
+#include "hlgs_math.h"
+
+namespace hlgs {
+
+// ------------------------------------------------------------------------------------------------
+// Preprocess: one thread per rasterised Gaussian.
+// ------------------------------------------------------------------------------------------------
+template <bool HIER>
+__global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, int* __restrict__ radii,
+                                                    uint32_t* __restrict__ tile_count, int gx, int gy, float fx,
+                                                    float fy)
+{
+    const int t_idx = blockIdx.x * 256 + threadIdx.x;
+    if (t_idx >= a.P) return;
+    const int r_idx = HIER ? a.indices[t_idx] : t_idx;
+    radii[t_idx] = 0;
+    g.tiles_touched[t_idx] = 0;
+    g.rects[t_idx] = make_int2(0, 0);
+    g.clamped[t_idx] = 0;
+
+    bool use_parent = false;
+    int p_idx = 0;
+    float t = 0.f;
+    f3 p_orig = mk(a.means3D[3 * r_idx], a.means3D[3 * r_idx + 1], a.means3D[3 * r_idx + 2]);
+    if (HIER) {
+        p_idx = a.parent_indices[t_idx];
+        if (p_idx != -1) { use_parent = true; t = a.ts[t_idx]; }
+        else p_idx = 0;
+        if (use_parent) {
+            f3 pa = mk(a.means3D[3 * p_idx], a.means3D[3 * p_idx + 1], a.means3D[3 * p_idx + 2]);
+            p_orig = mk(t * p_orig.x + (1.0f - t) * pa.x, t * p_orig.y + (1.0f - t) * pa.y,
+                        t * p_orig.z + (1.0f - t) * pa.z);
+        }
+    }
+    const float* proj = a.projmatrix;
+    const float* view = a.viewmatrix;
+    float hx = proj[0] * p_orig.x + proj[4] * p_orig.y + proj[8] * p_orig.z + proj[12];
+    float hy = proj[1] * p_orig.x + proj[5] * p_orig.y + proj[9] * p_orig.z + proj[13];
+    float hw = xform44w(p_orig, proj);
+    float p_w = 1.0f / (hw + 0.0000001f);
+    float ppx = hx * p_w, ppy = hy * p_w;
+    f3 p_view = xform43(p_orig, view);
+    if (p_view.z <= 0.2f) return;
+
+    float c3[6];
+    const float* cov3D;
+    if (a.cov3D_precomp == nullptr) {
+        f3 scale = mk(a.scales[3 * r_idx], a.scales[3 * r_idx + 1], a.scales[3 * r_idx + 2]);
+        float4 rq = reinterpret_cast<const float4*>(a.rotations)[r_idx];
+        float rot[4] = {rq.x, rq.y, rq.z, rq.w};
+        if (HIER && use_parent) {
+            f3 ps = mk(a.scales[3 * p_idx], a.scales[3 * p_idx + 1], a.scales[3 * p_idx + 2]);
+            scale = add(scl(t, scale), scl(1.0f - t, ps));
+            float4 oq = reinterpret_cast<const float4*>(a.rotations)[p_idx];
+            float orot[4] = {oq.x, oq.y, oq.z, oq.w};
+            float dp = rot[0] * orot[0] + rot[1] * orot[1] + rot[2] * orot[2] + rot[3] * orot[3];
+            if (dp < 0.0f)
+                for (int i = 0; i < 4; i++) orot[i] = -orot[i];
+            for (int i = 0; i < 4; i++) rot[i] = t * rot[i] + (1.0f - t) * orot[i];
+        }
+        cov3d_fwd(scale, a.scale_modifier, rot, c3);
+        cov3D = c3;
+    } else {
+        // the reference leaves cov3D unassigned here; we take the evident intent.
+        for (int i = 0; i < 6; i++) c3[i] = a.cov3D_precomp[6 * t_idx + i];
+        cov3D = c3;
+    }
+    float2* c3o = reinterpret_cast<float2*>(g.cov3D + 6 * (size_t)t_idx);
+    c3o[0] = make_float2(c3[0], c3[1]);
+    c3o[1] = make_float2(c3[2], c3[3]);
+    c3o[2] = make_float2(c3[4], c3[5]);
+
+    Cov2D k;
+    cov2d_eval(p_orig, fx, fy, a.tanfovx, a.tanfovy, cov3D, view, k);
+    float cx = k.cov.m[0][0], cy = k.cov.m[0][1], cz = k.cov.m[1][1];
+    const float h_var = 0.3f;
+    const float det_cov = cx * cz - cy * cy;
+    cx += h_var;
+    cz += h_var;
+    const float det_h = cx * cz - cy * cy;
+    const float h_scale = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    const float det = det_h;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float conic_x = cz * det_inv, conic_y = -cy * det_inv, conic_z = cx * det_inv;
+    const float mid = 0.5f * (cx + cz);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    const float pix_x = ndc2pix(ppx, a.W), pix_y = ndc2pix(ppy, a.H);
+    const int ex = (int)ceilf(3.f * sqrtf(cx)), ey = (int)ceilf(3.f * sqrtf(cz));
+    g.rects[t_idx] = make_int2(ex, ey);
+    int x0, y0, x1, y1;
+    tile_rect(pix_x, pix_y, ex, ey, gx, gy, x0, y0, x1, y1);
+    const uint32_t area = (uint32_t)(x1 - x0) * (uint32_t)(y1 - y0);
+    if (area == 0) return;
+
+    if (a.colors_precomp == nullptr) {
+        const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+        const f3 mean_r = mk(a.means3D[3 * r_idx], a.means3D[3 * r_idx + 1], a.means3D[3 * r_idx + 2]);
+        const float* sc = a.shs + (size_t)r_idx * a.M * 3;
+        uint32_t cb = 0;
+        f3 rgb;
+        if (!(HIER && use_parent)) {
+            rgb = sh_to_rgb(a.D, [&](int c) { return mk(sc[3 * c], sc[3 * c + 1], sc[3 * c + 2]); }, mean_r, campos, cb);
+        } else {
+            // forward.cu:86-138: every coefficient lerped child<->parent, view direction from the child
+            const float* sp = a.shs + (size_t)p_idx * a.M * 3;
+            const float tt = t;
+            rgb = sh_to_rgb(a.D, [&](int c) {
+                return mk(tt * sc[3 * c] + (1.0f - tt) * sp[3 * c], tt * sc[3 * c + 1] + (1.0f - tt) * sp[3 * c + 1],
+                          tt * sc[3 * c + 2] + (1.0f - tt) * sp[3 * c + 2]);
+            }, mean_r, campos, cb);
+        }
+        g.clamped[t_idx] = cb;
+        g.rgb[3 * t_idx] = rgb.x;
+        g.rgb[3 * t_idx + 1] = rgb.y;
+        g.rgb[3 * t_idx + 2] = rgb.z;
+    }
+    g.depths[t_idx] = p_view.z;
+    radii[t_idx] = (int)my_radius;
+    g.means2D[t_idx] = make_float2(pix_x, pix_y);
+    float opacity = a.opacities[r_idx];
+    if (HIER && use_parent) opacity = t * opacity + (1.0f - t) * a.opacities[p_idx];
+    g.conic_opacity[t_idx] = make_float4(conic_x, conic_y, conic_z, opacity * h_scale);
+    g.tiles_touched[t_idx] = area;
+    for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
+}
+
+// ranges[t] = [incl[t] - count[t], incl[t]); misc[0] = R, misc[1] = max count; cursor reset for the scatter.
+__global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict__ count, uint32_t* incl_and_cursor,
+                                                     uint2* __restrict__ ranges, uint32_t* __restrict__ misc, int T)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t c = count[t], e = incl_and_cursor[t];
+    ranges[t] = make_uint2(e - c, e);
+    incl_and_cursor[t] = 0;
+    if (t == T - 1) misc[0] = e;
+    if (c) atomicMax(&misc[1], c);
+}
+
+// One thread per Gaussian: drop (depth, index) keys into each touched tile's segment.
+__global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restrict__ radii, Geom g,
+                                                      const uint2* __restrict__ ranges, uint32_t* cursor,
+                                                      uint64_t* __restrict__ keys, int gx, int gy)
+{
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= P || radii[idx] <= 0) return;
+    const float2 xy = g.means2D[idx];
+    const int2 ext = g.rects[idx];
+    int x0, y0, x1, y1;
+    tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
+    const uint64_t key = ((uint64_t)__float_as_uint(g.depths[idx]) << 32) | (uint32_t)idx;
+    for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++) {
+            const int tile = y * gx + x;
+            const uint32_t slot = atomicAdd(&cursor[tile], 1u);
+            keys[ranges[tile].x + slot] = key;
+        }
+}
+
+// One 256-thread block per tile: bitonic sort of the tile's keys in LDS.  Tiles longer than kSortCap
+// are sorted in kSortCap runs here and merged by k_merge_runs.
+__global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ranges, uint64_t* keys,
+                                                   uint32_t* __restrict__ point_list, int T)
+{
+    __shared__ uint64_t s[kSortCap];
+    const int tile = xcd_remap(blockIdx.x, T);
+    const uint2 r = ranges[tile];
+    const uint32_t cnt = r.y - r.x;
+    if (cnt == 0) return;
+    const int tid = threadIdx.x;
+    const bool big = cnt > (uint32_t)kSortCap;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += kSortCap) {
+        const uint32_t n = min((uint32_t)kSortCap, cnt - c0);
+        uint32_t np = 2;
+        while (np < n) np <<= 1;
+        for (uint32_t i = tid; i < np; i += 256) s[i] = i < n ? keys[r.x + c0 + i] : ~0ull;
+        __syncthreads();
+        for (uint32_t kk = 2; kk <= np; kk <<= 1)
+            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < np / 2; i += 256) {
+                    const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                    const bool asc = (lo & kk) == 0;
+                    const uint64_t x = s[lo], y = s[hi];
+                    if ((x > y) == asc) { s[lo] = y; s[hi] = x; }
+                }
+                __syncthreads();
+            }
+        if (big)
+            for (uint32_t i = tid; i < n; i += 256) keys[r.x + c0 + i] = s[i];
+        else
+            for (uint32_t i = tid; i < n; i += 256) point_list[r.x + c0 + i] = (uint32_t)s[i];
+        __syncthreads();
+    }
+}
+
+// Merge pass for long tiles: element of run r finds its rank in the partner run by binary search.
+__global__ void __launch_bounds__(256) k_merge_runs(const uint2* __restrict__ ranges, const uint64_t* __restrict__ src,
+                                                    uint64_t* __restrict__ dst, uint32_t* __restrict__ point_list,
+                                                    uint32_t L, int last)
+{
+    const int tile = blockIdx.y;
+    const uint2 r = ranges[tile];
+    const uint32_t cnt = r.y - r.x;
+    if (cnt <= (uint32_t)kSortCap) return;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= cnt) return;
+    const uint64_t key = src[r.x + i];
+    const uint32_t run = i / L, a = i - run * L;
+    const uint32_t prun = run ^ 1u;
+    uint32_t out = i;
+    const uint64_t pstart64 = (uint64_t)prun * L;
+    if (pstart64 < cnt) {
+        const uint32_t ps = (uint32_t)pstart64, pe = min(cnt, ps + L);
+        uint32_t lo = ps, hi = pe;  // count partner keys < key (keys are unique)
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (src[r.x + mid] < key) lo = mid + 1; else hi = mid;
+        }
+        out = min(run, prun) * L + a + (lo - ps);
+    }
+    dst[r.x + out] = key;
+    if (last) point_list[r.x + out] = (uint32_t)key;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Front-to-back blend: one wave64 per 16x16 tile, four pixels per lane (rows ly, ly+4, ly+8, ly+12),
+// 64-splat batches staged in LDS and read back as broadcasts.
+// ------------------------------------------------------------------------------------------------
+template <bool INTERP, bool DEPTH>
+__global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
+                                                  int W, int H, int gx, int T, const float2* __restrict__ means2D,
+                                                  const float* __restrict__ features,
+                                                  const float4* __restrict__ conic_opacity,
+                                                  const float* __restrict__ depths, const float* __restrict__ ts,
+                                                  const int* __restrict__ kids, float* __restrict__ final_T,
+                                                  uint32_t* __restrict__ n_contrib, const float* __restrict__ bg,
+                                                  float* __restrict__ out_color, float* __restrict__ out_invdepth,
+                                                  int* __restrict__ seen)
+{
+    __shared__ float4 s_xy[64];   // x, y, id bits, 1/depth
+    __shared__ float4 s_co[64];   // conic x,y,z, opacity
+    __shared__ float4 s_col[64];  // r, g, b, interpolation t
+    __shared__ float s_fr[64];    // 1 / kids
+    const int tile = xcd_remap(blockIdx.x, T);
+    const int lane = threadIdx.x;
+    const int tx = tile % gx, ty = tile / gx;
+    const int px = tx * HLGS_TILE + (lane & 15);
+    const int py0 = ty * HLGS_TILE + (lane >> 4);
+    const float pxf = (float)px;
+    const uint2 range = ranges[tile];
+
+    float Tt[4], C0[4], C1[4], C2[4], D[4];
+    uint32_t last[4];
+    bool done[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        Tt[k] = 1.0f; C0[k] = C1[k] = C2[k] = D[k] = 0.0f; last[k] = 0;
+        done[k] = !(px < W && py0 + 4 * k < H);
+    }
+    for (uint32_t base = range.x; base < range.y; base += 64) {
+        if (__all(done[0] && done[1] && done[2] && done[3])) break;
+        const uint32_t pos = base + lane;
+        uint32_t my_id = 0;
+        if (pos < range.y) {
+            my_id = point_list[pos];
+            const float2 xy = means2D[my_id];
+            s_xy[lane] = make_float4(xy.x, xy.y, __uint_as_float(my_id), DEPTH ? 1 / depths[my_id] : 0.f);
+            s_co[lane] = conic_opacity[my_id];
+            s_col[lane] = make_float4(features[3 * my_id], features[3 * my_id + 1], features[3 * my_id + 2],
+                                      INTERP ? ts[my_id] : 0.f);
+            if (INTERP) s_fr[lane] = 1.0f / (float)kids[my_id];
+        }
+        __syncthreads();
+        const int n = (int)min(64u, range.y - base);
+        uint64_t seen_mask = 0;
+        for (int j = 0; j < n; j++) {
+            const float4 xy = s_xy[j];
+            const float4 co = s_co[j];
+            const uint32_t contrib = base - range.x + j + 1;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (done[k]) continue;
+                const float dx = xy.x - pxf, dy = xy.y - (float)(py0 + 4 * k);
+                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                if (power > 0.0f) continue;
+                const float my_alpha = fminf(0.99f, co.w * __expf(power));
+                float alpha = my_alpha;
+                if (INTERP) {
+                    const float tt = s_col[j].w;
+                    const float ka = 1.0f - __powf(1.0f - my_alpha, s_fr[j]);
+                    alpha = tt * my_alpha + (1.0f - tt) * ka;
+                }
+                if (alpha < 1.0f / 255.0f) continue;
+                const float test_T = Tt[k] * (1 - alpha);
+                if (test_T < 0.0001f) { done[k] = true; continue; }
+                const float4 c = s_col[j];
+                C0[k] += c.x * alpha * Tt[k];
+                C1[k] += c.y * alpha * Tt[k];
+                C2[k] += c.z * alpha * Tt[k];
+                if (DEPTH) D[k] += xy.w * alpha * Tt[k];
+                Tt[k] = test_T;
+                last[k] = contrib;
+                any = true;
+            }
+            if (__ballot(any)) seen_mask |= 1ull << j;
+        }
+        if (pos < range.y && ((seen_mask >> lane) & 1ull)) seen[my_id] = 1;
+        __syncthreads();
+    }
+    const size_t HW = (size_t)H * W;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int py = py0 + 4 * k;
+        if (px < W && py < H) {
+            const size_t pid = (size_t)W * py + px;
+            final_T[pid] = Tt[k];
+            n_contrib[pid] = last[k];
+            out_color[pid] = C0[k] + Tt[k] * bg[0];
+            out_color[HW + pid] = C1[k] + Tt[k] * bg[1];
+            out_color[2 * HW + pid] = C2[k] + Tt[k] * bg[2];
+            if (DEPTH) out_invdepth[pid] = D[k];
+        }
+    }
+}
+
+// rasterizer_impl.cu:54-66 with auxiliary.h:164-189 (prefiltered = false)
+__global__ void __launch_bounds__(256) k_mark_visible(int P, const float* __restrict__ means, const float* view,
+                                                      uint8_t* __restrict__ present)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    const f3 p = mk(means[3 * i], means[3 * i + 1], means[3 * i + 2]);
+    present[i] = !(xform43(p, view).z <= 0.2f);
+}
+
+// utils.cu:6-36 (MCMC relocation, eq. 9 of 3DGS-as-MCMC)
+__global__ void __launch_bounds__(256) k_relocation(int P, const float* __restrict__ op_old, const float* __restrict__ sc_old,
+                                                    const int* __restrict__ N, const float* __restrict__ binoms,
+                                                    int n_max, float* __restrict__ op_new, float* __restrict__ sc_new)
+{
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= P) return;
+    const int n = N[idx];
+    float denom = 0.0f;
+    const float on = 1.0f - powf(1.0f - op_old[idx], 1.0f / n);
+    op_new[idx] = on;
+    for (int i = 1; i <= n; ++i)
+        for (int k = 0; k <= i - 1; ++k) {
+            const float b = binoms[(i - 1) * n_max + k];
+            const float term = (float)(((k & 1) ? -1.0 : 1.0) / sqrt((double)(k + 1)) * pow((double)on, k + 1));
+            denom += b * term;
+        }
+    const float coeff = op_old[idx] / denom;
+    for (int i = 0; i < 3; ++i) sc_new[3 * idx + i] = coeff * sc_old[3 * idx + i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------------
+void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
+                       hipStream_t s)
+{
+    const float fy = a.H / (2.0f * a.tanfovy);
+    const float fx = a.W / (2.0f * a.tanfovx);
+    const dim3 grid((a.P + 255) / 256);
+    if (a.indices)
+        hipLaunchKernelGGL(k_preprocess<true>, grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
+    else
+        hipLaunchKernelGGL(k_preprocess<false>, grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
+}
+
+void launch_tile_ranges(const Img& im, int T, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_tile_ranges, dim3((T + 255) / 256), dim3(256), 0, s, im.tile_count, im.tile_cursor,
+                       im.ranges, im.misc, T);
+}
+
+void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b,
+                    int gx, int gy, uint32_t max_count, hipStream_t s, bool timing)
+{
+    const int T = gx * gy;
+    if (timing) stage_mark(s, 3, true);
+    hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
+                       im.tile_cursor, b.keys, gx, gy);
+    if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
+    hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, b.keys, b.point_list, T);
+    if (max_count > (uint32_t)kSortCap) {
+        uint64_t* src = b.keys;
+        uint64_t* dst = b.keys2;
+        for (uint32_t L = kSortCap; L < max_count; L <<= 1) {
+            const int last = (L << 1) >= max_count;
+            hipLaunchKernelGGL(k_merge_runs, dim3((max_count + 255) / 256, T), dim3(256), 0, s, im.ranges, src, dst,
+                               b.point_list, L, last);
+            uint64_t* t = src; src = dst; dst = t;
+        }
+    }
+    if (timing) stage_mark(s, 4, false);
+}
+
+void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, int gx, int gy,
+                      float* out_color, float* out_invdepth, int* seen, hipStream_t s)
+{
+    const int T = gx * gy;
+    const float* feat = a.colors_precomp ? a.colors_precomp : g.rgb;
+    const bool interp = a.ts != nullptr && a.kids != nullptr;
+    const bool depth = out_invdepth != nullptr;
+#define HLGS_BLEND(I, Dp)                                                                                       \
+    hipLaunchKernelGGL((k_blend_fwd<I, Dp>), dim3(T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, T, \
+                       g.means2D, feat, g.conic_opacity, g.depths, a.ts, a.kids, im.final_T, im.n_contrib, a.bg,   \
+                       out_color, out_invdepth, seen)
+    if (interp) { if (depth) HLGS_BLEND(true, true); else HLGS_BLEND(true, false); }
+    else { if (depth) HLGS_BLEND(false, true); else HLGS_BLEND(false, false); }
+#undef HLGS_BLEND
+}
+
+void launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, s, P, means, view, present);
+}
+
+void launch_relocation(int P, const float* oo, const float* so, const int* N, const float* binoms, int n_max,
+                       float* on, float* sn, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_relocation, dim3((P + 255) / 256), dim3(256), 0, s, P, oo, so, N, binoms, n_max, on, sn);
+}
+
+}  // namespace hlgs

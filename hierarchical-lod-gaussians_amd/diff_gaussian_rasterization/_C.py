@@ -1,0 +1,148 @@
+"""`diff_gaussian_rasterization._C` on MI355X.
+
+Same entry points, argument order and return tuples as the reference extension
+(submodules/hierarchy-rasterizer/ext.cpp:15-19, rasterize_points.cu:36-271), plus `mark_visible`, which
+the reference's Python wrapper calls (__init__.py:174) but never binds.  Tensors are
+allocated with torch on the current device; every kernel runs inside libhlgs.so (gfx950) on torch's
+current stream.
+"""
+import ctypes as C
+
+import torch
+
+from hlgs_core import _lib as L
+
+
+def _dev_f32(t, device):
+    """Small per-call tensors (bg, view/proj matrices, campos) must live on the device: the kernels
+    dereference them (rasterize_points.cu:109-125)."""
+    return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+def _opt(t, dtype=None):
+    """Empty tensor -> None (NULL); otherwise a contiguous view (rasterize_points.cu calls .contiguous())."""
+    if t is None or t.numel() == 0:
+        return None
+    t = t.contiguous()
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    return t
+
+
+def _raster_args(bg, render_indices, parent_indices, ts, kids, means3D, colors, opacity, scales, rotations,
+                 scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree,
+                 campos, prefiltered, debug):
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    dev = means3D.device
+    keep = dict(
+        bg=_dev_f32(bg, dev), means3D=means3D.contiguous(), colors=_opt(colors), opacity=_opt(opacity),
+        scales=_opt(scales), rotations=_opt(rotations), cov3D=_opt(cov3D_precomp),
+        view=_dev_f32(viewmatrix, dev), proj=_dev_f32(projmatrix, dev), campos=_dev_f32(campos, dev),
+        sh=_opt(sh), indices=_opt(render_indices, torch.int32), parents=_opt(parent_indices, torch.int32),
+        ts=_opt(ts, torch.float32), kids=_opt(kids, torch.int32))
+    L.require_gpu(*[v for v in keep.values() if isinstance(v, torch.Tensor)])
+    P_full = means3D.size(0)
+    P = keep["indices"].size(0) if keep["indices"] is not None else P_full
+    M = sh.size(1) if (sh is not None and sh.numel() and sh.size(0) != 0) else 0
+    a = L.RasterArgs(P=P, P_full=P_full, D=int(degree), M=M, W=int(W), H=int(H),
+                     bg=L.ptr(keep["bg"]), means3D=L.ptr(keep["means3D"]), shs=L.ptr(keep["sh"]),
+                     colors_precomp=L.ptr(keep["colors"]), opacities=L.ptr(keep["opacity"]),
+                     scales=L.ptr(keep["scales"]), rotations=L.ptr(keep["rotations"]),
+                     cov3D_precomp=L.ptr(keep["cov3D"]), viewmatrix=L.ptr(keep["view"]),
+                     projmatrix=L.ptr(keep["proj"]), campos=L.ptr(keep["campos"]),
+                     scale_modifier=float(scale_modifier), tanfovx=float(tan_fovx), tanfovy=float(tan_fovy),
+                     indices=L.ptr(keep["indices"]), parent_indices=L.ptr(keep["parents"]), ts=L.ptr(keep["ts"]),
+                     kids=L.ptr(keep["kids"]), prefiltered=int(bool(prefiltered)), debug=int(bool(debug)))
+    return a, keep, P, P_full, M
+
+
+def rasterize_gaussians(bg, render_indices, parent_indices, ts, kids, means3D, colors, opacity, scales, rotations,
+                        scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
+                        image_width, sh, degree, campos, prefiltered, debug, do_depth):
+    """-> (num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, invdepth, seen)
+    (rasterize_points.cu:36-139)."""
+    lib = L.load()
+    H, W = int(image_height), int(image_width)
+    a, keep, P, _, _ = _raster_args(bg, render_indices, parent_indices, ts, kids, means3D, colors, opacity, scales,
+                                    rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
+                                    tan_fovy, H, W, sh, degree, campos, prefiltered, debug)
+    dev = means3D.device
+    f32 = dict(dtype=torch.float32, device=dev)
+    color = torch.zeros((3, H, W), **f32)
+    invdepth = torch.zeros((1, H, W), **f32) if do_depth else torch.zeros((0, H, W), **f32)
+    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+    seen = torch.zeros((P,), dtype=torch.int32, device=dev)
+    u8 = dict(dtype=torch.uint8, device=dev)
+    geom = torch.empty((lib.hlgs_geom_buffer_size(P),), **u8)
+    img = torch.empty((lib.hlgs_image_buffer_size(W, H),), **u8)
+    info = L.FrameInfo()
+    binning = torch.empty((0,), **u8)
+    if P != 0:
+        s = L.stream()
+        L.check(lib.hlgs_rasterize_forward_prepare(C.byref(a), L.ptr(geom), L.ptr(img), L.ptr(radii), C.byref(info), s))
+        binning = torch.empty((lib.hlgs_binning_buffer_size(info.num_rendered),), **u8)
+        L.check(lib.hlgs_rasterize_forward_render(C.byref(a), L.ptr(radii), L.ptr(geom), L.ptr(img), L.ptr(binning),
+                                                  C.byref(info), L.ptr(color), L.ptr(invdepth) if do_depth else None,
+                                                  L.ptr(seen), s))
+    del keep
+    return int(info.num_rendered), color, radii, geom, binning, img, invdepth, seen
+
+
+def rasterize_gaussians_backward(bg, render_indices, parent_indices, ts, kids, means3D, radii, colors, opacities,
+                                 scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
+                                 tan_fovy, dL_dout_color, dL_dout_invdepth, sh, degree, campos, geomBuffer, R,
+                                 binningBuffer, imageBuffer, debug):
+    """-> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)
+    (rasterize_points.cu:141-245)."""
+    lib = L.load()
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    a, keep, P, P_full, M = _raster_args(bg, render_indices, parent_indices, ts, kids, means3D, colors, opacities,
+                                         scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+                                         tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
+    dev = means3D.device
+    f32 = dict(dtype=torch.float32, device=dev)
+    out = dict(dmean2D=torch.empty((P_full, 3), **f32), dcolor=torch.empty((P_full, 3), **f32),
+               dopacity=torch.empty((P_full, 1), **f32), dmean3D=torch.empty((P_full, 3), **f32),
+               dcov3D=torch.empty((P_full, 6), **f32), dsh=torch.empty((P_full, M, 3), **f32),
+               dscale=torch.empty((P_full, 3), **f32), drot=torch.empty((P_full, 4), **f32))
+    g = L.Grads(**{k: L.ptr(v) for k, v in out.items()})
+    dpix = dL_dout_color.contiguous().float()
+    dinv = None
+    if dL_dout_invdepth is not None and dL_dout_invdepth.numel() and dL_dout_invdepth.size(0) != 0:
+        dinv = dL_dout_invdepth.contiguous().float()
+    scratch = torch.empty((lib.hlgs_backward_scratch_size(P, int(R)),), dtype=torch.uint8, device=dev)
+    L.check(lib.hlgs_rasterize_backward(C.byref(a), L.ptr(radii.contiguous()), L.ptr(geomBuffer), L.ptr(imageBuffer),
+                                        L.ptr(binningBuffer), int(R), L.ptr(scratch), L.ptr(dpix), L.ptr(dinv),
+                                        C.byref(g), L.stream()))
+    del keep
+    return (out["dmean2D"], out["dcolor"], out["dopacity"], out["dmean3D"], out["dcov3D"], out["dsh"], out["dscale"],
+            out["drot"])
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """z > 0.2 view-space test per point (rasterizer_impl.cu:54-66) -> bool tensor."""
+    lib = L.load()
+    dev = means3D.device
+    m = means3D.contiguous().float()
+    L.require_gpu(m)
+    present = torch.zeros((m.size(0),), dtype=torch.bool, device=dev)
+    view, proj = _dev_f32(viewmatrix, dev), _dev_f32(projmatrix, dev)
+    L.check(lib.hlgs_mark_visible(m.size(0), L.ptr(m), L.ptr(view), L.ptr(proj), L.ptr(present), L.stream()))
+    return present
+
+
+def compute_relocation(opacity_old, scale_old, N, binoms, n_max):
+    """MCMC relocation (rasterize_points.cu:248-271) -> (opacity (P,), scale (3P,))."""
+    lib = L.load()
+    o = opacity_old.contiguous().float()
+    s = scale_old.contiguous().float()
+    n = N.contiguous().to(torch.int32)
+    b = binoms.contiguous().float()
+    L.require_gpu(o, s, n, b)
+    P = o.size(0)
+    new_o = torch.zeros((P,), dtype=torch.float32, device=o.device)
+    new_s = torch.zeros((3 * P,), dtype=torch.float32, device=o.device)
+    L.check(lib.hlgs_compute_relocation(P, L.ptr(o), L.ptr(s), L.ptr(n), L.ptr(b), int(n_max), L.ptr(new_o),
+                                        L.ptr(new_s), L.stream()))
+    return new_o, new_s

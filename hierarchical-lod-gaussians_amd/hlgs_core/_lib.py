@@ -1,0 +1,141 @@
+"""ctypes binding of libhlgs.so (include/hlgs.h).
+
+The library is the only compute path: if it is missing, or no GPU is present, calls raise -- there is
+no CPU fallback.  Tensors cross the boundary as raw device pointers taken from torch; work runs on
+torch's current HIP stream.
+"""
+import ctypes as C
+import os
+
+import torch
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libhlgs.so")
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "hlgs.h")
+
+_vp = C.c_void_p
+_i = C.c_int
+_f = C.c_float
+_sz = C.c_size_t
+
+
+class RasterArgs(C.Structure):
+    _fields_ = [("P", _i), ("P_full", _i), ("D", _i), ("M", _i), ("W", _i), ("H", _i),
+                ("bg", _vp), ("means3D", _vp), ("shs", _vp), ("colors_precomp", _vp), ("opacities", _vp),
+                ("scales", _vp), ("rotations", _vp), ("cov3D_precomp", _vp), ("viewmatrix", _vp),
+                ("projmatrix", _vp), ("campos", _vp), ("scale_modifier", _f), ("tanfovx", _f), ("tanfovy", _f),
+                ("indices", _vp), ("parent_indices", _vp), ("ts", _vp), ("kids", _vp), ("prefiltered", _i),
+                ("debug", _i)]
+
+
+class Grads(C.Structure):
+    _fields_ = [("dmean2D", _vp), ("dcolor", _vp), ("dopacity", _vp), ("dmean3D", _vp), ("dcov3D", _vp),
+                ("dsh", _vp), ("dscale", _vp), ("drot", _vp)]
+
+
+class FrameInfo(C.Structure):
+    _fields_ = [("num_rendered", _i), ("max_tile_count", _i)]
+
+
+_SIGS = {
+    "hlgs_last_error": (C.c_char_p, []),
+    "hlgs_version": (C.c_char_p, []),
+    "hlgs_geom_buffer_size": (_sz, [_i]),
+    "hlgs_image_buffer_size": (_sz, [_i, _i]),
+    "hlgs_binning_buffer_size": (_sz, [_i]),
+    "hlgs_backward_scratch_size": (_sz, [_i, _i]),
+    "hlgs_rasterize_forward_prepare": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, C.POINTER(FrameInfo), _vp]),
+    "hlgs_rasterize_forward_render": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, _vp, C.POINTER(FrameInfo), _vp,
+                                           _vp, _vp, _vp]),
+    "hlgs_rasterize_backward": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
+                                     C.POINTER(Grads), _vp]),
+    "hlgs_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "hlgs_compute_relocation": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
+    "hlgs_lod_scratch_size": (_sz, [_i]),
+    "hlgs_expand_to_size_dynamic": (_i, [_i, _f, _vp, _vp, _vp, _vp, C.POINTER(_f), _vp, _vp, _vp, _vp,
+                                         C.POINTER(_i), _vp]),
+    "hlgs_get_interpolation_weights_dynamic": (_i, [_i, _vp, _f, _vp, _vp, _vp, C.POINTER(_f), C.POINTER(_f), _vp,
+                                                    _vp, _vp]),
+    "hlgs_expand_to_size": (_i, [_i, _f, _vp, _vp, _vp, C.POINTER(_f), _vp, _vp, _vp, _vp, C.POINTER(_i), _vp]),
+    "hlgs_get_interpolation_weights": (_i, [_i, _vp, _f, _vp, _vp, C.POINTER(_f), C.POINTER(_f), _vp, _vp, _vp]),
+    "hlgs_spt_scratch_size": (_sz, [_i]),
+    "hlgs_spt_work_size": (_sz, [_i]),
+    "hlgs_spt_cut_prepare": (_i, [_i, _vp, _vp, _vp, _vp, _vp, C.POINTER(_i), _vp]),
+    "hlgs_spt_cut_finish": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, C.POINTER(_i), _vp]),
+    "hlgs_lod_interp_forward": (_i, [_i, _i, _i] + [_vp] * 14),
+    "hlgs_lod_interp_backward": (_i, [_i, _i, _i] + [_vp] * 15),
+    "hlgs_set_stage_timing": (None, [_i]),
+    "hlgs_stage_count": (_i, []),
+    "hlgs_stage_name": (C.c_char_p, [_i]),
+    "hlgs_stage_stats": (_i, [C.POINTER(_f), C.POINTER(_i), _i]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libhlgs.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libhlgs.so not found at {LIB_PATH}; run `python __graft_entry__.py build` "
+                               "(hipcc --offload-arch=gfx950) first -- there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().hlgs_last_error().decode(errors="replace")
+        raise RuntimeError(f"libhlgs error {rc}: {msg}")
+
+
+def require_gpu(*tensors):
+    if not torch.cuda.is_available():
+        raise RuntimeError("libhlgs needs a HIP device (MI355X); torch.cuda.is_available() is False")
+    for t in tensors:
+        if t is not None and t.numel() and not t.is_cuda:
+            raise RuntimeError("libhlgs expects device tensors")
+
+
+def ptr(t):
+    """Device pointer of a tensor, or NULL for None / empty tensors (the reference's data_ptr() of an
+    empty tensor is nullptr as well)."""
+    if t is None or t.numel() == 0:
+        return None
+    return _vp(t.data_ptr())
+
+
+def stream():
+    return _vp(torch.cuda.current_stream().cuda_stream)
+
+
+def f3(values):
+    arr = (_f * 3)(*[float(v) for v in values])
+    return arr
+
+
+def header_functions():
+    """Names of the functions declared in include/hlgs.h (used by the ABI test)."""
+    import re
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(hlgs_[a-z0-9_]+)\s*\(", txt)))
+
+
+def stage_stats():
+    """{stage name: (mean ms per launch, launches)} since the last set_stage_timing()."""
+    lib = load()
+    n = lib.hlgs_stage_count()
+    ms, calls = (_f * n)(), (_i * n)()
+    lib.hlgs_stage_stats(ms, calls, n)
+    return {lib.hlgs_stage_name(i).decode(): (float(ms[i]), int(calls[i])) for i in range(n)}
+
+
+def set_stage_timing(enable):
+    load().hlgs_set_stage_timing(int(bool(enable)))

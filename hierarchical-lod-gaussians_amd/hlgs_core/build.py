@@ -1,0 +1,52 @@
+"""Build libhlgs.so (gfx950) in-tree with hipcc.  No torch headers, no JIT cache: the .so lands in
+hierarchical-lod-gaussians_amd/lib/ and travels with the repository snapshot to the GPU box."""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+OBJDIR = os.path.join(PKG, "build", "obj")
+LIB = os.path.join(LIBDIR, "libhlgs.so")
+SOURCES = ["scan.hip", "raster_fwd.hip", "raster_bwd.hip", "lod.hip", "capi.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("HLGS_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wall",
+         "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+
+
+def _deps_mtime():
+    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(PKG, "..", "include", "hlgs.h")]
+    return max(os.path.getmtime(f) for f in files if os.path.exists(f))
+
+
+def _compile(src, extra):
+    obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+    cmd = [HIPCC] + FLAGS + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force=False, extra=None, verbose=False):
+    extra = list(extra or [])
+    os.makedirs(OBJDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
+        return LIB
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), 8)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, extra), SOURCES))
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

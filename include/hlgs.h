@@ -1,0 +1,183 @@
+/*
+ * hlgs.h -- C ABI of libhlgs.so, the MI355X (gfx950) differentiable Gaussian-splat rasterizer
+ * with hierarchical level-of-detail selection.
+ *
+ * Drop-in boundary: every entry point below replaces one native function the reference binds
+ * through pybind11 (paths relative to /root/reference):
+ *
+ *   hlgs_rasterize_forward_prepare/_render  <- RasterizeGaussiansCUDA
+ *        submodules/hierarchy-rasterizer/rasterize_points.cu:36-139 (bound as _C.rasterize_gaussians,
+ *        ext.cpp:16); split in two phases at the reference's own host sync (rasterizer_impl.cu:330-333)
+ *        so that the caller allocates the binning buffer, as the reference's resize lambda did
+ *        (rasterize_points.cu:28-34).
+ *   hlgs_rasterize_backward                 <- RasterizeGaussiansBackwardCUDA, rasterize_points.cu:141-245
+ *   hlgs_mark_visible                       <- CudaRasterizer::Rasterizer::markVisible,
+ *        rasterizer_impl.cu:145-157 (called as _C.mark_visible at diff_gaussian_rasterization/__init__.py:174)
+ *   hlgs_compute_relocation                 <- ComputeRelocationCUDA, rasterize_points.cu:248-271
+ *   hlgs_expand_to_size_dynamic             <- ExpandToSizeDynamic, gaussianhierarchy/torch/torch_interface.cpp:171-194
+ *   hlgs_get_interpolation_weights_dynamic  <- GetTsIndexedDynamic, torch_interface.cpp:222-244
+ *   hlgs_expand_to_size                     <- ExpandToSize, torch_interface.cpp:148-169
+ *   hlgs_get_interpolation_weights          <- GetTsIndexed, torch_interface.cpp:200-220
+ *   hlgs_spt_cut_prepare/_finish            <- GetSPTCut, torch_interface.cpp:287-316 (two phases at the
+ *        reference's candidate-count sync, runtime_switching.cu:926-931)
+ *   hlgs_lod_interp_forward/_backward       <- the Python child/parent lerp of render_post,
+ *        gaussian_renderer/__init__.py:304-339 (interp_python=True), and its autograd
+ *
+ * Conventions: all pointers are device pointers unless a parameter says "host"; float = IEEE fp32,
+ * int = int32; every array is dense and contiguous in the reference's layout (means (P,3), rotations
+ * (P,4) as [r,x,y,z], shs (P,M,3), view/proj 16 floats, color (3,H,W)).  Nothing is allocated inside
+ * the library: the caller passes buffers sized by the *_size() queries.  Work is launched on `stream`
+ * (a hipStream_t; NULL = legacy default stream).  Functions return HLGS_OK or an error code;
+ * hlgs_last_error() returns the message for the calling thread.
+ */
+#ifndef HLGS_H
+#define HLGS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HLGS_OK 0
+#define HLGS_ERR_ARG 1
+#define HLGS_ERR_DEVICE 2
+
+/* Arguments of one rasterizer call: the tensors RasterizeGaussiansCUDA receives. */
+typedef struct hlgs_raster_args {
+    int P;            /* Gaussians rasterised: indices.size(0) if non-empty, else means3D rows */
+    int P_full;       /* means3D rows (gradients are P_full-sized, rasterize_points.cu:171) */
+    int D;            /* active SH degree */
+    int M;            /* SH coefficients per Gaussian (sh.size(1)), 0 when colors_precomp is used */
+    int W, H;
+    const float* bg;             /* 3 */
+    const float* means3D;        /* P_full x 3 */
+    const float* shs;            /* P_full x M x 3, or NULL */
+    const float* colors_precomp; /* P x 3, or NULL */
+    const float* opacities;      /* P_full */
+    const float* scales;         /* P_full x 3 (activated), or NULL with cov3D_precomp */
+    const float* rotations;      /* P_full x 4, or NULL with cov3D_precomp */
+    const float* cov3D_precomp;  /* P x 6, or NULL */
+    const float* viewmatrix;     /* 16 */
+    const float* projmatrix;     /* 16 */
+    const float* campos;         /* 3 */
+    float scale_modifier, tanfovx, tanfovy;
+    const int* indices;          /* in-kernel hierarchy mode (all four non-NULL) or NULL */
+    const int* parent_indices;
+    const float* ts;
+    const int* kids;
+    int prefiltered;
+    int debug;                   /* synchronise + check after every stage (auxiliary.h:23-30) */
+} hlgs_raster_args;
+
+/* Gradient outputs, all P_full rows; written completely by hlgs_rasterize_backward (no pre-zeroing). */
+typedef struct hlgs_grads {
+    float* dmean2D;   /* P_full x 3 (z stays 0) */
+    float* dcolor;    /* P_full x 3 */
+    float* dopacity;  /* P_full */
+    float* dmean3D;   /* P_full x 3 */
+    float* dcov3D;    /* P_full x 6 */
+    float* dsh;       /* P_full x M x 3 (may be NULL when M == 0) */
+    float* dscale;    /* P_full x 3 */
+    float* drot;      /* P_full x 4 */
+} hlgs_grads;
+
+const char* hlgs_last_error(void);
+const char* hlgs_version(void);
+
+/* ---- rasterizer buffer sizing (bytes) ---- */
+size_t hlgs_geom_buffer_size(int P);
+size_t hlgs_image_buffer_size(int W, int H);
+size_t hlgs_binning_buffer_size(int R);
+size_t hlgs_backward_scratch_size(int P, int R);
+
+/* Host-side result of phase 1. */
+typedef struct hlgs_frame_info {
+    int num_rendered;    /* R: Gaussian/tile instances (the reference's num_rendered) */
+    int max_tile_count;  /* longest per-tile list (selects the binning plan) */
+} hlgs_frame_info;
+
+/* Phase 1: preprocess + scans.  Writes radii (P), fills geom/img and *info (host).  One host
+ * synchronisation, as the reference has (rasterizer_impl.cu:330-331). */
+int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* img, int* radii,
+                                   hlgs_frame_info* info, void* stream);
+/* Phase 2: binning (per-tile depth sort) + front-to-back blend.  out_color (3,H,W) and out_invdepth
+ * (H,W, or NULL when do_depth is off) and seen (P) must be zero-initialised by the caller.  With R == 0
+ * this is a no-op (the output stays 0, not bg: rasterizer_impl.cu:332-333). */
+int hlgs_rasterize_forward_render(const hlgs_raster_args* a, const int* radii, void* geom, void* img,
+                                  void* binning, const hlgs_frame_info* info, float* out_color,
+                                  float* out_invdepth, int* seen, void* stream);
+/* Backward: blend backward (per-tile partial sums, no float atomics) + fused covariance / SH / scale-
+ * rotation backward.  dL_dinvdepth may be NULL (rasterize_points.cu:195-201). */
+int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,
+                            const void* binning, int R, void* scratch, const float* dL_dcolor,
+                            const float* dL_dinvdepth, const hlgs_grads* out, void* stream);
+
+/* z > 0.2 visibility (auxiliary.h:164-189); present is P bytes (bool) */
+int hlgs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                      uint8_t* present, void* stream);
+/* MCMC relocation, utils.cu:6-36.  scale_new is 3P floats. */
+int hlgs_compute_relocation(int P, const float* opacity_old, const float* scale_old, const int* N,
+                            const float* binoms, int n_max, float* opacity_new, float* scale_new, void* stream);
+
+/* ---- hierarchical LOD ---- */
+size_t hlgs_lod_scratch_size(int N);
+/* nodes: N x 6 int32 HierarchyNode rows; viewpoint: device float3; viewdir: host float[3].
+ * Writes the first *count entries of render_indices / parent_indices / nodes_for_render_indices
+ * (parent_indices is left untouched for roots, runtime_switching.cu:104-107). */
+int hlgs_expand_to_size_dynamic(int N, float target_size, const int* nodes, const float* positions,
+                                const float* scales, const float* viewpoint, const float* viewdir_host,
+                                int* render_indices, int* parent_indices, int* nodes_for_render_indices,
+                                void* scratch, int* count, void* stream);
+/* viewpoint_host / viewdir_host: host float[3] (torch_interface.cpp:240-241) */
+int hlgs_get_interpolation_weights_dynamic(int n, const int* node_indices, float target_size, const int* nodes,
+                                           const float* positions, const float* scales,
+                                           const float* viewpoint_host, const float* viewdir_host, float* ts,
+                                           int* kids, void* stream);
+/* static (.hier) variant: nodes N x 7 int32, boxes N x 8 float (minn xyzw, maxx xyzw) */
+int hlgs_expand_to_size(int N, float target_size, const int* nodes, const float* boxes, const float* viewpoint,
+                        const float* viewdir_host, int* render_indices, int* parent_indices,
+                        int* nodes_for_render_indices, void* scratch, int* count, void* stream);
+int hlgs_get_interpolation_weights(int n, const int* node_indices, float target_size, const int* nodes,
+                                   const float* boxes, const float* viewpoint_host, const float* viewdir_host,
+                                   float* ts, int* kids, void* stream);
+
+/* SPT cut (runtime_switching.cu:878-994).  prepare() computes per-SPT candidate intervals into
+ * scratch (hlgs_spt_scratch_size(s) bytes) and returns the candidate total in *n_candidates (host);
+ * finish() needs work >= hlgs_spt_work_size(n_candidates) bytes and writes the kept Gaussian indices to
+ * cut[0..*count) and the exclusive prefix of per-SPT kept counts to counts_prefix (s).  compat != 0
+ * reproduces the reference bit for bit (App. A-10 boundary attribution + dropping index 0). */
+size_t hlgs_spt_scratch_size(int s);
+size_t hlgs_spt_work_size(int n_candidates);
+int hlgs_spt_cut_prepare(int s, const int* SPT_starts, const float* SPT_max, const int* SPT_indices,
+                         const float* SPT_distances, void* scratch, int* n_candidates, void* stream);
+int hlgs_spt_cut_finish(int s, int E, int n_candidates, const int* gaussian_indices, const int* SPT_starts,
+                        const float* SPT_min, const int* SPT_indices, const float* SPT_distances, int compat,
+                        void* scratch, void* work, int* cut, int* counts_prefix, int* count, void* stream);
+
+/* LOD interpolation (render_post lerp).  M3 = floats of SH per Gaussian (0: no SH).  Outputs have
+ * S + n rows: rows [0,S) copy the skybox prefix, row S+i lerps child ridx[i] with parent pidx[i]. */
+int hlgs_lod_interp_forward(int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
+                            const float* means, const float* scales, const float* rots, const float* opac,
+                            const float* shs, float* o_means, float* o_scales, float* o_rots, float* o_opac,
+                            float* o_shs, void* stream);
+/* Gradient of the lerp: accumulates into P-row d_* arrays, which the caller zero-initialises. */
+int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
+                             const float* rots, const float* g_means, const float* g_scales, const float* g_rots,
+                             const float* g_opac, const float* g_shs, float* d_means, float* d_scales,
+                             float* d_rots, float* d_opac, float* d_shs, void* stream);
+
+/* ---- measurement hooks (bench.py) ---- */
+/* When enabled, every launch of each rasterizer stage is bracketed by hipEvents on its launch stream.
+ * hlgs_stage_stats returns, per stage, the mean duration in ms over all launches recorded since the
+ * last hlgs_set_stage_timing call and the number of launches (synchronises).  Off by default. */
+void hlgs_set_stage_timing(int enable);
+int hlgs_stage_count(void);
+const char* hlgs_stage_name(int i);
+int hlgs_stage_stats(float* mean_ms, int* calls, int max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
