@@ -223,6 +223,17 @@ size_t hlgs_backward_scratch_size(int P, int R)
 
 static void* aligned(const void* p) { return (void*)align_up((size_t)p); }
 
+size_t hlgs_binning_point_list_offset(int R)
+{
+    Bin b = carve_bin(nullptr, R < 0 ? 0 : R, nullptr);
+    return (size_t)b.point_list;
+}
+size_t hlgs_image_ranges_offset(int W, int H)
+{
+    Img im = carve_img(nullptr, W, H, nullptr);
+    return (size_t)im.ranges;
+}
+
 int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* img, int* radii,
                                    hlgs_frame_info* info, void* stream)
 {

@@ -146,3 +146,21 @@ def compute_relocation(opacity_old, scale_old, N, binoms, n_max):
     L.check(lib.hlgs_compute_relocation(P, L.ptr(o), L.ptr(s), L.ptr(n), L.ptr(b), int(n_max), L.ptr(new_o),
                                         L.ptr(new_s), L.stream()))
     return new_o, new_s
+
+
+def _field(buf, offset, count, dtype):
+    base = buf.data_ptr()
+    shift = ((base + 255) & ~255) - base
+    nbytes = count * torch.tensor([], dtype=dtype).element_size()
+    return buf[shift + offset: shift + offset + nbytes].view(dtype)
+
+
+def inspect_point_list(binningBuffer, R):
+    """Sorted per-tile Gaussian ids (tile-major, front to back) held in a forward's binning buffer."""
+    return _field(binningBuffer, L.load().hlgs_binning_point_list_offset(int(R)), int(R), torch.int32)
+
+
+def inspect_ranges(imageBuffer, W, H):
+    """[start, end) of every tile's list (tiles row-major) held in a forward's image buffer."""
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    return _field(imageBuffer, L.load().hlgs_image_ranges_offset(int(W), int(H)), 2 * T, torch.int32).view(T, 2)

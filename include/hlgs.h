@@ -168,6 +168,11 @@ int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* p
                              const float* g_opac, const float* g_shs, float* d_means, float* d_scales,
                              float* d_rots, float* d_opac, float* d_shs, void* stream);
 
+/* ---- inspection (tests): byte offsets of fields inside the caller's buffers, counted from the
+ * buffer's first 256-byte-aligned address ---- */
+size_t hlgs_binning_point_list_offset(int R);  /* uint32 point_list[R] */
+size_t hlgs_image_ranges_offset(int W, int H);  /* uint2 ranges[tiles] */
+
 /* ---- measurement hooks (bench.py) ---- */
 /* When enabled, every launch of each rasterizer stage is bracketed by hipEvents on its launch stream.
  * hlgs_stage_stats returns, per stage, the mean duration in ms over all launches recorded since the

@@ -1084,3 +1084,17 @@ void orc_lod_interp_backward(int S, int n, int M3, const int *ridx, const int *p
             }
     }
 }
+
+/* SH -> RGB for a batch (the colour step of preprocessCUDA, HR/forward.cu:25-76), for fixture checks. */
+void orc_sh_colors(int P, int D, int M, const float *shs, const float *means, const float *campos, float *rgb,
+                   uint8_t *clamped)
+{
+    v3 cp = V3(campos[0], campos[1], campos[2]);
+    for (int i = 0; i < P; i++) {
+        v3 c = sh_to_rgb(D, shs + (size_t)i * M * 3, V3(means[3 * i], means[3 * i + 1], means[3 * i + 2]), cp,
+                         &clamped[i]);
+        rgb[3 * i] = c.x;
+        rgb[3 * i + 1] = c.y;
+        rgb[3 * i + 2] = c.z;
+    }
+}

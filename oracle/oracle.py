@@ -82,6 +82,7 @@ def lib():
                                              _f, _f, _f, _f, _f]
         L.orc_lod_interp_backward.argtypes = [C.c_int, C.c_int, C.c_int, _i, _i, _f, _f, _f, _f, _f, _f,
                                               _f, _f, _f, _f, _f, _f]
+        L.orc_sh_colors.argtypes = [C.c_int, C.c_int, C.c_int, _f, _f, _f, _f, _b]
         _lib = L
     return _lib
 
@@ -275,3 +276,11 @@ def lod_interp_backward(S, ridx, pidx, w, rots, P, g):
                                   _p(gs), _p(d["means"]), _p(d["scales"]), _p(d["rots"]), _p(d["opac"]),
                                   _p(d["shs"]))
     return d
+
+
+def sh_colors(shs, means, campos, deg):
+    s, m, c = _f32(shs), _f32(means), _f32(campos)
+    P, M = s.shape[0], s.shape[1]
+    rgb, cl = np.zeros((P, 3), np.float32), np.zeros(P, np.uint8)
+    lib().orc_sh_colors(P, int(deg), M, _p(s), _p(m), _p(c), _p(rgb), _p(cl, _b))
+    return rgb, cl

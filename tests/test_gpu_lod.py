@@ -1,0 +1,179 @@
+"""HIP LOD kernels, SPT cut, render_post lerp and the in-kernel hierarchy rasterizer mode against the
+oracle.  Integer outputs (selected nodes, parents, cut lists, per-tile lists) must be bit-exact; float
+weights within 1e-6; lerp gradients within 1e-5 (float atomics change summation order only)."""
+import numpy as np
+import pytest
+import torch
+
+from hlgs_core import synthetic as S
+from oracle import oracle as O
+from helpers import gpu_render, oracle_render, rel_err, settings_for, image_check
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tree(n=600, sky=0, seed=0):
+    cam = S.make_camera(128, 96)
+    return S.make_dynamic_hierarchy(S.make_gaussians(n, 3, cam, seed=seed), skybox_points=sky, seed=seed), cam
+
+
+def test_point_list_and_ranges_bit_exact():
+    from diff_gaussian_rasterization import _C
+    cam = S.make_camera(200, 120)
+    sc = S.make_gaussians(5000, 1, cam, seed=11)
+    sc["means3D"][::7, 2] = 9.0  # depth ties
+    fr = O.forward(dict(sc), S.cam_numpy(cam))
+    t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
+    e = torch.empty(0, device=DEV)
+    out = _C.rasterize_gaussians(cam["bg"], e, e, e, e, t(sc["means3D"]), e, t(sc["opacities"]), t(sc["scales"]),
+                                 t(sc["rotations"]), 1.0, e, cam["viewmatrix"], cam["projmatrix"], cam["tanfovx"],
+                                 cam["tanfovy"], 120, 200, t(sc["shs"]), 1, cam["campos"], False, True, True)
+    R = out[0]
+    assert R == fr.R
+    pl = _C.inspect_point_list(out[4], R).cpu().numpy().astype(np.uint32)
+    rg = _C.inspect_ranges(out[5], 200, 120).cpu().numpy().astype(np.uint32)
+    np.testing.assert_array_equal(rg, fr.ranges)
+    np.testing.assert_array_equal(pl, fr.point_list[:R])
+    np.testing.assert_array_equal(out[7].cpu().numpy(), fr.seen)
+
+
+@pytest.mark.parametrize("sky", [0, 4])
+def test_expand_to_size_dynamic_and_weights(sky):
+    import gaussian_hierarchy as GH
+    h, cam = _tree(800, sky=sky)
+    nodes, pos, sc = h["nodes"], h["means3D"], h["scales"]
+    N = nodes.shape[0]
+    vp = np.array([0.05, 0.0, -0.1], np.float32)
+    vd = np.array([0.0, 0.0, 1.0], np.float32)
+    for target in (0.0008, 0.003, 0.01):
+        ri = torch.zeros(N, dtype=torch.int32, device=DEV)
+        pi = torch.zeros(N, dtype=torch.int32, device=DEV)
+        ni = torch.zeros(N, dtype=torch.int32, device=DEV)
+        n = GH.expand_to_size_dynamic(torch.tensor(nodes, device=DEV), torch.tensor(pos, device=DEV),
+                                      torch.tensor(sc, device=DEV), target, torch.tensor(vp, device=DEV),
+                                      torch.tensor(vd), ri, pi, ni)
+        n_o, ri_o, pi_o, ni_o = O.expand_to_size_dynamic(nodes, pos, sc, target, vp, vd)
+        assert n == n_o and n > 0
+        np.testing.assert_array_equal(ri[:n].cpu().numpy(), ri_o[:n])
+        np.testing.assert_array_equal(ni[:n].cpu().numpy(), ni_o[:n])
+        np.testing.assert_array_equal(pi[:n].cpu().numpy(), pi_o[:n])
+        ts = torch.zeros(N, device=DEV)
+        kids = torch.zeros(N, dtype=torch.int32, device=DEV)
+        GH.get_interpolation_weights_dynamic(ni[:n], target, torch.tensor(nodes, device=DEV),
+                                             torch.tensor(pos, device=DEV), torch.tensor(sc, device=DEV),
+                                             torch.tensor(vp), torch.tensor(vd), ts, kids)
+        ts_o, kids_o = O.interp_weights_dynamic(ni_o[:n], target, nodes, pos, sc, vp)
+        np.testing.assert_allclose(ts[:n].cpu().numpy(), ts_o, rtol=0, atol=1e-6)
+        np.testing.assert_array_equal(kids[:n].cpu().numpy(), kids_o)
+
+
+def test_expand_to_size_static():
+    import gaussian_hierarchy as GH
+    rng = np.random.default_rng(1)
+    N = 500
+    nodes = np.zeros((N, 7), np.int32)
+    nodes[:, 1] = [-1] + [int(rng.integers(0, i)) for i in range(1, N)]
+    nodes[:, 0] = rng.integers(0, 4, N)
+    nodes[:, 2] = np.arange(N) * 2
+    nodes[:, 3] = rng.integers(0, 3, N)
+    nodes[:, 4] = rng.integers(0, 2, N)
+    nodes[:, 6] = np.bincount(nodes[1:, 1], minlength=N)
+    c = rng.uniform(-3, 3, (N, 3))
+    e = rng.uniform(0.05, 1.0, (N, 3))
+    boxes = np.zeros((N, 8), np.float32)
+    boxes[:, :3], boxes[:, 4:7], boxes[:, 3] = c - e, c + e, e.max(1) * 2
+    vp = np.array([0.3, 0.1, -0.2], np.float32)
+    cap = int(nodes[:, 3].sum() + nodes[:, 4].sum()) + 1
+    ri, pi, ni = (torch.zeros(cap, dtype=torch.int32, device=DEV) for _ in range(3))
+    n = GH.expand_to_size(torch.tensor(nodes, device=DEV), torch.tensor(boxes, device=DEV), 0.3,
+                          torch.tensor(vp, device=DEV), torch.zeros(3), ri, pi, ni)
+    n_o, ri_o, pi_o, ni_o = O.expand_to_size(nodes, boxes, 0.3, vp)
+    assert n == n_o
+    for a, b in ((ri, ri_o), (pi, pi_o), (ni, ni_o)):
+        np.testing.assert_array_equal(a[:n].cpu().numpy(), b[:n])
+    ts = torch.zeros(N, device=DEV)
+    kids = torch.zeros(N, dtype=torch.int32, device=DEV)
+    idx = torch.arange(N, dtype=torch.int32, device=DEV)
+    GH.get_interpolation_weights(idx, 0.3, torch.tensor(nodes, device=DEV), torch.tensor(boxes, device=DEV),
+                                 torch.tensor(vp), torch.zeros(3), ts, kids)
+    ts_o, kids_o = O.interp_weights(np.arange(N, dtype=np.int32), 0.3, nodes, boxes, vp)
+    np.testing.assert_allclose(ts.cpu().numpy(), ts_o, atol=1e-6)
+    np.testing.assert_array_equal(kids.cpu().numpy(), kids_o)
+
+
+@pytest.mark.parametrize("compat", [True, False])
+def test_spt_cut(compat):
+    import gaussian_hierarchy as GH
+    from test_oracle_lod import _random_spts
+    for seed in range(4):
+        gidx, starts, smax, smin, sidx, sdist = _random_spts(seed, S_count=300, sel=200)
+        if seed == 0:
+            gidx[0] = 0  # exercises the reference's DeviceSelect(x != 0) drop
+        t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
+        cut, cp = GH.get_spt_cut_cuda(len(sidx), t(gidx), t(starts), t(smax), t(smin), t(sidx), t(sdist), compat=compat)
+        cut_o, cp_o = O.spt_cut(gidx, starts, smax, smin, sidx, sdist, compat=compat)
+        np.testing.assert_array_equal(cut.cpu().numpy(), cut_o)
+        np.testing.assert_array_equal(cp.cpu().numpy(), cp_o)
+
+
+def test_lod_interpolation_forward_backward():
+    import gaussian_hierarchy as GH
+    h, cam = _tree(1000, sky=6)
+    N = h["nodes"].shape[0]
+    vp = np.zeros(3, np.float32)
+    n, ri, pi, ni = O.expand_to_size_dynamic(h["nodes"], h["means3D"], h["scales"], 0.002, vp,
+                                             np.array([0, 0, 1], np.float32))
+    ts, _ = O.interp_weights_dynamic(ni[:n], 0.002, h["nodes"], h["means3D"], h["scales"], vp)
+    pi = pi.copy()
+    pi[n:] = 0
+    Sk = 6
+    leaf = lambda a: torch.tensor(a, device=DEV, requires_grad=True)  # noqa: E731
+    m, s, r, o, sh = leaf(h["means3D"]), leaf(h["scales"]), leaf(h["rotations"]), leaf(h["opacities"]), leaf(h["shs"])
+    outs = GH.interpolate_lod(m, s, r, o, sh, torch.tensor(ri[:n], device=DEV), torch.tensor(pi, device=DEV),
+                              torch.tensor(np.pad(ts, (0, N - n)), device=DEV), Sk)
+    ref = O.lod_interp_forward(Sk, ri[:n], pi[:n], ts, h["means3D"], h["scales"], h["rotations"], h["opacities"],
+                               h["shs"])
+    for got, key in zip(outs, ("means", "scales", "rots", "opac", "shs")):
+        np.testing.assert_allclose(got.detach().cpu().numpy().reshape(ref[key].shape), ref[key], rtol=1e-6, atol=1e-6)
+    rng = np.random.default_rng(0)
+    gs = [rng.normal(size=tuple(x.shape)).astype(np.float32) for x in outs]
+    sum((x * torch.tensor(g, device=DEV)).sum() for x, g in zip(outs, gs)).backward()
+    d = O.lod_interp_backward(Sk, ri[:n], pi[:n], ts, h["rotations"], N,
+                              dict(means=gs[0], scales=gs[1], rots=gs[2], opac=gs[3], shs=gs[4]))
+    for leaf_t, key in zip((m, s, r, o, sh), ("means", "scales", "rots", "opac", "shs")):
+        np.testing.assert_allclose(leaf_t.grad.cpu().numpy().reshape(d[key].shape), d[key], rtol=1e-5, atol=1e-5)
+
+
+def test_in_kernel_hierarchy_mode_matches_oracle():
+    """render_indices / parent_indices / interpolation_weights / num_node_kids non-empty: the reference's
+    in-kernel lerp and kids-alpha path (forward.cu:268-349,522-558; backward.cu:626-718,458-494)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    h, _ = _tree(1500)
+    cam = S.make_camera(128, 96)
+    N = h["nodes"].shape[0]
+    vp = cam["campos"].numpy()
+    n, ri, pi, ni = O.expand_to_size_dynamic(h["nodes"], h["means3D"], h["scales"], 0.004, vp,
+                                             np.array([0, 0, 1], np.float32))
+    ts, kids = O.interp_weights_dynamic(ni[:n], 0.004, h["nodes"], h["means3D"], h["scales"], vp)
+    roots = h["nodes"][ri[:n], 1] < 0
+    pidx = np.where(roots, -1, pi[:n]).astype(np.int32)
+    scene = dict(means3D=h["means3D"], opacities=h["opacities"], shs=h["shs"], scales=h["scales"],
+                 rotations=h["rotations"], sh_degree=3, indices=ri[:n], parent_indices=pidx, ts=ts, kids=kids)
+    fr = O.forward(scene, S.cam_numpy(cam))
+    g, gd = S.upstream_grads(128, 96)
+    gr = O.backward(fr, scene, g, gd)
+    t = lambda a, rg=False: torch.tensor(a, device=DEV, requires_grad=rg)  # noqa: E731
+    hier = dict(render_indices=t(ri[:n]), parent_indices=t(pidx), interpolation_weights=t(ts), num_node_kids=t(kids))
+    rast = GaussianRasterizer(settings_for(cam, 3, DEV, hierarchy=hier))
+    m, o, sh, s, r = t(h["means3D"], True), t(h["opacities"], True), t(h["shs"], True), t(h["scales"], True), \
+        t(h["rotations"], True)
+    m2 = torch.zeros_like(m, requires_grad=True)
+    color, radii, invd = rast(means3D=m, means2D=m2, opacities=o, shs=sh, scales=s, rotations=r)
+    np.testing.assert_array_equal(radii.cpu().numpy(), fr.radii)
+    mx, nbad, ok = image_check(color.detach().cpu().numpy(), fr.color)
+    assert ok, (mx, nbad)
+    ((color * t(g)).sum() + (invd * t(gd)).sum()).backward()
+    for name, leaf_t in (("dmean3D", m), ("dopacity", o), ("dscale", s), ("drot", r), ("dsh", sh), ("dmean2D", m2)):
+        e = rel_err(leaf_t.grad.cpu().numpy(), gr[name])
+        assert e <= 1e-3, (name, e)

@@ -1,0 +1,225 @@
+"""Pin the oracle (CPU restatement) before trusting it as the GPU checker.
+
+* SH->RGB against golden vectors produced by the reference's own utils/sh_utils.eval_sh
+  (tests/golden/make_golden.py).
+* Camera matrices against golden vectors from the reference's utils/graphics_utils.
+* Forward image and every gradient against an independent float64 torch-autograd restatement of the
+  reference forward (preprocessCUDA + renderCUDA semantics, vectorised per tile).  The reference's
+  analytic backward (backward.cu) must equal autograd of its forward wherever the forward is smooth.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from hlgs_core import synthetic as S
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("deg", [0, 1, 2, 3])
+def test_sh_colors_match_reference_eval_sh(deg):
+    z = np.load(os.path.join(GOLD, "golden_sh.npz"))
+    rgb, clamped = O.sh_colors(z[f"shs_{deg}"], z[f"means_{deg}"], z[f"campos_{deg}"], deg)
+    np.testing.assert_allclose(rgb, z[f"rgb_{deg}"], rtol=2e-6, atol=2e-6)
+    assert np.all((clamped != 0) == (z[f"rgb_{deg}"] == 0).any(1) | (clamped != 0))
+
+
+def test_camera_matches_reference_graphics_utils():
+    z = np.load(os.path.join(GOLD, "golden_camera.npz"))
+    for i in range(4):
+        W, H = [int(v) for v in z[f"WH_{i}"]]
+        cam = S.make_camera(W, H, R=z[f"R_{i}"], T=z[f"T_{i}"])
+        np.testing.assert_array_equal(cam["viewmatrix"].numpy(), z[f"view_{i}"])
+        np.testing.assert_array_equal(cam["projmatrix"].numpy(), z[f"proj_{i}"])
+        np.testing.assert_allclose(cam["campos"].numpy(), z[f"campos_{i}"], rtol=0, atol=1e-6)
+
+
+# ------------------------------------------------------------------------------------------------------
+# float64 autograd restatement
+# ------------------------------------------------------------------------------------------------------
+C0 = 0.28209479177387814
+C1 = 0.4886025119029199
+C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396]
+C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+      1.445305721320277, -0.5900435899266435]
+
+
+def _sh_rgb(deg, sh, d):
+    x, y, z = d[:, 0:1], d[:, 1:2], d[:, 2:3]
+    r = C0 * sh[:, 0]
+    if deg > 0:
+        r = r - C1 * y * sh[:, 1] + C1 * z * sh[:, 2] - C1 * x * sh[:, 3]
+    if deg > 1:
+        xx, yy, zz, xy, yz, xz = x * x, y * y, z * z, x * y, y * z, x * z
+        r = (r + C2[0] * xy * sh[:, 4] + C2[1] * yz * sh[:, 5] + C2[2] * (2 * zz - xx - yy) * sh[:, 6]
+             + C2[3] * xz * sh[:, 7] + C2[4] * (xx - yy) * sh[:, 8])
+    if deg > 2:
+        r = (r + C3[0] * y * (3 * xx - yy) * sh[:, 9] + C3[1] * xy * z * sh[:, 10]
+             + C3[2] * y * (4 * zz - xx - yy) * sh[:, 11] + C3[3] * z * (2 * zz - 3 * xx - 3 * yy) * sh[:, 12]
+             + C3[4] * x * (4 * zz - xx - yy) * sh[:, 13] + C3[5] * z * (xx - yy) * sh[:, 14]
+             + C3[6] * x * (xx - 3 * yy) * sh[:, 15])
+    return torch.clamp_min(r + 0.5, 0.0)
+
+
+class _AAScale(torch.autograd.Function):
+    """h = sqrt(max(2.5e-5, det(cov)/det(cov + 0.3 I))) with the reference's backward
+    (backward.cu:212-246).  Quirk: that backward evaluates d(ratio)/d(cov), derived for the undilated
+    covariance, at the *dilated* entries (c_xx, c_yy already include +0.3), so it is not the exact
+    derivative of its own forward.  Every other term of this restatement is plain autograd."""
+
+    @staticmethod
+    def forward(ctx, a, b, c):
+        w = 0.3
+        ratio = (a * c - b * b) / ((a + w) * (c + w) - b * b)
+        h = torch.sqrt(torch.clamp_min(ratio, 2.5e-5))
+        ctx.save_for_backward(a, b, c, ratio, h)
+        return h
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, c, ratio, h = ctx.saved_tensors
+        w = 0.3
+        d_inside = torch.where(ratio <= 2.5e-5, torch.zeros_like(g), g / (2 * h))
+        x, y, z = a + w, c + w, b  # dilated, as the reference uses them
+        den = d_inside / (w * w + w * (x + y) + x * y - z * z) ** 2
+        return w * (w * y + y * y + z * z) * den, -2.0 * w * z * (w + x + y) * den, w * (w * x + x * x + z * z) * den
+
+
+def torch_render(sc, cam, fr, deg):
+    """Differentiable float64 forward with the reference's semantics; the per-tile sorted lists come from
+    the oracle frame (the sort itself has no gradient)."""
+    dt = torch.float64
+    leaf = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=dt, requires_grad=True)  # noqa: E731
+    P = sc["means3D"].shape[0]
+    means, scales, rots = leaf(sc["means3D"]), leaf(sc["scales"]), leaf(sc["rotations"])
+    opac, shs = leaf(sc["opacities"]), leaf(sc["shs"])
+    W, H = cam["W"], cam["H"]
+    view = torch.tensor(cam["viewmatrix"].numpy().reshape(4, 4), dtype=dt)
+    proj = torch.tensor(cam["projmatrix"].numpy().reshape(4, 4), dtype=dt)
+    campos = torch.tensor(cam["campos"].numpy(), dtype=dt)
+    fx = W / (2 * cam["tanfovx"])
+    fy = H / (2 * cam["tanfovy"])
+    ph = torch.cat([means, torch.ones(P, 1, dtype=dt)], 1)
+    tview = ph @ view
+    hom = ph @ proj
+    ndc = hom[:, :2] / (hom[:, 3:4] + 1e-7)
+    ndc.retain_grad()
+    pix = ((ndc + 1) * torch.tensor([W, H], dtype=dt) - 1) * 0.5
+    # cov3D = R diag(s^2) R^T with the reference's (unnormalised) quaternion polynomial
+    r, x, y, z = rots[:, 0], rots[:, 1], rots[:, 2], rots[:, 3]
+    Rs = torch.stack([
+        torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y)], -1),
+        torch.stack([2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x)], -1),
+        torch.stack([2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], -1)], -2)
+    Sig = Rs @ torch.diag_embed(scales ** 2) @ Rs.transpose(1, 2)
+    A = view[:3, :3].T  # linear part of the view transform acting on column vectors
+    tz = tview[:, 2]
+    limx, limy = 1.3 * cam["tanfovx"], 1.3 * cam["tanfovy"]
+    tx = torch.clamp(tview[:, 0] / tz, -limx, limx) * tz
+    ty = torch.clamp(tview[:, 1] / tz, -limy, limy) * tz
+    zero = torch.zeros_like(tz)
+    J = torch.stack([torch.stack([fx / tz, zero, -fx * tx / (tz * tz)], -1),
+                     torch.stack([zero, fy / tz, -fy * ty / (tz * tz)], -1)], -2)
+    JA = J @ A
+    cov2 = JA @ Sig @ JA.transpose(1, 2)
+    a, b, c = cov2[:, 0, 0], cov2[:, 0, 1], cov2[:, 1, 1]
+    hs = _AAScale.apply(a, b, c)
+    a, c = a + 0.3, c + 0.3
+    det = a * c - b * b
+    conic = torch.stack([c / det, -b / det, a / det], -1)
+    o2 = opac[:, 0] * hs
+    d = means - campos
+    rgb = _sh_rgb(deg, shs, d / d.norm(dim=1, keepdim=True))
+    invz = 1.0 / tz
+    bg = torch.tensor(cam["bg"].numpy(), dtype=dt)
+    gx = (W + 15) // 16
+    color = torch.zeros(3, H, W, dtype=dt)
+    inv = torch.zeros(1, H, W, dtype=dt)
+    for t, (s, e) in enumerate(fr.ranges.astype(np.int64)):
+        tx0, ty0 = (t % gx) * 16, (t // gx) * 16
+        xs = torch.arange(tx0, min(tx0 + 16, W), dtype=dt)
+        ys = torch.arange(ty0, min(ty0 + 16, H), dtype=dt)
+        py, px = torch.meshgrid(ys, xs, indexing="ij")
+        px, py = px.reshape(-1, 1), py.reshape(-1, 1)
+        if e > s:
+            ids = torch.tensor(fr.point_list[s:e].astype(np.int64))
+            dx = pix[ids, 0][None] - px
+            dy = pix[ids, 1][None] - py
+            cn = conic[ids]
+            power = -0.5 * (cn[None, :, 0] * dx * dx + cn[None, :, 2] * dy * dy) - cn[None, :, 1] * dx * dy
+            alpha = torch.clamp(o2[ids][None] * torch.exp(power), max=0.99)
+            keep = (power <= 0) & (alpha >= 1.0 / 255.0)
+            alpha = torch.where(keep, alpha, torch.zeros_like(alpha))
+            one_m = 1 - alpha
+            Tb = torch.cumprod(torch.cat([torch.ones_like(one_m[:, :1]), one_m[:, :-1]], 1), 1)
+            stop = keep & (Tb * one_m < 1e-4)
+            dead = torch.cumsum(stop.to(torch.int64), 1) > 0  # the stopping splat and everything behind it
+            alpha = torch.where(dead, torch.zeros_like(alpha), alpha)
+            Tb = torch.cumprod(torch.cat([torch.ones_like(alpha[:, :1]), (1 - alpha)[:, :-1]], 1), 1)
+            w = alpha * Tb
+            Tf = Tb[:, -1] * (1 - alpha[:, -1])
+            col = w @ rgb[ids] + Tf[:, None] * bg[None]
+            dep = w @ invz[ids]
+        else:
+            col = bg[None].expand(px.shape[0], 3)
+            dep = torch.zeros(px.shape[0], dtype=dt)
+        hh, ww = len(ys), len(xs)
+        color[:, ty0:ty0 + hh, tx0:tx0 + ww] = col.T.reshape(3, hh, ww)
+        inv[0, ty0:ty0 + hh, tx0:tx0 + ww] = dep.reshape(hh, ww)
+    return dict(color=color, invdepth=inv, means=means, scales=scales, rots=rots, opac=opac, shs=shs, ndc=ndc)
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
+
+
+@pytest.mark.parametrize("P,deg,W,H,bg", [(250, 3, 64, 48, (0.0, 0.0, 0.0)), (300, 1, 48, 40, (0.2, 0.5, 0.8)),
+                                          (150, 0, 40, 40, (0.1, 0.1, 0.1))])
+def test_oracle_matches_float64_autograd(P, deg, W, H, bg):
+    cam = S.make_camera(W, H, bg=bg)
+    sc = S.make_gaussians(P, deg, cam, seed=P)
+    fr = O.forward(sc, S.cam_numpy(cam))
+    g, gd = S.upstream_grads(W, H)
+    gr = O.backward(fr, sc, g, gd)
+    tr = torch_render(sc, cam, fr, deg)
+    assert _rel(fr.color, tr["color"].detach().numpy()) < 1e-5
+    assert _rel(fr.invdepth, tr["invdepth"].detach().numpy()) < 1e-5
+    loss = (tr["color"] * torch.tensor(g, dtype=torch.float64)).sum() + \
+        (tr["invdepth"] * torch.tensor(gd, dtype=torch.float64)).sum()
+    loss.backward()
+    vis = fr.radii > 0
+    checks = [("dmean3D", tr["means"].grad), ("dscale", tr["scales"].grad), ("drot", tr["rots"].grad),
+              ("dopacity", tr["opac"].grad), ("dsh", tr["shs"].grad)]
+    for name, ref in checks:
+        e = _rel(gr[name][vis], ref.numpy()[vis])
+        assert e < 2e-3, f"{name}: oracle vs autograd rel err {e}"
+    e = _rel(gr["dmean2D"][vis, :2], tr["ndc"].grad.numpy()[vis])
+    assert e < 2e-3, f"dmean2D: {e}"
+    # invisible Gaussians receive exactly zero
+    for name in ("dmean3D", "dscale", "drot", "dopacity", "dsh"):
+        assert np.all(gr[name][~vis] == 0)
+
+
+def test_oracle_zero_instances_and_empty():
+    cam = S.make_camera(32, 32, bg=(0.5, 0.5, 0.5))
+    sc = S.make_gaussians(50, 0, cam, seed=1)
+    sc["means3D"][:, 2] = -3.0
+    fr = O.forward(sc, S.cam_numpy(cam))
+    assert fr.R == 0 and np.all(fr.color == 0)  # App. A-7: 0, not bg
+    gr = O.backward(fr, sc, *S.upstream_grads(32, 32))
+    assert all(np.all(v == 0) for v in gr.values() if v is not None)
+
+
+def test_oracle_point_list_is_stable_tile_depth_order():
+    cam = S.make_camera(64, 64)
+    sc = S.make_gaussians(500, 0, cam, seed=2)
+    sc["means3D"][::2, 2] = 7.0  # many exact depth ties
+    fr = O.forward(sc, S.cam_numpy(cam))
+    for s, e in fr.ranges:
+        ids = fr.point_list[s:e]
+        keys = [(fr.depths[i], i) for i in ids]
+        assert keys == sorted(keys)
