@@ -173,12 +173,60 @@ __device__ __forceinline__ f3 dnormvdv(f3 v, f3 dv)
     return r;
 }
 
+// Conservative 4-bit mask of the 8x8 quadrants of the tile at (x0, y0) that can contain a pixel where
+// this splat reaches alpha >= 1/255.  alpha = min(0.99, o * exp(power)) >= 1/255 needs
+// d^T Q d <= 2 ln(255 o) (Q = conic), an ellipse whose half-extents are sqrt(2 ln(255 o) Q^-1_xx|yy).
+// Pairs outside are exactly the ones the reference skips (forward.cu:539-561, backward.cu:614-643);
+// the kids-alpha of hierarchy mode is never larger than alpha, so the mask stays conservative there.
+// Margins absorb the float rounding of power/exp.
+__device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, int x0, int y0)
+{
+    const float o = co.w;
+    if (o != o || co.x != co.x || co.y != co.y || co.z != co.z) return 0xFu;
+    if (o < (1.0f / 255.0f) * 0.999f) return 0u;
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.f) || !(co.x > 0.f) || !(co.z > 0.f)) return 0xFu;
+    const float t = fmaxf(2.0f * logf(255.0f * o), 0.f) * 1.002f + 1e-3f;
+    const float ex = sqrtf(t * co.z / det) * 1.001f + 0.01f;
+    const float ey = sqrtf(t * co.x / det) * 1.001f + 0.01f;
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float qx = (float)(x0 + 8 * (q & 1)), qy = (float)(y0 + 8 * (q >> 1));
+        if (x + ex >= qx && x - ex <= qx + 7.f && y + ey >= qy && y - ey <= qy + 7.f) m |= 1u << q;
+    }
+    return m;
+}
+
 // Bijective XCD-aware block remap (cdna_hip_programming.md section 5): consecutive logical blocks
 // land on the same XCD so neighbouring tiles share that XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg)
 {
     const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+// Ten independent full-wave (64-lane) sums in one block of fused v_add_f32_dpp instructions; the totals
+// land in lane 63.  Interleaving the ten chains keeps every DPP source at least nine instructions
+// behind its producer, so only the block entry needs the VALU->DPP wait state (s_nop 1).
+__device__ __forceinline__ void wave_sum10_to_lane63(float& a0, float& a1, float& a2, float& a3, float& a4,
+                                                     float& a5, float& a6, float& a7, float& a8, float& a9)
+{
+#define HLGS_DPP_STEP(ctrl)                                                                                \
+    "v_add_f32_dpp %0, %0, %0 " ctrl "\n\tv_add_f32_dpp %1, %1, %1 " ctrl "\n\tv_add_f32_dpp %2, %2, %2 " ctrl \
+    "\n\tv_add_f32_dpp %3, %3, %3 " ctrl "\n\tv_add_f32_dpp %4, %4, %4 " ctrl "\n\tv_add_f32_dpp %5, %5, %5 " ctrl \
+    "\n\tv_add_f32_dpp %6, %6, %6 " ctrl "\n\tv_add_f32_dpp %7, %7, %7 " ctrl "\n\tv_add_f32_dpp %8, %8, %8 " ctrl \
+    "\n\tv_add_f32_dpp %9, %9, %9 " ctrl "\n\t"
+    asm volatile("s_nop 1\n\t"
+                 HLGS_DPP_STEP("quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1")
+                 HLGS_DPP_STEP("quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1")
+                 HLGS_DPP_STEP("row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+                 HLGS_DPP_STEP("row_ror:8 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+                 HLGS_DPP_STEP("row_bcast:15 row_mask:0xa bank_mask:0xf")
+                 HLGS_DPP_STEP("row_bcast:31 row_mask:0xc bank_mask:0xf")
+                 "s_nop 1"
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8), "+v"(a9));
+#undef HLGS_DPP_STEP
 }
 
 // Full-wave (64-lane) sum with DPP; the total lands in lane 63.

@@ -16,6 +16,72 @@
 
 namespace hlgs {
 
+// Per-pixel state of the back-to-front replay (backward.cu:549-572).
+struct PixB {
+    float T;        // transmittance in front of the current splat
+    float TB;       // T_final * <bg, dL/dpixel>
+    float ar, ag, ab, la, lr, lg, lb;  // accum_rec, last_alpha, last_color
+    float dr, dg, db;                  // dL/dpixel
+    float dinv, ainv, linv;            // inverse-depth terms
+    uint32_t last;                     // n_contrib
+};
+
+// One (pixel, splat) step of renderCUDA backward (backward.cu:601-718); adds this pixel's share of the
+// splat's ten gradient terms to acc.  Returns false for the pairs the reference skips.
+template <bool INTERP, bool DEPTH>
+__device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& co, const float4& col,
+                                         float invz, float tt, float ddelx_dx, float ddely_dy, float (&acc)[10])
+{
+    // the skip tests of the reference, evaluated as one predicate so the update below is one region
+    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+    const float G = __expf(power);
+    const float test_alpha = co.w * G;
+    const float my_alpha = fminf(0.99f, test_alpha);
+    float alpha = my_alpha;
+    if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, col.w));
+    const bool valid = li < p.last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+    if (valid) {
+        const float r1m = __builtin_amdgcn_rcpf(1.f - alpha);  // 1/(1-alpha), alpha <= 0.99
+        p.T = p.T * r1m;
+        const float weight = alpha * p.T;
+        const float omla = 1.f - p.la;
+        p.ar = p.la * p.lr + omla * p.ar;
+        p.ag = p.la * p.lg + omla * p.ag;
+        p.ab = p.la * p.lb + omla * p.ab;
+        float dL_dalpha = (col.x - p.ar) * p.dr + (col.y - p.ag) * p.dg + (col.z - p.ab) * p.db;
+        p.lr = col.x;
+        p.lg = col.y;
+        p.lb = col.z;
+        acc[6] += weight * p.dr;
+        acc[7] += weight * p.dg;
+        acc[8] += weight * p.db;
+        if (DEPTH) {
+            p.ainv = p.la * p.linv + omla * p.ainv;
+            p.linv = invz;
+            dL_dalpha += (invz - p.ainv) * p.dinv;
+            acc[9] += weight * p.dinv;
+        }
+        dL_dalpha *= p.T;
+        p.la = alpha;
+        dL_dalpha -= p.TB * r1m;
+        dL_dalpha = test_alpha > 0.99f ? 0.f : dL_dalpha;
+        const float dL_dG = co.w * dL_dalpha;
+        const float gdx = G * dx, gdy = G * dy;
+        const float dG_ddelx = -gdx * co.x - gdy * co.y;
+        const float dG_ddely = -gdy * co.z - gdx * co.y;
+        acc[0] += dL_dG * dG_ddelx * ddelx_dx;
+        acc[1] += dL_dG * dG_ddely * ddely_dy;
+        const float hG = -0.5f * dL_dG;
+        acc[2] += hG * gdx * dx;
+        acc[3] += hG * gdx * dy;
+        acc[4] += hG * gdy * dy;
+        float mult = 1.0f;
+        if (INTERP) mult = tt - powf(1.0f - my_alpha, col.w - 1.0f) * (tt - 1.0f) * col.w;
+        acc[5] += mult * G * dL_dalpha;
+    }
+    return valid;
+}
+
 template <bool INTERP, bool DEPTH>
 __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                                                   int W, int H, int gx, int gy, int T, Geom g,
@@ -25,53 +91,55 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
                                                   const float* __restrict__ dL_dinvdepths, const float* __restrict__ ts,
                                                   const int* __restrict__ kids, BwdScratch rec)
 {
-    __shared__ float4 s_xy[64];   // x, y, 1/depth, t
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, quadrant mask bits
     __shared__ float4 s_co[64];
     __shared__ float4 s_col[64];  // r, g, b, 1/kids
+    __shared__ float s_t[64];     // interpolation t
     __shared__ float4 s_ra[64];
     __shared__ float4 s_rb[64];
     __shared__ float2 s_rc[64];
     const int tile = xcd_remap(blockIdx.x, T);
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
-    const int px = tx * HLGS_TILE + (lane & 15);
-    const int py0 = ty * HLGS_TILE + (lane >> 4);
-    const float pxf = (float)px;
+    const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
     const uint2 range = ranges[tile];
     const uint32_t cnt = range.y - range.x;
     if (cnt == 0) return;
     const size_t HW = (size_t)H * W;
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+    const float lx = (float)(tx0 + (lane & 7)), ly = (float)(ty0 + (lane >> 3));
 
-    float Tcur[4], Tfin[4], ar[4], ag[4], ab[4], la[4], lr[4], lg[4], lb[4], dr[4], dgc[4], db[4], bgd[4];
-    float dinv[4], ainv[4], linv[4];
-    uint32_t lastc[4];
-    uint32_t maxlast = 0;
+    // lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant k
+    PixB ps[4];
+    uint32_t qlast[4];  // wave-uniform per quadrant: furthest-back position any of its pixels needs
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int py = py0 + 4 * k;
+        const int px = tx0 + 8 * (k & 1) + (lane & 7), py = ty0 + 8 * (k >> 1) + (lane >> 3);
         const bool inside = px < W && py < H;
         const size_t pid = (size_t)W * py + px;
-        Tfin[k] = inside ? final_Ts[pid] : 0.f;
-        Tcur[k] = Tfin[k];
-        lastc[k] = inside ? n_contrib[pid] : 0u;
-        maxlast = max(maxlast, lastc[k]);
-        ar[k] = ag[k] = ab[k] = la[k] = lr[k] = lg[k] = lb[k] = 0.f;
-        dr[k] = inside ? dL_dpixels[pid] : 0.f;
-        dgc[k] = inside ? dL_dpixels[HW + pid] : 0.f;
-        db[k] = inside ? dL_dpixels[2 * HW + pid] : 0.f;
-        bgd[k] = 0.f;
-        bgd[k] += bg[0] * dr[k];
-        bgd[k] += bg[1] * dgc[k];
-        bgd[k] += bg[2] * db[k];
-        dinv[k] = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
-        ainv[k] = linv[k] = 0.f;
+        PixB& p = ps[k];
+        const float tf = inside ? final_Ts[pid] : 0.f;
+        p.T = tf;
+        p.last = inside ? n_contrib[pid] : 0u;
+        p.ar = p.ag = p.ab = p.la = p.lr = p.lg = p.lb = 0.f;
+        p.dr = inside ? dL_dpixels[pid] : 0.f;
+        p.dg = inside ? dL_dpixels[HW + pid] : 0.f;
+        p.db = inside ? dL_dpixels[2 * HW + pid] : 0.f;
+        float bgd = 0.f;
+        bgd += bg[0] * p.dr;
+        bgd += bg[1] * p.dg;
+        bgd += bg[2] * p.db;
+        p.TB = tf * bgd;
+        p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
+        p.ainv = p.linv = 0.f;
+        uint32_t m = p.last;
+        for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        qlast[k] = __builtin_amdgcn_readfirstlane(m);
     }
-    // wave-uniform: the furthest-back position any pixel of this tile still needs
-    for (int off = 32; off > 0; off >>= 1) maxlast = max(maxlast, (uint32_t)__shfl_xor((int)maxlast, off, 64));
+    const uint32_t maxlast = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
 
     for (uint32_t b0 = 0; b0 < cnt; b0 += 64) {
-        // batch covers local positions cnt-1-b0 down to cnt-1-b0-(n-1)
+        // batch covers local positions cnt-1-b0 down to cnt-1-b0-(n-1), loaded back to front
         const int n = (int)min(64u, cnt - b0);
         const uint32_t li_top = cnt - 1 - b0;
         const bool lane_valid = lane < n;
@@ -80,10 +148,13 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
             const uint32_t pos = range.x + li_top - lane;
             const uint32_t id = point_list[pos];
             const float2 xy = g.means2D[id];
-            s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1.f / g.depths[id] : 0.f, INTERP ? ts[id] : 0.f);
-            s_co[lane] = g.conic_opacity[id];
+            const float4 co = g.conic_opacity[id];
+            const uint32_t qm = quad_mask(xy.x, xy.y, co, tx0, ty0);
+            s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1.f / g.depths[id] : 0.f, __uint_as_float(qm));
+            s_co[lane] = co;
             s_col[lane] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2],
                                       INTERP ? 1.0f / (float)kids[id] : 0.f);
+            if (INTERP) s_t[lane] = ts[id];
             const int2 ext = g.rects[id];
             int x0, y0, x1, y1;
             tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
@@ -93,84 +164,34 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
             s_rc[lane] = make_float2(0.f, 0.f);
         }
         __syncthreads();
-        // every splat of this batch lies behind all contributors of every pixel: records stay zero
+        // a batch entirely behind every pixel's last contributor leaves its records zero
         const uint32_t li_bot = li_top - (uint32_t)(n - 1);
         if (li_bot < maxlast) {
             for (int j = 0; j < n; j++) {
                 const uint32_t li = li_top - (uint32_t)j;
-                if (li >= maxlast) continue;
                 const float4 xy = s_xy[j];
+                uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(xy.w));
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (li >= qlast[k]) qm &= ~(1u << k);
+                if (qm == 0) continue;
                 const float4 co = s_co[j];
                 const float4 col = s_col[j];
-                float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f, g4 = 0.f, g5 = 0.f, g6 = 0.f, g7 = 0.f, g8 = 0.f, g9 = 0.f;
+                const float tt = INTERP ? s_t[j] : 0.f;
+                float acc[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                 bool any = false;
+                const float dx0 = xy.x - lx, dy0 = xy.y - ly;
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    if (li >= lastc[k]) continue;
-                    const float dx = xy.x - pxf, dy = xy.y - (float)(py0 + 4 * k);
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                    if (power > 0.0f) continue;
-                    const float G = __expf(power);
-                    const float test_alpha = co.w * G;
-                    const bool nullalpha = test_alpha > 0.99f;
-                    const float my_alpha = fminf(0.99f, test_alpha);
-                    float alpha = my_alpha;
-                    if (INTERP) alpha = xy.w * my_alpha + (1.0f - xy.w) * (1.0f - powf(1.0f - my_alpha, col.w));
-                    if (alpha < 1.0f / 255.0f) continue;
-                    any = true;
-                    Tcur[k] = Tcur[k] / (1.f - alpha);
-                    const float weight = alpha * Tcur[k];
-                    float dL_dalpha = 0.0f;
-                    ar[k] = la[k] * lr[k] + (1.f - la[k]) * ar[k];
-                    lr[k] = col.x;
-                    dL_dalpha += (col.x - ar[k]) * dr[k];
-                    g6 += weight * dr[k];
-                    ag[k] = la[k] * lg[k] + (1.f - la[k]) * ag[k];
-                    lg[k] = col.y;
-                    dL_dalpha += (col.y - ag[k]) * dgc[k];
-                    g7 += weight * dgc[k];
-                    ab[k] = la[k] * lb[k] + (1.f - la[k]) * ab[k];
-                    lb[k] = col.z;
-                    dL_dalpha += (col.z - ab[k]) * db[k];
-                    g8 += weight * db[k];
-                    if (DEPTH) {
-                        ainv[k] = la[k] * linv[k] + (1.f - la[k]) * ainv[k];
-                        linv[k] = xy.z;
-                        dL_dalpha += (xy.z - ainv[k]) * dinv[k];
-                        g9 += weight * dinv[k];
-                    }
-                    dL_dalpha *= Tcur[k];
-                    la[k] = alpha;
-                    dL_dalpha += (-Tfin[k] / (1.f - alpha)) * bgd[k];
-                    dL_dalpha = nullalpha ? 0.f : dL_dalpha;
-                    const float dL_dG = co.w * dL_dalpha;
-                    const float gdx = G * dx, gdy = G * dy;
-                    const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                    const float dG_ddely = -gdy * co.z - gdx * co.y;
-                    g0 += dL_dG * dG_ddelx * ddelx_dx;
-                    g1 += dL_dG * dG_ddely * ddely_dy;
-                    g2 += -0.5f * gdx * dx * dL_dG;
-                    g3 += -0.5f * gdx * dy * dL_dG;
-                    g4 += -0.5f * gdy * dy * dL_dG;
-                    float mult = 1.0f;
-                    if (INTERP) mult = xy.w - powf(1.0f - my_alpha, col.w - 1.0f) * (xy.w - 1.0f) * col.w;
-                    g5 += mult * G * dL_dalpha;
-                }
+                for (int k = 0; k < 4; k++)
+                    if ((qm >> k) & 1u)  // uniform branch
+                        any |= bwd_pair<INTERP, DEPTH>(ps[k], li, dx0 - 8.f * (k & 1), dy0 - 8.f * (k >> 1), co, col,
+                                                       xy.z, tt, ddelx_dx, ddely_dy, acc);
                 if (__ballot(any)) {
-                    g0 = wave_sum_to_lane63(g0);
-                    g1 = wave_sum_to_lane63(g1);
-                    g2 = wave_sum_to_lane63(g2);
-                    g3 = wave_sum_to_lane63(g3);
-                    g4 = wave_sum_to_lane63(g4);
-                    g5 = wave_sum_to_lane63(g5);
-                    g6 = wave_sum_to_lane63(g6);
-                    g7 = wave_sum_to_lane63(g7);
-                    g8 = wave_sum_to_lane63(g8);
-                    if (DEPTH) g9 = wave_sum_to_lane63(g9);
+                    wave_sum10_to_lane63(acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7], acc[8], acc[9]);
                     if (lane == 63) {
-                        s_ra[j] = make_float4(g0, g1, g2, g3);
-                        s_rb[j] = make_float4(g4, g5, g6, g7);
-                        s_rc[j] = make_float2(g8, g9);
+                        s_ra[j] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+                        s_rb[j] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+                        s_rc[j] = make_float2(acc[8], acc[9]);
                     }
                 }
             }

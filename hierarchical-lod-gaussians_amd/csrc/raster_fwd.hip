@@ -242,8 +242,10 @@ __global__ void __launch_bounds__(256) k_merge_runs(const uint2* __restrict__ ra
 }
 
 // ------------------------------------------------------------------------------------------------
-// Front-to-back blend: one wave64 per 16x16 tile, four pixels per lane (rows ly, ly+4, ly+8, ly+12),
-// 64-splat batches staged in LDS and read back as broadcasts.
+// Front-to-back blend: one wave64 per 16x16 tile.  Lane l owns pixel (l & 7, l >> 3) of each of the
+// four 8x8 quadrants; 64-splat batches are staged in LDS and read back as broadcasts.  Every splat
+// carries a wave-uniform quadrant mask (quad_mask), so quadrants its alpha >= 1/255 footprint cannot
+// reach are skipped by a scalar branch instead of being evaluated and discarded pixel by pixel.
 // ------------------------------------------------------------------------------------------------
 template <bool INTERP, bool DEPTH>
 __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
@@ -256,35 +258,40 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
                                                   float* __restrict__ out_color, float* __restrict__ out_invdepth,
                                                   int* __restrict__ seen)
 {
-    __shared__ float4 s_xy[64];   // x, y, id bits, 1/depth
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, quadrant mask bits
     __shared__ float4 s_co[64];   // conic x,y,z, opacity
     __shared__ float4 s_col[64];  // r, g, b, interpolation t
     __shared__ float s_fr[64];    // 1 / kids
     const int tile = xcd_remap(blockIdx.x, T);
     const int lane = threadIdx.x;
-    const int tx = tile % gx, ty = tile / gx;
-    const int px = tx * HLGS_TILE + (lane & 15);
-    const int py0 = ty * HLGS_TILE + (lane >> 4);
-    const float pxf = (float)px;
+    const int tx0 = (tile % gx) * HLGS_TILE, ty0 = (tile / gx) * HLGS_TILE;
     const uint2 range = ranges[tile];
 
-    float Tt[4], C0[4], C1[4], C2[4], D[4];
+    float pxf[4], pyf[4], Tt[4], C0[4], C1[4], C2[4], D[4];
     uint32_t last[4];
     bool done[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
+        const int px = tx0 + 8 * (k & 1) + (lane & 7), py = ty0 + 8 * (k >> 1) + (lane >> 3);
+        pxf[k] = (float)px;
+        pyf[k] = (float)py;
         Tt[k] = 1.0f; C0[k] = C1[k] = C2[k] = D[k] = 0.0f; last[k] = 0;
-        done[k] = !(px < W && py0 + 4 * k < H);
+        done[k] = !(px < W && py < H);
     }
-    for (uint32_t base = range.x; base < range.y; base += 64) {
-        if (__all(done[0] && done[1] && done[2] && done[3])) break;
+    uint32_t live = 0;  // wave-uniform: quadrants with a pixel still accumulating
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (!__all(done[k])) live |= 1u << k;
+    for (uint32_t base = range.x; base < range.y && live; base += 64) {
         const uint32_t pos = base + lane;
         uint32_t my_id = 0;
         if (pos < range.y) {
             my_id = point_list[pos];
             const float2 xy = means2D[my_id];
-            s_xy[lane] = make_float4(xy.x, xy.y, __uint_as_float(my_id), DEPTH ? 1 / depths[my_id] : 0.f);
-            s_co[lane] = conic_opacity[my_id];
+            const float4 co = conic_opacity[my_id];
+            const uint32_t qm = quad_mask(xy.x, xy.y, co, tx0, ty0);
+            s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1 / depths[my_id] : 0.f, __uint_as_float(qm));
+            s_co[lane] = co;
             s_col[lane] = make_float4(features[3 * my_id], features[3 * my_id + 1], features[3 * my_id + 2],
                                       INTERP ? ts[my_id] : 0.f);
             if (INTERP) s_fr[lane] = 1.0f / (float)kids[my_id];
@@ -294,30 +301,32 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
         uint64_t seen_mask = 0;
         for (int j = 0; j < n; j++) {
             const float4 xy = s_xy[j];
+            const uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(xy.w)) & live;
+            if (qm == 0) continue;
             const float4 co = s_co[j];
+            const float4 c = s_col[j];
             const uint32_t contrib = base - range.x + j + 1;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
+                if (!((qm >> k) & 1u)) continue;  // uniform branch
                 if (done[k]) continue;
-                const float dx = xy.x - pxf, dy = xy.y - (float)(py0 + 4 * k);
+                const float dx = xy.x - pxf[k], dy = xy.y - pyf[k];
                 const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
                 if (power > 0.0f) continue;
                 const float my_alpha = fminf(0.99f, co.w * __expf(power));
                 float alpha = my_alpha;
                 if (INTERP) {
-                    const float tt = s_col[j].w;
                     const float ka = 1.0f - __powf(1.0f - my_alpha, s_fr[j]);
-                    alpha = tt * my_alpha + (1.0f - tt) * ka;
+                    alpha = c.w * my_alpha + (1.0f - c.w) * ka;
                 }
                 if (alpha < 1.0f / 255.0f) continue;
                 const float test_T = Tt[k] * (1 - alpha);
                 if (test_T < 0.0001f) { done[k] = true; continue; }
-                const float4 c = s_col[j];
                 C0[k] += c.x * alpha * Tt[k];
                 C1[k] += c.y * alpha * Tt[k];
                 C2[k] += c.z * alpha * Tt[k];
-                if (DEPTH) D[k] += xy.w * alpha * Tt[k];
+                if (DEPTH) D[k] += xy.z * alpha * Tt[k];
                 Tt[k] = test_T;
                 last[k] = contrib;
                 any = true;
@@ -325,12 +334,15 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
             if (__ballot(any)) seen_mask |= 1ull << j;
         }
         if (pos < range.y && ((seen_mask >> lane) & 1ull)) seen[my_id] = 1;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (((live >> k) & 1u) && __all(done[k])) live &= ~(1u << k);
         __syncthreads();
     }
     const size_t HW = (size_t)H * W;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int py = py0 + 4 * k;
+        const int px = (int)pxf[k], py = (int)pyf[k];
         if (px < W && py < H) {
             const size_t pid = (size_t)W * py + px;
             final_T[pid] = Tt[k];

@@ -13,7 +13,7 @@ LIB = os.path.join(LIBDIR, "libhlgs.so")
 SOURCES = ["scan.hip", "raster_fwd.hip", "raster_bwd.hip", "lod.hip", "capi.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HLGS_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-Wall",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
 
 
