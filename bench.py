@@ -35,6 +35,7 @@ def algorithmic_bytes(stage, P, V, R, N, T, M, D):
     return {
         "preprocess": P * (44 + 12 * M) + 83 * P,
         "scan": 8 * P,
+        "count_tiles": 20 * P + 4 * T,
         "scatter": 28 * V + 12 * R,
         "tile_sort": 24 * R,
         "tile_ranges": 8 * R + 8 * T,

@@ -17,6 +17,8 @@ namespace hlgs {
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
                        hipStream_t s);
 void launch_tile_ranges(const Img& im, int T, hipStream_t s);
+bool lds_binning(int gx, int gy);
+void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, hipStream_t s);
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
                     int gy, uint32_t max_count, hipStream_t s, bool timing);
 void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, int gx, int gy,
@@ -142,9 +144,10 @@ static int check_stage(hipStream_t s, bool debug, const char* stage)
     return HLGS_OK;
 }
 
-enum Stage { ST_PRE = 0, ST_SCAN, ST_RANGES, ST_SCATTER, ST_SORT, ST_BLEND_FWD, ST_BLEND_BWD, ST_GAUSS_BWD, ST_COUNT };
+enum Stage { ST_PRE = 0, ST_SCAN, ST_RANGES, ST_SCATTER, ST_SORT, ST_BLEND_FWD, ST_BLEND_BWD, ST_GAUSS_BWD,
+             ST_COUNT_TILES, ST_COUNT };
 static const char* kStageNames[ST_COUNT] = {"preprocess", "scan", "tile_ranges", "scatter", "tile_sort",
-                                            "blend_fwd", "blend_bwd", "gauss_bwd"};
+                                            "blend_fwd", "blend_bwd", "gauss_bwd", "count_tiles"};
 static bool g_timing = false;
 // event pool per stage: launch i of a stage uses pair i (grown on demand, reused after a reset)
 static std::vector<hipEvent_t> g_ev[ST_COUNT][2];
@@ -249,9 +252,15 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     hipGetLastError();
     HLGS_TRY_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
     HLGS_TRY_HIP(hipMemsetAsync(im.misc, 0, sizeof(uint32_t) * 16, s));
+    const bool lds_bins = lds_binning(gx, gy);
     stage_mark(s, ST_PRE, true);
-    launch_preprocess(*a, g, radii, im.tile_count, gx, gy, s);
+    launch_preprocess(*a, g, radii, lds_bins ? nullptr : im.tile_count, gx, gy, s);
     stage_mark(s, ST_PRE, false);
+    if (lds_bins) {
+        stage_mark(s, ST_COUNT_TILES, true);
+        launch_count_tiles(a->P, radii, g, im.tile_count, gx, gy, s);
+        stage_mark(s, ST_COUNT_TILES, false);
+    }
     if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
     stage_mark(s, ST_SCAN, true);
     scan_inclusive_u32(g.tiles_touched, g.point_offsets, (size_t)a->P, g.scan_tmp, s);

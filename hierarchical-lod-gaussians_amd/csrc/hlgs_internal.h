@@ -11,6 +11,9 @@ namespace hlgs {
 constexpr int kScanItems = 2048;    // elements per scan block (256 threads x 8)
 constexpr int kSortCap = 4096;      // largest per-tile list sorted in one LDS pass
 constexpr size_t kAlign = 256;
+constexpr int kBinThreads = 1024;   // LDS-histogram binning: threads per block
+constexpr int kBinGauss = 4096;     // Gaussians per binning block
+constexpr int kBinMaxTiles = 16384; // tile grids up to this use LDS histograms (2 x 64 KiB)
 
 inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 size_t scan_scratch_elems(size_t n);

@@ -139,8 +139,71 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
     if (HIER && use_parent) opacity = t * opacity + (1.0f - t) * a.opacities[p_idx];
     g.conic_opacity[t_idx] = make_float4(conic_x, conic_y, conic_z, opacity * h_scale);
     g.tiles_touched[t_idx] = area;
-    for (int y = y0; y < y1; y++)
-        for (int x = x0; x < x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
+    if (tile_count)  // only when the tile grid is too large for the LDS-histogram binning
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tile binning with block-level LDS histograms.  A block owns kBinGauss consecutive Gaussians; its
+// instances are counted per tile in LDS and each non-empty bin costs one coalesced device atomic,
+// instead of one lane-scattered atomic per (Gaussian, tile) instance.
+// ------------------------------------------------------------------------------------------------
+template <typename F>
+__device__ __forceinline__ void for_each_instance(int P, const int* __restrict__ radii, const Geom& g, int gx, int gy,
+                                                  F&& f)
+{
+    const int g0 = blockIdx.x * kBinGauss, g1 = min(P, g0 + kBinGauss);
+    for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += kBinThreads) {
+        if (radii[idx] <= 0) continue;
+        const float2 xy = g.means2D[idx];
+        const int2 ext = g.rects[idx];
+        int x0, y0, x1, y1;
+        tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) f(idx, y * gx + x);
+    }
+}
+
+__global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
+                                                             uint32_t* __restrict__ tile_count, int gx, int gy)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+    const int T = gx * gy;
+    for (int t = threadIdx.x; t < T; t += kBinThreads) s_hist[t] = 0;
+    __syncthreads();
+    for_each_instance(P, radii, g, gx, gy, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += kBinThreads) {
+        const uint32_t c = s_hist[t];
+        if (c) atomicAdd(&tile_count[t], c);
+    }
+}
+
+// Same block -> Gaussian mapping as k_count_tiles: reserve the block's run inside every tile segment
+// with one returning atomic per bin, then hand out slots from LDS.  Slot order inside a tile is
+// irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
+__global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
+                                                                  const uint2* __restrict__ ranges, uint32_t* cursor,
+                                                                  uint64_t* __restrict__ keys, int gx, int gy)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+    const int T = gx * gy;
+    uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
+    uint32_t* s_rank = s_hist + T; // per-tile running rank
+    for (int t = threadIdx.x; t < T; t += kBinThreads) { s_cnt[t] = 0; s_rank[t] = 0; }
+    __syncthreads();
+    for_each_instance(P, radii, g, gx, gy, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += kBinThreads) {
+        const uint32_t c = s_cnt[t];
+        s_cnt[t] = c ? ranges[t].x + atomicAdd(&cursor[t], c) : 0u;
+    }
+    __syncthreads();
+    for_each_instance(P, radii, g, gx, gy, [&](int idx, int tile) {
+        const uint32_t r = atomicAdd(&s_rank[tile], 1u);
+        keys[s_cnt[tile] + r] = ((uint64_t)__float_as_uint(g.depths[idx]) << 32) | (uint32_t)idx;
+    });
 }
 
 // ranges[t] = [incl[t] - count[t], incl[t]); misc[0] = R, misc[1] = max count; cursor reset for the scatter.
@@ -389,6 +452,26 @@ __global__ void __launch_bounds__(256) k_relocation(int P, const float* __restri
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
+bool lds_binning(int gx, int gy) { return gx * gy <= kBinMaxTiles; }
+
+// Dynamic LDS above 64 KiB must be opted into per kernel (idempotent; done once per process).
+static void allow_big_lds()
+{
+    static bool done = false;
+    if (done) return;
+    hipFuncSetAttribute((const void*)k_count_tiles, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)k_scatter_keys_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    done = true;
+}
+
+void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, hipStream_t s)
+{
+    const size_t lds = sizeof(uint32_t) * (size_t)gx * gy;
+    allow_big_lds();
+    hipLaunchKernelGGL(k_count_tiles, dim3((P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads), lds, s, P, radii, g,
+                       tile_count, gx, gy);
+}
+
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
                        hipStream_t s)
 {
@@ -412,8 +495,13 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
 {
     const int T = gx * gy;
     if (timing) stage_mark(s, 3, true);
-    hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
-                       im.tile_cursor, b.keys, gx, gy);
+    if (lds_binning(gx, gy)) {
+        allow_big_lds();
+        hipLaunchKernelGGL(k_scatter_keys_lds, dim3((a.P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads),
+                           2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy);
+    } else
+        hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
+                           im.tile_cursor, b.keys, gx, gy);
     if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
     hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, b.keys, b.point_list, T);
     if (max_count > (uint32_t)kSortCap) {

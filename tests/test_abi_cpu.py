@@ -37,7 +37,7 @@ def test_stage_names():
     lib = L.load()
     names = [lib.hlgs_stage_name(i).decode() for i in range(lib.hlgs_stage_count())]
     assert names == ["preprocess", "scan", "tile_ranges", "scatter", "tile_sort", "blend_fwd", "blend_bwd",
-                     "gauss_bwd"]
+                     "gauss_bwd", "count_tiles"]
 
 
 def test_settings_fields_match_reference_order():
