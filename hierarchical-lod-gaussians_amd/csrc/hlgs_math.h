@@ -198,6 +198,20 @@ __device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, int x
     return m;
 }
 
+// Does the alpha >= 1/255 footprint of a splat (see quad_mask) reach the 8x8 pixel block at (qx, qy)?
+__device__ __forceinline__ bool touches_quad(float x, float y, float4 co, float qx, float qy)
+{
+    const float o = co.w;
+    if (o != o || co.x != co.x || co.y != co.y || co.z != co.z) return true;
+    if (o < (1.0f / 255.0f) * 0.999f) return false;
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.f) || !(co.x > 0.f) || !(co.z > 0.f)) return true;
+    const float t = fmaxf(2.0f * logf(255.0f * o), 0.f) * 1.002f + 1e-3f;
+    const float ex = sqrtf(t * co.z / det) * 1.001f + 0.01f;
+    const float ey = sqrtf(t * co.x / det) * 1.001f + 0.01f;
+    return x + ex >= qx && x - ex <= qx + 7.f && y + ey >= qy && y - ey <= qy + 7.f;
+}
+
 // Bijective XCD-aware block remap (cdna_hip_programming.md section 5): consecutive logical blocks
 // land on the same XCD so neighbouring tiles share that XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg)
@@ -206,44 +220,40 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-// Ten independent full-wave (64-lane) sums in one block of fused v_add_f32_dpp instructions; the totals
-// land in lane 63.  Interleaving the ten chains keeps every DPP source at least nine instructions
-// behind its producer, so only the block entry needs the VALU->DPP wait state (s_nop 1).
-__device__ __forceinline__ void wave_sum10_to_lane63(float& a0, float& a1, float& a2, float& a3, float& a4,
-                                                     float& a5, float& a6, float& a7, float& a8, float& a9)
+// Butterfly reduce-scatter of ten per-lane values over the 64-lane wave.  v_permlane32_swap folds two
+// values at once (rows 0-1 keep the sum of one, rows 2-3 of the other), v_permlane16_swap folds again
+// across row pairs, and four fused row-DPP adds finish inside each 16-lane row: 28 VALU instructions
+// where ten independent full-wave DPP sums take 60.  Totals land in every lane of a row:
+//   r0 rows 0..3 = v0, v2, v1, v3;   r1 rows 0..3 = v4, v6, v5, v7;   r2 rows 0..3 = v8, v8, v9, v9.
+__device__ __forceinline__ float fold32(float x, float y)
 {
-#define HLGS_DPP_STEP(ctrl)                                                                                \
-    "v_add_f32_dpp %0, %0, %0 " ctrl "\n\tv_add_f32_dpp %1, %1, %1 " ctrl "\n\tv_add_f32_dpp %2, %2, %2 " ctrl \
-    "\n\tv_add_f32_dpp %3, %3, %3 " ctrl "\n\tv_add_f32_dpp %4, %4, %4 " ctrl "\n\tv_add_f32_dpp %5, %5, %5 " ctrl \
-    "\n\tv_add_f32_dpp %6, %6, %6 " ctrl "\n\tv_add_f32_dpp %7, %7, %7 " ctrl "\n\tv_add_f32_dpp %8, %8, %8 " ctrl \
-    "\n\tv_add_f32_dpp %9, %9, %9 " ctrl "\n\t"
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float fold16(float x, float y)
+{
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void wave_reduce10(const float (&v)[10], float& r0, float& r1, float& r2)
+{
+    const float a0 = fold32(v[0], v[1]), a2 = fold32(v[2], v[3]), a4 = fold32(v[4], v[5]);
+    const float a6 = fold32(v[6], v[7]), a8 = fold32(v[8], v[9]);
+    r0 = fold16(a0, a2);
+    r1 = fold16(a4, a6);
+    r2 = fold16(a8, a8);
+#define HLGS_DPP_ROW(ctrl)                                                                                 \
+    "v_add_f32_dpp %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                        \
+    "v_add_f32_dpp %1, %1, %1 " ctrl " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                        \
+    "v_add_f32_dpp %2, %2, %2 " ctrl " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
     asm volatile("s_nop 1\n\t"
-                 HLGS_DPP_STEP("quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1")
-                 HLGS_DPP_STEP("quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1")
-                 HLGS_DPP_STEP("row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-                 HLGS_DPP_STEP("row_ror:8 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-                 HLGS_DPP_STEP("row_bcast:15 row_mask:0xa bank_mask:0xf")
-                 HLGS_DPP_STEP("row_bcast:31 row_mask:0xc bank_mask:0xf")
+                 HLGS_DPP_ROW("quad_perm:[1,0,3,2]")
+                 HLGS_DPP_ROW("quad_perm:[2,3,0,1]")
+                 HLGS_DPP_ROW("row_ror:4")
+                 HLGS_DPP_ROW("row_ror:8")
                  "s_nop 1"
-                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8), "+v"(a9));
-#undef HLGS_DPP_STEP
-}
-
-// Full-wave (64-lane) sum with DPP; the total lands in lane 63.
-template <int CTRL, int ROW, bool BC>
-__device__ __forceinline__ float dpp(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW, 0xF, BC));
-}
-__device__ __forceinline__ float wave_sum_to_lane63(float v)
-{
-    v += dpp<0xB1, 0xF, true>(v);   // quad_perm [1,0,3,2]
-    v += dpp<0x4E, 0xF, true>(v);   // quad_perm [2,3,0,1]
-    v += dpp<0x124, 0xF, true>(v);  // row_ror:4
-    v += dpp<0x128, 0xF, true>(v);  // row_ror:8 -> every lane holds its row sum
-    v += dpp<0x142, 0xA, false>(v); // row_bcast:15 into rows 1,3
-    v += dpp<0x143, 0xC, false>(v); // row_bcast:31 into rows 2,3
-    return v;
+                 : "+v"(r0), "+v"(r1), "+v"(r2));
+#undef HLGS_DPP_ROW
 }
 
 }  // namespace hlgs

@@ -6,8 +6,8 @@
 //                 + preprocessCUDA<3> backward  backward.cu:398-495 (SH :23-142, cov3D :330-393)
 //
 // The reference issues one global float atomic per (pixel, Gaussian, gradient component)
-// (backward.cu:669-718).  Here each wave owns one tile: every lane folds its four pixels, a DPP
-// wave reduction folds the 64 lanes, and the per-(tile, Gaussian) partial is stored once -- with
+// (backward.cu:669-718).  Here each wave owns one tile: every lane folds its four pixels, a
+// permlane/DPP reduce-scatter folds the 64 lanes, and the per-(tile, Gaussian) partial is stored once -- with
 // a plain store -- into a Gaussian-major record slot (the Gaussian's point_offsets range, indexed by
 // the tile's position inside its rect).  k_gauss_bwd then sums each Gaussian's contiguous records
 // in a fixed order, so the backward has no float atomics and is bitwise reproducible.
@@ -187,11 +187,13 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
                         any |= bwd_pair<INTERP, DEPTH>(ps[k], li, dx0 - 8.f * (k & 1), dy0 - 8.f * (k >> 1), co, col,
                                                        xy.z, tt, ddelx_dx, ddely_dy, acc);
                 if (__ballot(any)) {
-                    wave_sum10_to_lane63(acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7], acc[8], acc[9]);
-                    if (lane == 63) {
-                        s_ra[j] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-                        s_rb[j] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-                        s_rc[j] = make_float2(acc[8], acc[9]);
+                    float r0, r1, r2;
+                    wave_reduce10(acc, r0, r1, r2);
+                    if ((lane & 15) == 0) {
+                        const int row = lane >> 4, c = ((row & 1) << 1) | (row >> 1);
+                        reinterpret_cast<float*>(s_ra)[4 * j + c] = r0;
+                        reinterpret_cast<float*>(s_rb)[4 * j + c] = r1;
+                        if (!(row & 1)) reinterpret_cast<float*>(s_rc)[2 * j + (row >> 1)] = r2;
                     }
                 }
             }

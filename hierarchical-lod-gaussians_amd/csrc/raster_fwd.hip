@@ -305,10 +305,11 @@ __global__ void __launch_bounds__(256) k_merge_runs(const uint2* __restrict__ ra
 }
 
 // ------------------------------------------------------------------------------------------------
-// Front-to-back blend: one wave64 per 16x16 tile.  Lane l owns pixel (l & 7, l >> 3) of each of the
-// four 8x8 quadrants; 64-splat batches are staged in LDS and read back as broadcasts.  Every splat
-// carries a wave-uniform quadrant mask (quad_mask), so quadrants its alpha >= 1/255 footprint cannot
-// reach are skipped by a scalar branch instead of being evaluated and discarded pixel by pixel.
+// Front-to-back blend.  One wave64 per 8x8 quadrant of a 16x16 tile, one pixel per lane; the four
+// quadrant waves of a tile are independent blocks placed on one XCD (xcd_remap) so the tile's splat
+// gathers hit the same L2.  Each 64-splat batch is staged in LDS; a ballot builds the wave-uniform bit
+// set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
+// visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
 // ------------------------------------------------------------------------------------------------
 template <bool INTERP, bool DEPTH>
 __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
@@ -321,100 +322,81 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
                                                   float* __restrict__ out_color, float* __restrict__ out_invdepth,
                                                   int* __restrict__ seen)
 {
-    __shared__ float4 s_xy[64];   // x, y, 1/depth, quadrant mask bits
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, interpolation t
     __shared__ float4 s_co[64];   // conic x,y,z, opacity
-    __shared__ float4 s_col[64];  // r, g, b, interpolation t
-    __shared__ float s_fr[64];    // 1 / kids
-    const int tile = xcd_remap(blockIdx.x, T);
+    __shared__ float4 s_col[64];  // r, g, b, 1/kids
+    const int L = xcd_remap(blockIdx.x, 4 * T);
+    const int tile = L >> 2, q = L & 3;
     const int lane = threadIdx.x;
-    const int tx0 = (tile % gx) * HLGS_TILE, ty0 = (tile / gx) * HLGS_TILE;
+    const int qx0 = (tile % gx) * HLGS_TILE + 8 * (q & 1), qy0 = (tile / gx) * HLGS_TILE + 8 * (q >> 1);
+    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+    const float pxf = (float)px, pyf = (float)py;
+    const float fqx = (float)qx0, fqy = (float)qy0;
     const uint2 range = ranges[tile];
 
-    float pxf[4], pyf[4], Tt[4], C0[4], C1[4], C2[4], D[4];
-    uint32_t last[4];
-    bool done[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int px = tx0 + 8 * (k & 1) + (lane & 7), py = ty0 + 8 * (k >> 1) + (lane >> 3);
-        pxf[k] = (float)px;
-        pyf[k] = (float)py;
-        Tt[k] = 1.0f; C0[k] = C1[k] = C2[k] = D[k] = 0.0f; last[k] = 0;
-        done[k] = !(px < W && py < H);
-    }
-    uint32_t live = 0;  // wave-uniform: quadrants with a pixel still accumulating
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (!__all(done[k])) live |= 1u << k;
-    for (uint32_t base = range.x; base < range.y && live; base += 64) {
+    float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
+    uint32_t last = 0;
+    bool done = !(px < W && py < H);
+    for (uint32_t base = range.x; base < range.y; base += 64) {
+        if (__all(done)) break;
         const uint32_t pos = base + lane;
         uint32_t my_id = 0;
+        bool hit = false;
         if (pos < range.y) {
             my_id = point_list[pos];
             const float2 xy = means2D[my_id];
             const float4 co = conic_opacity[my_id];
-            const uint32_t qm = quad_mask(xy.x, xy.y, co, tx0, ty0);
-            s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1 / depths[my_id] : 0.f, __uint_as_float(qm));
+            hit = touches_quad(xy.x, xy.y, co, fqx, fqy);
+            s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1 / depths[my_id] : 0.f, INTERP ? ts[my_id] : 0.f);
             s_co[lane] = co;
             s_col[lane] = make_float4(features[3 * my_id], features[3 * my_id + 1], features[3 * my_id + 2],
-                                      INTERP ? ts[my_id] : 0.f);
-            if (INTERP) s_fr[lane] = 1.0f / (float)kids[my_id];
+                                      INTERP ? 1.0f / (float)kids[my_id] : 0.f);
         }
+        uint64_t todo = __ballot(hit);
         __syncthreads();
-        const int n = (int)min(64u, range.y - base);
         uint64_t seen_mask = 0;
-        for (int j = 0; j < n; j++) {
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
             const float4 xy = s_xy[j];
-            const uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(xy.w)) & live;
-            if (qm == 0) continue;
             const float4 co = s_co[j];
             const float4 c = s_col[j];
-            const uint32_t contrib = base - range.x + j + 1;
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (!((qm >> k) & 1u)) continue;  // uniform branch
-                if (done[k]) continue;
-                const float dx = xy.x - pxf[k], dy = xy.y - pyf[k];
+            bool blended = false;
+            if (!done) {
+                const float dx = xy.x - pxf, dy = xy.y - pyf;
                 const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                if (power > 0.0f) continue;
                 const float my_alpha = fminf(0.99f, co.w * __expf(power));
                 float alpha = my_alpha;
-                if (INTERP) {
-                    const float ka = 1.0f - __powf(1.0f - my_alpha, s_fr[j]);
-                    alpha = c.w * my_alpha + (1.0f - c.w) * ka;
+                if (INTERP) alpha = xy.w * my_alpha + (1.0f - xy.w) * (1.0f - __powf(1.0f - my_alpha, c.w));
+                if (!(power > 0.0f) && !(alpha < 1.0f / 255.0f)) {
+                    const float test_T = Tt * (1 - alpha);
+                    if (test_T < 0.0001f) {
+                        done = true;
+                    } else {
+                        C0 += c.x * alpha * Tt;
+                        C1 += c.y * alpha * Tt;
+                        C2 += c.z * alpha * Tt;
+                        if (DEPTH) D += xy.z * alpha * Tt;
+                        Tt = test_T;
+                        last = base - range.x + (uint32_t)j + 1;
+                        blended = true;
+                    }
                 }
-                if (alpha < 1.0f / 255.0f) continue;
-                const float test_T = Tt[k] * (1 - alpha);
-                if (test_T < 0.0001f) { done[k] = true; continue; }
-                C0[k] += c.x * alpha * Tt[k];
-                C1[k] += c.y * alpha * Tt[k];
-                C2[k] += c.z * alpha * Tt[k];
-                if (DEPTH) D[k] += xy.z * alpha * Tt[k];
-                Tt[k] = test_T;
-                last[k] = contrib;
-                any = true;
             }
-            if (__ballot(any)) seen_mask |= 1ull << j;
+            if (__ballot(blended)) seen_mask |= 1ull << j;
         }
-        if (pos < range.y && ((seen_mask >> lane) & 1ull)) seen[my_id] = 1;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (((live >> k) & 1u) && __all(done[k])) live &= ~(1u << k);
+        if ((seen_mask >> lane) & 1ull) seen[my_id] = 1;
         __syncthreads();
     }
-    const size_t HW = (size_t)H * W;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int px = (int)pxf[k], py = (int)pyf[k];
-        if (px < W && py < H) {
-            const size_t pid = (size_t)W * py + px;
-            final_T[pid] = Tt[k];
-            n_contrib[pid] = last[k];
-            out_color[pid] = C0[k] + Tt[k] * bg[0];
-            out_color[HW + pid] = C1[k] + Tt[k] * bg[1];
-            out_color[2 * HW + pid] = C2[k] + Tt[k] * bg[2];
-            if (DEPTH) out_invdepth[pid] = D[k];
-        }
+    if (px < W && py < H) {
+        const size_t HW = (size_t)H * W;
+        const size_t pid = (size_t)W * py + px;
+        final_T[pid] = Tt;
+        n_contrib[pid] = last;
+        out_color[pid] = C0 + Tt * bg[0];
+        out_color[HW + pid] = C1 + Tt * bg[1];
+        out_color[2 * HW + pid] = C2 + Tt * bg[2];
+        if (DEPTH) out_invdepth[pid] = D;
     }
 }
 
@@ -525,7 +507,7 @@ void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     const bool depth = out_invdepth != nullptr;
 #define HLGS_BLEND(I, Dp)                                                                                       \
-    hipLaunchKernelGGL((k_blend_fwd<I, Dp>), dim3(T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, T, \
+    hipLaunchKernelGGL((k_blend_fwd<I, Dp>), dim3(4 * T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, T, \
                        g.means2D, feat, g.conic_opacity, g.depths, a.ts, a.kids, im.final_T, im.n_contrib, a.bg,   \
                        out_color, out_invdepth, seen)
     if (interp) { if (depth) HLGS_BLEND(true, true); else HLGS_BLEND(true, false); }
