@@ -198,6 +198,19 @@ __device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, int x
     return m;
 }
 
+// Splat falloff in base 2.  conic_q pre-scales the conic by -log2(e) * (1/2, 1, 1/2); splat_e2 returns
+// power * log2(e) for the reference's power = -(a dx^2 + c dy^2)/2 - b dx dy (forward.cu:377-379), with
+// one fixed operation order so the forward and backward blends make identical alpha decisions.
+__device__ __forceinline__ float4 conic_q(float4 co)
+{
+    constexpr float kL2E = 1.4426950408889634f;
+    return make_float4(-0.5f * kL2E * co.x, -kL2E * co.y, -0.5f * kL2E * co.z, co.w);
+}
+__device__ __forceinline__ float splat_e2(float4 q, float dx, float dy)
+{
+    return fmaf(q.z * dy, dy, fmaf(q.y, dy, q.x * dx) * dx);
+}
+
 // Does the alpha >= 1/255 footprint of a splat (see quad_mask) reach the 8x8 pixel block at (qx, qy)?
 __device__ __forceinline__ bool touches_quad(float x, float y, float4 co, float qx, float qy)
 {

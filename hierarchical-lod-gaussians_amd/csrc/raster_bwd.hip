@@ -16,70 +16,79 @@
 
 namespace hlgs {
 
-// Per-pixel state of the back-to-front replay (backward.cu:549-572).
+// Per-pixel state of the back-to-front replay (backward.cu:549-572).  The reference keeps the
+// accumulated colour/inverse-depth behind the current splat and the previous splat's alpha and colour
+// (accum_rec, last_alpha, last_color) only to form dL/dalpha = <c - accum, dL/dpixel>, which is linear
+// in the accumulators; so one scalar ARD = <accum, dL/dpixel> (+ depth term), updated by the current
+// splat once its own step is done, carries the same information.
 struct PixB {
-    float T;        // transmittance in front of the current splat
-    float TB;       // T_final * <bg, dL/dpixel>
-    float ar, ag, ab, la, lr, lg, lb;  // accum_rec, last_alpha, last_color
-    float dr, dg, db;                  // dL/dpixel
-    float dinv, ainv, linv;            // inverse-depth terms
-    uint32_t last;                     // n_contrib
+    float T;                 // transmittance in front of the current splat
+    float TB;                // T_final * <bg, dL/dpixel>
+    float ARD;               // <accum_rec, dL/dpixel> + accum_invdepth * dL/dinvdepth
+    float dr, dg, db, dinv;  // dL/dpixel, dL/dinvdepth
+    uint32_t last;           // n_contrib
 };
 
-// One (pixel, splat) step of renderCUDA backward (backward.cu:601-718); adds this pixel's share of the
-// splat's ten gradient terms to acc.  Returns false for the pairs the reference skips.
+// One (pixel, splat) step of renderCUDA backward (backward.cu:601-718).  The splat's gradient terms
+// are linear in w = G * dL/dalpha and its moments over the pixels,
+//   dL/dmean2D = -o * (conic * [Sum w dx, Sum w dy]) * (W/2, H/2),
+//   dL/dconic  = -o/2 * [Sum w dx^2, Sum w dx dy, Sum w dy^2],   dL/dopacity = Sum w (x mult if lerped),
+// so each pixel adds ten moments to acc and finish_record() applies the per-splat factors once.
+//   acc = [Sum w dx, Sum w dy, Sum w dx^2, Sum w dx dy, Sum w dy^2, Sum w*mult, dcolor r g b, dinvdepth]
+// q = (-a/2, -b, -c/2) * log2(e) so that G = exp2(q0 dx^2 + q1 dx dy + q2 dy^2) = exp(power).
 template <bool INTERP, bool DEPTH>
-__device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& co, const float4& col,
-                                         float invz, float tt, float ddelx_dx, float ddely_dy, float (&acc)[10])
+__device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& q, const float4& col,
+                                         float invz, float tt, float (&acc)[10])
 {
-    // the skip tests of the reference, evaluated as one predicate so the update below is one region
-    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-    const float G = __expf(power);
-    const float test_alpha = co.w * G;
+    const float e2 = splat_e2(q, dx, dy);  // power * log2(e)
+    const float G = __builtin_amdgcn_exp2f(e2);
+    const float test_alpha = q.w * G;
     const float my_alpha = fminf(0.99f, test_alpha);
     float alpha = my_alpha;
     if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, col.w));
-    const bool valid = li < p.last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+    const bool valid = li < p.last && !(e2 > 0.0f) && !(alpha < 1.0f / 255.0f);
     if (valid) {
         const float r1m = __builtin_amdgcn_rcpf(1.f - alpha);  // 1/(1-alpha), alpha <= 0.99
         p.T = p.T * r1m;
         const float weight = alpha * p.T;
-        const float omla = 1.f - p.la;
-        p.ar = p.la * p.lr + omla * p.ar;
-        p.ag = p.la * p.lg + omla * p.ag;
-        p.ab = p.la * p.lb + omla * p.ab;
-        float dL_dalpha = (col.x - p.ar) * p.dr + (col.y - p.ag) * p.dg + (col.z - p.ab) * p.db;
-        p.lr = col.x;
-        p.lg = col.y;
-        p.lb = col.z;
+        float cd = col.x * p.dr + col.y * p.dg + col.z * p.db;
+        if (DEPTH) cd += invz * p.dinv;
+        const float raw = cd - p.ARD;
+        p.ARD = fmaf(alpha, raw, p.ARD);
         acc[6] += weight * p.dr;
         acc[7] += weight * p.dg;
         acc[8] += weight * p.db;
-        if (DEPTH) {
-            p.ainv = p.la * p.linv + omla * p.ainv;
-            p.linv = invz;
-            dL_dalpha += (invz - p.ainv) * p.dinv;
-            acc[9] += weight * p.dinv;
-        }
-        dL_dalpha *= p.T;
-        p.la = alpha;
-        dL_dalpha -= p.TB * r1m;
+        if (DEPTH) acc[9] += weight * p.dinv;
+        float dL_dalpha = raw * p.T - p.TB * r1m;
         dL_dalpha = test_alpha > 0.99f ? 0.f : dL_dalpha;
-        const float dL_dG = co.w * dL_dalpha;
-        const float gdx = G * dx, gdy = G * dy;
-        const float dG_ddelx = -gdx * co.x - gdy * co.y;
-        const float dG_ddely = -gdy * co.z - gdx * co.y;
-        acc[0] += dL_dG * dG_ddelx * ddelx_dx;
-        acc[1] += dL_dG * dG_ddely * ddely_dy;
-        const float hG = -0.5f * dL_dG;
-        acc[2] += hG * gdx * dx;
-        acc[3] += hG * gdx * dy;
-        acc[4] += hG * gdy * dy;
-        float mult = 1.0f;
-        if (INTERP) mult = tt - powf(1.0f - my_alpha, col.w - 1.0f) * (tt - 1.0f) * col.w;
-        acc[5] += mult * G * dL_dalpha;
+        const float w = G * dL_dalpha;
+        const float wdx = w * dx, wdy = w * dy;
+        acc[0] += wdx;
+        acc[1] += wdy;
+        acc[2] = fmaf(wdx, dx, acc[2]);
+        acc[3] = fmaf(wdx, dy, acc[3]);
+        acc[4] = fmaf(wdy, dy, acc[4]);
+        if (INTERP) acc[5] += (tt - powf(1.0f - my_alpha, col.w - 1.0f) * (tt - 1.0f) * col.w) * w;
+        else acc[5] += w;
     }
     return valid;
+}
+
+// Per-splat record from the reduced moments (see bwd_pair); co = conic and opacity of the splat.
+__device__ __forceinline__ void finish_record(const float* m, float4 co, float ddelx_dx, float ddely_dy, float4& ra,
+                                              float4& rb, float2& rc)
+{
+    const float o = co.w;
+    ra.x = -o * (co.x * m[0] + co.y * m[1]) * ddelx_dx;
+    ra.y = -o * (co.z * m[1] + co.y * m[0]) * ddely_dy;
+    ra.z = -0.5f * o * m[2];
+    ra.w = -0.5f * o * m[3];
+    rb.x = -0.5f * o * m[4];
+    rb.y = m[5];
+    rb.z = m[6];
+    rb.w = m[7];
+    rc.x = m[8];
+    rc.y = m[9];
 }
 
 template <bool INTERP, bool DEPTH>
@@ -92,12 +101,10 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
                                                   const int* __restrict__ kids, BwdScratch rec)
 {
     __shared__ float4 s_xy[64];   // x, y, 1/depth, quadrant mask bits
-    __shared__ float4 s_co[64];
+    __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
     __shared__ float4 s_col[64];  // r, g, b, 1/kids
     __shared__ float s_t[64];     // interpolation t
-    __shared__ float4 s_ra[64];
-    __shared__ float4 s_rb[64];
-    __shared__ float2 s_rc[64];
+    __shared__ float s_m[64 * 10];  // reduced moments per splat
     const int tile = xcd_remap(blockIdx.x, T);
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
@@ -121,7 +128,7 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
         const float tf = inside ? final_Ts[pid] : 0.f;
         p.T = tf;
         p.last = inside ? n_contrib[pid] : 0u;
-        p.ar = p.ag = p.ab = p.la = p.lr = p.lg = p.lb = 0.f;
+        p.ARD = 0.f;
         p.dr = inside ? dL_dpixels[pid] : 0.f;
         p.dg = inside ? dL_dpixels[HW + pid] : 0.f;
         p.db = inside ? dL_dpixels[2 * HW + pid] : 0.f;
@@ -131,7 +138,6 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
         bgd += bg[2] * p.db;
         p.TB = tf * bgd;
         p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
-        p.ainv = p.linv = 0.f;
         uint32_t m = p.last;
         for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
         qlast[k] = __builtin_amdgcn_readfirstlane(m);
@@ -144,6 +150,7 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
         const uint32_t li_top = cnt - 1 - b0;
         const bool lane_valid = lane < n;
         uint32_t slot = 0;
+        float4 my_co = make_float4(0.f, 0.f, 0.f, 0.f);
         if (lane_valid) {
             const uint32_t pos = range.x + li_top - lane;
             const uint32_t id = point_list[pos];
@@ -151,7 +158,8 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
             const float4 co = g.conic_opacity[id];
             const uint32_t qm = quad_mask(xy.x, xy.y, co, tx0, ty0);
             s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1.f / g.depths[id] : 0.f, __uint_as_float(qm));
-            s_co[lane] = co;
+            s_q[lane] = conic_q(co);
+            my_co = co;
             s_col[lane] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2],
                                       INTERP ? 1.0f / (float)kids[id] : 0.f);
             if (INTERP) s_t[lane] = ts[id];
@@ -159,10 +167,9 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
             int x0, y0, x1, y1;
             tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
             slot = g.point_offsets[id] - g.tiles_touched[id] + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
-            s_ra[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-            s_rb[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-            s_rc[lane] = make_float2(0.f, 0.f);
         }
+#pragma unroll
+        for (int v = 0; v < 10; v++) s_m[64 * v + lane] = 0.f;
         __syncthreads();
         // a batch entirely behind every pixel's last contributor leaves its records zero
         const uint32_t li_bot = li_top - (uint32_t)(n - 1);
@@ -175,34 +182,39 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
                 for (int k = 0; k < 4; k++)
                     if (li >= qlast[k]) qm &= ~(1u << k);
                 if (qm == 0) continue;
-                const float4 co = s_co[j];
+                const float4 co = s_q[j];
                 const float4 col = s_col[j];
                 const float tt = INTERP ? s_t[j] : 0.f;
                 float acc[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                 bool any = false;
-                const float dx0 = xy.x - lx, dy0 = xy.y - ly;
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     if ((qm >> k) & 1u)  // uniform branch
-                        any |= bwd_pair<INTERP, DEPTH>(ps[k], li, dx0 - 8.f * (k & 1), dy0 - 8.f * (k >> 1), co, col,
-                                                       xy.z, tt, ddelx_dx, ddely_dy, acc);
+                        any |= bwd_pair<INTERP, DEPTH>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), co, col,
+                                                       xy.z, tt, acc);
                 if (__ballot(any)) {
                     float r0, r1, r2;
                     wave_reduce10(acc, r0, r1, r2);
                     if ((lane & 15) == 0) {
                         const int row = lane >> 4, c = ((row & 1) << 1) | (row >> 1);
-                        reinterpret_cast<float*>(s_ra)[4 * j + c] = r0;
-                        reinterpret_cast<float*>(s_rb)[4 * j + c] = r1;
-                        if (!(row & 1)) reinterpret_cast<float*>(s_rc)[2 * j + (row >> 1)] = r2;
+                        s_m[64 * c + j] = r0;
+                        s_m[64 * (4 + c) + j] = r1;
+                        if (!(row & 1)) s_m[64 * (8 + (row >> 1)) + j] = r2;
                     }
                 }
             }
         }
         __syncthreads();
         if (lane_valid) {
-            rec.recA[slot] = s_ra[lane];
-            rec.recB[slot] = s_rb[lane];
-            rec.recC[slot] = s_rc[lane];
+            float m[10];
+#pragma unroll
+            for (int v = 0; v < 10; v++) m[v] = s_m[64 * v + lane];
+            float4 ra, rb;
+            float2 rc;
+            finish_record(m, my_co, ddelx_dx, ddely_dy, ra, rb, rc);
+            rec.recA[slot] = ra;
+            rec.recB[slot] = rb;
+            rec.recC[slot] = rc;
         }
         __syncthreads();
     }

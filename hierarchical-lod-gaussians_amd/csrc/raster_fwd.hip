@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
                                                   int* __restrict__ seen)
 {
     __shared__ float4 s_xy[64];   // x, y, 1/depth, interpolation t
-    __shared__ float4 s_co[64];   // conic x,y,z, opacity
+    __shared__ float4 s_co[64];   // conic_q, opacity
     __shared__ float4 s_col[64];  // r, g, b, 1/kids
     const int L = xcd_remap(blockIdx.x, 4 * T);
     const int tile = L >> 2, q = L & 3;
@@ -348,7 +348,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
             const float4 co = conic_opacity[my_id];
             hit = touches_quad(xy.x, xy.y, co, fqx, fqy);
             s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1 / depths[my_id] : 0.f, INTERP ? ts[my_id] : 0.f);
-            s_co[lane] = co;
+            s_co[lane] = conic_q(co);
             s_col[lane] = make_float4(features[3 * my_id], features[3 * my_id + 1], features[3 * my_id + 2],
                                       INTERP ? 1.0f / (float)kids[my_id] : 0.f);
         }
@@ -363,12 +363,11 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
             const float4 c = s_col[j];
             bool blended = false;
             if (!done) {
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                const float my_alpha = fminf(0.99f, co.w * __expf(power));
+                const float e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
+                const float my_alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(e2));
                 float alpha = my_alpha;
                 if (INTERP) alpha = xy.w * my_alpha + (1.0f - xy.w) * (1.0f - __powf(1.0f - my_alpha, c.w));
-                if (!(power > 0.0f) && !(alpha < 1.0f / 255.0f)) {
+                if (!(e2 > 0.0f) && !(alpha < 1.0f / 255.0f)) {
                     const float test_T = Tt * (1 - alpha);
                     if (test_T < 0.0001f) {
                         done = true;
