@@ -361,27 +361,23 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
             const float4 xy = s_xy[j];
             const float4 co = s_co[j];
             const float4 c = s_col[j];
-            bool blended = false;
-            if (!done) {
-                const float e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
-                const float my_alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(e2));
-                float alpha = my_alpha;
-                if (INTERP) alpha = xy.w * my_alpha + (1.0f - xy.w) * (1.0f - __powf(1.0f - my_alpha, c.w));
-                if (!(e2 > 0.0f) && !(alpha < 1.0f / 255.0f)) {
-                    const float test_T = Tt * (1 - alpha);
-                    if (test_T < 0.0001f) {
-                        done = true;
-                    } else {
-                        C0 += c.x * alpha * Tt;
-                        C1 += c.y * alpha * Tt;
-                        C2 += c.z * alpha * Tt;
-                        if (DEPTH) D += xy.z * alpha * Tt;
-                        Tt = test_T;
-                        last = base - range.x + (uint32_t)j + 1;
-                        blended = true;
-                    }
-                }
-            }
+            // straight-line step: the reference's skip / stop tests become lane predicates
+            const float e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
+            const float my_alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(e2));
+            float alpha = my_alpha;
+            if (INTERP) alpha = xy.w * my_alpha + (1.0f - xy.w) * (1.0f - __powf(1.0f - my_alpha, c.w));
+            const float test_T = Tt * (1 - alpha);
+            const bool valid = !done && !(e2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const bool stop = valid && test_T < 0.0001f;
+            const bool blended = valid && !stop;
+            const float wgt = blended ? alpha * Tt : 0.f;
+            C0 = fmaf(c.x, wgt, C0);
+            C1 = fmaf(c.y, wgt, C1);
+            C2 = fmaf(c.z, wgt, C2);
+            if (DEPTH) D = fmaf(xy.z, wgt, D);
+            Tt = blended ? test_T : Tt;
+            last = blended ? base - range.x + (uint32_t)j + 1 : last;
+            done = done || stop;
             if (__ballot(blended)) seen_mask |= 1ull << j;
         }
         if ((seen_mask >> lane) & 1ull) seen[my_id] = 1;
