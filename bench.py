@@ -7,8 +7,8 @@ SH degree 3 (BASELINE.json configs[1]), one training view per GPU.
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = one view rendered through the public GaussianRasterizer API (forward, including its
-num_rendered host sync), loss = <dL/dcolor, color> + <dL/dinvdepth, invdepth> with fixed synthetic
-upstream gradients, full backward, and -- for N > 1 -- the RCCL all-reduce of every Gaussian gradient
+num_rendered host sync), full backward of fixed synthetic upstream gradients dL/dcolor and dL/dinvdepth
+(fed to autograd directly: the gradient of loss = <dL/dcolor, color> + <dL/dinvdepth, invdepth>), and -- for N > 1 -- the RCCL all-reduce of every Gaussian gradient
 (view-data parallel, weak scaling: each rank renders its own view of its own 1M-Gaussian replica).
 Inputs are synthetic (seeded), resident in HBM before timing starts.  Rank 0 prints one JSON line.
 """
@@ -126,8 +126,7 @@ def main():
         means2D = torch.zeros_like(means3D, requires_grad=True)
         color, radii, invd = rast(means3D=means3D, means2D=means2D, opacities=opac, shs=shs, scales=scales,
                                   rotations=rots)
-        loss = (color * g_col).sum() + (invd * g_inv).sum()
-        loss.backward()
+        torch.autograd.backward([color, invd], [g_col, g_inv])
         if exchange is not None:
             exchange.allreduce()
         return radii

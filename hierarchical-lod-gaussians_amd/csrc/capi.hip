@@ -244,6 +244,7 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     if (rc) return rc;
     info->num_rendered = 0;
     info->max_tile_count = 0;
+    info->rendered = 0;
     if (a->P == 0) return HLGS_OK;
     hipStream_t s = (hipStream_t)stream;
     const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16, T = gx * gy;
@@ -298,6 +299,32 @@ int hlgs_rasterize_forward_render(const hlgs_raster_args* a, const int* radii, v
     launch_blend_fwd(*a, g, im, b, gx, gy, out_color, out_invdepth, seen, s);
     stage_mark(s, ST_BLEND_FWD, false);
     return check_stage(s, a->debug, "blend_fwd");
+}
+
+int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int* radii, void* binning,
+                           size_t binning_bytes, hlgs_frame_info* info, float* out_color, float* out_invdepth,
+                           int* seen, void* stream)
+{
+    int rc = validate(a);
+    if (rc) return rc;
+    info->rendered = 0;
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    if (a->P > 0) HLGS_TRY_HIP(hipMemsetAsync(seen, 0, sizeof(int) * (size_t)a->P, s));
+    if ((rc = hlgs_rasterize_forward_prepare(a, geom, img, radii, info, stream))) return rc;
+    if (a->P == 0 || info->num_rendered == 0) {
+        const size_t HW = (size_t)a->W * a->H;
+        HLGS_TRY_HIP(hipMemsetAsync(out_color, 0, 3 * sizeof(float) * HW, s));
+        if (out_invdepth) HLGS_TRY_HIP(hipMemsetAsync(out_invdepth, 0, sizeof(float) * HW, s));
+        info->rendered = 1;
+        return HLGS_OK;
+    }
+    if (!binning || hlgs_binning_buffer_size(info->num_rendered) > binning_bytes) return HLGS_OK;
+    if ((rc = hlgs_rasterize_forward_render(a, radii, geom, img, binning, info, out_color, out_invdepth, seen,
+                                            stream)))
+        return rc;
+    info->rendered = 1;
+    return HLGS_OK;
 }
 
 int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,

@@ -185,7 +185,14 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
                 const float4 co = s_q[j];
                 const float4 col = s_col[j];
                 const float tt = INTERP ? s_t[j] : 0.f;
-                float acc[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                float acc[10];
+#pragma unroll
+                for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
+                    uint64_t z;
+                    asm volatile("v_mov_b64 %0, 0" : "=v"(z));
+                    acc[v] = __uint_as_float((uint32_t)z);
+                    acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
+                }
                 bool any = false;
 #pragma unroll
                 for (int k = 0; k < 4; k++)

@@ -57,6 +57,9 @@ def _raster_args(bg, render_indices, parent_indices, ts, kids, means3D, colors, 
     return a, keep, P, P_full, M
 
 
+_binning_hint = {}
+
+
 def rasterize_gaussians(bg, render_indices, parent_indices, ts, kids, means3D, colors, opacity, scales, rotations,
                         scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
                         image_width, sh, degree, campos, prefiltered, debug, do_depth):
@@ -69,22 +72,28 @@ def rasterize_gaussians(bg, render_indices, parent_indices, ts, kids, means3D, c
                                     tan_fovy, H, W, sh, degree, campos, prefiltered, debug)
     dev = means3D.device
     f32 = dict(dtype=torch.float32, device=dev)
-    color = torch.zeros((3, H, W), **f32)
-    invdepth = torch.zeros((1, H, W), **f32) if do_depth else torch.zeros((0, H, W), **f32)
-    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
-    seen = torch.zeros((P,), dtype=torch.int32, device=dev)
+    color = torch.empty((3, H, W), **f32)
+    invdepth = torch.empty((1 if do_depth else 0, H, W), **f32)
+    radii = torch.empty((P,), dtype=torch.int32, device=dev)
+    seen = torch.empty((P,), dtype=torch.int32, device=dev)
     u8 = dict(dtype=torch.uint8, device=dev)
     geom = torch.empty((lib.hlgs_geom_buffer_size(P),), **u8)
     img = torch.empty((lib.hlgs_image_buffer_size(W, H),), **u8)
     info = L.FrameInfo()
-    binning = torch.empty((0,), **u8)
-    if P != 0:
-        s = L.stream()
-        L.check(lib.hlgs_rasterize_forward_prepare(C.byref(a), L.ptr(geom), L.ptr(img), L.ptr(radii), C.byref(info), s))
-        binning = torch.empty((lib.hlgs_binning_buffer_size(info.num_rendered),), **u8)
+    # The binning buffer is sized from the largest frame seen on this device (+15%), so prepare and render
+    # run in one library call; a frame that outgrows it gets an exact buffer and a second call.
+    binning = torch.empty((_binning_hint.get(dev, 0),), **u8)
+    s = L.stream()
+    L.check(lib.hlgs_rasterize_forward(C.byref(a), L.ptr(geom), L.ptr(img), L.ptr(radii), L.ptr(binning),
+                                       binning.numel(), C.byref(info), L.ptr(color),
+                                       L.ptr(invdepth) if do_depth else None, L.ptr(seen), s))
+    if not info.rendered:
+        need = lib.hlgs_binning_buffer_size(info.num_rendered)
+        binning = torch.empty((need,), **u8)
         L.check(lib.hlgs_rasterize_forward_render(C.byref(a), L.ptr(radii), L.ptr(geom), L.ptr(img), L.ptr(binning),
                                                   C.byref(info), L.ptr(color), L.ptr(invdepth) if do_depth else None,
                                                   L.ptr(seen), s))
+        _binning_hint[dev] = int(need * 1.15)
     del keep
     return int(info.num_rendered), color, radii, geom, binning, img, invdepth, seen
 

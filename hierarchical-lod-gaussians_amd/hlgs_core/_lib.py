@@ -34,7 +34,7 @@ class Grads(C.Structure):
 
 
 class FrameInfo(C.Structure):
-    _fields_ = [("num_rendered", _i), ("max_tile_count", _i)]
+    _fields_ = [("num_rendered", _i), ("max_tile_count", _i), ("rendered", _i)]
 
 
 _SIGS = {
@@ -47,6 +47,8 @@ _SIGS = {
     "hlgs_rasterize_forward_prepare": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, C.POINTER(FrameInfo), _vp]),
     "hlgs_rasterize_forward_render": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, _vp, C.POINTER(FrameInfo), _vp,
                                            _vp, _vp, _vp]),
+    "hlgs_rasterize_forward": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _sz, C.POINTER(FrameInfo), _vp, _vp,
+                                    _vp, _vp]),
     "hlgs_rasterize_backward": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
                                      C.POINTER(Grads), _vp]),
     "hlgs_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),

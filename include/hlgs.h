@@ -96,18 +96,29 @@ size_t hlgs_backward_scratch_size(int P, int R);
 typedef struct hlgs_frame_info {
     int num_rendered;    /* R: Gaussian/tile instances (the reference's num_rendered) */
     int max_tile_count;  /* longest per-tile list (selects the binning plan) */
+    int rendered;        /* hlgs_rasterize_forward: 1 when phase 2 ran inside the call */
 } hlgs_frame_info;
 
 /* Phase 1: preprocess + scans.  Writes radii (P), fills geom/img and *info (host).  One host
  * synchronisation, as the reference has (rasterizer_impl.cu:330-331). */
 int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* img, int* radii,
                                    hlgs_frame_info* info, void* stream);
-/* Phase 2: binning (per-tile depth sort) + front-to-back blend.  out_color (3,H,W) and out_invdepth
- * (H,W, or NULL when do_depth is off) and seen (P) must be zero-initialised by the caller.  With R == 0
- * this is a no-op (the output stays 0, not bg: rasterizer_impl.cu:332-333). */
+/* Phase 2: binning (per-tile depth sort) + front-to-back blend.  Every pixel of out_color (3,H,W) and
+ * out_invdepth (H,W, or NULL when do_depth is off) is written; seen (P) must be zero-initialised by the
+ * caller.  With R == 0 this is a no-op (the caller's zeroed output stays 0, not bg:
+ * rasterizer_impl.cu:332-333). */
 int hlgs_rasterize_forward_render(const hlgs_raster_args* a, const int* radii, void* geom, void* img,
                                   void* binning, const hlgs_frame_info* info, float* out_color,
                                   float* out_invdepth, int* seen, void* stream);
+/* Both phases in one call, with one host synchronisation and no return to the caller between them:
+ * prepare, then -- when hlgs_binning_buffer_size(num_rendered) <= binning_bytes -- render into
+ * `binning` and set info->rendered = 1.  Otherwise info->rendered = 0 and the caller allocates a
+ * binning buffer of the reported size and calls hlgs_rasterize_forward_render.  seen is cleared here;
+ * out_color / out_invdepth need no initialisation (with R == 0 they are set to 0).
+ * Replaces the forward of RasterizeGaussiansCUDA (rasterize_points.cu:36-139). */
+int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int* radii, void* binning,
+                           size_t binning_bytes, hlgs_frame_info* info, float* out_color, float* out_invdepth,
+                           int* seen, void* stream);
 /* Backward: blend backward (per-tile partial sums, no float atomics) + fused covariance / SH / scale-
  * rotation backward.  dL_dinvdepth may be NULL (rasterize_points.cu:195-201). */
 int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,

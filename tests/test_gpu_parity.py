@@ -110,6 +110,23 @@ def test_backward_is_deterministic():
         np.testing.assert_array_equal(a[k], b[k])
 
 
+def test_binning_capacity_fallback_matches():
+    """One-call forward with a too-small cached binning buffer (second call path), an exact one and an
+    oversized one all give the same frame and the same backward."""
+    from diff_gaussian_rasterization import _C
+    sc, cam = _scene(2500, 2, 160, 120, seed=21)
+    g = S.upstream_grads(160, 120)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    runs = []
+    for hint in (1, 0, 1 << 26):
+        _C._binning_hint[dev] = hint
+        runs.append(gpu_render(sc, cam, grads=g))
+    _C._binning_hint.pop(dev, None)
+    for r in runs[1:]:
+        for k in ("color", "invdepth", "radii", "dmean3D", "dopacity", "d_shs"):
+            np.testing.assert_array_equal(runs[0][k], r[k])
+
+
 def test_mark_visible_and_relocation():
     from diff_gaussian_rasterization import GaussianRasterizer, compute_relocation
     from oracle import oracle as O
