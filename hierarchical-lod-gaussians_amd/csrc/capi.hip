@@ -176,7 +176,7 @@ static int validate(const hlgs_raster_args* a)
         return fail(HLGS_ERR_ARG, "missing required tensor (means3D/opacities/viewmatrix/projmatrix/bg/campos)");
     if (!a->shs && !a->colors_precomp)
         return fail(HLGS_ERR_ARG, "For non-RGB, provide precomputed Gaussian colors!");
-    if (a->shs && a->M <= 0) return fail(HLGS_ERR_ARG, "shs given but M == 0");
+    if (a->shs && (a->M <= 0 || a->M > 16)) return fail(HLGS_ERR_ARG, "shs rows must hold 1..16 coefficients");
     if (!a->cov3D_precomp && (!a->scales || !a->rotations))
         return fail(HLGS_ERR_ARG, "provide scales+rotations or cov3D_precomp");
     if (a->D < 0 || a->D > 3) return fail(HLGS_ERR_ARG, "sh_degree must be in [0,3]");

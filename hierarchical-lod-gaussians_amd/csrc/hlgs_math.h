@@ -233,6 +233,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// One DPP lane permutation of v (ctrl: quad_perm / row_ror / row_bcast encodings).
+template <int CTRL, int ROW, bool BC>
+__device__ __forceinline__ float dpp(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW, 0xF, BC));
+}
+
 // Butterfly reduce-scatter of ten per-lane values over the 64-lane wave.  v_permlane32_swap folds two
 // values at once (rows 0-1 keep the sum of one, rows 2-3 of the other), v_permlane16_swap folds again
 // across row pairs, and four fused row-DPP adds finish inside each 16-lane row: 28 VALU instructions

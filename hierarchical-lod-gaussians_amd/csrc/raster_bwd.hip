@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             o.dopacity[idx] = 0.f;
             o.dmean3D[3 * idx] = 0.f; o.dmean3D[3 * idx + 1] = 0.f; o.dmean3D[3 * idx + 2] = 0.f;
             for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = 0.f;
-            if (o.dsh)
+            if (o.dsh && !a.shs)
                 for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
             o.dscale[3 * idx] = 0.f; o.dscale[3 * idx + 1] = 0.f; o.dscale[3 * idx + 2] = 0.f;
             reinterpret_cast<float4*>(o.drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -351,91 +351,10 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     d2.z = (proj[8] * m_w - proj[11] * mul1) * s0 + (proj[9] * m_w - proj[11] * mul2) * s1;
     dmean = add(dmean, d2);
 
-    // ---- SH backward (backward.cu:23-142)
-    if (a.shs) {
-        const int deg = a.D;
-        const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
-        const f3 dir_orig = sub(m, campos);
-        const float len = sqrtf(dot(dir_orig, dir_orig));
-        const f3 dir = mk(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
-        const float* sh = a.shs + (size_t)idx * M3;
-        auto SHV = [&](int c) { return mk(sh[3 * c], sh[3 * c + 1], sh[3 * c + 2]); };
-        const uint32_t cl = g.clamped[t_idx];
-        f3 dRGB = mk(s6, s7, s8);
-        dRGB.x *= (cl & 1u) ? 0 : 1;
-        dRGB.y *= (cl & 2u) ? 0 : 1;
-        dRGB.z *= (cl & 4u) ? 0 : 1;
-        f3 ddx = mk(0, 0, 0), ddy = mk(0, 0, 0), ddz = mk(0, 0, 0);
-        const float x = dir.x, y = dir.y, z = dir.z;
-        float* dsh = o.dsh + (size_t)idx * M3;
-        int written = 1;
-        auto PUT = [&](int c, float s) {
-            const f3 v = scl(s, dRGB);
-            dsh[3 * c] = v.x; dsh[3 * c + 1] = v.y; dsh[3 * c + 2] = v.z;
-        };
-        PUT(0, kSH_C0);
-        if (deg > 0) {
-            PUT(1, -kSH_C1 * y);
-            PUT(2, kSH_C1 * z);
-            PUT(3, -kSH_C1 * x);
-            written = 4;
-            ddx = scl(-kSH_C1, SHV(3));
-            ddy = scl(-kSH_C1, SHV(1));
-            ddz = scl(kSH_C1, SHV(2));
-            if (deg > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                PUT(4, kSH_C2[0] * xy);
-                PUT(5, kSH_C2[1] * yz);
-                PUT(6, kSH_C2[2] * (2.f * zz - xx - yy));
-                PUT(7, kSH_C2[3] * xz);
-                PUT(8, kSH_C2[4] * (xx - yy));
-                written = 9;
-                ddx = add(ddx, add(add(add(scl(kSH_C2[0] * y, SHV(4)), scl(kSH_C2[2] * 2.f * -x, SHV(6))),
-                                       scl(kSH_C2[3] * z, SHV(7))), scl(kSH_C2[4] * 2.f * x, SHV(8))));
-                ddy = add(ddy, add(add(add(scl(kSH_C2[0] * x, SHV(4)), scl(kSH_C2[1] * z, SHV(5))),
-                                       scl(kSH_C2[2] * 2.f * -y, SHV(6))), scl(kSH_C2[4] * 2.f * -y, SHV(8))));
-                ddz = add(ddz, add(add(scl(kSH_C2[1] * y, SHV(5)), scl(kSH_C2[2] * 2.f * 2.f * z, SHV(6))),
-                                   scl(kSH_C2[3] * x, SHV(7))));
-                if (deg > 2) {
-                    PUT(9, kSH_C3[0] * y * (3.f * xx - yy));
-                    PUT(10, kSH_C3[1] * xy * z);
-                    PUT(11, kSH_C3[2] * y * (4.f * zz - xx - yy));
-                    PUT(12, kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy));
-                    PUT(13, kSH_C3[4] * x * (4.f * zz - xx - yy));
-                    PUT(14, kSH_C3[5] * z * (xx - yy));
-                    PUT(15, kSH_C3[6] * x * (xx - 3.f * yy));
-                    written = 16;
-                    f3 sx = scl(2.f * xy, scl(3.f, scl(kSH_C3[0], SHV(9))));
-                    sx = add(sx, scl(yz, scl(kSH_C3[1], SHV(10))));
-                    sx = add(sx, scl(xy, scl(-2.f, scl(kSH_C3[2], SHV(11)))));
-                    sx = add(sx, scl(2.f * xz, scl(-3.f, scl(kSH_C3[3], SHV(12)))));
-                    sx = add(sx, scl(-3.f * xx + 4.f * zz - yy, scl(kSH_C3[4], SHV(13))));
-                    sx = add(sx, scl(xz, scl(2.f, scl(kSH_C3[5], SHV(14)))));
-                    sx = add(sx, scl(xx - yy, scl(3.f, scl(kSH_C3[6], SHV(15)))));
-                    ddx = add(ddx, sx);
-                    f3 sy = scl(xx - yy, scl(3.f, scl(kSH_C3[0], SHV(9))));
-                    sy = add(sy, scl(xz, scl(kSH_C3[1], SHV(10))));
-                    sy = add(sy, scl(-3.f * yy + 4.f * zz - xx, scl(kSH_C3[2], SHV(11))));
-                    sy = add(sy, scl(2.f * yz, scl(-3.f, scl(kSH_C3[3], SHV(12)))));
-                    sy = add(sy, scl(xy, scl(-2.f, scl(kSH_C3[4], SHV(13)))));
-                    sy = add(sy, scl(yz, scl(-2.f, scl(kSH_C3[5], SHV(14)))));
-                    sy = add(sy, scl(2.f * xy, scl(-3.f, scl(kSH_C3[6], SHV(15)))));
-                    ddy = add(ddy, sy);
-                    f3 sz = scl(xy, scl(kSH_C3[1], SHV(10)));
-                    sz = add(sz, scl(2.f * yz, scl(4.f, scl(kSH_C3[2], SHV(11)))));
-                    sz = add(sz, scl(2.f * zz - xx - yy, scl(3.f, scl(kSH_C3[3], SHV(12)))));
-                    sz = add(sz, scl(2.f * xz, scl(4.f, scl(kSH_C3[4], SHV(13)))));
-                    sz = add(sz, scl(xx - yy, scl(kSH_C3[5], SHV(14))));
-                    ddz = add(ddz, sz);
-                }
-            }
-        }
-        for (int i = 3 * written; i < M3; i++) dsh[i] = 0.f;
-        const f3 dL_ddir = mk(dot(ddx, dRGB), dot(ddy, dRGB), dot(ddz, dRGB));
-        dmean = add(dmean, dnormvdv(dir_orig, dL_ddir));
-    } else if (o.dsh) {
+    // ---- SH backward (backward.cu:23-142) runs in k_sh_bwd, which adds its view-direction term to
+    //      dmean3D (or to the parent-deferred share) after this kernel.
+    if (!a.shs && o.dsh)
         for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
-    }
 
     // ---- cov3D backward (backward.cu:330-393)
     float dscale[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
@@ -478,8 +397,6 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             rec.parent_dmean[3 * t_idx + 1] = (1.0f - tt) * dmean.y;
             rec.parent_dmean[3 * t_idx + 2] = (1.0f - tt) * dmean.z;
             dmean = mk(0.f, 0.f, 0.f);
-            if (o.dsh)
-                for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
         }
     }
     o.dopacity[idx] = dop_out;
@@ -491,6 +408,99 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     o.dscale[3 * idx + 1] = dscale[1];
     o.dscale[3 * idx + 2] = dscale[2];
     reinterpret_cast<float4*>(o.drot)[idx] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+}
+
+// Basis function c of the reference's SH colour (forward.cu:20-67) and its gradient with respect to the
+// normalised view direction (the dRGBdx/dy/dz terms of backward.cu:55-139, per coefficient).
+__device__ __forceinline__ float sh_basis(int c, float x, float y, float z, float& gx, float& gy, float& gz)
+{
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    gx = gy = gz = 0.f;
+    switch (c) {
+    case 0: return kSH_C0;
+    case 1: gy = -kSH_C1; return -kSH_C1 * y;
+    case 2: gz = kSH_C1; return kSH_C1 * z;
+    case 3: gx = -kSH_C1; return -kSH_C1 * x;
+    case 4: gx = kSH_C2[0] * y; gy = kSH_C2[0] * x; return kSH_C2[0] * xy;
+    case 5: gy = kSH_C2[1] * z; gz = kSH_C2[1] * y; return kSH_C2[1] * yz;
+    case 6: gx = kSH_C2[2] * 2.f * -x; gy = kSH_C2[2] * 2.f * -y; gz = kSH_C2[2] * 2.f * 2.f * z;
+            return kSH_C2[2] * (2.f * zz - xx - yy);
+    case 7: gx = kSH_C2[3] * z; gz = kSH_C2[3] * x; return kSH_C2[3] * xz;
+    case 8: gx = kSH_C2[4] * 2.f * x; gy = kSH_C2[4] * 2.f * -y; return kSH_C2[4] * (xx - yy);
+    case 9: gx = kSH_C3[0] * 3.f * 2.f * xy; gy = kSH_C3[0] * 3.f * (xx - yy); return kSH_C3[0] * y * (3.f * xx - yy);
+    case 10: gx = kSH_C3[1] * yz; gy = kSH_C3[1] * xz; gz = kSH_C3[1] * xy; return kSH_C3[1] * xy * z;
+    case 11: gx = kSH_C3[2] * -2.f * xy; gy = kSH_C3[2] * (-3.f * yy + 4.f * zz - xx); gz = kSH_C3[2] * 4.f * 2.f * yz;
+             return kSH_C3[2] * y * (4.f * zz - xx - yy);
+    case 12: gx = kSH_C3[3] * -3.f * 2.f * xz; gy = kSH_C3[3] * -3.f * 2.f * yz;
+             gz = kSH_C3[3] * 3.f * (2.f * zz - xx - yy); return kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+    case 13: gx = kSH_C3[4] * (-3.f * xx + 4.f * zz - yy); gy = kSH_C3[4] * -2.f * xy; gz = kSH_C3[4] * 4.f * 2.f * xz;
+             return kSH_C3[4] * x * (4.f * zz - xx - yy);
+    case 14: gx = kSH_C3[5] * 2.f * xz; gy = kSH_C3[5] * -2.f * yz; gz = kSH_C3[5] * (xx - yy);
+             return kSH_C3[5] * z * (xx - yy);
+    default: gx = kSH_C3[6] * 3.f * (xx - yy); gy = kSH_C3[6] * -3.f * 2.f * xy; return kSH_C3[6] * x * (xx - 3.f * yy);
+    }
+}
+
+// SH backward (backward.cu:23-142), one 16-lane row per Gaussian and one lane per coefficient: the
+// coefficient rows are read and dsh written as contiguous 16-lane runs, and the view-direction gradient
+// sum_c (sh_c . dRGB) * dB_c/ddir is a 16-lane DPP row reduction.  Runs after k_gauss_bwd, whose dcolor
+// output is dL/dRGB, and adds dnormvdv(.) to dmean3D -- or, for a hierarchy child with a parent, (1 - t)
+// of it to the parent-deferred share (backward.cu:458-494).
+template <bool HIER>
+__global__ void __launch_bounds__(256) k_sh_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
+                                                BwdScratch rec, hlgs_grads o)
+{
+    const int t_idx = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int c = threadIdx.x & 15;
+    if (t_idx >= a.P) return;  // whole rows leave together
+    const int idx = HIER ? a.indices[t_idx] : t_idx;
+    const int M = a.M;
+    const bool lane_has = c < M;
+    float* dsh = o.dsh + (size_t)idx * M * 3;
+    const bool vis = radii[t_idx] > 0;
+    const bool dropped = HIER && a.parent_indices && a.parent_indices[t_idx] != -1;
+    if (!vis) {
+        if (!HIER && lane_has) { dsh[3 * c] = 0.f; dsh[3 * c + 1] = 0.f; dsh[3 * c + 2] = 0.f; }
+        return;
+    }
+    const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+    const f3 m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    const f3 dir_orig = sub(m, campos);
+    const float len = sqrtf(dot(dir_orig, dir_orig));
+    const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+    const uint32_t cl = g.clamped[t_idx];
+    const float dR = (cl & 1u) ? 0.f : o.dcolor[3 * idx];
+    const float dG = (cl & 2u) ? 0.f : o.dcolor[3 * idx + 1];
+    const float dB = (cl & 4u) ? 0.f : o.dcolor[3 * idx + 2];
+    const int ncoef = (a.D + 1) * (a.D + 1);
+    float gx = 0.f, gy = 0.f, gz = 0.f, basis = 0.f, proj = 0.f;
+    if (lane_has && c < ncoef) {
+        basis = sh_basis(c, x, y, z, gx, gy, gz);
+        const float* sh = a.shs + (size_t)idx * M * 3 + 3 * c;
+        proj = sh[0] * dR + sh[1] * dG + sh[2] * dB;
+    }
+    if (lane_has && !dropped) {
+        dsh[3 * c] = basis * dR;
+        dsh[3 * c + 1] = basis * dG;
+        dsh[3 * c + 2] = basis * dB;
+    }
+    float vx = proj * gx, vy = proj * gy, vz = proj * gz;
+    vx += dpp<0xB1, 0xF, true>(vx); vy += dpp<0xB1, 0xF, true>(vy); vz += dpp<0xB1, 0xF, true>(vz);
+    vx += dpp<0x4E, 0xF, true>(vx); vy += dpp<0x4E, 0xF, true>(vy); vz += dpp<0x4E, 0xF, true>(vz);
+    vx += dpp<0x124, 0xF, true>(vx); vy += dpp<0x124, 0xF, true>(vy); vz += dpp<0x124, 0xF, true>(vz);
+    vx += dpp<0x128, 0xF, true>(vx); vy += dpp<0x128, 0xF, true>(vy); vz += dpp<0x128, 0xF, true>(vz);
+    if (c != 0) return;
+    const f3 d = dnormvdv(dir_orig, mk(vx, vy, vz));
+    if (dropped) {
+        const float w = 1.0f - a.ts[t_idx];
+        rec.parent_dmean[3 * t_idx] += w * d.x;
+        rec.parent_dmean[3 * t_idx + 1] += w * d.y;
+        rec.parent_dmean[3 * t_idx + 2] += w * d.z;
+    } else {
+        o.dmean3D[3 * idx] += d.x;
+        o.dmean3D[3 * idx + 1] += d.y;
+        o.dmean3D[3 * idx + 2] += d.z;
+    }
 }
 
 __global__ void __launch_bounds__(256) k_parent_mean_add(int P, const int* __restrict__ radii,
@@ -523,14 +533,16 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
 {
     const float fy = a.H / (2.0f * a.tanfovy);
     const float fx = a.W / (2.0f * a.tanfovx);
-    const dim3 grid((a.P + 255) / 256);
+    const dim3 grid((a.P + 255) / 256), grid_sh((a.P + 15) / 16);
     if (a.indices) {
         hipLaunchKernelGGL(k_gauss_bwd<true>, grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
+        if (a.shs) hipLaunchKernelGGL(k_sh_bwd<true>, grid_sh, dim3(256), 0, s, a, radii, g, rs, o);
         if (a.parent_indices)
             hipLaunchKernelGGL(k_parent_mean_add, grid, dim3(256), 0, s, a.P, radii, a.parent_indices,
                                rs.parent_dmean, o.dmean3D);
     } else {
         hipLaunchKernelGGL(k_gauss_bwd<false>, grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
+        if (a.shs) hipLaunchKernelGGL(k_sh_bwd<false>, grid_sh, dim3(256), 0, s, a, radii, g, rs, o);
     }
 }
 
