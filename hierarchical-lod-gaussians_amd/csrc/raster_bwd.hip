@@ -441,66 +441,117 @@ __device__ __forceinline__ float sh_basis(int c, float x, float y, float z, floa
     }
 }
 
-// SH backward (backward.cu:23-142), one 16-lane row per Gaussian and one lane per coefficient: the
-// coefficient rows are read and dsh written as contiguous 16-lane runs, and the view-direction gradient
-// sum_c (sh_c . dRGB) * dB_c/ddir is a 16-lane DPP row reduction.  Runs after k_gauss_bwd, whose dcolor
-// output is dL/dRGB, and adds dnormvdv(.) to dmean3D -- or, for a hierarchy child with a parent, (1 - t)
-// of it to the parent-deferred share (backward.cu:458-494).
-template <bool HIER>
-__global__ void __launch_bounds__(256) k_sh_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
-                                                BwdScratch rec, hlgs_grads o)
+// Copy n rows of M3 floats between global memory (row r at base + rows[r] * M3) and LDS (row r at
+// lds + r * kShStride) with all 64 lanes on consecutive floats / float4s of the block's rows.
+constexpr int kShStride = 49;  // odd stride: the per-thread row walks hit 64 distinct banks
+template <int M3T, bool TO_LDS>  // M3T = 0: row length m3 known only at run time
+__device__ __forceinline__ void sh_rows_copy(float* gbase, float* lds, const int* rows, int n, int lane, int m3)
 {
-    const int t_idx = blockIdx.x * 16 + (threadIdx.x >> 4);
-    const int c = threadIdx.x & 15;
-    if (t_idx >= a.P) return;  // whole rows leave together
-    const int idx = HIER ? a.indices[t_idx] : t_idx;
-    const int M = a.M;
-    const bool lane_has = c < M;
-    float* dsh = o.dsh + (size_t)idx * M * 3;
-    const bool vis = radii[t_idx] > 0;
-    const bool dropped = HIER && a.parent_indices && a.parent_indices[t_idx] != -1;
-    if (!vis) {
-        if (!HIER && lane_has) { dsh[3 * c] = 0.f; dsh[3 * c + 1] = 0.f; dsh[3 * c + 2] = 0.f; }
-        return;
-    }
-    const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
-    const f3 m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-    const f3 dir_orig = sub(m, campos);
-    const float len = sqrtf(dot(dir_orig, dir_orig));
-    const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
-    const uint32_t cl = g.clamped[t_idx];
-    const float dR = (cl & 1u) ? 0.f : o.dcolor[3 * idx];
-    const float dG = (cl & 2u) ? 0.f : o.dcolor[3 * idx + 1];
-    const float dB = (cl & 4u) ? 0.f : o.dcolor[3 * idx + 2];
-    const int ncoef = (a.D + 1) * (a.D + 1);
-    float gx = 0.f, gy = 0.f, gz = 0.f, basis = 0.f, proj = 0.f;
-    if (lane_has && c < ncoef) {
-        basis = sh_basis(c, x, y, z, gx, gy, gz);
-        const float* sh = a.shs + (size_t)idx * M * 3 + 3 * c;
-        proj = sh[0] * dR + sh[1] * dG + sh[2] * dB;
-    }
-    if (lane_has && !dropped) {
-        dsh[3 * c] = basis * dR;
-        dsh[3 * c + 1] = basis * dG;
-        dsh[3 * c + 2] = basis * dB;
-    }
-    float vx = proj * gx, vy = proj * gy, vz = proj * gz;
-    vx += dpp<0xB1, 0xF, true>(vx); vy += dpp<0xB1, 0xF, true>(vy); vz += dpp<0xB1, 0xF, true>(vz);
-    vx += dpp<0x4E, 0xF, true>(vx); vy += dpp<0x4E, 0xF, true>(vy); vz += dpp<0x4E, 0xF, true>(vz);
-    vx += dpp<0x124, 0xF, true>(vx); vy += dpp<0x124, 0xF, true>(vy); vz += dpp<0x124, 0xF, true>(vz);
-    vx += dpp<0x128, 0xF, true>(vx); vy += dpp<0x128, 0xF, true>(vy); vz += dpp<0x128, 0xF, true>(vz);
-    if (c != 0) return;
-    const f3 d = dnormvdv(dir_orig, mk(vx, vy, vz));
-    if (dropped) {
-        const float w = 1.0f - a.ts[t_idx];
-        rec.parent_dmean[3 * t_idx] += w * d.x;
-        rec.parent_dmean[3 * t_idx + 1] += w * d.y;
-        rec.parent_dmean[3 * t_idx + 2] += w * d.z;
+    const int M3 = M3T ? M3T : m3;
+    if constexpr (M3T > 0 && M3T % 4 == 0) {
+        constexpr int M3 = M3T;
+        constexpr int Q = M3 / 4;
+        for (int f = lane; f < n * Q; f += 64) {
+            const int r = f / Q, q = f - r * Q;
+            float4* gp = reinterpret_cast<float4*>(gbase + (size_t)rows[r] * M3) + q;
+            float* lp = lds + r * kShStride + 4 * q;
+            if (TO_LDS) {
+                const float4 v = *gp;
+                lp[0] = v.x; lp[1] = v.y; lp[2] = v.z; lp[3] = v.w;
+            } else {
+                *gp = make_float4(lp[0], lp[1], lp[2], lp[3]);
+            }
+        }
     } else {
-        o.dmean3D[3 * idx] += d.x;
-        o.dmean3D[3 * idx + 1] += d.y;
-        o.dmean3D[3 * idx + 2] += d.z;
+        for (int f = lane; f < n * M3; f += 64) {
+            const int r = f / M3, q = f - r * M3;
+            float* gp = gbase + (size_t)rows[r] * M3 + q;
+            if (TO_LDS) lds[r * kShStride + q] = *gp;
+            else *gp = lds[r * kShStride + q];
+        }
     }
+}
+
+// SH backward (backward.cu:23-142), one thread per Gaussian.  The wave's 64 coefficient rows are staged
+// through LDS so global reads of shs and writes of dsh are contiguous float4 runs; each thread then
+// walks its own LDS row (coefficient loop unrolled at compile time), writes its dsh row in place and
+// the wave stores the rows back.  Runs after k_gauss_bwd, whose dcolor output is dL/dRGB, and adds
+// dnormvdv(dir, dL/ddir) to dmean3D -- or, for a hierarchy child with a parent, (1 - t) of it to the
+// parent-deferred share (backward.cu:458-494).
+template <bool HIER, int MT>  // MT = 0: coefficient count a.M known only at run time (up to 16)
+__global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
+                                               BwdScratch rec, hlgs_grads o)
+{
+    constexpr int MC = MT ? MT : 16;
+    const int M = MT ? MT : a.M;
+    const int M3 = 3 * M;
+    __shared__ float s_rows[64 * kShStride];
+    __shared__ int s_idx[64];
+    const int lane = threadIdx.x;
+    const int t0 = blockIdx.x * 64;
+    const int n = min(64, a.P - t0);
+    const int t_idx = t0 + lane;
+    const bool active = lane < n;
+    const int idx = active ? (HIER ? a.indices[t_idx] : t_idx) : 0;
+    s_idx[lane] = idx;
+    __syncthreads();
+    sh_rows_copy<3 * MT, true>(const_cast<float*>(a.shs), s_rows, s_idx, n, lane, M3);
+    __syncthreads();
+    float* row = s_rows + lane * kShStride;
+    if (active) {
+        const bool vis = radii[t_idx] > 0;
+        const bool dropped = HIER && a.parent_indices && a.parent_indices[t_idx] != -1;
+        if (!vis) {
+#pragma unroll
+            for (int i = 0; i < 3 * MC; i++)
+                if (i < M3) row[i] = 0.f;
+        } else {
+            const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+            const f3 m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+            const f3 dir_orig = sub(m, campos);
+            const float len = sqrtf(dot(dir_orig, dir_orig));
+            const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+            const uint32_t cl = g.clamped[t_idx];
+            const float dR = (cl & 1u) ? 0.f : o.dcolor[3 * idx];
+            const float dG = (cl & 2u) ? 0.f : o.dcolor[3 * idx + 1];
+            const float dB = (cl & 4u) ? 0.f : o.dcolor[3 * idx + 2];
+            const int ncoef = (a.D + 1) * (a.D + 1);
+            float vx = 0.f, vy = 0.f, vz = 0.f;
+            float basis[MC];
+#pragma unroll
+            for (int c = 0; c < MC; c++) {
+                float gx, gy, gz;
+                basis[c] = c < ncoef ? sh_basis(c, x, y, z, gx, gy, gz) : 0.f;
+                if (c > 0 && c < ncoef) {
+                    const float proj = row[3 * c] * dR + row[3 * c + 1] * dG + row[3 * c + 2] * dB;
+                    vx += proj * gx;
+                    vy += proj * gy;
+                    vz += proj * gz;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < MC; c++) {
+                if (c >= M) break;
+                const float bs = dropped ? 0.f : basis[c];
+                row[3 * c] = bs * dR;
+                row[3 * c + 1] = bs * dG;
+                row[3 * c + 2] = bs * dB;
+            }
+            const f3 d = dnormvdv(dir_orig, mk(vx, vy, vz));
+            if (dropped) {
+                const float w = 1.0f - a.ts[t_idx];
+                rec.parent_dmean[3 * t_idx] += w * d.x;
+                rec.parent_dmean[3 * t_idx + 1] += w * d.y;
+                rec.parent_dmean[3 * t_idx + 2] += w * d.z;
+            } else {
+                o.dmean3D[3 * idx] += d.x;
+                o.dmean3D[3 * idx + 1] += d.y;
+                o.dmean3D[3 * idx + 2] += d.z;
+            }
+        }
+    }
+    __syncthreads();
+    sh_rows_copy<3 * MT, false>(o.dsh, s_rows, s_idx, n, lane, M3);
 }
 
 __global__ void __launch_bounds__(256) k_parent_mean_add(int P, const int* __restrict__ radii,
@@ -533,17 +584,26 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
 {
     const float fy = a.H / (2.0f * a.tanfovy);
     const float fx = a.W / (2.0f * a.tanfovx);
-    const dim3 grid((a.P + 255) / 256), grid_sh((a.P + 15) / 16);
+    const dim3 grid((a.P + 255) / 256), grid_sh((a.P + 63) / 64);
+#define HLGS_SHB(H)                                                                                        \
+    switch (a.M) {                                                                                         \
+    case 1: hipLaunchKernelGGL((k_sh_bwd<H, 1>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;      \
+    case 4: hipLaunchKernelGGL((k_sh_bwd<H, 4>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;      \
+    case 9: hipLaunchKernelGGL((k_sh_bwd<H, 9>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;      \
+    case 16: hipLaunchKernelGGL((k_sh_bwd<H, 16>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;   \
+    default: hipLaunchKernelGGL((k_sh_bwd<H, 0>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;     \
+    }
     if (a.indices) {
         hipLaunchKernelGGL(k_gauss_bwd<true>, grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
-        if (a.shs) hipLaunchKernelGGL(k_sh_bwd<true>, grid_sh, dim3(256), 0, s, a, radii, g, rs, o);
+        if (a.shs) HLGS_SHB(true)
         if (a.parent_indices)
             hipLaunchKernelGGL(k_parent_mean_add, grid, dim3(256), 0, s, a.P, radii, a.parent_indices,
                                rs.parent_dmean, o.dmean3D);
     } else {
         hipLaunchKernelGGL(k_gauss_bwd<false>, grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
-        if (a.shs) hipLaunchKernelGGL(k_sh_bwd<false>, grid_sh, dim3(256), 0, s, a, radii, g, rs, o);
+        if (a.shs) HLGS_SHB(false)
     }
+#undef HLGS_SHB
 }
 
 }  // namespace hlgs

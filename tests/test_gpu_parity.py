@@ -110,6 +110,14 @@ def test_backward_is_deterministic():
         np.testing.assert_array_equal(a[k], b[k])
 
 
+def test_sh_rows_with_unusual_coefficient_count():
+    """shs rows of 6 coefficients at degree 1 (not a square count): the generic SH paths."""
+    sc, cam = _scene(1800, 2, 96, 80, seed=33)
+    sc["shs"] = np.ascontiguousarray(sc["shs"][:, :6])
+    sc["sh_degree"] = 1
+    _compare(sc, cam)
+
+
 def test_binning_capacity_fallback_matches():
     """One-call forward with a too-small cached binning buffer (second call path), an exact one and an
     oversized one all give the same frame and the same backward."""
