@@ -10,6 +10,7 @@ namespace hlgs {
 
 constexpr int kScanItems = 2048;    // elements per scan block (256 threads x 8)
 constexpr int kSortCap = 4096;      // largest per-tile list sorted in one LDS pass
+constexpr int kWaveSortCap = 1024;  // longest per-tile list sorted in registers by one wave
 constexpr size_t kAlign = 256;
 constexpr int kBinThreads = 1024;   // LDS-histogram binning: threads per block
 constexpr int kBinGauss = 4096;     // Gaussians per binning block

@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
     const int tile = xcd_remap(blockIdx.x, T);
     const uint2 r = ranges[tile];
     const uint32_t cnt = r.y - r.x;
-    if (cnt == 0) return;
+    if (cnt <= (uint32_t)kWaveSortCap) return;  // sorted by k_tile_sort_wave
     const int tid = threadIdx.x;
     const bool big = cnt > (uint32_t)kSortCap;
     for (uint32_t c0 = 0; c0 < cnt; c0 += kSortCap) {
@@ -273,6 +273,73 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
             for (uint32_t i = tid; i < n; i += 256) point_list[r.x + c0 + i] = (uint32_t)s[i];
         __syncthreads();
     }
+}
+
+// Per-tile sort of up to 64 * KPL keys by one wave, entirely in registers: lane l holds elements
+// l * KPL .. l * KPL + KPL - 1; bitonic stages with partner distance < KPL are compare-exchanges inside
+// a lane, longer ones exchange with lane l ^ (j / KPL).  No LDS, no barriers.
+template <int KPL>
+__device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list,
+                                               uint32_t base, uint32_t n, int lane)
+{
+    constexpr uint32_t NP = 64u * KPL;
+    uint64_t v[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; i++) {
+        const uint32_t e = (uint32_t)lane * KPL + i;
+        v[i] = e < n ? keys[base + e] : ~0ull;
+    }
+#pragma unroll
+    for (uint32_t kk = 2; kk <= NP; kk <<= 1) {
+#pragma unroll
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= (uint32_t)KPL) {
+                const int pl = (int)(j / KPL);
+                const bool lower = (lane & pl) == 0;
+#pragma unroll
+                for (int i = 0; i < KPL; i++) {
+                    const uint32_t e = (uint32_t)lane * KPL + i;
+                    const bool asc = (e & kk) == 0;
+                    const uint64_t y = __shfl_xor(v[i], pl, 64);
+                    const bool take_min = lower == asc;
+                    v[i] = take_min ? (y < v[i] ? y : v[i]) : (y > v[i] ? y : v[i]);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < KPL; i++) {
+                    if (i & j) continue;
+                    const int k = i | (int)j;
+                    const uint32_t e = (uint32_t)lane * KPL + i;
+                    const bool asc = (e & kk) == 0;
+                    const uint64_t x = v[i], y = v[k];
+                    const bool sw = (x > y) == asc;
+                    v[i] = sw ? y : x;
+                    v[k] = sw ? x : y;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < KPL; i++) {
+        const uint32_t e = (uint32_t)lane * KPL + i;
+        if (e < n) point_list[base + e] = (uint32_t)v[i];
+    }
+}
+
+// Tiles of up to kWaveSortCap instances: one wave each (k_tile_sort handles the longer ones).
+__global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__ ranges, uint64_t* keys,
+                                                       uint32_t* __restrict__ point_list, int T)
+{
+    const int tile = xcd_remap(blockIdx.x, T);
+    const uint2 r = ranges[tile];
+    const uint32_t n = r.y - r.x;
+    const int lane = threadIdx.x;
+    if (n == 0 || n > (uint32_t)kWaveSortCap) return;
+    if (n <= 64) wave_sort_tile<1>(keys, point_list, r.x, n, lane);
+    else if (n <= 128) wave_sort_tile<2>(keys, point_list, r.x, n, lane);
+    else if (n <= 256) wave_sort_tile<4>(keys, point_list, r.x, n, lane);
+    else if (n <= 512) wave_sort_tile<8>(keys, point_list, r.x, n, lane);
+    else wave_sort_tile<16>(keys, point_list, r.x, n, lane);
 }
 
 // Merge pass for long tiles: element of run r finds its rank in the partner run by binary search.
@@ -480,7 +547,9 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
                            im.tile_cursor, b.keys, gx, gy);
     if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
-    hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, b.keys, b.point_list, T);
+    hipLaunchKernelGGL(k_tile_sort_wave, dim3(T), dim3(64), 0, s, im.ranges, b.keys, b.point_list, T);
+    if (max_count > (uint32_t)kWaveSortCap)
+        hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, b.keys, b.point_list, T);
     if (max_count > (uint32_t)kSortCap) {
         uint64_t* src = b.keys;
         uint64_t* dst = b.keys2;
