@@ -225,6 +225,37 @@ __device__ __forceinline__ bool touches_quad(float x, float y, float4 co, float 
     return x + ex >= qx && x - ex <= qx + 7.f && y + ey >= qy && y - ey <= qy + 7.f;
 }
 
+// Copy n rows of M3 floats between global memory (row r at base + rows[r] * M3) and LDS (row r at
+// lds + r * kShStride) with all 64 lanes on consecutive floats / float4s of the block's rows.
+constexpr int kShStride = 49;  // odd stride: the per-thread row walks hit 64 distinct banks
+template <int M3T, bool TO_LDS>  // M3T = 0: row length m3 known only at run time
+__device__ __forceinline__ void sh_rows_copy(float* gbase, float* lds, const int* rows, int n, int lane, int m3)
+{
+    const int M3 = M3T ? M3T : m3;
+    if constexpr (M3T > 0 && M3T % 4 == 0) {
+        constexpr int M3 = M3T;
+        constexpr int Q = M3 / 4;
+        for (int f = lane; f < n * Q; f += 64) {
+            const int r = f / Q, q = f - r * Q;
+            float4* gp = reinterpret_cast<float4*>(gbase + (size_t)rows[r] * M3) + q;
+            float* lp = lds + r * kShStride + 4 * q;
+            if (TO_LDS) {
+                const float4 v = *gp;
+                lp[0] = v.x; lp[1] = v.y; lp[2] = v.z; lp[3] = v.w;
+            } else {
+                *gp = make_float4(lp[0], lp[1], lp[2], lp[3]);
+            }
+        }
+    } else {
+        for (int f = lane; f < n * M3; f += 64) {
+            const int r = f / M3, q = f - r * M3;
+            float* gp = gbase + (size_t)rows[r] * M3 + q;
+            if (TO_LDS) lds[r * kShStride + q] = *gp;
+            else *gp = lds[r * kShStride + q];
+        }
+    }
+}
+
 // Bijective XCD-aware block remap (cdna_hip_programming.md section 5): consecutive logical blocks
 // land on the same XCD so neighbouring tiles share that XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg)

@@ -18,21 +18,26 @@ def _tree(n=600, sky=0, seed=0):
     return S.make_dynamic_hierarchy(S.make_gaussians(n, 3, cam, seed=seed), skybox_points=sky, seed=seed), cam
 
 
-def test_point_list_and_ranges_bit_exact():
+@pytest.mark.parametrize("P,W,H,band", [(300, 200, 120, 64), (5000, 200, 120, 256), (12000, 200, 120, 512),
+                                        (30000, 200, 120, 1024), (60000, 128, 128, 4096)])
+def test_point_list_and_ranges_bit_exact(P, W, H, band):
+    """Tile lists across every sort path: one-wave register sorts of 64..1024 keys and the block sort."""
     from diff_gaussian_rasterization import _C
-    cam = S.make_camera(200, 120)
-    sc = S.make_gaussians(5000, 1, cam, seed=11)
+    cam = S.make_camera(W, H)
+    sc = S.make_gaussians(P, 1, cam, seed=11)
     sc["means3D"][::7, 2] = 9.0  # depth ties
     fr = O.forward(dict(sc), S.cam_numpy(cam))
+    counts = fr.ranges[:, 1] - fr.ranges[:, 0]
+    assert counts.max() <= band and (band == 64 or counts.max() > band // 2), counts.max()
     t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
     e = torch.empty(0, device=DEV)
     out = _C.rasterize_gaussians(cam["bg"], e, e, e, e, t(sc["means3D"]), e, t(sc["opacities"]), t(sc["scales"]),
                                  t(sc["rotations"]), 1.0, e, cam["viewmatrix"], cam["projmatrix"], cam["tanfovx"],
-                                 cam["tanfovy"], 120, 200, t(sc["shs"]), 1, cam["campos"], False, True, True)
+                                 cam["tanfovy"], H, W, t(sc["shs"]), 1, cam["campos"], False, True, True)
     R = out[0]
     assert R == fr.R
     pl = _C.inspect_point_list(out[4], R).cpu().numpy().astype(np.uint32)
-    rg = _C.inspect_ranges(out[5], 200, 120).cpu().numpy().astype(np.uint32)
+    rg = _C.inspect_ranges(out[5], W, H).cpu().numpy().astype(np.uint32)
     np.testing.assert_array_equal(rg, fr.ranges)
     np.testing.assert_array_equal(pl, fr.point_list[:R])
     np.testing.assert_array_equal(out[7].cpu().numpy(), fr.seen)
