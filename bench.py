@@ -45,6 +45,25 @@ def algorithmic_bytes(stage, P, V, R, N, T, M, D):
     }[stage]
 
 
+STAGE_KERNEL = {"preprocess": "k_preprocess", "count_tiles": "k_count_tiles", "scatter": "k_scatter_keys",
+                "tile_sort": "k_tile_sort", "tile_ranges": "k_tile_ranges", "blend_fwd": "k_blend_fwd",
+                "blend_bwd": "k_blend_bwd", "gauss_bwd": "k_gauss_bwd"}
+
+
+def pmc_traffic(stage):
+    """Per-launch HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) of the stage's kernel from the latest committed
+    rocprofv3 PMC profile (tools/profile_round.sh + tools/summarize_profile.py), or None."""
+    prof = os.path.join(ROOT, "profiles")
+    rounds = sorted(d for d in os.listdir(prof) if os.path.exists(os.path.join(prof, d, "pmc_traffic.json"))) \
+        if os.path.isdir(prof) else []
+    if not rounds or stage not in STAGE_KERNEL:
+        return None, None
+    path = os.path.join(prof, rounds[-1], "pmc_traffic.json")
+    ks = json.load(open(path))["kernels"]
+    hits = [v["hbm_bytes"] for k, v in ks.items() if STAGE_KERNEL[stage] in k]
+    return (sum(hits) if hits else None), os.path.relpath(path, ROOT)
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -175,8 +194,9 @@ def main():
             stage_report[name] = dict(ms=round(ms, 4), calls=calls, alg_GBs=round(b / (ms * 1e-3) / 1e9, 1))
         dom = max(stage_report, key=lambda k: stage_report[k]["ms"])
         ach = stage_report[dom]["alg_GBs"]
+        traffic, src = pmc_traffic(dom)
         roofline = dict(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                        traffic=None, kernel=dom)
+                        traffic=traffic, traffic_unit="bytes/launch", traffic_source=src, kernel=dom)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(P, deg, W, H)

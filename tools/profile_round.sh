@@ -1,0 +1,17 @@
+# Round profile: bench under rocprofv3 kernel-trace/stats, then FETCH_SIZE and WRITE_SIZE in their own
+# passes (never combined with sys/runtime traces).  Summaries land in gpurun_out/round/; copy with
+# tools/summarize_profile.py into profiles/<round>/.
+set -eu
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/round
+mkdir -p $O
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 > $O/bench_line.log 2>&1
+echo "trace ok"
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-stage-timing > $O/fetch.log 2>&1
+echo "fetch ok"
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-stage-timing > $O/write.log 2>&1
+echo "write ok"
+timeout -k 10 300 python3 bench.py > $O/bench_plain.log 2>&1
+echo "plain ok"
+tail -1 $O/bench_plain.log

@@ -1,0 +1,53 @@
+"""Copy a tools/profile_round.sh run into profiles/<round>/: rocprofv3 kernel stats, the bench JSON line,
+and per-launch HBM traffic of every hlgs kernel from the FETCH_SIZE / WRITE_SIZE passes.
+
+FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KiB.  On gfx950 FETCH_SIZE counts half the bytes of
+wide coalesced reads (MI355X_MICROARCH.md, HBM section), so fetched bytes are taken as 2 x FETCH_SIZE;
+WRITE_SIZE is used as is.  Both count L2->fabric traffic, so Infinity-Cache hits are included.
+
+    python tools/summarize_profile.py gpurun_out/round profiles/r01
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def per_kernel(path, counter):
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = r["Kernel_Name"].split("(")[0]
+        if "hlgs::" in name:
+            vals[name].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "bench_kernel_stats.csv"))
+    dom = os.path.join(src, "trace", "run_domain_stats.csv")
+    if os.path.exists(dom):
+        shutil.copy(dom, os.path.join(dst, "bench_domain_stats.csv"))
+    line = open(os.path.join(src, "bench_plain.log")).read().strip().splitlines()[-1]
+    json.loads(line)
+    open(os.path.join(dst, "bench_line.json"), "w").write(line + "\n")
+    traced = open(os.path.join(src, "bench_line.log")).read().strip().splitlines()[-1]
+    open(os.path.join(dst, "bench_line_under_rocprof.json"), "w").write(traced + "\n")
+    fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f = 2 * 1024 * fetch.get(k, 0.0)
+        w = 1024 * write.get(k, 0.0)
+        out[k] = dict(fetch_bytes=round(f), write_bytes=round(w), hbm_bytes=round(f + w))
+    json.dump(dict(note="per launch; fetch = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE; KiB -> bytes",
+                   kernels=out), open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
