@@ -69,11 +69,10 @@ Geom carve_geom(void* base, int P, size_t* total)
     g.clamped = take<uint32_t>(p, P);
     g.means2D = take<float2>(p, P);
     g.cov3D = take<float>(p, 6 * (size_t)P);
-    g.conic_opacity = take<float4>(p, P);
-    g.rgb = take<float>(p, 3 * (size_t)P);
     g.tiles_touched = take<uint32_t>(p, P);
     g.point_offsets = take<uint32_t>(p, P);
     g.rects = take<int2>(p, P);
+    g.splat = take<float4>(p, 4 * (size_t)P);
     g.scan_tmp = take<uint32_t>(p, scan_scratch_elems(P));
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return g;

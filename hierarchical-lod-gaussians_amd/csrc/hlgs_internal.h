@@ -26,13 +26,18 @@ struct Geom {
     uint32_t* clamped;        // P, bit c = colour channel c clamped at 0
     float2* means2D;          // P, pixel-space centre
     float* cov3D;             // P x 6
-    float4* conic_opacity;    // P
-    float* rgb;               // P x 3
     uint32_t* tiles_touched;  // P
     uint32_t* point_offsets;  // P, inclusive scan of tiles_touched
     int2* rects;              // P, per-axis 3-sigma extent in pixels
+    float4* splat;            // P x 4: the blend kernels' per-Gaussian record (see SplatRec)
     uint32_t* scan_tmp;
 };
+
+// 64-byte per-Gaussian record read by the blend kernels: one half cache line per (tile, Gaussian)
+// instance instead of one line per attribute array.
+//   [0] x, y, conic.a, conic.b      [1] conic.c, opacity, r, g
+//   [2] b, 1/depth, t, 1/num_kids    [3] record-slot base (bits), first tile x, first tile y, rect width (bits)
+// [3].x = point_offsets - tiles_touched is written by the scatter, after the scan; the rest by the preprocess.
 Geom carve_geom(void* base, int P, size_t* total);
 
 // Per-pixel / per-tile state (ImageState, rasterizer_impl.h:47-54) plus binning counters.

@@ -94,11 +94,10 @@ __device__ __forceinline__ void finish_record(const float* m, float4 co, float d
 template <bool INTERP, bool DEPTH>
 __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
                                                   int W, int H, int gx, int gy, int T, Geom g,
-                                                  const float* __restrict__ colors, const float* __restrict__ final_Ts,
+                                                  const float* __restrict__ final_Ts,
                                                   const uint32_t* __restrict__ n_contrib, const float* __restrict__ bg,
                                                   const float* __restrict__ dL_dpixels,
-                                                  const float* __restrict__ dL_dinvdepths, const float* __restrict__ ts,
-                                                  const int* __restrict__ kids, BwdScratch rec)
+                                                  const float* __restrict__ dL_dinvdepths, BwdScratch rec)
 {
     __shared__ float4 s_xy[64];   // x, y, 1/depth, quadrant mask bits
     __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
@@ -154,19 +153,17 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
         if (lane_valid) {
             const uint32_t pos = range.x + li_top - lane;
             const uint32_t id = point_list[pos];
-            const float2 xy = g.means2D[id];
-            const float4 co = g.conic_opacity[id];
-            const uint32_t qm = quad_mask(xy.x, xy.y, co, tx0, ty0);
-            s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1.f / g.depths[id] : 0.f, __uint_as_float(qm));
+            const float4* sr = g.splat + 4 * (size_t)id;
+            const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
+            const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
+            const uint32_t qm = quad_mask(r0.x, r0.y, co, tx0, ty0);
+            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, __uint_as_float(qm));
             s_q[lane] = conic_q(co);
             my_co = co;
-            s_col[lane] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2],
-                                      INTERP ? 1.0f / (float)kids[id] : 0.f);
-            if (INTERP) s_t[lane] = ts[id];
-            const int2 ext = g.rects[id];
-            int x0, y0, x1, y1;
-            tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
-            slot = g.point_offsets[id] - g.tiles_touched[id] + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
+            s_col[lane] = make_float4(r1.z, r1.w, r2.x, INTERP ? r2.w : 0.f);
+            if (INTERP) s_t[lane] = r2.z;
+            const int x0 = __float_as_int(r3.y), y0 = __float_as_int(r3.z), w = __float_as_int(r3.w);
+            slot = __float_as_uint(r3.x) + (uint32_t)((ty - y0) * w + (tx - x0));
         }
 #pragma unroll
         for (int v = 0; v < 10; v++) s_m[64 * v + lane] = 0.f;
@@ -538,11 +535,10 @@ void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
                       int gx, int gy, const float* dL_dpix, const float* dL_dinv, hipStream_t s)
 {
     const int T = gx * gy;
-    const float* colors = a.colors_precomp ? a.colors_precomp : g.rgb;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
 #define HLGS_BB(I, Dp)                                                                                              \
     hipLaunchKernelGGL((k_blend_bwd<I, Dp>), dim3(T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, \
-                       colors, im.final_T, im.n_contrib, a.bg, dL_dpix, dL_dinv, a.ts, a.kids, rs)
+                       im.final_T, im.n_contrib, a.bg, dL_dpix, dL_dinv, rs)
     if (interp) { if (dL_dinv) HLGS_BB(true, true); else HLGS_BB(true, false); }
     else { if (dL_dinv) HLGS_BB(false, true); else HLGS_BB(false, false); }
 #undef HLGS_BB

@@ -110,7 +110,10 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
     const uint32_t area = (uint32_t)(x1 - x0) * (uint32_t)(y1 - y0);
     if (area == 0) return;
 
-    if (a.colors_precomp == nullptr) {
+    f3 col;
+    if (a.colors_precomp) {
+        col = mk(a.colors_precomp[3 * t_idx], a.colors_precomp[3 * t_idx + 1], a.colors_precomp[3 * t_idx + 2]);
+    } else {
         const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
         const f3 mean_r = mk(a.means3D[3 * r_idx], a.means3D[3 * r_idx + 1], a.means3D[3 * r_idx + 2]);
         const float* sc = a.shs + (size_t)r_idx * a.M * 3;
@@ -128,17 +131,24 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
             }, mean_r, campos, cb);
         }
         g.clamped[t_idx] = cb;
-        g.rgb[3 * t_idx] = rgb.x;
-        g.rgb[3 * t_idx + 1] = rgb.y;
-        g.rgb[3 * t_idx + 2] = rgb.z;
+        col = rgb;
     }
     g.depths[t_idx] = p_view.z;
     radii[t_idx] = (int)my_radius;
     g.means2D[t_idx] = make_float2(pix_x, pix_y);
     float opacity = a.opacities[r_idx];
     if (HIER && use_parent) opacity = t * opacity + (1.0f - t) * a.opacities[p_idx];
-    g.conic_opacity[t_idx] = make_float4(conic_x, conic_y, conic_z, opacity * h_scale);
     g.tiles_touched[t_idx] = area;
+    {
+        const float cr = col.x, cg = col.y, cbl = col.z;
+        const bool interp = a.ts && a.kids;
+        float4* rec = g.splat + 4 * (size_t)t_idx;
+        rec[0] = make_float4(pix_x, pix_y, conic_x, conic_y);
+        rec[1] = make_float4(conic_z, opacity * h_scale, cr, cg);
+        rec[2] = make_float4(cbl, 1.f / p_view.z, interp ? a.ts[t_idx] : 0.f,
+                             interp ? 1.0f / (float)a.kids[t_idx] : 0.f);
+        rec[3] = make_float4(0.f, __int_as_float(x0), __int_as_float(y0), __int_as_float(x1 - x0));
+    }
     if (tile_count)  // only when the tile grid is too large for the LDS-histogram binning
         for (int y = y0; y < y1; y++)
             for (int x = x0; x < x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
@@ -192,6 +202,12 @@ __global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const i
     uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
     uint32_t* s_rank = s_hist + T; // per-tile running rank
     for (int t = threadIdx.x; t < T; t += kBinThreads) { s_cnt[t] = 0; s_rank[t] = 0; }
+    {
+        const int g0 = blockIdx.x * kBinGauss, g1 = min(P, g0 + kBinGauss);
+        for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += kBinThreads)
+            if (radii[idx] > 0)
+                g.splat[4 * (size_t)idx + 3].x = __uint_as_float(g.point_offsets[idx] - g.tiles_touched[idx]);
+    }
     __syncthreads();
     for_each_instance(P, radii, g, gx, gy, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
     __syncthreads();
@@ -226,6 +242,7 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
 {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= P || radii[idx] <= 0) return;
+    g.splat[4 * (size_t)idx + 3].x = __uint_as_float(g.point_offsets[idx] - g.tiles_touched[idx]);
     const float2 xy = g.means2D[idx];
     const int2 ext = g.rects[idx];
     int x0, y0, x1, y1;
@@ -380,11 +397,8 @@ __global__ void __launch_bounds__(256) k_merge_runs(const uint2* __restrict__ ra
 // ------------------------------------------------------------------------------------------------
 template <bool INTERP, bool DEPTH>
 __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
-                                                  int W, int H, int gx, int T, const float2* __restrict__ means2D,
-                                                  const float* __restrict__ features,
-                                                  const float4* __restrict__ conic_opacity,
-                                                  const float* __restrict__ depths, const float* __restrict__ ts,
-                                                  const int* __restrict__ kids, float* __restrict__ final_T,
+                                                  int W, int H, int gx, int T, const float4* __restrict__ splat,
+                                                  float* __restrict__ final_T,
                                                   uint32_t* __restrict__ n_contrib, const float* __restrict__ bg,
                                                   float* __restrict__ out_color, float* __restrict__ out_invdepth,
                                                   int* __restrict__ seen)
@@ -411,13 +425,13 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
         bool hit = false;
         if (pos < range.y) {
             my_id = point_list[pos];
-            const float2 xy = means2D[my_id];
-            const float4 co = conic_opacity[my_id];
-            hit = touches_quad(xy.x, xy.y, co, fqx, fqy);
-            s_xy[lane] = make_float4(xy.x, xy.y, DEPTH ? 1 / depths[my_id] : 0.f, INTERP ? ts[my_id] : 0.f);
+            const float4* rec = splat + 4 * (size_t)my_id;
+            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+            const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
+            hit = touches_quad(r0.x, r0.y, co, fqx, fqy);
+            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, INTERP ? r2.z : 0.f);
             s_co[lane] = conic_q(co);
-            s_col[lane] = make_float4(features[3 * my_id], features[3 * my_id + 1], features[3 * my_id + 2],
-                                      INTERP ? 1.0f / (float)kids[my_id] : 0.f);
+            s_col[lane] = make_float4(r1.z, r1.w, r2.x, INTERP ? r2.w : 0.f);
         }
         uint64_t todo = __ballot(hit);
         __syncthreads();
@@ -567,13 +581,11 @@ void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
                       float* out_color, float* out_invdepth, int* seen, hipStream_t s)
 {
     const int T = gx * gy;
-    const float* feat = a.colors_precomp ? a.colors_precomp : g.rgb;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     const bool depth = out_invdepth != nullptr;
 #define HLGS_BLEND(I, Dp)                                                                                       \
     hipLaunchKernelGGL((k_blend_fwd<I, Dp>), dim3(4 * T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, T, \
-                       g.means2D, feat, g.conic_opacity, g.depths, a.ts, a.kids, im.final_T, im.n_contrib, a.bg,   \
-                       out_color, out_invdepth, seen)
+                       g.splat, im.final_T, im.n_contrib, a.bg, out_color, out_invdepth, seen)
     if (interp) { if (depth) HLGS_BLEND(true, true); else HLGS_BLEND(true, false); }
     else { if (depth) HLGS_BLEND(false, true); else HLGS_BLEND(false, false); }
 #undef HLGS_BLEND
