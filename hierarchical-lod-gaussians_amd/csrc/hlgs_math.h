@@ -173,28 +173,59 @@ __device__ __forceinline__ f3 dnormvdv(f3 v, f3 dv)
     return r;
 }
 
-// Conservative 4-bit mask of the 8x8 quadrants of the tile at (x0, y0) that can contain a pixel where
-// this splat reaches alpha >= 1/255.  alpha = min(0.99, o * exp(power)) >= 1/255 needs
-// d^T Q d <= 2 ln(255 o) (Q = conic), an ellipse whose half-extents are sqrt(2 ln(255 o) Q^-1_xx|yy).
-// Pairs outside are exactly the ones the reference skips (forward.cu:539-561, backward.cu:614-643);
-// the kids-alpha of hierarchy mode is never larger than alpha, so the mask stays conservative there.
-// Margins absorb the float rounding of power/exp.
+// Which 8x8 pixel blocks can hold a pixel where this splat reaches alpha >= 1/255?
+// alpha = min(0.99, o * exp(power)) >= 1/255 needs Q(u, v) = a u^2 + 2 b u v + c v^2 <= 2 ln(255 o) for
+// (u, v) = pixel - centre (Q = conic).  The minimum of the convex Q over a block's box is 0 when the
+// centre is inside, else the smallest of the four edge minima (vertex of the 1-D quadratic clamped to
+// the edge).  Pairs outside are exactly the ones the reference skips (forward.cu:539-561,
+// backward.cu:614-643); the kids-alpha of hierarchy mode is never larger than alpha, so the test stays
+// conservative there.  Margins absorb the float rounding of power/exp.
+struct SplatFoot {
+    float x, y, a, b, c, kv, ku, t;  // kv = -b/c, ku = -b/a, t = threshold on Q
+    int mode;                        // 0: test, 1: always (non-finite / degenerate), 2: never
+};
+__device__ __forceinline__ SplatFoot splat_foot(float x, float y, float4 co)
+{
+    SplatFoot f;
+    f.x = x; f.y = y; f.a = co.x; f.b = co.y; f.c = co.z;
+    f.kv = f.ku = f.t = 0.f;
+    f.mode = 0;
+    const float o = co.w;
+    if (o != o || co.x != co.x || co.y != co.y || co.z != co.z || x != x || y != y) { f.mode = 1; return f; }
+    if (o < (1.0f / 255.0f) * 0.999f) { f.mode = 2; return f; }
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.f) || !(co.x > 0.f) || !(co.z > 0.f)) { f.mode = 1; return f; }
+    f.t = fmaxf(2.0f * logf(255.0f * o), 0.f) * 1.002f + 2e-3f;
+    f.kv = -co.y / co.z;
+    f.ku = -co.y / co.x;
+    return f;
+}
+__device__ __forceinline__ float q_edge_u(const SplatFoot& f, float U, float v0, float v1)  // u = U fixed
+{
+    const float v = __builtin_amdgcn_fmed3f(f.kv * U, v0, v1);
+    return U * fmaf(f.a, U, 2.f * f.b * v) + f.c * v * v;
+}
+__device__ __forceinline__ float q_edge_v(const SplatFoot& f, float V, float u0, float u1)  // v = V fixed
+{
+    const float u = __builtin_amdgcn_fmed3f(f.ku * V, u0, u1);
+    return V * fmaf(f.c, V, 2.f * f.b * u) + f.a * u * u;
+}
+__device__ __forceinline__ bool foot_touches(const SplatFoot& f, float qx, float qy)
+{
+    if (f.mode) return f.mode == 1;
+    const float u0 = qx - f.x, u1 = u0 + 7.f, v0 = qy - f.y, v1 = v0 + 7.f;
+    if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return true;
+    const float m = fminf(fminf(q_edge_u(f, u0, v0, v1), q_edge_u(f, u1, v0, v1)),
+                          fminf(q_edge_v(f, v0, u0, u1), q_edge_v(f, v1, u0, u1)));
+    return m <= f.t;
+}
 __device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, int x0, int y0)
 {
-    const float o = co.w;
-    if (o != o || co.x != co.x || co.y != co.y || co.z != co.z) return 0xFu;
-    if (o < (1.0f / 255.0f) * 0.999f) return 0u;
-    const float det = co.x * co.z - co.y * co.y;
-    if (!(det > 0.f) || !(co.x > 0.f) || !(co.z > 0.f)) return 0xFu;
-    const float t = fmaxf(2.0f * logf(255.0f * o), 0.f) * 1.002f + 1e-3f;
-    const float ex = sqrtf(t * co.z / det) * 1.001f + 0.01f;
-    const float ey = sqrtf(t * co.x / det) * 1.001f + 0.01f;
+    const SplatFoot f = splat_foot(x, y, co);
     uint32_t m = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const float qx = (float)(x0 + 8 * (q & 1)), qy = (float)(y0 + 8 * (q >> 1));
-        if (x + ex >= qx && x - ex <= qx + 7.f && y + ey >= qy && y - ey <= qy + 7.f) m |= 1u << q;
-    }
+    for (int q = 0; q < 4; q++)
+        if (foot_touches(f, (float)(x0 + 8 * (q & 1)), (float)(y0 + 8 * (q >> 1)))) m |= 1u << q;
     return m;
 }
 
@@ -214,15 +245,7 @@ __device__ __forceinline__ float splat_e2(float4 q, float dx, float dy)
 // Does the alpha >= 1/255 footprint of a splat (see quad_mask) reach the 8x8 pixel block at (qx, qy)?
 __device__ __forceinline__ bool touches_quad(float x, float y, float4 co, float qx, float qy)
 {
-    const float o = co.w;
-    if (o != o || co.x != co.x || co.y != co.y || co.z != co.z) return true;
-    if (o < (1.0f / 255.0f) * 0.999f) return false;
-    const float det = co.x * co.z - co.y * co.y;
-    if (!(det > 0.f) || !(co.x > 0.f) || !(co.z > 0.f)) return true;
-    const float t = fmaxf(2.0f * logf(255.0f * o), 0.f) * 1.002f + 1e-3f;
-    const float ex = sqrtf(t * co.z / det) * 1.001f + 0.01f;
-    const float ey = sqrtf(t * co.x / det) * 1.001f + 0.01f;
-    return x + ex >= qx && x - ex <= qx + 7.f && y + ey >= qy && y - ey <= qy + 7.f;
+    return foot_touches(splat_foot(x, y, co), qx, qy);
 }
 
 // Copy n rows of M3 floats between global memory (row r at base + rows[r] * M3) and LDS (row r at
