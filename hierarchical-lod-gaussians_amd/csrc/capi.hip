@@ -5,6 +5,7 @@
 //
 // Re-entrancy: no device memory is allocated here and no scratch is static; every buffer is passed
 // in.  The only process-wide state is the opt-in stage-timing instrumentation used by bench.py.
+#include <algorithm>
 #include <stdio.h>
 #include <string.h>
 
@@ -20,9 +21,9 @@ void launch_tile_ranges(const Img& im, int T, hipStream_t s);
 bool lds_binning(int gx, int gy);
 void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, hipStream_t s);
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
-                    int gy, uint32_t max_count, hipStream_t s, bool timing);
+                    int gy, uint32_t max_count, hipStream_t s, bool timing, Guard gd);
 void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, int gx, int gy,
-                      float* out_color, float* out_invdepth, int* seen, hipStream_t s);
+                      float* out_color, float* out_invdepth, int* seen, hipStream_t s, Guard gd);
 void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, const BwdScratch& rs,
                       int gx, int gy, const float* dL_dpix, const float* dL_dinv, hipStream_t s);
 void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
@@ -99,9 +100,9 @@ Bin carve_bin(void* base, int R, size_t* total)
 {
     char* p = static_cast<char*>(base);
     Bin b;
+    b.point_list = take<uint32_t>(p, R);  // first: its offset does not depend on R
     b.keys = take<uint64_t>(p, R);
     b.keys2 = take<uint64_t>(p, R);
-    b.point_list = take<uint32_t>(p, R);
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return b;
 }
@@ -236,16 +237,10 @@ size_t hlgs_image_ranges_offset(int W, int H)
     return (size_t)im.ranges;
 }
 
-int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* img, int* radii,
-                                   hlgs_frame_info* info, void* stream)
+namespace hlgs {
+// Phase 1 without the host read-back: preprocess, tile counts, scans, tile ranges (misc = R, longest list).
+static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int* radii, hipStream_t s)
 {
-    int rc = validate(a);
-    if (rc) return rc;
-    info->num_rendered = 0;
-    info->max_tile_count = 0;
-    info->rendered = 0;
-    if (a->P == 0) return HLGS_OK;
-    hipStream_t s = (hipStream_t)stream;
     const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16, T = gx * gy;
     Geom g = carve_geom(aligned(geom), a->P, nullptr);
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
@@ -261,6 +256,7 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
         launch_count_tiles(a->P, radii, g, im.tile_count, gx, gy, s);
         stage_mark(s, ST_COUNT_TILES, false);
     }
+    int rc;
     if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
     stage_mark(s, ST_SCAN, true);
     scan_inclusive_u32(g.tiles_touched, g.point_offsets, (size_t)a->P, g.scan_tmp, s);
@@ -269,7 +265,68 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     scan_inclusive_u32(im.tile_count, im.tile_cursor, (size_t)T, im.scan_tmp, s);
     launch_tile_ranges(im, T, s);
     stage_mark(s, ST_RANGES, false);
-    if ((rc = check_stage(s, a->debug, "scan"))) return rc;
+    return check_stage(s, a->debug, "scan");
+}
+
+static int render_launch(const hlgs_raster_args* a, const int* radii, void* geom, void* img, void* binning, int R_carve,
+                         uint32_t max_count, float* out_color, float* out_invdepth, int* seen, hipStream_t s, Guard gd)
+{
+    const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16;
+    Geom g = carve_geom(aligned(geom), a->P, nullptr);
+    Img im = carve_img(aligned(img), a->W, a->H, nullptr);
+    Bin b = carve_bin(aligned(binning), R_carve, nullptr);
+    hipGetLastError();
+    launch_binning(*a, radii, g, im, b, gx, gy, max_count, s, g_timing, gd);
+    int rc;
+    if ((rc = check_stage(s, a->debug, "binning"))) return rc;
+    stage_mark(s, ST_BLEND_FWD, true);
+    launch_blend_fwd(*a, g, im, b, gx, gy, out_color, out_invdepth, seen, s, gd);
+    stage_mark(s, ST_BLEND_FWD, false);
+    return check_stage(s, a->debug, "blend_fwd");
+}
+
+// Largest R whose binning layout fits in `bytes`.
+static int binning_capacity(size_t bytes)
+{
+    if (bytes <= 4 * kAlign) return 0;
+    long r = (long)((bytes - 4 * kAlign) / 20);
+    while (r > 0 && hlgs_binning_buffer_size((int)r) > bytes) r--;
+    return (int)std::min<long>(r, 0x7fffffff);
+}
+
+// Pinned read-back slot and event for the speculative forward, per thread and device.
+struct Readback {
+    uint32_t* host = nullptr;
+    hipEvent_t ev = nullptr;
+    uint32_t last_maxc = 0;  // longest tile list of the previous frame (plans the speculative sort)
+};
+static int readback_for(hipStream_t s, Readback** out)
+{
+    static thread_local Readback rb[64];
+    int dev = 0;
+    HLGS_TRY_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(HLGS_ERR_DEVICE, "device index out of range");
+    Readback& r = rb[dev];
+    if (!r.host) HLGS_TRY_HIP(hipHostMalloc((void**)&r.host, 16 * sizeof(uint32_t), hipHostMallocDefault));
+    if (!r.ev) HLGS_TRY_HIP(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
+    (void)s;
+    *out = &r;
+    return HLGS_OK;
+}
+}  // namespace hlgs
+
+int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* img, int* radii,
+                                   hlgs_frame_info* info, void* stream)
+{
+    int rc = validate(a);
+    if (rc) return rc;
+    info->num_rendered = 0;
+    info->max_tile_count = 0;
+    info->rendered = 0;
+    if (a->P == 0) return HLGS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if ((rc = prepare_launch(a, geom, img, radii, s))) return rc;
+    Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     uint32_t misc[2];
     HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipStreamSynchronize(s));
@@ -286,18 +343,8 @@ int hlgs_rasterize_forward_render(const hlgs_raster_args* a, const int* radii, v
     if (rc) return rc;
     const int R = info->num_rendered;
     if (a->P == 0 || R == 0) return HLGS_OK;  // rasterizer_impl.cu:332-333: output stays 0
-    hipStream_t s = (hipStream_t)stream;
-    const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16;
-    Geom g = carve_geom(aligned(geom), a->P, nullptr);
-    Img im = carve_img(aligned(img), a->W, a->H, nullptr);
-    Bin b = carve_bin(aligned(binning), R, nullptr);
-    hipGetLastError();
-    launch_binning(*a, radii, g, im, b, gx, gy, (uint32_t)info->max_tile_count, s, g_timing);
-    if ((rc = check_stage(s, a->debug, "binning"))) return rc;
-    stage_mark(s, ST_BLEND_FWD, true);
-    launch_blend_fwd(*a, g, im, b, gx, gy, out_color, out_invdepth, seen, s);
-    stage_mark(s, ST_BLEND_FWD, false);
-    return check_stage(s, a->debug, "blend_fwd");
+    return render_launch(a, radii, geom, img, binning, R, (uint32_t)info->max_tile_count, out_color, out_invdepth,
+                         seen, (hipStream_t)stream, Guard{nullptr, 0u, 0u});
 }
 
 int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int* radii, void* binning,
@@ -306,22 +353,50 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
 {
     int rc = validate(a);
     if (rc) return rc;
+    info->num_rendered = 0;
+    info->max_tile_count = 0;
     info->rendered = 0;
     hipStream_t s = (hipStream_t)stream;
     hipGetLastError();
-    if (a->P > 0) HLGS_TRY_HIP(hipMemsetAsync(seen, 0, sizeof(int) * (size_t)a->P, s));
-    if ((rc = hlgs_rasterize_forward_prepare(a, geom, img, radii, info, stream))) return rc;
-    if (a->P == 0 || info->num_rendered == 0) {
-        const size_t HW = (size_t)a->W * a->H;
+    const size_t HW = (size_t)a->W * a->H;
+    if (a->P == 0) {
         HLGS_TRY_HIP(hipMemsetAsync(out_color, 0, 3 * sizeof(float) * HW, s));
         if (out_invdepth) HLGS_TRY_HIP(hipMemsetAsync(out_invdepth, 0, sizeof(float) * HW, s));
         info->rendered = 1;
         return HLGS_OK;
     }
-    if (!binning || hlgs_binning_buffer_size(info->num_rendered) > binning_bytes) return HLGS_OK;
-    if ((rc = hlgs_rasterize_forward_render(a, radii, geom, img, binning, info, out_color, out_invdepth, seen,
-                                            stream)))
+    HLGS_TRY_HIP(hipMemsetAsync(seen, 0, sizeof(int) * (size_t)a->P, s));
+    if ((rc = prepare_launch(a, geom, img, radii, s))) return rc;
+    Readback* rb;
+    if ((rc = readback_for(s, &rb))) return rc;
+    Img im = carve_img(aligned(img), a->W, a->H, nullptr);
+    HLGS_TRY_HIP(hipMemcpyAsync(rb->host, im.misc, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HLGS_TRY_HIP(hipEventRecord(rb->ev, s));
+    // Queue the render before knowing R: it is sized for the caller's buffer and for lists the one-wave and
+    // block sorts handle; the kernels exit at once if the frame exceeds either (Guard).
+    const int capR = binning ? binning_capacity(binning_bytes) : 0;
+    const bool spec = capR > 0;
+    const uint32_t cap_n = rb->last_maxc <= (uint32_t)kWaveSortCap ? (uint32_t)kWaveSortCap : (uint32_t)kSortCap;
+    if (spec && (rc = render_launch(a, radii, geom, img, binning, capR, cap_n, out_color, out_invdepth, seen, s,
+                                    Guard{im.misc, (uint32_t)capR, cap_n})))
         return rc;
+    HLGS_TRY_HIP(hipEventSynchronize(rb->ev));
+    const uint32_t R = rb->host[0], maxc = rb->host[1];
+    rb->last_maxc = maxc;
+    info->num_rendered = (int)R;
+    info->max_tile_count = (int)maxc;
+    if (R == 0) {  // rasterizer_impl.cu:332-333: the output stays 0 (not bg)
+        HLGS_TRY_HIP(hipMemsetAsync(out_color, 0, 3 * sizeof(float) * HW, s));
+        if (out_invdepth) HLGS_TRY_HIP(hipMemsetAsync(out_invdepth, 0, sizeof(float) * HW, s));
+        info->rendered = 1;
+        return HLGS_OK;
+    }
+    if (R > (uint32_t)capR) return HLGS_OK;  // caller allocates hlgs_binning_buffer_size(R), calls _render
+    if (!spec || maxc > cap_n) {
+        if ((rc = render_launch(a, radii, geom, img, binning, capR, maxc, out_color, out_invdepth, seen, s,
+                                Guard{nullptr, 0u, 0u})))
+            return rc;
+    }
     info->rendered = 1;
     return HLGS_OK;
 }

@@ -70,6 +70,17 @@ struct BwdScratch {
 };
 BwdScratch carve_bwd(void* base, int P, int R, size_t* total);
 
+// Speculative render (hlgs_rasterize_forward): the render kernels are queued before the host has read
+// R and the longest tile list; each exits at once when they exceed what the launch was sized for.
+struct Guard {
+    const uint32_t* misc;  // Img::misc (R, longest list) or nullptr = no check
+    uint32_t cap_R, cap_n;
+};
+__device__ __forceinline__ bool guard_fail(const Guard& gd)
+{
+    return gd.misc && (gd.misc[0] > gd.cap_R || gd.misc[1] > gd.cap_n);
+}
+
 // scan.hip
 void scan_inclusive_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp, hipStream_t s);
 

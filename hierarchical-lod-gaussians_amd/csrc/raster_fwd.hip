@@ -195,8 +195,9 @@ __global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* _
 // irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
 __global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
-                                                                  uint64_t* __restrict__ keys, int gx, int gy)
+                                                                  uint64_t* __restrict__ keys, int gx, int gy, Guard gd)
 {
+    if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     const int T = gx * gy;
     uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
@@ -238,8 +239,9 @@ __global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict_
 // One thread per Gaussian: drop (depth, index) keys into each touched tile's segment.
 __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restrict__ radii, Geom g,
                                                       const uint2* __restrict__ ranges, uint32_t* cursor,
-                                                      uint64_t* __restrict__ keys, int gx, int gy)
+                                                      uint64_t* __restrict__ keys, int gx, int gy, Guard gd)
 {
+    if (guard_fail(gd)) return;
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= P || radii[idx] <= 0) return;
     g.splat[4 * (size_t)idx + 3].x = __uint_as_float(g.point_offsets[idx] - g.tiles_touched[idx]);
@@ -259,8 +261,9 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
 // One 256-thread block per tile: bitonic sort of the tile's keys in LDS.  Tiles longer than kSortCap
 // are sorted in kSortCap runs here and merged by k_merge_runs.
 __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ranges, uint64_t* keys,
-                                                   uint32_t* __restrict__ point_list, int T)
+                                                   uint32_t* __restrict__ point_list, int T, Guard gd)
 {
+    if (guard_fail(gd)) return;
     __shared__ uint64_t s[kSortCap];
     const int tile = xcd_remap(blockIdx.x, T);
     const uint2 r = ranges[tile];
@@ -345,8 +348,9 @@ __device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ keys, uint
 
 // Tiles of up to kWaveSortCap instances: one wave each (k_tile_sort handles the longer ones).
 __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__ ranges, uint64_t* keys,
-                                                       uint32_t* __restrict__ point_list, int T)
+                                                       uint32_t* __restrict__ point_list, int T, Guard gd)
 {
+    if (guard_fail(gd)) return;
     const int tile = xcd_remap(blockIdx.x, T);
     const uint2 r = ranges[tile];
     const uint32_t n = r.y - r.x;
@@ -401,8 +405,9 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
                                                   float* __restrict__ final_T,
                                                   uint32_t* __restrict__ n_contrib, const float* __restrict__ bg,
                                                   float* __restrict__ out_color, float* __restrict__ out_invdepth,
-                                                  int* __restrict__ seen)
+                                                  int* __restrict__ seen, Guard gd)
 {
+    if (guard_fail(gd)) return;
     __shared__ float4 s_xy[64];   // x, y, 1/depth, interpolation t
     __shared__ float4 s_co[64];   // conic_q, opacity
     __shared__ float4 s_col[64];  // r, g, b, 1/kids
@@ -549,21 +554,22 @@ void launch_tile_ranges(const Img& im, int T, hipStream_t s)
 }
 
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b,
-                    int gx, int gy, uint32_t max_count, hipStream_t s, bool timing)
+                    int gx, int gy, uint32_t max_count, hipStream_t s, bool timing, Guard gd)
 {
     const int T = gx * gy;
     if (timing) stage_mark(s, 3, true);
     if (lds_binning(gx, gy)) {
         allow_big_lds();
         hipLaunchKernelGGL(k_scatter_keys_lds, dim3((a.P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads),
-                           2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy);
+                           2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy,
+                           gd);
     } else
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
-                           im.tile_cursor, b.keys, gx, gy);
+                           im.tile_cursor, b.keys, gx, gy, gd);
     if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
-    hipLaunchKernelGGL(k_tile_sort_wave, dim3(T), dim3(64), 0, s, im.ranges, b.keys, b.point_list, T);
+    hipLaunchKernelGGL(k_tile_sort_wave, dim3(T), dim3(64), 0, s, im.ranges, b.keys, b.point_list, T, gd);
     if (max_count > (uint32_t)kWaveSortCap)
-        hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, b.keys, b.point_list, T);
+        hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, b.keys, b.point_list, T, gd);
     if (max_count > (uint32_t)kSortCap) {
         uint64_t* src = b.keys;
         uint64_t* dst = b.keys2;
@@ -578,14 +584,14 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
 }
 
 void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, int gx, int gy,
-                      float* out_color, float* out_invdepth, int* seen, hipStream_t s)
+                      float* out_color, float* out_invdepth, int* seen, hipStream_t s, Guard gd)
 {
     const int T = gx * gy;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     const bool depth = out_invdepth != nullptr;
 #define HLGS_BLEND(I, Dp)                                                                                       \
     hipLaunchKernelGGL((k_blend_fwd<I, Dp>), dim3(4 * T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, T, \
-                       g.splat, im.final_T, im.n_contrib, a.bg, out_color, out_invdepth, seen)
+                       g.splat, im.final_T, im.n_contrib, a.bg, out_color, out_invdepth, seen, gd)
     if (interp) { if (depth) HLGS_BLEND(true, true); else HLGS_BLEND(true, false); }
     else { if (depth) HLGS_BLEND(false, true); else HLGS_BLEND(false, false); }
 #undef HLGS_BLEND
