@@ -148,6 +148,7 @@ enum Stage { ST_PRE = 0, ST_SCAN, ST_RANGES, ST_SCATTER, ST_SORT, ST_BLEND_FWD, 
              ST_COUNT_TILES, ST_COUNT };
 static const char* kStageNames[ST_COUNT] = {"preprocess", "scan", "tile_ranges", "scatter", "tile_sort",
                                             "blend_fwd", "blend_bwd", "gauss_bwd", "count_tiles"};
+static uint32_t g_timing_mask = 0;  // bit i: time stage i
 static bool g_timing = false;
 // event pool per stage: launch i of a stage uses pair i (grown on demand, reused after a reset)
 static std::vector<hipEvent_t> g_ev[ST_COUNT][2];
@@ -155,7 +156,7 @@ static int g_calls[ST_COUNT];
 
 void stage_mark(hipStream_t s, int stage, bool begin)
 {
-    if (!g_timing) return;
+    if (!((g_timing_mask >> stage) & 1u)) return;
     const size_t i = (size_t)g_calls[stage];
     auto& pool = g_ev[stage][begin ? 0 : 1];
     if (pool.size() <= i) {
@@ -670,9 +671,10 @@ int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* p
 }
 
 // ---------------------------------------------------------------- timing hooks
-void hlgs_set_stage_timing(int enable)
+void hlgs_set_stage_timing(int mask)
 {
-    g_timing = enable != 0;
+    g_timing_mask = (uint32_t)mask;
+    g_timing = mask != 0;
     for (int i = 0; i < ST_COUNT; i++) g_calls[i] = 0;
 }
 int hlgs_stage_count(void) { return ST_COUNT; }

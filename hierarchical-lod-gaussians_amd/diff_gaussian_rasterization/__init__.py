@@ -55,6 +55,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities,
                               geom_buf, binning_buf, img_buf)
         ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for radii (or an unused output)
         return color, radii, invdepth
 
     @staticmethod
@@ -62,6 +63,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         rs = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, geom_buf, binning_buf,
          img_buf) = ctx.saved_tensors
+        if grad_color is None:  # only the inverse depth reached the loss
+            grad_color = torch.zeros((3, rs.image_height, rs.image_width), dtype=torch.float32, device=means3D.device)
         d_means2D, d_colors, d_opac, d_means3D, d_cov3D, d_sh, d_scales, d_rots = _C.rasterize_gaussians_backward(
             rs.bg, *_hierarchy(rs), means3D, radii, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
             cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_color, grad_invdepth, sh,

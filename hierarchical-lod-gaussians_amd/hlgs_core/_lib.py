@@ -141,5 +141,14 @@ def stage_stats():
     return {lib.hlgs_stage_name(i).decode(): (float(ms[i]), int(calls[i])) for i in range(n)}
 
 
-def set_stage_timing(enable):
-    load().hlgs_set_stage_timing(int(bool(enable)))
+def set_stage_timing(enable, stages=None):
+    """Time every stage (enable=True), only the named stages, or none (enable=False)."""
+    lib = load()
+    if not enable:
+        mask = 0
+    elif stages is None:
+        mask = -1
+    else:
+        names = [lib.hlgs_stage_name(i).decode() for i in range(lib.hlgs_stage_count())]
+        mask = sum(1 << names.index(n) for n in stages)
+    lib.hlgs_set_stage_timing(mask)

@@ -185,10 +185,11 @@ size_t hlgs_binning_point_list_offset(int R);  /* uint32 point_list[R] */
 size_t hlgs_image_ranges_offset(int W, int H);  /* uint2 ranges[tiles] */
 
 /* ---- measurement hooks (bench.py) ---- */
-/* When enabled, every launch of each rasterizer stage is bracketed by hipEvents on its launch stream.
- * hlgs_stage_stats returns, per stage, the mean duration in ms over all launches recorded since the
- * last hlgs_set_stage_timing call and the number of launches (synchronises).  Off by default. */
-void hlgs_set_stage_timing(int enable);
+/* Stage timing: every launch of each selected rasterizer stage (bit i of mask = stage i, -1 = all,
+ * 0 = off) is bracketed by hipEvents on its launch stream.  hlgs_stage_stats returns, per stage, the
+ * mean duration in ms over all launches recorded since the last hlgs_set_stage_timing call and the
+ * number of launches (synchronises).  Off by default. */
+void hlgs_set_stage_timing(int mask);
 int hlgs_stage_count(void);
 const char* hlgs_stage_name(int i);
 int hlgs_stage_stats(float* mean_ms, int* calls, int max);

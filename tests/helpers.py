@@ -42,7 +42,7 @@ def gpu_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_cov=
     out = dict(color=color.detach().cpu().numpy(), radii=radii.cpu().numpy(), invdepth=invd.detach().cpu().numpy())
     if grads is not None:
         g, gd = grads
-        loss = (color * torch.tensor(g, device=device)).sum()
+        loss = (color * torch.tensor(g, device=device)).sum() if g is not None else 0.0
         if do_depth and gd is not None:
             loss = loss + (invd * torch.tensor(gd, device=device)).sum()
         loss.backward()

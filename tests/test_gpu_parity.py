@@ -135,6 +135,21 @@ def test_binning_capacity_fallback_matches():
             np.testing.assert_array_equal(runs[0][k], r[k])
 
 
+def test_loss_through_one_output_only():
+    """A loss on invdepth alone (color gradient None) or on color alone (invdepth gradient None) gives the
+    same gradients as passing explicit zero upstream gradients."""
+    sc, cam = _scene(1500, 1, 96, 64, seed=41)
+    g, gd = S.upstream_grads(96, 64, seed=2)
+    zero_g, zero_gd = np.zeros_like(g), np.zeros_like(gd)
+    only_depth = gpu_render(sc, cam, grads=(None, gd))
+    ref_depth = gpu_render(sc, cam, grads=(zero_g, gd))
+    only_color = gpu_render(sc, cam, grads=(g, None))
+    ref_color = gpu_render(sc, cam, grads=(g, zero_gd))
+    for k in ("dmean3D", "dmean2D", "dopacity", "d_shs", "d_scales", "d_rotations"):
+        np.testing.assert_array_equal(only_depth[k], ref_depth[k])
+        np.testing.assert_array_equal(only_color[k], ref_color[k])
+
+
 def test_mark_visible_and_relocation():
     from diff_gaussian_rasterization import GaussianRasterizer, compute_relocation
     from oracle import oracle as O
