@@ -28,6 +28,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles each, 2400 MHz max clock
+VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 4
 
 
 def algorithmic_bytes(stage, P, V, R, N, T, M, D):
@@ -50,9 +52,10 @@ STAGE_KERNEL = {"preprocess": "k_preprocess", "count_tiles": "k_count_tiles", "s
                 "blend_bwd": "k_blend_bwd", "gauss_bwd": "k_gauss_bwd"}
 
 
-def pmc_traffic(stage):
-    """Per-launch HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) of the stage's kernel from the latest committed
-    rocprofv3 PMC profile (tools/profile_round.sh + tools/summarize_profile.py), or None."""
+def pmc_traffic(stage, field="hbm_bytes"):
+    """Per-launch HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) -- or another field, e.g. valu_wave_instr -- of the
+    stage's kernel from the latest committed rocprofv3 PMC profile (tools/profile_round.sh +
+    tools/summarize_profile.py), or None."""
     prof = os.path.join(ROOT, "profiles")
     rounds = sorted(d for d in os.listdir(prof) if os.path.exists(os.path.join(prof, d, "pmc_traffic.json"))) \
         if os.path.isdir(prof) else []
@@ -60,7 +63,7 @@ def pmc_traffic(stage):
         return None, None
     path = os.path.join(prof, rounds[-1], "pmc_traffic.json")
     ks = json.load(open(path))["kernels"]
-    hits = [v["hbm_bytes"] for k, v in ks.items() if STAGE_KERNEL[stage] in k]
+    hits = [v[field] for k, v in ks.items() if STAGE_KERNEL[stage] in k and v.get(field)]
     return (sum(hits) if hits else None), os.path.relpath(path, ROOT)
 
 
@@ -208,6 +211,11 @@ def main():
         roofline = dict(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                         traffic=traffic, traffic_unit="bytes/launch", traffic_source=src, kernel=dom,
                         kernel_ms=round(ms, 4), launches=stats[dom][1])
+        valu, _ = pmc_traffic(dom, "valu_wave_instr")
+        if valu:
+            rate = valu / (ms * 1e-3) / 1e9
+            roofline["valu_issue"] = dict(wave_instr_per_launch=valu, achieved_Ginstr_s=round(rate, 1),
+                                          peak_Ginstr_s=VALU_PEAK_GINSTR, frac=round(rate / VALU_PEAK_GINSTR, 4))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(P, deg, W, H)

@@ -12,6 +12,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/fetch -o run -
 echo "fetch ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-stage-timing > $O/write.log 2>&1
 echo "write ok"
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES -d $O/sq -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-stage-timing > $O/sq.log 2>&1
+echo "sq ok"
 timeout -k 10 300 python3 bench.py > $O/bench_plain.log 2>&1
 echo "plain ok"
 tail -1 $O/bench_plain.log

@@ -39,12 +39,19 @@ def main(src, dst):
     open(os.path.join(dst, "bench_line_under_rocprof.json"), "w").write(traced + "\n")
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    sqp = os.path.join(src, "sq", "run_counter_collection.csv")
+    valu = per_kernel(sqp, "SQ_INSTS_VALU") if os.path.exists(sqp) else {}
+    salu = per_kernel(sqp, "SQ_INSTS_SALU") if os.path.exists(sqp) else {}
+    lds = per_kernel(sqp, "SQ_INSTS_LDS") if os.path.exists(sqp) else {}
     out = {}
     for k in sorted(set(fetch) | set(write)):
         f = 2 * 1024 * fetch.get(k, 0.0)
         w = 1024 * write.get(k, 0.0)
-        out[k] = dict(fetch_bytes=round(f), write_bytes=round(w), hbm_bytes=round(f + w))
-    json.dump(dict(note="per launch; fetch = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE; KiB -> bytes",
+        out[k] = dict(fetch_bytes=round(f), write_bytes=round(w), hbm_bytes=round(f + w),
+                      valu_wave_instr=round(valu.get(k, 0.0)), salu_wave_instr=round(salu.get(k, 0.0)),
+                      lds_wave_instr=round(lds.get(k, 0.0)))
+    json.dump(dict(note="per launch; fetch = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE (KiB -> bytes); "
+                        "*_wave_instr = SQ_INSTS_* (wave instructions issued, all CUs)",
                    kernels=out), open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
