@@ -10,7 +10,7 @@ import os
 import torch
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libhlgs.so")
+LIB_PATH = os.environ.get("HLGS_LIBRARY") or os.path.join(PKG_DIR, "lib", "libhlgs.so")  # HLGS_LIBRARY: an alternative in-tree build (experiments)
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "hlgs.h")
 
 _vp = C.c_void_p
