@@ -78,20 +78,44 @@ def cpu_model():
 
 
 def cpu_baseline(P, deg, W, H):
-    """The oracle (C restatement of the reference algorithm, 1 thread) on one full frame: fwd + bwd."""
+    """The oracle (C restatement of the reference algorithm, 1 thread) on one full frame: fwd + bwd.
+    Returns the timing summary and the oracle's outputs (same scene, camera and upstream gradients as
+    rank 0's GPU step) for the full-size parity check."""
     from oracle import oracle as O
     from hlgs_core import synthetic as S
     cam = S.make_camera(W, H)
     sc = S.make_gaussians(P, deg, cam, seed=0)
-    g, gd = S.upstream_grads(W, H)
+    g, gd = S.upstream_grads(W, H, seed=1)
     O.build()
     t0 = time.perf_counter()
     fr = O.forward(sc, S.cam_numpy(cam), do_depth=True)
-    O.backward(fr, sc, g, gd)
+    gr = O.backward(fr, sc, g, gd)
     dt = time.perf_counter() - t0
-    return dict(value=round(W * H / dt / 1e6, 4), unit="Mpix/s", cores=1, kind="port",
-                sample=f"one full frame: {P} Gaussians, SH deg {deg}, {W}x{H}, forward+backward, "
-                       f"{dt:.2f} s on 1 thread of {cpu_model()} (os.cpu_count()={os.cpu_count()})")
+    summary = dict(value=round(W * H / dt / 1e6, 4), unit="Mpix/s", cores=1, kind="port",
+                   sample=f"one full frame: {P} Gaussians, SH deg {deg}, {W}x{H}, forward+backward, "
+                          f"{dt:.2f} s on 1 thread of {cpu_model()} (os.cpu_count()={os.cpu_count()})")
+    ref = dict(color=fr.color, invdepth=fr.invdepth, dmean3D=gr["dmean3D"], dmean2D=gr["dmean2D"],
+               dopacity=gr["dopacity"], dscale=gr["dscale"], drot=gr["drot"], dsh=gr["dsh"])
+    return summary, ref
+
+
+def parity_report(gpu, ref):
+    """Full-size parity of rank 0's step against the oracle: forward per-pixel L-inf and, per gradient
+    tensor, max-abs error and max-abs error relative to the oracle tensor's max-abs."""
+    out = dict(vs="oracle (C restatement of the reference), identical inputs, full configs[1] frame")
+    out["color_linf"] = float(np.abs(gpu["color"] - ref["color"]).max())
+    out["invdepth_linf"] = float(np.abs(gpu["invdepth"] - ref["invdepth"]).max())
+    per = {}
+    for k in ("dmean3D", "dmean2D", "dopacity", "dscale", "drot", "dsh"):
+        a, b = gpu[k].reshape(ref[k].shape[0], -1), ref[k].reshape(ref[k].shape[0], -1)
+        a = a[:, :b.shape[1]]
+        err = float(np.abs(a - b).max())
+        per[k] = dict(max_abs_err=err, rel=err / max(float(np.abs(b).max()), 1e-30))
+    out["grad_max_abs_err"] = max(v["max_abs_err"] for v in per.values())
+    out["grad_max_rel_err"] = max(v["rel"] for v in per.values())
+    out["grads"] = per
+    out["tolerance"] = dict(fwd_linf=1e-4, grad_rel=1e-3)
+    return out
 
 
 def main():
@@ -216,12 +240,23 @@ def main():
             rate = valu / (ms * 1e-3) / 1e9
             roofline["valu_issue"] = dict(wave_instr_per_launch=valu, achieved_Ginstr_s=round(rate, 1),
                                           peak_Ginstr_s=VALU_PEAK_GINSTR, frac=round(rate / VALU_PEAK_GINSTR, 4))
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(P, deg, W, H)
+        cpu, ref = cpu_baseline(P, deg, W, H)
+        for p in params:  # one more step on the same inputs, outputs kept for the parity check
+            p.grad = None
+        means2D = torch.zeros_like(means3D, requires_grad=True)
+        color, _, invd = rast(means3D=means3D, means2D=means2D, opacities=opac, shs=shs, scales=scales,
+                              rotations=rots)
+        torch.autograd.backward([color, invd], [g_col, g_inv])
+        npy = lambda t: t.detach().cpu().numpy()  # noqa: E731
+        gpu = dict(color=npy(color), invdepth=npy(invd), dmean3D=npy(means3D.grad), dmean2D=npy(means2D.grad),
+                   dopacity=npy(opac.grad), dscale=npy(scales.grad), drot=npy(rots.grad), dsh=npy(shs.grad))
+        parity = parity_report(gpu, ref)
     if rank == 0:
         line = {
-            "metric": "forward+backward Mpix/s at 1080p (1M Gaussians)", "value": round(value, 3), "unit": "Mpix/s",
+            "metric": "forward+backward Mpix/s at 1080p (1M Gaussians); grad max-abs-err vs ref",
+            "value": round(value, 3), "unit": "Mpix/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded PCG64 scene and upstream gradients; no dataset)",
@@ -229,7 +264,7 @@ def main():
                                    f"one view per GPU" + (", RCCL grad all-reduce" if world > 1 else ""),
                        "num_rendered": nr, "visible": V, "tiles": T,
                        "parallelism": f"view-dp{world}"},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
             "stages": stage_report, "stages_note": "untimed pass with events around every stage",
         }
         print(json.dumps(line))

@@ -232,6 +232,11 @@ size_t hlgs_binning_point_list_offset(int R)
     Bin b = carve_bin(nullptr, R < 0 ? 0 : R, nullptr);
     return (size_t)b.point_list;
 }
+size_t hlgs_geom_splat_offset(int P)
+{
+    Geom g = carve_geom(nullptr, P < 0 ? 0 : P, nullptr);
+    return (size_t)g.splat;
+}
 size_t hlgs_image_ranges_offset(int W, int H)
 {
     Img im = carve_img(nullptr, W, H, nullptr);

@@ -36,7 +36,8 @@ struct Geom {
 // 64-byte per-Gaussian record read by the blend kernels: one half cache line per (tile, Gaussian)
 // instance instead of one line per attribute array.
 //   [0] x, y, conic.a, conic.b      [1] conic.c, opacity, r, g
-//   [2] b, 1/depth, t, 1/num_kids    [3] record-slot base (bits), first tile x, first tile y, rect width (bits)
+//   [2] b, 1/depth, t, 1/num_kids    [3] record-slot base, first tile x | y << 16, rect width (int bits),
+//                                        alpha threshold on e2 (alpha_e2_threshold)
 // [3].x = point_offsets - tiles_touched is written by the scatter, after the scan; the rest by the preprocess.
 Geom carve_geom(void* base, int P, size_t* total);
 

@@ -242,6 +242,38 @@ __device__ __forceinline__ float splat_e2(float4 q, float dx, float dy)
     return fmaf(q.z * dy, dy, fmaf(q.y, dy, q.x * dx) * dx);
 }
 
+// The reference skips a pair when alpha < 1/255 (forward.cu:560, backward.cu:643).  Float alpha depends
+// on the exp implementation, and for elongated splats the float power itself carries ~1e-3 relative error
+// (the quadratic form cancels), so a float test would make different implementations keep different
+// splats.  Instead, with e2 = power * log2(e) evaluated in one fixed IEEE operation order (splat_e2 --
+// bit-identical here and in the oracle), "alpha >= 1/255" is decided as e2 >= thr, where thr is the
+// smallest float at or above the exact real threshold: -log2(255 o) (the 0.99 clamp cannot matter), or,
+// with hierarchy interpolation, log2(a_star / o) for the a_star that makes t a + (1 - t)(1 - (1 - a)^fr) = 1/255.
+// thr is computed once per Gaussian in double (preprocess; oracle alpha_e2_threshold), so the blend's
+// keep/skip test is a single float compare with identical results everywhere.
+__device__ inline float alpha_e2_threshold(float o, bool interp, float t, float fr)
+{
+    if (o != o) return -INFINITY;          // NaN opacity: the reference's fminf(0.99, NaN) keeps the pair
+    if (!(o > 0.f)) return INFINITY;       // alpha <= 0 never reaches 1/255
+    const double target = 1.0 / 255.0;
+    double a = target;
+    if (interp) {
+        const double td = t, fd = fr;
+        auto g = [&](double x) { return td * x + (1.0 - td) * (1.0 - pow(1.0 - x, fd)); };
+        if (g(0.99) < target) return INFINITY;
+        double lo = 0.0, hi = 0.99;        // g is increasing: bisect to double resolution
+        for (int i = 0; i < 64; i++) {
+            const double mid = 0.5 * (lo + hi);
+            if (g(mid) >= target) hi = mid; else lo = mid;
+        }
+        a = hi;
+    }
+    const double thr = log2(a / (double)o);
+    float f = (float)thr;
+    if ((double)f < thr) f = nextafterf(f, INFINITY);
+    return f;
+}
+
 // Does the alpha >= 1/255 footprint of a splat (see quad_mask) reach the 8x8 pixel block at (qx, qy)?
 __device__ __forceinline__ bool touches_quad(float x, float y, float4 co, float qx, float qy)
 {

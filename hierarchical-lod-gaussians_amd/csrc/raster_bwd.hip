@@ -38,15 +38,15 @@ struct PixB {
 // q = (-a/2, -b, -c/2) * log2(e) so that G = exp2(q0 dx^2 + q1 dx dy + q2 dy^2) = exp(power).
 template <bool INTERP, bool DEPTH>
 __device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& q, const float4& col,
-                                         float invz, float tt, float (&acc)[10])
+                                         float invz, float tt, float fr, float thr, float (&acc)[10])
 {
     const float e2 = splat_e2(q, dx, dy);  // power * log2(e)
     const float G = __builtin_amdgcn_exp2f(e2);
     const float test_alpha = q.w * G;
     const float my_alpha = fminf(0.99f, test_alpha);
     float alpha = my_alpha;
-    if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, col.w));
-    const bool valid = li < p.last && !(e2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+    if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
+    const bool valid = li < p.last && !(e2 > 0.0f) && !(e2 < thr);  // alpha >= 1/255 (alpha_e2_threshold)
     if (valid) {
         const float r1m = __builtin_amdgcn_rcpf(1.f - alpha);  // 1/(1-alpha), alpha <= 0.99
         p.T = p.T * r1m;
@@ -68,7 +68,7 @@ __device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float d
         acc[2] = fmaf(wdx, dx, acc[2]);
         acc[3] = fmaf(wdx, dy, acc[3]);
         acc[4] = fmaf(wdy, dy, acc[4]);
-        if (INTERP) acc[5] += (tt - powf(1.0f - my_alpha, col.w - 1.0f) * (tt - 1.0f) * col.w) * w;
+        if (INTERP) acc[5] += (tt - powf(1.0f - my_alpha, fr - 1.0f) * (tt - 1.0f) * fr) * w;
         else acc[5] += w;
     }
     return valid;
@@ -91,20 +91,43 @@ __device__ __forceinline__ void finish_record(const float* m, float4 co, float d
     rc.y = m[9];
 }
 
+struct BwdArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    int W, H, gx, gy, T;
+    Geom g;
+    const float* final_Ts;
+    const uint32_t* n_contrib;  // bit 31: the forward's exact pass rendered this pixel
+    const float* bg;
+    const float* dL_dpixels;
+    const float* dL_dinvdepths;
+    BwdScratch rec;
+};
+
+// Exact replay of a tile some of whose pixels the forward rendered with exact alpha-band decisions (rare):
+// one quadrant at a time, one pixel per lane (little register state next to the double-precision test),
+// each pass adding its per-(tile, Gaussian) records to the slots the first pass stored.  Records are
+// linear in the moments, so the sum equals the one-pass record up to float rounding.
+// One wave per tile, back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant.
 template <bool INTERP, bool DEPTH>
-__global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
-                                                  int W, int H, int gx, int gy, int T, Geom g,
-                                                  const float* __restrict__ final_Ts,
-                                                  const uint32_t* __restrict__ n_contrib, const float* __restrict__ bg,
-                                                  const float* __restrict__ dL_dpixels,
-                                                  const float* __restrict__ dL_dinvdepths, BwdScratch rec)
+__global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
 {
+    const int tile = xcd_remap(blockIdx.x, A.T);
+    const uint2* __restrict__ ranges = A.ranges;
+    const uint32_t* __restrict__ point_list = A.point_list;
+    const int W = A.W, H = A.H, gx = A.gx;
+    const Geom& g = A.g;
+    const float* __restrict__ final_Ts = A.final_Ts;
+    const uint32_t* __restrict__ n_contrib = A.n_contrib;
+    const float* __restrict__ bg = A.bg;
+    const float* __restrict__ dL_dpixels = A.dL_dpixels;
+    const float* __restrict__ dL_dinvdepths = A.dL_dinvdepths;
+    const BwdScratch& rec = A.rec;
     __shared__ float4 s_xy[64];   // x, y, 1/depth, quadrant mask bits
     __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
-    __shared__ float4 s_col[64];  // r, g, b, 1/kids
-    __shared__ float s_t[64];     // interpolation t
+    __shared__ float4 s_col[64];  // r, g, b, alpha threshold on e2
+    __shared__ float2 s_tf[64];   // interpolation t, 1/kids
     __shared__ float s_m[64 * 10];  // reduced moments per splat
-    const int tile = xcd_remap(blockIdx.x, T);
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
     const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
@@ -160,9 +183,10 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
             s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, __uint_as_float(qm));
             s_q[lane] = conic_q(co);
             my_co = co;
-            s_col[lane] = make_float4(r1.z, r1.w, r2.x, INTERP ? r2.w : 0.f);
-            if (INTERP) s_t[lane] = r2.z;
-            const int x0 = __float_as_int(r3.y), y0 = __float_as_int(r3.z), w = __float_as_int(r3.w);
+            s_col[lane] = make_float4(r1.z, r1.w, r2.x, r3.w);
+            if (INTERP) s_tf[lane] = make_float2(r2.z, r2.w);
+            const int x0 = __float_as_int(r3.y) & 0xffff, y0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
+            const int w = __float_as_int(r3.z);
             slot = __float_as_uint(r3.x) + (uint32_t)((ty - y0) * w + (tx - x0));
         }
 #pragma unroll
@@ -181,7 +205,7 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
                 if (qm == 0) continue;
                 const float4 co = s_q[j];
                 const float4 col = s_col[j];
-                const float tt = INTERP ? s_t[j] : 0.f;
+                const float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
                 float acc[10];
 #pragma unroll
                 for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
@@ -195,7 +219,7 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
                 for (int k = 0; k < 4; k++)
                     if ((qm >> k) & 1u)  // uniform branch
                         any |= bwd_pair<INTERP, DEPTH>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), co, col,
-                                                       xy.z, tt, acc);
+                                                       xy.z, tf.x, tf.y, col.w, acc);
                 if (__ballot(any)) {
                     float r0, r1, r2;
                     wave_reduce10(acc, r0, r1, r2);
@@ -223,6 +247,7 @@ __global__ void __launch_bounds__(64) k_blend_bwd(const uint2* __restrict__ rang
         __syncthreads();
     }
 }
+
 
 // One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
 // backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
@@ -536,9 +561,8 @@ void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
 {
     const int T = gx * gy;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
-#define HLGS_BB(I, Dp)                                                                                              \
-    hipLaunchKernelGGL((k_blend_bwd<I, Dp>), dim3(T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, \
-                       im.final_T, im.n_contrib, a.bg, dL_dpix, dL_dinv, rs)
+    BwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, im.final_T, im.n_contrib, a.bg, dL_dpix, dL_dinv, rs};
+#define HLGS_BB(I, Dp) hipLaunchKernelGGL((k_blend_bwd<I, Dp>), dim3(T), dim3(64), 0, s, A)
     if (interp) { if (dL_dinv) HLGS_BB(true, true); else HLGS_BB(true, false); }
     else { if (dL_dinv) HLGS_BB(false, true); else HLGS_BB(false, false); }
 #undef HLGS_BB

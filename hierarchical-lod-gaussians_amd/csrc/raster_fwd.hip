@@ -145,9 +145,10 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
         float4* rec = g.splat + 4 * (size_t)t_idx;
         rec[0] = make_float4(pix_x, pix_y, conic_x, conic_y);
         rec[1] = make_float4(conic_z, opacity * h_scale, cr, cg);
-        rec[2] = make_float4(cbl, 1.f / p_view.z, interp ? a.ts[t_idx] : 0.f,
-                             interp ? 1.0f / (float)a.kids[t_idx] : 0.f);
-        rec[3] = make_float4(0.f, __int_as_float(x0), __int_as_float(y0), __int_as_float(x1 - x0));
+        const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+        rec[2] = make_float4(cbl, 1.f / p_view.z, tt, fr);
+        rec[3] = make_float4(0.f, __int_as_float(x0 | (y0 << 16)), __int_as_float(x1 - x0),
+                             alpha_e2_threshold(opacity * h_scale, interp, tt, fr));
     }
     if (tile_count)  // only when the tile grid is too large for the LDS-histogram binning
         for (int y = y0; y < y1; y++)
@@ -392,51 +393,61 @@ __global__ void __launch_bounds__(256) k_merge_runs(const uint2* __restrict__ ra
     if (last) point_list[r.x + out] = (uint32_t)key;
 }
 
+struct FwdArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    int W, H, gx, T;
+    const float4* splat;
+    float* final_T;
+    uint32_t* n_contrib;
+    const float* bg;
+    float* out_color;
+    float* out_invdepth;
+    int* seen;
+};
+
 // ------------------------------------------------------------------------------------------------
 // Front-to-back blend.  One wave64 per 8x8 quadrant of a 16x16 tile, one pixel per lane; the four
 // quadrant waves of a tile are independent blocks placed on one XCD (xcd_remap) so the tile's splat
-// gathers hit the same L2.  Each 64-splat batch is staged in LDS; a ballot builds the wave-uniform bit
+// reads hit the same L2.  Each 64-splat batch is staged in LDS; a ballot builds the wave-uniform bit
 // set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
 // visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
 // ------------------------------------------------------------------------------------------------
 template <bool INTERP, bool DEPTH>
-__global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
-                                                  int W, int H, int gx, int T, const float4* __restrict__ splat,
-                                                  float* __restrict__ final_T,
-                                                  uint32_t* __restrict__ n_contrib, const float* __restrict__ bg,
-                                                  float* __restrict__ out_color, float* __restrict__ out_invdepth,
-                                                  int* __restrict__ seen, Guard gd)
+__global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 {
     if (guard_fail(gd)) return;
-    __shared__ float4 s_xy[64];   // x, y, 1/depth, interpolation t
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, alpha threshold on e2
     __shared__ float4 s_co[64];   // conic_q, opacity
     __shared__ float4 s_col[64];  // r, g, b, 1/kids
-    const int L = xcd_remap(blockIdx.x, 4 * T);
+    __shared__ float s_t[64];     // interpolation t
+    const int L = xcd_remap(blockIdx.x, 4 * A.T);
     const int tile = L >> 2, q = L & 3;
     const int lane = threadIdx.x;
-    const int qx0 = (tile % gx) * HLGS_TILE + 8 * (q & 1), qy0 = (tile / gx) * HLGS_TILE + 8 * (q >> 1);
+    const int qx0 = (tile % A.gx) * HLGS_TILE + 8 * (q & 1), qy0 = (tile / A.gx) * HLGS_TILE + 8 * (q >> 1);
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const float pxf = (float)px, pyf = (float)py;
     const float fqx = (float)qx0, fqy = (float)qy0;
-    const uint2 range = ranges[tile];
+    const uint2 range = A.ranges[tile];
 
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     uint32_t last = 0;
-    bool done = !(px < W && py < H);
+    bool done = !(px < A.W && py < A.H);
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if (__all(done)) break;
         const uint32_t pos = base + lane;
         uint32_t my_id = 0;
         bool hit = false;
         if (pos < range.y) {
-            my_id = point_list[pos];
-            const float4* rec = splat + 4 * (size_t)my_id;
-            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+            my_id = A.point_list[pos];
+            const float4* rec = A.splat + 4 * (size_t)my_id;
+            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
             hit = touches_quad(r0.x, r0.y, co, fqx, fqy);
-            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, INTERP ? r2.z : 0.f);
+            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, r3.w);
             s_co[lane] = conic_q(co);
             s_col[lane] = make_float4(r1.z, r1.w, r2.x, INTERP ? r2.w : 0.f);
+            if (INTERP) s_t[lane] = r2.z;
         }
         uint64_t todo = __ballot(hit);
         __syncthreads();
@@ -451,9 +462,12 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
             const float e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
             const float my_alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(e2));
             float alpha = my_alpha;
-            if (INTERP) alpha = xy.w * my_alpha + (1.0f - xy.w) * (1.0f - __powf(1.0f - my_alpha, c.w));
+            if (INTERP) {
+                const float tt = s_t[j];
+                alpha = tt * my_alpha + (1.0f - tt) * (1.0f - __powf(1.0f - my_alpha, c.w));
+            }
             const float test_T = Tt * (1 - alpha);
-            const bool valid = !done && !(e2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const bool valid = !done && !(e2 > 0.0f) && !(e2 < xy.w);  // alpha >= 1/255 (alpha_e2_threshold)
             const bool stop = valid && test_T < 0.0001f;
             const bool blended = valid && !stop;
             const float wgt = blended ? alpha * Tt : 0.f;
@@ -466,18 +480,18 @@ __global__ void __launch_bounds__(64) k_blend_fwd(const uint2* __restrict__ rang
             done = done || stop;
             if (__ballot(blended)) seen_mask |= 1ull << j;
         }
-        if ((seen_mask >> lane) & 1ull) seen[my_id] = 1;
+        if ((seen_mask >> lane) & 1ull) A.seen[my_id] = 1;
         __syncthreads();
     }
-    if (px < W && py < H) {
-        const size_t HW = (size_t)H * W;
-        const size_t pid = (size_t)W * py + px;
-        final_T[pid] = Tt;
-        n_contrib[pid] = last;
-        out_color[pid] = C0 + Tt * bg[0];
-        out_color[HW + pid] = C1 + Tt * bg[1];
-        out_color[2 * HW + pid] = C2 + Tt * bg[2];
-        if (DEPTH) out_invdepth[pid] = D;
+    if (px < A.W && py < A.H) {
+        const size_t HW = (size_t)A.H * A.W;
+        const size_t pid = (size_t)A.W * py + px;
+        A.final_T[pid] = Tt;
+        A.n_contrib[pid] = last;
+        A.out_color[pid] = C0 + Tt * A.bg[0];
+        A.out_color[HW + pid] = C1 + Tt * A.bg[1];
+        A.out_color[2 * HW + pid] = C2 + Tt * A.bg[2];
+        if (DEPTH) A.out_invdepth[pid] = D;
     }
 }
 
@@ -589,9 +603,9 @@ void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
     const int T = gx * gy;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     const bool depth = out_invdepth != nullptr;
-#define HLGS_BLEND(I, Dp)                                                                                       \
-    hipLaunchKernelGGL((k_blend_fwd<I, Dp>), dim3(4 * T), dim3(64), 0, s, im.ranges, b.point_list, a.W, a.H, gx, T, \
-                       g.splat, im.final_T, im.n_contrib, a.bg, out_color, out_invdepth, seen, gd)
+    FwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, T, g.splat, im.final_T, im.n_contrib, a.bg, out_color,
+              out_invdepth, seen};
+#define HLGS_BLEND(I, Dp) hipLaunchKernelGGL((k_blend_fwd<I, Dp>), dim3(4 * T), dim3(64), 0, s, A, gd)
     if (interp) { if (depth) HLGS_BLEND(true, true); else HLGS_BLEND(true, false); }
     else { if (depth) HLGS_BLEND(false, true); else HLGS_BLEND(false, false); }
 #undef HLGS_BLEND

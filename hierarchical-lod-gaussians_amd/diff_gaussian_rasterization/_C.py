@@ -173,3 +173,9 @@ def inspect_ranges(imageBuffer, W, H):
     """[start, end) of every tile's list (tiles row-major) held in a forward's image buffer."""
     T = ((W + 15) // 16) * ((H + 15) // 16)
     return _field(imageBuffer, L.load().hlgs_image_ranges_offset(int(W), int(H)), 2 * T, torch.int32).view(T, 2)
+
+
+def inspect_splats(geomBuffer, P):
+    """(P, 16) float32 per-Gaussian blend records held in a forward's geometry buffer:
+    x, y, conic a, b, conic c, opacity, r, g, b, 1/depth, t, 1/kids, record base, tile x0, y0, width."""
+    return _field(geomBuffer, L.load().hlgs_geom_splat_offset(int(P)), 16 * int(P), torch.float32).view(int(P), 16)

@@ -68,6 +68,7 @@ _SIGS = {
     "hlgs_lod_interp_backward": (_i, [_i, _i, _i] + [_vp] * 15),
     "hlgs_binning_point_list_offset": (_sz, [_i]),
     "hlgs_image_ranges_offset": (_sz, [_i, _i]),
+    "hlgs_geom_splat_offset": (_sz, [_i]),
     "hlgs_set_stage_timing": (None, [_i]),
     "hlgs_stage_count": (_i, []),
     "hlgs_stage_name": (C.c_char_p, [_i]),

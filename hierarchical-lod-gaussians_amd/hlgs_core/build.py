@@ -22,9 +22,15 @@ def _deps_mtime():
     return max(os.path.getmtime(f) for f in files if os.path.exists(f))
 
 
+# raster_fwd.hip: no a*b+c contraction, so the preprocess rounds every product and sum as the oracle
+# does (-ffp-contract=off there) and its per-Gaussian outputs are bit-identical; the blend's hot
+# arithmetic is written with explicit fmaf and is unaffected.
+PER_FILE = {"raster_fwd.hip": ["-ffp-contract=off"]}
+
+
 def _compile(src, extra):
     obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
-    cmd = [HIPCC] + FLAGS + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+    cmd = [HIPCC] + FLAGS + PER_FILE.get(src, []) + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

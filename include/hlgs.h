@@ -183,6 +183,8 @@ int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* p
  * buffer's first 256-byte-aligned address ---- */
 size_t hlgs_binning_point_list_offset(int R);  /* uint32 point_list[R] */
 size_t hlgs_image_ranges_offset(int W, int H);  /* uint2 ranges[tiles] */
+size_t hlgs_geom_splat_offset(int P);           /* float4 splat[P][4]: x, y, conic a, b | conic c, opacity, r, g |
+                                                   b, 1/depth, t, 1/kids | record base, tile x0, y0, width */
 
 /* ---- measurement hooks (bench.py) ---- */
 /* Stage timing: every launch of each selected rasterizer stage (bit i of mask = stage i, -1 = all,

@@ -353,6 +353,62 @@ typedef struct {
 } orc_img;
 
 /* Forward phase 2: duplicate, stable sort, ranges, blend (HR/rasterizer_impl.cu:335-399, HR/forward.cu:450-596) */
+
+/* Splat falloff and the alpha >= 1/255 test (forward.cu:539-560, backward.cu:614-643), restated so
+ * that every implementation in this repository makes the same keep/skip decisions ("alpha
+ * threshold"):
+ *  - power is evaluated as e2 = power * log2(e) = (qa dx + qb dy) dx + qc dy^2 with the conic pre-scaled
+ *    by -log2(e) * (1/2, 1, 1/2), in one fixed IEEE order with fused multiply-adds -- bit-identical to the
+ *    HIP kernels' splat_e2; G = exp2(e2) = exp(power);
+ *  - "alpha >= 1/255" is e2 >= thr, thr = the smallest float at or above the exact real threshold
+ *    (-log2(255 o); with lerp, log2(a_star / o) for t a_star + (1 - t)(1 - (1 - a_star)^fr) = 1/255), computed once per
+ *    Gaussian in double.  A float alpha test instead would depend on the exp implementation and, for
+ *    elongated splats, on the ~1e-3 relative error of the cancelling float quadratic form. */
+static inline void conic_q(const float *co, float *q)
+{
+    const float kL2E = 1.4426950408889634f;
+    q[0] = -0.5f * kL2E * co[0];
+    q[1] = -kL2E * co[1];
+    q[2] = -0.5f * kL2E * co[2];
+}
+static inline float splat_e2(const float *q, float dx, float dy)
+{
+    return fmaf(q[2] * dy, dy, fmaf(q[1], dy, q[0] * dx) * dx);
+}
+static float alpha_e2_threshold(float o, int interp, float t, float fr)
+{
+    if (o != o) return -INFINITY;
+    if (!(o > 0.0f)) return INFINITY;
+    const double target = 1.0 / 255.0;
+    double a = target;
+    if (interp) {
+        const double td = t, fd = fr;
+#define G_(x) (td * (x) + (1.0 - td) * (1.0 - pow(1.0 - (x), fd)))
+        if (G_(0.99) < target) return INFINITY;
+        double lo = 0.0, hi = 0.99;
+        for (int i = 0; i < 64; i++) {
+            const double mid = 0.5 * (lo + hi);
+            if (G_(mid) >= target) hi = mid; else lo = mid;
+        }
+#undef G_
+        a = hi;
+    }
+    const double thr = log2(a / (double)o);
+    float f = (float)thr;
+    if ((double)f < thr) f = nextafterf(f, INFINITY);
+    return f;
+}
+/* per-Gaussian thresholds of a frame (caller frees) */
+static float *alpha_thresholds(const orc_args *a, const orc_geom *g)
+{
+    float *thr = (float *)malloc(sizeof(float) * (size_t)(a->P > 0 ? a->P : 1));
+    const int interp = a->ts != NULL && a->kids != NULL;
+    for (int i = 0; i < a->P; i++)
+        thr[i] = alpha_e2_threshold(g->conic_opacity[4 * i + 3], interp, interp ? a->ts[i] : 0.0f,
+                                    interp ? 1.0f / (float)a->kids[i] : 0.0f);
+    return thr;
+}
+
 void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R, float *out_color,
                         float *out_invdepth, int *seen)
 {
@@ -395,6 +451,7 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
     free(buf);
     const float *feat = a->colors_precomp ? a->colors_precomp : g->rgb;
     int do_interp = (a->ts != NULL && a->kids != NULL);
+    float *thr = alpha_thresholds(a, g);
     /* renderCUDA<3> per pixel, HR/forward.cu:450-596 */
     for (int ty = 0; ty < gy; ty++)
         for (int tx = 0; tx < gx; tx++) {
@@ -408,16 +465,18 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
                         uint32_t id = im->point_list[j];
                         float dx = g->means2D[2 * id] - (float)px, dy = g->means2D[2 * id + 1] - (float)py;
                         const float *co = g->conic_opacity + 4 * id;
-                        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-                        if (power > 0.0f) continue;
-                        float my_alpha = fminf(0.99f, co[3] * expf(power));
+                        float q[3];
+                        conic_q(co, q);
+                        const float e2 = splat_e2(q, dx, dy); /* power * log2(e) */
+                        if (e2 > 0.0f) continue;
+                        float my_alpha = fminf(0.99f, co[3] * exp2f(e2));
                         float alpha = my_alpha;
                         if (do_interp && (int)id < a->P) {
                             float tt = a->ts[id], fr = 1.0f / (float)a->kids[id];
                             float ka = 1.0f - exp2f(fr * log2f(1.0f - my_alpha)); /* __powf */
                             alpha = tt * my_alpha + (1.0f - tt) * ka;
                         }
-                        if (alpha < 1.0f / 255.0f) continue;
+                        if (e2 < thr[id]) continue; /* alpha < 1/255 */
                         float test_T = Tt * (1 - alpha);
                         if (test_T < 0.0001f) break; /* done */
                         if (seen) seen[id] = 1;
@@ -433,6 +492,7 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
                     if (out_invdepth) out_invdepth[pid] = inv;
                 }
         }
+    free(thr);
 }
 
 /* Backward gradient outputs; every array has P_full rows and must be zero on entry. */
@@ -453,6 +513,7 @@ typedef struct {
 static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *im, const float *dL_dpix,
                            const float *dL_dinv, orc_grads *o)
 {
+    float *thr = alpha_thresholds(a, g);
     int gx = (a->W + TILE - 1) / TILE, gy = (a->H + TILE - 1) / TILE;
     int W = a->W, H = a->H;
     const float *col = a->colors_precomp ? a->colors_precomp : g->rgb;
@@ -479,9 +540,11 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
                         uint32_t id = im->point_list[j];
                         float dx = g->means2D[2 * id] - (float)px, dy = g->means2D[2 * id + 1] - (float)py;
                         const float *co = g->conic_opacity + 4 * id;
-                        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-                        if (power > 0.0f) continue;
-                        float G = expf(power);
+                        float q[3];
+                        conic_q(co, q);
+                        const float e2 = splat_e2(q, dx, dy); /* power * log2(e) */
+                        if (e2 > 0.0f) continue;
+                        float G = exp2f(e2);
                         float test_alpha = co[3] * G;
                         int nullalpha = test_alpha > 0.99f;
                         float my_alpha = fminf(0.99f, test_alpha), alpha = my_alpha, tt = 0, fr = 0;
@@ -490,7 +553,7 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
                             fr = 1.0f / (float)a->kids[id];
                             alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
                         }
-                        if (alpha < 1.0f / 255.0f) continue;
+                        if (e2 < thr[id]) continue; /* alpha < 1/255 */
                         T = T / (1.f - alpha);
                         const float weight = alpha * T;
                         float dL_dalpha = 0.0f;
@@ -530,6 +593,7 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
                     }
                 }
         }
+    free(thr);
 }
 
 /* HR/auxiliary.h:132-142 */
