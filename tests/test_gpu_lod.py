@@ -43,6 +43,37 @@ def test_point_list_and_ranges_bit_exact(P, W, H, band):
     np.testing.assert_array_equal(out[7].cpu().numpy(), fr.seen)
 
 
+@pytest.mark.parametrize("deg", [0, 3])
+def test_decisions_bit_exact_for_elongated_splats(deg):
+    """Strongly anisotropic splats (the float quadratic form cancels): the GPU keeps and skips exactly the
+    oracle's pairs -- n_contrib, seen and point_list bit-exact, preprocess records bit-exact, image <= 1e-6."""
+    from diff_gaussian_rasterization import _C
+    W, H = 256, 192
+    cam = S.make_camera(W, H)
+    sc = S.make_gaussians(6000, deg, cam, seed=17)
+    rng = np.random.default_rng(5)
+    sc["scales"] = np.ascontiguousarray(sc["scales"] * np.exp(rng.uniform(-2.5, 2.5, sc["scales"].shape))
+                                        .astype(np.float32))
+    fr = O.forward(dict(sc), S.cam_numpy(cam))
+    t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
+    e = torch.empty(0, device=DEV)
+    out = _C.rasterize_gaussians(cam["bg"], e, e, e, e, t(sc["means3D"]), e, t(sc["opacities"]), t(sc["scales"]),
+                                 t(sc["rotations"]), 1.0, e, cam["viewmatrix"], cam["projmatrix"], cam["tanfovx"],
+                                 cam["tanfovy"], H, W, t(sc["shs"]), deg, cam["campos"], False, False, True)
+    R = out[0]
+    assert R == fr.R
+    np.testing.assert_array_equal(_C.inspect_point_list(out[4], R).cpu().numpy().astype(np.uint32),
+                                  fr.point_list[:R])
+    N = W * H
+    n_contrib = _C._field(out[5], (4 * N + 255) // 256 * 256, N, torch.int32).cpu().numpy()
+    np.testing.assert_array_equal(n_contrib, fr.n_contrib.astype(np.int32))
+    np.testing.assert_array_equal(out[7].cpu().numpy(), fr.seen)
+    rec = _C.inspect_splats(out[3], 6000).cpu().numpy()
+    vis = out[2].cpu().numpy() > 0
+    np.testing.assert_array_equal(rec[vis][:, 2:6], fr.conic_opacity[vis])
+    assert np.abs(out[1].cpu().numpy() - fr.color).max() <= 1e-6
+
+
 @pytest.mark.parametrize("sky", [0, 4])
 def test_expand_to_size_dynamic_and_weights(sky):
     import gaussian_hierarchy as GH
