@@ -1,0 +1,34 @@
+"""Brute-force check that the ellipse-vs-8x8-block culling test (hlgs_math.h foot_touches) never rejects a
+block holding a pixel with alpha >= 1/255 (float32 test vs float64 pixel oracle, 4e5 random splats)."""
+import numpy as np
+rng = np.random.default_rng(0)
+N = 400000
+f32 = np.float32
+x = rng.uniform(-20, 28, N).astype(f32); y = rng.uniform(-20, 28, N).astype(f32)
+# random PD covariance -> conic (dilated like the renderer)
+s1 = np.exp(rng.uniform(np.log(0.3), np.log(30), N)); s2 = np.exp(rng.uniform(np.log(0.3), np.log(30), N))
+th = rng.uniform(0, np.pi, N)
+c, s = np.cos(th), np.sin(th)
+cxx = c*c*s1**2 + s*s*s2**2 + 0.3; cyy = s*s*s1**2 + c*c*s2**2 + 0.3; cxy = c*s*(s1**2 - s2**2)
+det = cxx*cyy - cxy*cxy
+a = (cyy/det).astype(f32); b = (-cxy/det).astype(f32); cc = (cxx/det).astype(f32)
+o = rng.uniform(0.0, 1.0, N).astype(f32)
+# brute force over the 8x8 block at (0,0): any pixel with alpha >= 1/255 (float64 reference)
+px, py = np.meshgrid(np.arange(8), np.arange(8))
+px = px.ravel(); py = py.ravel()
+dx = x[:, None].astype(np.float64) - px; dy = y[:, None].astype(np.float64) - py
+power = -0.5*(a[:, None]*dx*dx + cc[:, None]*dy*dy) - b[:, None]*dx*dy
+alpha = np.minimum(0.99, o[:, None]*np.exp(power))
+truth = ((power <= 0) & (alpha >= 1/255)).any(1)
+# the float32 test
+t = (np.maximum(2*np.log(f32(255)*o), 0).astype(f32)*f32(1.002) + f32(2e-3))
+kv = (-b/cc).astype(f32); ku = (-b/a).astype(f32)
+u0 = (0 - x).astype(f32); u1 = u0 + f32(7); v0 = (0 - y).astype(f32); v1 = v0 + f32(7)
+def qu(U):
+    v = np.clip(kv*U, v0, v1); return U*(a*U + 2*b*v) + cc*v*v
+def qv(V):
+    u = np.clip(ku*V, u0, u1); return V*(cc*V + 2*b*u) + a*u*u
+m = np.minimum(np.minimum(qu(u0), qu(u1)), np.minimum(qv(v0), qv(v1)))
+inside = (u0 <= 0) & (u1 >= 0) & (v0 <= 0) & (v1 >= 0)
+test = np.where(o < f32(1/255*0.999), False, inside | (m <= t))
+print("missed (must be 0):", int((truth & ~test).sum()), " true:", int(truth.sum()), " test:", int(test.sum()))
