@@ -17,9 +17,10 @@
 namespace hlgs {
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
                        hipStream_t s);
-void launch_tile_ranges(const Img& im, int T, hipStream_t s);
+void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s);
 bool lds_binning(int gx, int gy);
-void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, hipStream_t s);
+void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
+                        hipStream_t s);
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
                     int gy, uint32_t max_count, hipStream_t s, bool timing, Guard gd);
 void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, int gx, int gy,
@@ -31,6 +32,8 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
 void launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t s);
 void launch_relocation(int P, const float* oo, const float* so, const int* N, const float* binoms, int n_max,
                        float* on, float* sn, hipStream_t s);
+void launch_adam(float* param, const float* grad, float* m, float* v, const uint8_t* vis, float lr, float b1, float b2,
+                 float eps, uint32_t N, uint32_t M, hipStream_t s);
 void launch_expand_dynamic(int N, float target, const int* nodes, const float* pos, const float* scales,
                            const float* vp, const float* vd, int* ri, int* pi, int* ni, uint32_t* counts,
                            uint32_t* incl, uint32_t* tmp, hipStream_t s);
@@ -172,9 +175,24 @@ static int validate(const hlgs_raster_args* a)
 {
     if (!a) return fail(HLGS_ERR_ARG, "null args");
     if (a->P < 0 || a->W <= 0 || a->H <= 0) return fail(HLGS_ERR_ARG, "invalid P/W/H");
+    if (a->variant != HLGS_VARIANT_HIERARCHY && a->variant != HLGS_VARIANT_ALT)
+        return fail(HLGS_ERR_ARG, "unknown rasterizer variant");
     if (a->P == 0) return HLGS_OK;
     if (!a->means3D || !a->opacities || !a->viewmatrix || !a->projmatrix || !a->bg || !a->campos)
         return fail(HLGS_ERR_ARG, "missing required tensor (means3D/opacities/viewmatrix/projmatrix/bg/campos)");
+    if (a->variant == HLGS_VARIANT_ALT) {
+        // alt-rasterizer: SH as dc (degree 0) + shs (the M higher-order coefficients)
+        if (!a->dc && !a->colors_precomp) return fail(HLGS_ERR_ARG, "For non-RGB, provide precomputed Gaussian colors!");
+        if (a->indices || a->parent_indices || a->ts || a->kids)
+            return fail(HLGS_ERR_ARG, "the alt rasterizer has no hierarchy mode");
+        if (a->shs && (a->M <= 0 || a->M > 15)) return fail(HLGS_ERR_ARG, "shs rows must hold 1..15 coefficients");
+        if (!a->colors_precomp && (a->D < 0 || a->D > 3 || (a->D + 1) * (a->D + 1) - 1 > (a->shs ? a->M : 0)))
+            return fail(HLGS_ERR_ARG, "sh_degree needs more SH coefficients than given");
+        if (!a->cov3D_precomp && (!a->scales || !a->rotations))
+            return fail(HLGS_ERR_ARG, "provide scales+rotations or cov3D_precomp");
+        if (a->P != a->P_full) return fail(HLGS_ERR_ARG, "P must equal P_full");
+        return HLGS_OK;
+    }
     if (!a->shs && !a->colors_precomp)
         return fail(HLGS_ERR_ARG, "For non-RGB, provide precomputed Gaussian colors!");
     if (a->shs && (a->M <= 0 || a->M > 16)) return fail(HLGS_ERR_ARG, "shs rows must hold 1..16 coefficients");
@@ -254,12 +272,13 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
     HLGS_TRY_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
     HLGS_TRY_HIP(hipMemsetAsync(im.misc, 0, sizeof(uint32_t) * 16, s));
     const bool lds_bins = lds_binning(gx, gy);
+    const bool alt = a->variant == HLGS_VARIANT_ALT;
     stage_mark(s, ST_PRE, true);
     launch_preprocess(*a, g, radii, lds_bins ? nullptr : im.tile_count, gx, gy, s);
     stage_mark(s, ST_PRE, false);
     if (lds_bins) {
         stage_mark(s, ST_COUNT_TILES, true);
-        launch_count_tiles(a->P, radii, g, im.tile_count, gx, gy, s);
+        launch_count_tiles(a->P, radii, g, im.tile_count, gx, gy, alt, s);
         stage_mark(s, ST_COUNT_TILES, false);
     }
     int rc;
@@ -269,7 +288,7 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
     stage_mark(s, ST_SCAN, false);
     stage_mark(s, ST_RANGES, true);
     scan_inclusive_u32(im.tile_count, im.tile_cursor, (size_t)T, im.scan_tmp, s);
-    launch_tile_ranges(im, T, s);
+    launch_tile_ranges(im, T, g.point_offsets, a->P, s);
     stage_mark(s, ST_RANGES, false);
     return check_stage(s, a->debug, "scan");
 }
@@ -329,15 +348,17 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     info->num_rendered = 0;
     info->max_tile_count = 0;
     info->rendered = 0;
+    info->num_binned = 0;
     if (a->P == 0) return HLGS_OK;
     hipStream_t s = (hipStream_t)stream;
     if ((rc = prepare_launch(a, geom, img, radii, s))) return rc;
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
-    uint32_t misc[2];
+    uint32_t misc[3];
     HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipStreamSynchronize(s));
-    info->num_rendered = (int)misc[0];
+    info->num_binned = (int)misc[0];
     info->max_tile_count = (int)misc[1];
+    info->num_rendered = (int)misc[2];
     return HLGS_OK;
 }
 
@@ -347,8 +368,10 @@ int hlgs_rasterize_forward_render(const hlgs_raster_args* a, const int* radii, v
 {
     int rc = validate(a);
     if (rc) return rc;
-    const int R = info->num_rendered;
-    if (a->P == 0 || R == 0) return HLGS_OK;  // rasterizer_impl.cu:332-333: output stays 0
+    const int R = info->num_binned;
+    if (a->P == 0) return HLGS_OK;
+    // rasterizer_impl.cu:332-333: the hierarchy rasterizer's output stays 0; the alt rasterizer blends anyway (bg)
+    if (R == 0 && a->variant != HLGS_VARIANT_ALT) return HLGS_OK;
     return render_launch(a, radii, geom, img, binning, R, (uint32_t)info->max_tile_count, out_color, out_invdepth,
                          seen, (hipStream_t)stream, Guard{nullptr, 0u, 0u});
 }
@@ -362,21 +385,23 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     info->num_rendered = 0;
     info->max_tile_count = 0;
     info->rendered = 0;
+    info->num_binned = 0;
     hipStream_t s = (hipStream_t)stream;
     hipGetLastError();
     const size_t HW = (size_t)a->W * a->H;
+    const bool alt = a->variant == HLGS_VARIANT_ALT;
     if (a->P == 0) {
         HLGS_TRY_HIP(hipMemsetAsync(out_color, 0, 3 * sizeof(float) * HW, s));
         if (out_invdepth) HLGS_TRY_HIP(hipMemsetAsync(out_invdepth, 0, sizeof(float) * HW, s));
         info->rendered = 1;
         return HLGS_OK;
     }
-    HLGS_TRY_HIP(hipMemsetAsync(seen, 0, sizeof(int) * (size_t)a->P, s));
+    if (seen) HLGS_TRY_HIP(hipMemsetAsync(seen, 0, sizeof(int) * (size_t)a->P, s));
     if ((rc = prepare_launch(a, geom, img, radii, s))) return rc;
     Readback* rb;
     if ((rc = readback_for(s, &rb))) return rc;
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
-    HLGS_TRY_HIP(hipMemcpyAsync(rb->host, im.misc, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HLGS_TRY_HIP(hipMemcpyAsync(rb->host, im.misc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipEventRecord(rb->ev, s));
     // Queue the render before knowing R: it is sized for the caller's buffer and for lists the one-wave and
     // block sorts handle; the kernels exit at once if the frame exceeds either (Guard).
@@ -389,9 +414,10 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     HLGS_TRY_HIP(hipEventSynchronize(rb->ev));
     const uint32_t R = rb->host[0], maxc = rb->host[1];
     rb->last_maxc = maxc;
-    info->num_rendered = (int)R;
+    info->num_binned = (int)R;
+    info->num_rendered = (int)rb->host[2];
     info->max_tile_count = (int)maxc;
-    if (R == 0) {  // rasterizer_impl.cu:332-333: the output stays 0 (not bg)
+    if (R == 0 && !alt) {  // rasterizer_impl.cu:332-333: the output stays 0 (not bg)
         HLGS_TRY_HIP(hipMemsetAsync(out_color, 0, 3 * sizeof(float) * HW, s));
         if (out_invdepth) HLGS_TRY_HIP(hipMemsetAsync(out_invdepth, 0, sizeof(float) * HW, s));
         info->rendered = 1;
@@ -414,7 +440,7 @@ int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const v
     int rc = validate(a);
     if (rc) return rc;
     if (!out || !out->dmean2D || !out->dcolor || !out->dopacity || !out->dmean3D || !out->dcov3D || !out->dscale ||
-        !out->drot || (a->M > 0 && !out->dsh))
+        !out->drot || (a->M > 0 && !out->dsh) || (a->variant == HLGS_VARIANT_ALT && !out->ddc))
         return fail(HLGS_ERR_ARG, "missing gradient output");
     hipStream_t s = (hipStream_t)stream;
     hipGetLastError();
@@ -427,6 +453,7 @@ int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const v
         HLGS_TRY_HIP(hipMemsetAsync(out->dmean3D, 0, 12 * Pf, s));
         HLGS_TRY_HIP(hipMemsetAsync(out->dcov3D, 0, 24 * Pf, s));
         if (out->dsh && a->M > 0) HLGS_TRY_HIP(hipMemsetAsync(out->dsh, 0, 12 * (size_t)a->M * Pf, s));
+        if (out->ddc) HLGS_TRY_HIP(hipMemsetAsync(out->ddc, 0, 12 * Pf, s));
         HLGS_TRY_HIP(hipMemsetAsync(out->dscale, 0, 12 * Pf, s));
         HLGS_TRY_HIP(hipMemsetAsync(out->drot, 0, 16 * Pf, s));
     }
@@ -469,6 +496,18 @@ int hlgs_compute_relocation(int P, const float* opacity_old, const float* scale_
     hipGetLastError();
     launch_relocation(P, opacity_old, scale_old, N, binoms, n_max, opacity_new, scale_new, s);
     return check_stage(s, false, "compute_relocation");
+}
+
+int hlgs_adam_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const uint8_t* visible,
+                     float lr, float b1, float b2, float eps, uint32_t N, uint32_t M, void* stream)
+{
+    if ((uint64_t)N * M == 0) return HLGS_OK;
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !visible) return fail(HLGS_ERR_ARG, "missing tensor");
+    if ((uint64_t)N * M > 0xffffffffull) return fail(HLGS_ERR_ARG, "N * M exceeds 2^32 elements");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_adam(param, grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps, N, M, s);
+    return check_stage(s, false, "adam_update");
 }
 
 // ---------------------------------------------------------------- LOD

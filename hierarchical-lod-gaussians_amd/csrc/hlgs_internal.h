@@ -48,7 +48,7 @@ struct Img {
     uint2* ranges;         // T: [start, end) into point_list
     uint32_t* tile_count;  // T
     uint32_t* tile_cursor; // T
-    uint32_t* misc;        // 16: [0] = R, [1] = max per-tile count
+    uint32_t* misc;        // 16: [0] = binned instances, [1] = longest per-tile list, [2] = record slots (point_offsets[P-1])
     uint32_t* scan_tmp;
 };
 Img carve_img(void* base, int W, int H, size_t* total);

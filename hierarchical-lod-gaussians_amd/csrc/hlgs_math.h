@@ -274,6 +274,45 @@ __device__ inline float alpha_e2_threshold(float o, bool interp, float t, float 
     return f;
 }
 
+// Alt rasterizer's exact per-tile culling (alt-rasterizer/cuda_rasterizer/rasterizer_impl.cu:52-101 with
+// PATCH = 15, applied at :147-179): the instance (Gaussian, tile (tx, ty)) exists only if the power at the
+// point of the tile's pixel box the reference takes as the closest one does not exceed log(o / (1/255)).
+// The binning and the backward's record reduction must decide identically, so the float operations keep the
+// reference's order with contraction off in every translation unit; the logarithm is taken in double and
+// rounded (the oracle's alt_tile_keep does the same), co = conic a, b, c and opacity.
+__device__ __forceinline__ float alt_keep_threshold(float o)
+{
+    return (float)log((double)(o / (1.0f / 255.0f)));
+}
+__device__ __forceinline__ bool alt_tile_keep(float mx, float my, float4 co, float thr, int tx, int ty)
+{
+#pragma clang fp contract(off)
+    const float rminx = (float)(tx * HLGS_TILE), rminy = (float)(ty * HLGS_TILE);
+    const float rmaxx = (float)((tx + 1) * HLGS_TILE - 1), rmaxy = (float)((ty + 1) * HLGS_TILE - 1);
+    const float x_min_diff = rminx - mx;
+    const float x_left = x_min_diff > 0.0f ? 1.0f : 0.0f;
+    const float not_in_x = x_left + (mx > rmaxx ? 1.0f : 0.0f);
+    const float y_min_diff = rminy - my;
+    const float y_above = y_min_diff > 0.0f ? 1.0f : 0.0f;
+    const float not_in_y = y_above + (my > rmaxy ? 1.0f : 0.0f);
+    float power = 0.0f;
+    if ((not_in_y + not_in_x) > 0.0f) {
+        const float px = x_left * rminx + (1.0f - x_left) * rmaxx;
+        const float py = y_above * rminy + (1.0f - y_above) * rmaxy;
+        const float dx = copysignf(15.0f, x_min_diff), dy = copysignf(15.0f, y_min_diff);
+        const float diffx = mx - px, diffy = my - py;
+        const float rcx = 1.0f / (225.0f * co.x), rcz = 1.0f / (225.0f * co.z);  // __frcp_rn: IEEE reciprocal
+        float sx = (dx * co.x * diffx + dx * co.y * diffy) * rcx;
+        float sy = (dy * co.y * diffx + dy * co.z * diffy) * rcz;
+        sx = sx != sx ? 0.0f : fminf(fmaxf(sx, 0.0f), 1.0f);  // __saturatef (NaN -> 0)
+        sy = sy != sy ? 0.0f : fminf(fmaxf(sy, 0.0f), 1.0f);
+        const float qx = px + not_in_y * sx * dx, qy = py + not_in_x * sy * dy;
+        const float ddx = mx - qx, ddy = my - qy;
+        power = 0.5f * (co.x * ddx * ddx + co.z * ddy * ddy) + co.y * ddx * ddy;
+    }
+    return power <= thr;
+}
+
 // Does the alpha >= 1/255 footprint of a splat (see quad_mask) reach the 8x8 pixel block at (qx, qy)?
 __device__ __forceinline__ bool touches_quad(float x, float y, float4 co, float qx, float qy)
 {

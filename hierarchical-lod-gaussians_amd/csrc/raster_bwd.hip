@@ -36,7 +36,9 @@ struct PixB {
 // so each pixel adds ten moments to acc and finish_record() applies the per-splat factors once.
 //   acc = [Sum w dx, Sum w dy, Sum w dx^2, Sum w dx dy, Sum w dy^2, Sum w*mult, dcolor r g b, dinvdepth]
 // q = (-a/2, -b, -c/2) * log2(e) so that G = exp2(q0 dx^2 + q1 dx dy + q2 dy^2) = exp(power).
-template <bool INTERP, bool DEPTH>
+// ALT: the alt rasterizer's backward (alt-rasterizer/cuda_rasterizer/backward.cu:596-624) has no
+// o * G > 0.99 => dL/dalpha = 0 rule; its doubled background term is folded into p.TB by the caller.
+template <bool INTERP, bool DEPTH, bool ALT>
 __device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& q, const float4& col,
                                          float invz, float tt, float fr, float thr, float (&acc)[10])
 {
@@ -60,7 +62,7 @@ __device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float d
         acc[8] += weight * p.db;
         if (DEPTH) acc[9] += weight * p.dinv;
         float dL_dalpha = raw * p.T - p.TB * r1m;
-        dL_dalpha = test_alpha > 0.99f ? 0.f : dL_dalpha;
+        if (!ALT) dL_dalpha = test_alpha > 0.99f ? 0.f : dL_dalpha;
         const float w = G * dL_dalpha;
         const float wdx = w * dx, wdy = w * dy;
         acc[0] += wdx;
@@ -109,7 +111,7 @@ struct BwdArgs {
 // each pass adding its per-(tile, Gaussian) records to the slots the first pass stored.  Records are
 // linear in the moments, so the sum equals the one-pass record up to float rounding.
 // One wave per tile, back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant.
-template <bool INTERP, bool DEPTH>
+template <bool INTERP, bool DEPTH, bool ALT>
 __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
 {
     const int tile = xcd_remap(blockIdx.x, A.T);
@@ -158,7 +160,9 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
         bgd += bg[0] * p.dr;
         bgd += bg[1] * p.dg;
         bgd += bg[2] * p.db;
-        p.TB = tf * bgd;
+        // the alt rasterizer's ar includes the final colour's T_final * bg and adds the bg term once more
+        // (alt-rasterizer backward.cu:608, 619): the background enters dL/dalpha twice
+        p.TB = ALT ? 2.f * (tf * bgd) : tf * bgd;
         p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
         uint32_t m = p.last;
         for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
@@ -218,7 +222,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     if ((qm >> k) & 1u)  // uniform branch
-                        any |= bwd_pair<INTERP, DEPTH>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), co, col,
+                        any |= bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), co, col,
                                                        xy.z, tf.x, tf.y, col.w, acc);
                 if (__ballot(any)) {
                     float r0, r1, r2;
@@ -251,7 +255,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
 
 // One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
 // backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
-template <bool HIER>
+template <bool HIER, bool ALT>
 __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
                                                    BwdScratch rec, hlgs_grads o, float fx, float fy, int has_depth)
 {
@@ -268,6 +272,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = 0.f;
             if (o.dsh && !a.shs)
                 for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+            if (o.ddc && !a.shs) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
             o.dscale[3 * idx] = 0.f; o.dscale[3 * idx + 1] = 0.f; o.dscale[3 * idx + 2] = 0.f;
             reinterpret_cast<float4*>(o.drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -275,8 +280,26 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     }
     // ---- per-Gaussian sum of the blend records (fixed order => deterministic)
     const uint32_t end = g.point_offsets[t_idx], start = end - g.tiles_touched[t_idx];
+    constexpr bool alt = ALT;
+    float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
+    float kx = 0.f, ky = 0.f, kthr = 0.f;
+    int kx0 = 0, ky0 = 0, kw = 1;
+    if (alt) {  // slots of tiles the binning culled (alt_tile_keep) hold no record: skip them
+        const float4 r0 = g.splat[4 * (size_t)t_idx], r1 = g.splat[4 * (size_t)t_idx + 1];
+        const float4 r3 = g.splat[4 * (size_t)t_idx + 3];
+        kx = r0.x; ky = r0.y;
+        kco = make_float4(r0.z, r0.w, r1.x, r1.y);
+        kthr = alt_keep_threshold(kco.w);
+        kx0 = __float_as_int(r3.y) & 0xffff;
+        ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
+        kw = __float_as_int(r3.z);
+    }
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f, s8 = 0.f, s9 = 0.f;
     for (uint32_t r = start; r < end; r++) {
+        if (alt) {
+            const int k = (int)(r - start);
+            if (!alt_tile_keep(kx, ky, kco, kthr, kx0 + k % kw, ky0 + k / kw)) continue;
+        }
         const float4 A = rec.recA[r];
         const float4 B = rec.recB[r];
         const float2 Cc = rec.recC[r];
@@ -306,12 +329,13 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     c_xx += h_var;
     c_yy += h_var;
     const float det_h = c_xx * c_yy - c_xy * c_xy;
-    const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
-    const float d_hs = s5 * a.opacities[idx];
-    const float dop = s5 * hs;
-    const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
-    float dxx, dxy, dyy;
-    {
+    float dop = s5;
+    float dxx = 0.f, dxy = 0.f, dyy = 0.f;
+    if (!alt || a.antialiasing) {  // the alt rasterizer applies the AA term only with antialiasing (backward.cu:212-245)
+        const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+        const float d_hs = s5 * a.opacities[idx];
+        dop = s5 * hs;
+        const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
         const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
         const float sqv = w * w + w * (x + y) + x * y - z * z;
         const float denom_f = d_inside / (sqv * sqv);
@@ -356,7 +380,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     const float dtx = xg * -fx * tz2 * dJ02;
     const float dty = yg * -fy * tz2 * dJ12;
     float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * t.x) * tz3 * dJ02 + (2 * fy * t.y) * tz3 * dJ12;
-    if (has_depth) dtz -= s9 / (t.z * t.z);
+    if (has_depth) dtz -= alt ? s9 * tz2 : s9 / (t.z * t.z);  // alt-rasterizer backward.cu:312
     const float* vm = a.viewmatrix;
     f3 dmean = mk(vm[0] * dtx + vm[1] * dty + vm[2] * dtz, vm[4] * dtx + vm[5] * dty + vm[6] * dtz,
                   vm[8] * dtx + vm[9] * dty + vm[10] * dtz);
@@ -377,6 +401,9 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     //      dmean3D (or to the parent-deferred share) after this kernel.
     if (!a.shs && o.dsh)
         for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+    // alt without higher-order coefficients: the reference skips the whole SH backward (backward.cu:443),
+    // so even dc gets no gradient
+    if (!a.shs && o.ddc) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
 
     // ---- cov3D backward (backward.cu:330-393)
     float dscale[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
@@ -469,11 +496,14 @@ __device__ __forceinline__ float sh_basis(int c, float x, float y, float z, floa
 // the wave stores the rows back.  Runs after k_gauss_bwd, whose dcolor output is dL/dRGB, and adds
 // dnormvdv(dir, dL/ddir) to dmean3D -- or, for a hierarchy child with a parent, (1 - t) of it to the
 // parent-deferred share (backward.cu:458-494).
-template <bool HIER, int MT>  // MT = 0: coefficient count a.M known only at run time (up to 16)
+// ALT (alt-rasterizer backward.cu:23-146): coefficient 0 is the separate dc row (gradient to ddc), and the
+// staged rows hold the M higher-order coefficients 1..M.
+template <bool HIER, int MT, bool ALT>  // MT = 0: staged row count a.M known only at run time (up to 16)
 __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
                                                BwdScratch rec, hlgs_grads o)
 {
-    constexpr int MC = MT ? MT : 16;
+    constexpr int OFF = ALT ? 1 : 0;  // full coefficient index of staged row 0
+    constexpr int MC = MT ? MT : (16 - OFF);
     const int M = MT ? MT : a.M;
     const int M3 = 3 * M;
     __shared__ float s_rows[64 * kShStride];
@@ -496,6 +526,7 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
 #pragma unroll
             for (int i = 0; i < 3 * MC; i++)
                 if (i < M3) row[i] = 0.f;
+            if (ALT) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
         } else {
             const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
             const f3 m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
@@ -508,25 +539,31 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
             const float dB = (cl & 4u) ? 0.f : o.dcolor[3 * idx + 2];
             const int ncoef = (a.D + 1) * (a.D + 1);
             float vx = 0.f, vy = 0.f, vz = 0.f;
-            float basis[MC];
+            float basis[MC + OFF];
 #pragma unroll
-            for (int c = 0; c < MC; c++) {
+            for (int c = 0; c < MC + OFF; c++) {
                 float gx, gy, gz;
                 basis[c] = c < ncoef ? sh_basis(c, x, y, z, gx, gy, gz) : 0.f;
                 if (c > 0 && c < ncoef) {
-                    const float proj = row[3 * c] * dR + row[3 * c + 1] * dG + row[3 * c + 2] * dB;
+                    const float* sc = row + 3 * (c - OFF);
+                    const float proj = sc[0] * dR + sc[1] * dG + sc[2] * dB;
                     vx += proj * gx;
                     vy += proj * gy;
                     vz += proj * gz;
                 }
             }
+            if (ALT) {
+                o.ddc[3 * idx] = basis[0] * dR;
+                o.ddc[3 * idx + 1] = basis[0] * dG;
+                o.ddc[3 * idx + 2] = basis[0] * dB;
+            }
 #pragma unroll
-            for (int c = 0; c < MC; c++) {
-                if (c >= M) break;
+            for (int c = OFF; c < MC + OFF; c++) {
+                if (c - OFF >= M) break;
                 const float bs = dropped ? 0.f : basis[c];
-                row[3 * c] = bs * dR;
-                row[3 * c + 1] = bs * dG;
-                row[3 * c + 2] = bs * dB;
+                row[3 * (c - OFF)] = bs * dR;
+                row[3 * (c - OFF) + 1] = bs * dG;
+                row[3 * (c - OFF) + 2] = bs * dB;
             }
             const f3 d = dnormvdv(dir_orig, mk(vx, vy, vz));
             if (dropped) {
@@ -562,9 +599,10 @@ void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
     const int T = gx * gy;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     BwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, im.final_T, im.n_contrib, a.bg, dL_dpix, dL_dinv, rs};
-#define HLGS_BB(I, Dp) hipLaunchKernelGGL((k_blend_bwd<I, Dp>), dim3(T), dim3(64), 0, s, A)
-    if (interp) { if (dL_dinv) HLGS_BB(true, true); else HLGS_BB(true, false); }
-    else { if (dL_dinv) HLGS_BB(false, true); else HLGS_BB(false, false); }
+#define HLGS_BB(I, Dp, Al) hipLaunchKernelGGL((k_blend_bwd<I, Dp, Al>), dim3(T), dim3(64), 0, s, A)
+    if (a.variant == HLGS_VARIANT_ALT) { if (dL_dinv) HLGS_BB(false, true, true); else HLGS_BB(false, false, true); }
+    else if (interp) { if (dL_dinv) HLGS_BB(true, true, false); else HLGS_BB(true, false, false); }
+    else { if (dL_dinv) HLGS_BB(false, true, false); else HLGS_BB(false, false, false); }
 #undef HLGS_BB
 }
 
@@ -574,25 +612,41 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
     const float fy = a.H / (2.0f * a.tanfovy);
     const float fx = a.W / (2.0f * a.tanfovx);
     const dim3 grid((a.P + 255) / 256), grid_sh((a.P + 63) / 64);
+#define HLGS_SHK(H, MT, AL) hipLaunchKernelGGL((k_sh_bwd<H, MT, AL>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o)
 #define HLGS_SHB(H)                                                                                        \
     switch (a.M) {                                                                                         \
-    case 1: hipLaunchKernelGGL((k_sh_bwd<H, 1>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;      \
-    case 4: hipLaunchKernelGGL((k_sh_bwd<H, 4>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;      \
-    case 9: hipLaunchKernelGGL((k_sh_bwd<H, 9>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;      \
-    case 16: hipLaunchKernelGGL((k_sh_bwd<H, 16>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;   \
-    default: hipLaunchKernelGGL((k_sh_bwd<H, 0>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o); break;     \
+    case 1: HLGS_SHK(H, 1, false); break;                                                                  \
+    case 4: HLGS_SHK(H, 4, false); break;                                                                  \
+    case 9: HLGS_SHK(H, 9, false); break;                                                                  \
+    case 16: HLGS_SHK(H, 16, false); break;                                                                \
+    default: HLGS_SHK(H, 0, false); break;                                                                 \
     }
     if (a.indices) {
-        hipLaunchKernelGGL(k_gauss_bwd<true>, grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
+        hipLaunchKernelGGL((k_gauss_bwd<true, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
         if (a.shs) HLGS_SHB(true)
         if (a.parent_indices)
             hipLaunchKernelGGL(k_parent_mean_add, grid, dim3(256), 0, s, a.P, radii, a.parent_indices,
                                rs.parent_dmean, o.dmean3D);
     } else {
-        hipLaunchKernelGGL(k_gauss_bwd<false>, grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
-        if (a.shs) HLGS_SHB(false)
+        if (a.variant == HLGS_VARIANT_ALT)
+            hipLaunchKernelGGL((k_gauss_bwd<false, true>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy,
+                               (int)has_depth);
+        else
+            hipLaunchKernelGGL((k_gauss_bwd<false, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy,
+                               (int)has_depth);
+        if (a.shs && a.variant == HLGS_VARIANT_ALT) {
+            switch (a.M) {  // rest coefficients of degree 1, 2, 3
+            case 3: HLGS_SHK(false, 3, true); break;
+            case 8: HLGS_SHK(false, 8, true); break;
+            case 15: HLGS_SHK(false, 15, true); break;
+            default: HLGS_SHK(false, 0, true); break;
+            }
+        } else if (a.shs) {
+            HLGS_SHB(false)
+        }
     }
 #undef HLGS_SHB
+#undef HLGS_SHK
 }
 
 }  // namespace hlgs

@@ -20,7 +20,7 @@ namespace hlgs {
 // ------------------------------------------------------------------------------------------------
 // Preprocess: one thread per rasterised Gaussian.
 // ------------------------------------------------------------------------------------------------
-template <bool HIER>
+template <bool HIER, bool ALT>
 __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, int* __restrict__ radii,
                                                     uint32_t* __restrict__ tile_count, int gx, int gy, float fx,
                                                     float fy)
@@ -93,7 +93,9 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
     cx += h_var;
     cz += h_var;
     const float det_h = cx * cz - cy * cy;
-    const float h_scale = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    float h_scale = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    constexpr bool alt = ALT;
+    if (alt && !a.antialiasing) h_scale = 1.0f;  // alt-rasterizer forward.cu:226-229
     const float det = det_h;
     if (det == 0.0f) return;
     const float det_inv = 1.f / det;
@@ -103,7 +105,10 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
     const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
     const float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
     const float pix_x = ndc2pix(ppx, a.W), pix_y = ndc2pix(ppy, a.H);
-    const int ex = (int)ceilf(3.f * sqrtf(cx)), ey = (int)ceilf(3.f * sqrtf(cz));
+    // per-axis 3-sigma rect (forward.cu:398-403); the alt rasterizer bins the eigen-radius square (its
+    // forward.cu:249), whose tiles it then culls exactly (alt_tile_keep)
+    const int ex = alt ? (int)my_radius : (int)ceilf(3.f * sqrtf(cx));
+    const int ey = alt ? (int)my_radius : (int)ceilf(3.f * sqrtf(cz));
     g.rects[t_idx] = make_int2(ex, ey);
     int x0, y0, x1, y1;
     tile_rect(pix_x, pix_y, ex, ey, gx, gy, x0, y0, x1, y1);
@@ -119,7 +124,13 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
         const float* sc = a.shs + (size_t)r_idx * a.M * 3;
         uint32_t cb = 0;
         f3 rgb;
-        if (!(HIER && use_parent)) {
+        if (alt) {
+            // alt-rasterizer forward.cu:23-75: coefficient 0 from dc, coefficient c >= 1 from shs[c - 1]
+            const float* d0 = a.dc + 3 * (size_t)r_idx;
+            rgb = sh_to_rgb(a.D, [&](int c) {
+                return c == 0 ? mk(d0[0], d0[1], d0[2]) : mk(sc[3 * c - 3], sc[3 * c - 2], sc[3 * c - 1]);
+            }, mean_r, campos, cb);
+        } else if (!(HIER && use_parent)) {
             rgb = sh_to_rgb(a.D, [&](int c) { return mk(sc[3 * c], sc[3 * c + 1], sc[3 * c + 2]); }, mean_r, campos, cb);
         } else {
             // forward.cu:86-138: every coefficient lerped child<->parent, view direction from the child
@@ -150,9 +161,13 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
         rec[3] = make_float4(0.f, __int_as_float(x0 | (y0 << 16)), __int_as_float(x1 - x0),
                              alpha_e2_threshold(opacity * h_scale, interp, tt, fr));
     }
-    if (tile_count)  // only when the tile grid is too large for the LDS-histogram binning
+    if (tile_count) {  // only when the tile grid is too large for the LDS-histogram binning
+        const float4 co = make_float4(conic_x, conic_y, conic_z, opacity * h_scale);
+        const float kthr = alt ? alt_keep_threshold(co.w) : 0.f;
         for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
+            for (int x = x0; x < x1; x++)
+                if (!alt || alt_tile_keep(pix_x, pix_y, co, kthr, x, y)) atomicAdd(&tile_count[y * gx + x], 1u);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -160,9 +175,11 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
 // instances are counted per tile in LDS and each non-empty bin costs one coalesced device atomic,
 // instead of one lane-scattered atomic per (Gaussian, tile) instance.
 // ------------------------------------------------------------------------------------------------
+// Calls f(idx, tile) for every binned instance of the block's Gaussians: every tile of the rect, or for the
+// alt rasterizer the tiles alt_tile_keep leaves (rasterizer_impl.cu:147-179 of alt-rasterizer).
 template <typename F>
 __device__ __forceinline__ void for_each_instance(int P, const int* __restrict__ radii, const Geom& g, int gx, int gy,
-                                                  F&& f)
+                                                  bool alt, F&& f)
 {
     const int g0 = blockIdx.x * kBinGauss, g1 = min(P, g0 + kBinGauss);
     for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += kBinThreads) {
@@ -171,19 +188,28 @@ __device__ __forceinline__ void for_each_instance(int P, const int* __restrict__
         const int2 ext = g.rects[idx];
         int x0, y0, x1, y1;
         tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
-        for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) f(idx, y * gx + x);
+        if (alt) {
+            const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
+            const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
+            const float thr = alt_keep_threshold(co.w);
+            for (int y = y0; y < y1; y++)
+                for (int x = x0; x < x1; x++)
+                    if (alt_tile_keep(xy.x, xy.y, co, thr, x, y)) f(idx, y * gx + x);
+        } else {
+            for (int y = y0; y < y1; y++)
+                for (int x = x0; x < x1; x++) f(idx, y * gx + x);
+        }
     }
 }
 
 __global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
-                                                             uint32_t* __restrict__ tile_count, int gx, int gy)
+                                                             uint32_t* __restrict__ tile_count, int gx, int gy, int alt)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     const int T = gx * gy;
     for (int t = threadIdx.x; t < T; t += kBinThreads) s_hist[t] = 0;
     __syncthreads();
-    for_each_instance(P, radii, g, gx, gy, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
+    for_each_instance(P, radii, g, gx, gy, alt, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += kBinThreads) {
         const uint32_t c = s_hist[t];
@@ -196,7 +222,8 @@ __global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* _
 // irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
 __global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
-                                                                  uint64_t* __restrict__ keys, int gx, int gy, Guard gd)
+                                                                  uint64_t* __restrict__ keys, int gx, int gy, int alt,
+                                                                  Guard gd)
 {
     if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
@@ -211,36 +238,41 @@ __global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const i
                 g.splat[4 * (size_t)idx + 3].x = __uint_as_float(g.point_offsets[idx] - g.tiles_touched[idx]);
     }
     __syncthreads();
-    for_each_instance(P, radii, g, gx, gy, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
+    for_each_instance(P, radii, g, gx, gy, alt, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += kBinThreads) {
         const uint32_t c = s_cnt[t];
         s_cnt[t] = c ? ranges[t].x + atomicAdd(&cursor[t], c) : 0u;
     }
     __syncthreads();
-    for_each_instance(P, radii, g, gx, gy, [&](int idx, int tile) {
+    for_each_instance(P, radii, g, gx, gy, alt, [&](int idx, int tile) {
         const uint32_t r = atomicAdd(&s_rank[tile], 1u);
         keys[s_cnt[tile] + r] = ((uint64_t)__float_as_uint(g.depths[idx]) << 32) | (uint32_t)idx;
     });
 }
 
 // ranges[t] = [incl[t] - count[t], incl[t]); misc[0] = R, misc[1] = max count; cursor reset for the scatter.
+// misc[2] = point_offsets[P - 1]: instances over all tile rects (record slots; == misc[0] unless culled).
 __global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict__ count, uint32_t* incl_and_cursor,
-                                                     uint2* __restrict__ ranges, uint32_t* __restrict__ misc, int T)
+                                                     uint2* __restrict__ ranges, uint32_t* __restrict__ misc, int T,
+                                                     const uint32_t* __restrict__ point_offsets, int P)
 {
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t >= T) return;
     const uint32_t c = count[t], e = incl_and_cursor[t];
     ranges[t] = make_uint2(e - c, e);
     incl_and_cursor[t] = 0;
-    if (t == T - 1) misc[0] = e;
+    if (t == T - 1) {
+        misc[0] = e;
+        misc[2] = P > 0 ? point_offsets[P - 1] : 0u;
+    }
     if (c) atomicMax(&misc[1], c);
 }
 
 // One thread per Gaussian: drop (depth, index) keys into each touched tile's segment.
 __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restrict__ radii, Geom g,
                                                       const uint2* __restrict__ ranges, uint32_t* cursor,
-                                                      uint64_t* __restrict__ keys, int gx, int gy, Guard gd)
+                                                      uint64_t* __restrict__ keys, int gx, int gy, int alt, Guard gd)
 {
     if (guard_fail(gd)) return;
     const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -251,8 +283,12 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
     int x0, y0, x1, y1;
     tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
     const uint64_t key = ((uint64_t)__float_as_uint(g.depths[idx]) << 32) | (uint32_t)idx;
+    const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
+    const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
+    const float kthr = alt ? alt_keep_threshold(co.w) : 0.f;
     for (int y = y0; y < y1; y++)
         for (int x = x0; x < x1; x++) {
+            if (alt && !alt_tile_keep(xy.x, xy.y, co, kthr, x, y)) continue;
             const int tile = y * gx + x;
             const uint32_t slot = atomicAdd(&cursor[tile], 1u);
             keys[ranges[tile].x + slot] = key;
@@ -480,7 +516,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             done = done || stop;
             if (__ballot(blended)) seen_mask |= 1ull << j;
         }
-        if ((seen_mask >> lane) & 1ull) A.seen[my_id] = 1;
+        if (A.seen && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
         __syncthreads();
     }
     if (px < A.W && py < A.H) {
@@ -541,12 +577,13 @@ static void allow_big_lds()
     done = true;
 }
 
-void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, hipStream_t s)
+void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
+                        hipStream_t s)
 {
     const size_t lds = sizeof(uint32_t) * (size_t)gx * gy;
     allow_big_lds();
     hipLaunchKernelGGL(k_count_tiles, dim3((P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads), lds, s, P, radii, g,
-                       tile_count, gx, gy);
+                       tile_count, gx, gy, (int)alt);
 }
 
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
@@ -556,30 +593,33 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
     const float fx = a.W / (2.0f * a.tanfovx);
     const dim3 grid((a.P + 255) / 256);
     if (a.indices)
-        hipLaunchKernelGGL(k_preprocess<true>, grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
+        hipLaunchKernelGGL((k_preprocess<true, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
+    else if (a.variant == HLGS_VARIANT_ALT)
+        hipLaunchKernelGGL((k_preprocess<false, true>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
     else
-        hipLaunchKernelGGL(k_preprocess<false>, grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
+        hipLaunchKernelGGL((k_preprocess<false, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
 }
 
-void launch_tile_ranges(const Img& im, int T, hipStream_t s)
+void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s)
 {
     hipLaunchKernelGGL(k_tile_ranges, dim3((T + 255) / 256), dim3(256), 0, s, im.tile_count, im.tile_cursor,
-                       im.ranges, im.misc, T);
+                       im.ranges, im.misc, T, point_offsets, P);
 }
 
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b,
                     int gx, int gy, uint32_t max_count, hipStream_t s, bool timing, Guard gd)
 {
     const int T = gx * gy;
+    const int alt = a.variant == HLGS_VARIANT_ALT;
     if (timing) stage_mark(s, 3, true);
     if (lds_binning(gx, gy)) {
         allow_big_lds();
         hipLaunchKernelGGL(k_scatter_keys_lds, dim3((a.P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads),
                            2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy,
-                           gd);
+                           alt, gd);
     } else
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
-                           im.tile_cursor, b.keys, gx, gy, gd);
+                           im.tile_cursor, b.keys, gx, gy, alt, gd);
     if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
     hipLaunchKernelGGL(k_tile_sort_wave, dim3(T), dim3(64), 0, s, im.ranges, b.keys, b.point_list, T, gd);
     if (max_count > (uint32_t)kWaveSortCap)

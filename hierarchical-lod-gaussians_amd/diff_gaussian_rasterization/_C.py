@@ -53,7 +53,8 @@ def _raster_args(bg, render_indices, parent_indices, ts, kids, means3D, colors, 
                      projmatrix=L.ptr(keep["proj"]), campos=L.ptr(keep["campos"]),
                      scale_modifier=float(scale_modifier), tanfovx=float(tan_fovx), tanfovy=float(tan_fovy),
                      indices=L.ptr(keep["indices"]), parent_indices=L.ptr(keep["parents"]), ts=L.ptr(keep["ts"]),
-                     kids=L.ptr(keep["kids"]), prefiltered=int(bool(prefiltered)), debug=int(bool(debug)))
+                     kids=L.ptr(keep["kids"]), prefiltered=int(bool(prefiltered)), debug=int(bool(debug)),
+                     dc=None, antialiasing=1, variant=L.VARIANT_HIERARCHY)
     return a, keep, P, P_full, M
 
 
@@ -88,7 +89,7 @@ def rasterize_gaussians(bg, render_indices, parent_indices, ts, kids, means3D, c
                                        binning.numel(), C.byref(info), L.ptr(color),
                                        L.ptr(invdepth) if do_depth else None, L.ptr(seen), s))
     if not info.rendered:
-        need = lib.hlgs_binning_buffer_size(info.num_rendered)
+        need = lib.hlgs_binning_buffer_size(info.num_binned)
         binning = torch.empty((need,), **u8)
         L.check(lib.hlgs_rasterize_forward_render(C.byref(a), L.ptr(radii), L.ptr(geom), L.ptr(img), L.ptr(binning),
                                                   C.byref(info), L.ptr(color), L.ptr(invdepth) if do_depth else None,

@@ -25,16 +25,20 @@ class RasterArgs(C.Structure):
                 ("scales", _vp), ("rotations", _vp), ("cov3D_precomp", _vp), ("viewmatrix", _vp),
                 ("projmatrix", _vp), ("campos", _vp), ("scale_modifier", _f), ("tanfovx", _f), ("tanfovy", _f),
                 ("indices", _vp), ("parent_indices", _vp), ("ts", _vp), ("kids", _vp), ("prefiltered", _i),
-                ("debug", _i)]
+                ("debug", _i), ("dc", _vp), ("antialiasing", _i), ("variant", _i)]
+
+
+VARIANT_HIERARCHY = 0
+VARIANT_ALT = 1
 
 
 class Grads(C.Structure):
     _fields_ = [("dmean2D", _vp), ("dcolor", _vp), ("dopacity", _vp), ("dmean3D", _vp), ("dcov3D", _vp),
-                ("dsh", _vp), ("dscale", _vp), ("drot", _vp)]
+                ("dsh", _vp), ("dscale", _vp), ("drot", _vp), ("ddc", _vp)]
 
 
 class FrameInfo(C.Structure):
-    _fields_ = [("num_rendered", _i), ("max_tile_count", _i), ("rendered", _i)]
+    _fields_ = [("num_rendered", _i), ("max_tile_count", _i), ("rendered", _i), ("num_binned", _i)]
 
 
 _SIGS = {
@@ -53,6 +57,7 @@ _SIGS = {
                                      C.POINTER(Grads), _vp]),
     "hlgs_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "hlgs_compute_relocation": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
+    "hlgs_adam_update": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, C.c_uint32, C.c_uint32, _vp]),
     "hlgs_lod_scratch_size": (_sz, [_i]),
     "hlgs_expand_to_size_dynamic": (_i, [_i, _f, _vp, _vp, _vp, _vp, C.POINTER(_f), _vp, _vp, _vp, _vp,
                                          C.POINTER(_i), _vp]),

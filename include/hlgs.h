@@ -22,6 +22,12 @@
  *        reference's candidate-count sync, runtime_switching.cu:926-931)
  *   hlgs_lod_interp_forward/_backward       <- the Python child/parent lerp of render_post,
  *        gaussian_renderer/__init__.py:304-339 (interp_python=True), and its autograd
+ *   hlgs_adam_update                        <- adamUpdate, submodules/alt-rasterizer/rasterize_points.cu:255-281
+ *        (kernel cuda_rasterizer/adam.cu:9-36), bound as _C.adamUpdate (ext.cpp:19)
+ *
+ * The alt rasterizer (submodules/alt-rasterizer: RasterizeGaussiansCUDA rasterize_points.cu:44-137 and
+ * RasterizeGaussiansBackwardCUDA :138-232) goes through the same rasterizer entry points with
+ * variant = HLGS_VARIANT_ALT (see hlgs_raster_args).
  *
  * Conventions: all pointers are device pointers unless a parameter says "host"; float = IEEE fp32,
  * int = int32; every array is dense and contiguous in the reference's layout (means (P,3), rotations
@@ -43,6 +49,13 @@ extern "C" {
 #define HLGS_OK 0
 #define HLGS_ERR_ARG 1
 #define HLGS_ERR_DEVICE 2
+
+/* Rasterizer variants (hlgs_raster_args.variant). */
+#define HLGS_VARIANT_HIERARCHY 0 /* submodules/hierarchy-rasterizer (diff_gaussian_rasterization) */
+#define HLGS_VARIANT_ALT 1       /* submodules/alt-rasterizer (alt_gaussian_rasterization): SH split into dc +
+                                    rest, optional antialiasing, eigen-radius tile rect with exact per-tile
+                                    culling (rasterizer_impl.cu:52-191), background rendered when nothing is
+                                    binned, inverse depth always, and its backward (backward.cu:452-624) */
 
 /* Arguments of one rasterizer call: the tensors RasterizeGaussiansCUDA receives. */
 typedef struct hlgs_raster_args {
@@ -69,6 +82,10 @@ typedef struct hlgs_raster_args {
     const int* kids;
     int prefiltered;
     int debug;                   /* synchronise + check after every stage (auxiliary.h:23-30) */
+    const float* dc;             /* HLGS_VARIANT_ALT: P x 3 degree-0 SH coefficient; shs then holds the M
+                                    higher-order ones (P x M x 3).  NULL otherwise. */
+    int antialiasing;            /* EWA opacity compensation; the hierarchy rasterizer always applies it */
+    int variant;                 /* HLGS_VARIANT_* */
 } hlgs_raster_args;
 
 /* Gradient outputs, all P_full rows; written completely by hlgs_rasterize_backward (no pre-zeroing). */
@@ -81,6 +98,7 @@ typedef struct hlgs_grads {
     float* dsh;       /* P_full x M x 3 (may be NULL when M == 0) */
     float* dscale;    /* P_full x 3 */
     float* drot;      /* P_full x 4 */
+    float* ddc;       /* HLGS_VARIANT_ALT: P_full x 3, else NULL */
 } hlgs_grads;
 
 const char* hlgs_last_error(void);
@@ -94,9 +112,12 @@ size_t hlgs_backward_scratch_size(int P, int R);
 
 /* Host-side result of phase 1. */
 typedef struct hlgs_frame_info {
-    int num_rendered;    /* R: Gaussian/tile instances (the reference's num_rendered) */
+    int num_rendered;    /* the reference's num_rendered: Gaussian/tile instances over every tile rect (the alt
+                            variant counts its culled instances too); sizes hlgs_backward_scratch_size */
     int max_tile_count;  /* longest per-tile list (selects the binning plan) */
     int rendered;        /* hlgs_rasterize_forward: 1 when phase 2 ran inside the call */
+    int num_binned;      /* instances actually binned into the per-tile lists (== num_rendered for the
+                            hierarchy rasterizer); sizes hlgs_binning_buffer_size */
 } hlgs_frame_info;
 
 /* Phase 1: preprocess + scans.  Writes radii (P), fills geom/img and *info (host).  One host
@@ -104,9 +125,9 @@ typedef struct hlgs_frame_info {
 int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* img, int* radii,
                                    hlgs_frame_info* info, void* stream);
 /* Phase 2: binning (per-tile depth sort) + front-to-back blend.  Every pixel of out_color (3,H,W) and
- * out_invdepth (H,W, or NULL when do_depth is off) is written; seen (P) must be zero-initialised by the
- * caller.  With R == 0 this is a no-op (the caller's zeroed output stays 0, not bg:
- * rasterizer_impl.cu:332-333). */
+ * out_invdepth (H,W, or NULL when do_depth is off) is written; seen (P, or NULL for the alt variant) must
+ * be zero-initialised by the caller.  With nothing binned this is a no-op for the hierarchy rasterizer
+ * (the caller's zeroed output stays 0, not bg: rasterizer_impl.cu:332-333); the alt variant renders bg. */
 int hlgs_rasterize_forward_render(const hlgs_raster_args* a, const int* radii, void* geom, void* img,
                                   void* binning, const hlgs_frame_info* info, float* out_color,
                                   float* out_invdepth, int* seen, void* stream);
@@ -120,7 +141,7 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
                            size_t binning_bytes, hlgs_frame_info* info, float* out_color, float* out_invdepth,
                            int* seen, void* stream);
 /* Backward: blend backward (per-tile partial sums, no float atomics) + fused covariance / SH / scale-
- * rotation backward.  dL_dinvdepth may be NULL (rasterize_points.cu:195-201). */
+ * rotation backward.  dL_dinvdepth may be NULL (rasterize_points.cu:195-201).  R = info.num_rendered. */
 int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,
                             const void* binning, int R, void* scratch, const float* dL_dcolor,
                             const float* dL_dinvdepth, const hlgs_grads* out, void* stream);
@@ -131,6 +152,13 @@ int hlgs_mark_visible(int P, const float* means3D, const float* viewmatrix, cons
 /* MCMC relocation, utils.cu:6-36.  scale_new is 3P floats. */
 int hlgs_compute_relocation(int P, const float* opacity_old, const float* scale_old, const int* N,
                             const float* binoms, int n_max, float* opacity_new, float* scale_new, void* stream);
+
+/* Sparse Adam step of SparseGaussianAdam (alt_gaussian_rasterization/__init__.py:244-271, adam.cu:9-36):
+ * for every element p of the N x M parameter whose Gaussian p / M is visible (visible: N bytes),
+ * m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2, param -= lr m / (sqrt(v) + eps).  No bias correction and
+ * no step counter, as the reference. */
+int hlgs_adam_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const uint8_t* visible,
+                     float lr, float b1, float b2, float eps, uint32_t N, uint32_t M, void* stream);
 
 /* ---- hierarchical LOD ---- */
 size_t hlgs_lod_scratch_size(int N);

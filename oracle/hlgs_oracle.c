@@ -203,6 +203,12 @@ typedef struct {
     const int *parent_indices;
     const float *ts;
     const int *kids;
+    /* alt-rasterizer variant (submodules/alt-rasterizer, AR below): SH split into dc (P x 3, degree 0) and
+     * shs = the M higher-order coefficients; AA opacity scaling optional; radius rect with exact per-tile
+     * culling; its own blend backward (AR/backward.cu:424-605). */
+    const float *dc;
+    int antialiasing;
+    int alt;
 } orc_args;
 
 /* Per-Gaussian geometry produced by the forward preprocess (HR/rasterizer_impl.h:29-45) */
@@ -275,7 +281,8 @@ static void preprocess_one(const orc_args *a, const orc_geom *g, int t_idx, int 
     cx += h_var;
     cz += h_var;
     const float det_h = cx * cz - cy * cy;
-    const float h_scale = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    float h_scale = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    if (a->alt && !a->antialiasing) h_scale = 1.0f; /* AR/forward.cu:226-229 */
     const float det = det_h;
     if (det == 0.0f) return;
     float det_inv = 1.f / det;
@@ -286,6 +293,7 @@ static void preprocess_one(const orc_args *a, const orc_geom *g, int t_idx, int 
     float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
     float pix[2] = {ndc2pix(pp[0], a->W), ndc2pix(pp[1], a->H)};
     int ex = f2i(ceilf(3.f * sqrtf(cx))), ey = f2i(ceilf(3.f * sqrtf(cz)));
+    if (a->alt) ex = ey = f2i(my_radius); /* AR/forward.cu:249: getRect with the eigen radius */
     g->rects[2 * t_idx] = ex;
     g->rects[2 * t_idx + 1] = ey;
     int x0, y0, x1, y1;
@@ -296,7 +304,15 @@ static void preprocess_one(const orc_args *a, const orc_geom *g, int t_idx, int 
         v3 campos = V3(a->campos[0], a->campos[1], a->campos[2]);
         v3 mean_r = V3(a->means3D[3 * r_idx], a->means3D[3 * r_idx + 1], a->means3D[3 * r_idx + 2]);
         v3 rgb;
-        if (!use_parent) {
+        if (a->alt) {
+            /* AR/forward.cu:23-75, 257: coefficient 0 from dc, coefficient k >= 1 from shs[k - 1] */
+            float tmp[16 * 3];
+            memset(tmp, 0, sizeof(tmp));
+            memcpy(tmp, a->dc + 3 * (size_t)r_idx, 3 * sizeof(float));
+            int nrest = a->M < 15 ? a->M : 15;
+            if (a->shs) memcpy(tmp + 3, a->shs + (size_t)r_idx * a->M * 3, sizeof(float) * 3 * nrest);
+            rgb = sh_to_rgb(a->D, tmp, mean_r, campos, &g->clamped[t_idx]);
+        } else if (!use_parent) {
             rgb = sh_to_rgb(a->D, a->shs + (size_t)r_idx * a->M * 3, mean_r, campos, &g->clamped[t_idx]);
         } else {
             /* HR/forward.cu:86-138: lerp every coefficient, view dir from the child mean */
@@ -350,7 +366,44 @@ typedef struct {
     uint32_t *n_contrib;/* N */
     uint32_t *ranges;   /* T x 2 */
     uint32_t *point_list; /* R */
+    const float *pixel_colors;    /* alt: the forward's colour output (AR/rasterizer_impl.cu:459) */
+    const float *pixel_invdepths; /* alt: the forward's inverse depth */
 } orc_img;
+
+/* AR/rasterizer_impl.cu:52-101 (max_contrib_power_rect_gaussian_float<15, 15>) and :147-179: does the
+ * Gaussian keep its instance in tile (tx, ty)?  The power at the point of the tile's pixel box that the
+ * reference takes as the closest one must not exceed log(o / (1/255)).  The float operations follow the
+ * reference's order (no contraction); the logarithm is taken in double and rounded, so this restatement and
+ * the HIP kernels (hlgs_math.h alt_tile_keep) make identical decisions. */
+static int alt_tile_keep(float mx, float my, const float *co, int tx, int ty)
+{
+    const float rminx = (float)(tx * TILE), rminy = (float)(ty * TILE);
+    const float rmaxx = (float)((tx + 1) * TILE - 1), rmaxy = (float)((ty + 1) * TILE - 1);
+    const float x_min_diff = rminx - mx;
+    const float x_left = x_min_diff > 0.0f;
+    const float not_in_x = x_left + (mx > rmaxx);
+    const float y_min_diff = rminy - my;
+    const float y_above = y_min_diff > 0.0f;
+    const float not_in_y = y_above + (my > rmaxy);
+    float power = 0.0f;
+    if ((not_in_y + not_in_x) > 0.0f) {
+        const float px = x_left * rminx + (1.0f - x_left) * rmaxx;
+        const float py = y_above * rminy + (1.0f - y_above) * rmaxy;
+        const float dx = copysignf(15.0f, x_min_diff), dy = copysignf(15.0f, y_min_diff);
+        const float diffx = mx - px, diffy = my - py;
+        const float rcx = 1.0f / (225.0f * co[0]), rcz = 1.0f / (225.0f * co[2]);
+        float sx = (dx * co[0] * diffx + dx * co[1] * diffy) * rcx;
+        float sy = (dy * co[1] * diffx + dy * co[2] * diffy) * rcz;
+        sx = sx != sx ? 0.0f : fminf(fmaxf(sx, 0.0f), 1.0f); /* __saturatef (NaN -> 0) */
+        sy = sy != sy ? 0.0f : fminf(fmaxf(sy, 0.0f), 1.0f);
+        const float tx_ = not_in_y * sx, ty_ = not_in_x * sy;
+        const float qx = px + tx_ * dx, qy = py + ty_ * dy;
+        const float ddx = mx - qx, ddy = my - qy;
+        power = 0.5f * (co[0] * ddx * ddx + co[2] * ddy * ddy) + co[1] * ddx * ddy;
+    }
+    const float thr = (float)log((double)(co[3] / (1.0f / 255.0f)));
+    return power <= thr;
+}
 
 /* Forward phase 2: duplicate, stable sort, ranges, blend (HR/rasterizer_impl.cu:335-399, HR/forward.cu:450-596) */
 
@@ -416,43 +469,56 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
     int W = a->W, H = a->H;
     memset(out_color, 0, sizeof(float) * 3 * (size_t)W * H);
     if (out_invdepth) memset(out_invdepth, 0, sizeof(float) * (size_t)W * H);
-    if (R == 0) return; /* A-7: output stays 0, not bg */
-    kv *buf = (kv *)malloc(sizeof(kv) * (size_t)R);
-    /* duplicateWithKeys, HR/rasterizer_impl.cu:70-115 */
+    memset(im->ranges, 0, sizeof(uint32_t) * 2 * (size_t)T);
+    if (R == 0 && !a->alt) return; /* A-7: output stays 0, not bg (the alt rasterizer renders bg) */
+    kv *buf = (kv *)malloc(sizeof(kv) * (size_t)(R > 0 ? R : 1));
+    /* duplicateWithKeys, HR/rasterizer_impl.cu:70-115; AR/rasterizer_impl.cu:120-191 adds the per-tile
+     * culling: a culled instance gets the sentinel key (tile 0xFFFFFFFF, depth FLT_MAX) and sorts last */
+    const float fltmax = FLT_MAX;
+    uint32_t maxbits;
+    memcpy(&maxbits, &fltmax, 4);
     for (int i = 0; i < a->P; i++) {
         if (g->radii[i] <= 0) continue;
         uint32_t off = i == 0 ? 0 : g->point_offsets[i - 1];
+        const uint32_t off_to = g->point_offsets[i];
         int x0, y0, x1, y1;
         get_rect(g->means2D[2 * i], g->means2D[2 * i + 1], g->rects[2 * i], g->rects[2 * i + 1], gx, gy, &x0, &y0, &x1, &y1);
         uint32_t dbits;
         memcpy(&dbits, &g->depths[i], 4);
         for (int y = y0; y < y1; y++)
             for (int x = x0; x < x1; x++) {
+                if (a->alt && !alt_tile_keep(g->means2D[2 * i], g->means2D[2 * i + 1], g->conic_opacity + 4 * i, x, y))
+                    continue;
                 buf[off].key = ((uint64_t)(uint32_t)(y * gx + x) << 32) | dbits;
                 buf[off].pos = off;
                 buf[off].val = (uint32_t)i;
                 off++;
             }
+        for (; off < off_to; off++) {
+            buf[off].key = ((uint64_t)0xFFFFFFFFu << 32) | maxbits;
+            buf[off].pos = off;
+            buf[off].val = 0xFFFFFFFFu;
+        }
     }
     /* stable radix sort == sort by (key, input position), App. A-4 */
     qsort(buf, (size_t)R, sizeof(kv), kv_cmp);
     for (int i = 0; i < R; i++) im->point_list[i] = buf[i].val;
-    /* identifyTileRanges, HR/rasterizer_impl.cu:120-142 */
-    memset(im->ranges, 0, sizeof(uint32_t) * 2 * (size_t)T);
+    /* identifyTileRanges, HR/rasterizer_impl.cu:120-142 (AR/rasterizer_impl.cu:195-220 skips the sentinel) */
     for (int i = 0; i < R; i++) {
         uint32_t cur = (uint32_t)(buf[i].key >> 32);
-        if (i == 0) im->ranges[2 * cur] = 0;
+        int valid = cur != 0xFFFFFFFFu;
+        if (i == 0) { if (valid) im->ranges[2 * cur] = 0; }
         else {
             uint32_t prev = (uint32_t)(buf[i - 1].key >> 32);
-            if (cur != prev) { im->ranges[2 * prev + 1] = i; im->ranges[2 * cur] = i; }
+            if (cur != prev) { im->ranges[2 * prev + 1] = i; if (valid) im->ranges[2 * cur] = i; }
         }
-        if (i == R - 1) im->ranges[2 * cur + 1] = R;
+        if (i == R - 1 && valid) im->ranges[2 * cur + 1] = R;
     }
     free(buf);
     const float *feat = a->colors_precomp ? a->colors_precomp : g->rgb;
     int do_interp = (a->ts != NULL && a->kids != NULL);
     float *thr = alpha_thresholds(a, g);
-    /* renderCUDA<3> per pixel, HR/forward.cu:450-596 */
+    /* renderCUDA<3> per pixel, HR/forward.cu:450-596 (AR/forward.cu:282-430) */
     for (int ty = 0; ty < gy; ty++)
         for (int tx = 0; tx < gx; tx++) {
             uint32_t rs = im->ranges[2 * (ty * gx + tx)], re = im->ranges[2 * (ty * gx + tx) + 1];
@@ -507,6 +573,7 @@ typedef struct {
     float *dsh;      /* x M*3 */
     float *dscale;   /* x3 */
     float *drot;     /* x4 */
+    float *ddc;      /* x3 (alt variant: gradient of the degree-0 coefficient) */
 } orc_grads;
 
 /* HR/backward.cu:498-721 (renderCUDA<3> backward) */
@@ -596,6 +663,79 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
     free(thr);
 }
 
+
+/* AR/backward.cu:452-605 (PerGaussianRenderCUDA), restated per pixel.  The reference walks each 32-splat
+ * bucket over the tile's pixels starting from the forward's sampled state (T, accumulated colour and inverse
+ * depth at the bucket's first splat); walking every pixel's list front to back from T = 1 and zero
+ * accumulators visits the same (pixel, splat) pairs with the same state.  ar = accumulated - final colour,
+ * where the final colour includes T_final * bg, and the bg term is added again (AR/backward.cu:608, 619);
+ * there is no o * G > 0.99 rule. */
+static void blend_backward_alt(const orc_args *a, const orc_geom *g, const orc_img *im, const float *dL_dpix,
+                               const float *dL_dinv, orc_grads *o)
+{
+    float *thr = alpha_thresholds(a, g);
+    int gx = (a->W + TILE - 1) / TILE, gy = (a->H + TILE - 1) / TILE;
+    int W = a->W, H = a->H;
+    const size_t HW = (size_t)W * H;
+    const float *col = a->colors_precomp ? a->colors_precomp : g->rgb;
+    const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+    for (int ty = 0; ty < gy; ty++)
+        for (int tx = 0; tx < gx; tx++) {
+            uint32_t rs = im->ranges[2 * (ty * gx + tx)], re = im->ranges[2 * (ty * gx + tx) + 1];
+            for (int py = ty * TILE; py < imin((ty + 1) * TILE, H); py++)
+                for (int px = tx * TILE; px < imin((tx + 1) * TILE, W); px++) {
+                    const size_t pid = (size_t)py * W + px;
+                    const float T_final = im->final_T[pid];
+                    const uint32_t last = im->n_contrib[pid];
+                    float T = 1.0f, ar[3], ard, dpix[3], dinv = dL_dinv ? dL_dinv[pid] : 0.0f;
+                    for (int ch = 0; ch < 3; ch++) {
+                        ar[ch] = -im->pixel_colors[ch * HW + pid];
+                        dpix[ch] = dL_dpix[ch * HW + pid];
+                    }
+                    ard = -im->pixel_invdepths[pid];
+                    for (uint32_t j = rs; j < re; j++) {
+                        if (j - rs >= last) break;
+                        const uint32_t id = im->point_list[j];
+                        const float dx = g->means2D[2 * id] - (float)px, dy = g->means2D[2 * id + 1] - (float)py;
+                        const float *co = g->conic_opacity + 4 * id;
+                        float q[3];
+                        conic_q(co, q);
+                        const float e2 = splat_e2(q, dx, dy);
+                        if (e2 > 0.0f) continue;
+                        const float G = exp2f(e2);
+                        const float alpha = fminf(0.99f, co[3] * G);
+                        if (e2 < thr[id]) continue; /* alpha < 1/255 */
+                        const float weight = alpha * T;
+                        float bg_dot = 0.0f, dL_dalpha = 0.0f;
+                        for (int ch = 0; ch < 3; ch++) {
+                            const float c = col[3 * id + ch];
+                            ar[ch] += weight * c;
+                            o->dcolor[3 * id + ch] += weight * dpix[ch];
+                            dL_dalpha += ((c * T) - (1.0f / (1.0f - alpha)) * (-ar[ch])) * dpix[ch];
+                            bg_dot += a->bg[ch] * dpix[ch];
+                        }
+                        const float invd = 1.f / g->depths[id];
+                        ard += weight * invd;
+                        if (o->dinvdepth) o->dinvdepth[id] += weight * dinv;
+                        dL_dalpha += ((invd * T) - (1.0f / (1.0f - alpha)) * (-ard)) * dinv;
+                        dL_dalpha += (-T_final / (1.0f - alpha)) * bg_dot;
+                        T *= (1.0f - alpha);
+                        const float dL_dG = co[3] * dL_dalpha;
+                        const float gdx = G * dx, gdy = G * dy;
+                        const float dG_ddelx = -gdx * co[0] - gdy * co[1];
+                        const float dG_ddely = -gdy * co[2] - gdx * co[1];
+                        o->dmean2D[3 * id] += dL_dG * dG_ddelx * ddelx_dx;
+                        o->dmean2D[3 * id + 1] += dL_dG * dG_ddely * ddely_dy;
+                        o->dconic[4 * id] += -0.5f * gdx * dx * dL_dG;
+                        o->dconic[4 * id + 1] += -0.5f * gdx * dy * dL_dG;
+                        o->dconic[4 * id + 3] += -0.5f * gdy * dy * dL_dG;
+                        o->dopacity[id] += G * dL_dalpha;
+                    }
+                }
+        }
+    free(thr);
+}
+
 /* HR/auxiliary.h:132-142 */
 static v3 dnormvdv(v3 v, v3 dv)
 {
@@ -609,15 +749,15 @@ static v3 dnormvdv(v3 v, v3 dv)
 }
 
 /* HR/backward.cu:23-142 */
-static void sh_backward(int idx, int t_idx, const orc_args *a, const orc_geom *g, orc_grads *o)
+static void sh_backward_rows(int idx, int t_idx, const orc_args *a, const orc_geom *g, orc_grads *o,
+                             const float *sh, float *dsh)
 {
-    int deg = a->D, M = a->M;
+    int deg = a->D;
     v3 pos = V3(a->means3D[3 * idx], a->means3D[3 * idx + 1], a->means3D[3 * idx + 2]);
     v3 campos = V3(a->campos[0], a->campos[1], a->campos[2]);
     v3 dir_orig = vsub(pos, campos);
     float len = sqrtf(vdot(dir_orig, dir_orig));
     v3 dir = V3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
-    const float *sh = a->shs + (size_t)idx * M * 3;
 #define SHV(k) V3(sh[3 * (k)], sh[3 * (k) + 1], sh[3 * (k) + 2])
     v3 dRGB = V3(o->dcolor[3 * idx], o->dcolor[3 * idx + 1], o->dcolor[3 * idx + 2]);
     uint8_t cl = g->clamped[t_idx];
@@ -626,7 +766,6 @@ static void sh_backward(int idx, int t_idx, const orc_args *a, const orc_geom *g
     dRGB.z *= (cl & 4) ? 0 : 1;
     v3 ddx = V3(0, 0, 0), ddy = V3(0, 0, 0), ddz = V3(0, 0, 0);
     float x = dir.x, y = dir.y, z = dir.z;
-    float *dsh = o->dsh + (size_t)idx * M * 3;
 #define PUT(k, s) do { v3 _v = vscale((s), dRGB); dsh[3 * (k)] = _v.x; dsh[3 * (k) + 1] = _v.y; dsh[3 * (k) + 2] = _v.z; } while (0)
     PUT(0, SH_C0);
     if (deg > 0) {
@@ -692,6 +831,24 @@ static void sh_backward(int idx, int t_idx, const orc_args *a, const orc_geom *g
     o->dmean3D[3 * idx + 1] += dm.y;
     o->dmean3D[3 * idx + 2] += dm.z;
 }
+static void sh_backward(int idx, int t_idx, const orc_args *a, const orc_geom *g, orc_grads *o)
+{
+    if (!a->alt) {
+        sh_backward_rows(idx, t_idx, a, g, o, a->shs + (size_t)idx * a->M * 3, o->dsh + (size_t)idx * a->M * 3);
+        return;
+    }
+    /* AR/backward.cu:23-146: coefficient 0 (dc) gets its own gradient, coefficients k >= 1 come from shs[k-1] */
+    float sh[16 * 3], dsh[16 * 3];
+    memset(sh, 0, sizeof(sh));
+    memset(dsh, 0, sizeof(dsh));
+    int nrest = a->M < 15 ? a->M : 15;
+    memcpy(sh, a->dc + 3 * (size_t)idx, 3 * sizeof(float));
+    memcpy(sh + 3, a->shs + (size_t)idx * a->M * 3, sizeof(float) * 3 * nrest);
+    sh_backward_rows(idx, t_idx, a, g, o, sh, dsh);
+    memcpy(o->ddc + 3 * (size_t)idx, dsh, 3 * sizeof(float));
+    int ncoef = (a->D + 1) * (a->D + 1) - 1;
+    for (int i = 0; i < 3 * ncoef && i < 3 * nrest; i++) o->dsh[(size_t)idx * a->M * 3 + i] = dsh[3 + i];
+}
 
 /* HR/backward.cu:330-393 */
 static void cov3d_backward(int idx, v3 scale, float mod, const float *q, orc_grads *o)
@@ -728,7 +885,8 @@ void orc_backward(const orc_args *a, const orc_geom *g, const orc_img *im, int R
 {
     const float focal_y = a->H / (2.0f * a->tanfovy);
     const float focal_x = a->W / (2.0f * a->tanfovx);
-    if (R > 0) blend_backward(a, g, im, dL_dpix, dL_dinv, o);
+    if (a->alt) blend_backward_alt(a, g, im, dL_dpix, dL_dinv, o);
+    else if (R > 0) blend_backward(a, g, im, dL_dpix, dL_dinv, o);
     const float *cov3Ds = a->cov3D_precomp ? a->cov3D_precomp : g->cov3D;
     /* computeCov2DCUDA */
     for (int t_idx = 0; t_idx < a->P; t_idx++) {
@@ -748,13 +906,13 @@ void orc_backward(const orc_args *a, const orc_geom *g, const orc_img *im, int R
         c_xx += h_var;
         c_yy += h_var;
         const float det_h = c_xx * c_yy - c_xy * c_xy;
-        const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
-        const float dop_v = o->dopacity[idx];
-        const float d_hs = dop_v * a->opacities[idx];
-        o->dopacity[idx] = dop_v * hs;
-        const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
-        float dxx, dxy, dyy;
-        {
+        float dxx = 0.f, dxy = 0.f, dyy = 0.f;
+        if (!a->alt || a->antialiasing) { /* AR/backward.cu:212-245: only with antialiasing */
+            const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+            const float dop_v = o->dopacity[idx];
+            const float d_hs = dop_v * a->opacities[idx];
+            o->dopacity[idx] = dop_v * hs;
+            const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
             const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
             const float sqv = w * w + w * (x + y) + x * y - z * z;
             const float denom_f = d_inside / (sqv * sqv);
@@ -799,7 +957,7 @@ void orc_backward(const orc_args *a, const orc_geom *g, const orc_img *im, int R
         float dtx = xg * -focal_x * tz2 * dJ02;
         float dty = yg * -focal_y * tz2 * dJ12;
         float dtz = -focal_x * tz2 * dJ00 - focal_y * tz2 * dJ11 + (2 * focal_x * t.x) * tz3 * dJ02 + (2 * focal_y * t.y) * tz3 * dJ12;
-        if (o->dinvdepth) dtz -= o->dinvdepth[idx] / (t.z * t.z);
+        if (o->dinvdepth) dtz -= a->alt ? o->dinvdepth[idx] * tz2 : o->dinvdepth[idx] / (t.z * t.z); /* AR/backward.cu:312 */
         const float *vm = a->viewmatrix;
         o->dmean3D[3 * idx] = vm[0] * dtx + vm[1] * dty + vm[2] * dtz;
         o->dmean3D[3 * idx + 1] = vm[4] * dtx + vm[5] * dty + vm[6] * dtz;

@@ -36,7 +36,8 @@ class _Args(C.Structure):
                 ("bg", _f), ("means3D", _f), ("shs", _f), ("colors_precomp", _f), ("opacities", _f),
                 ("scales", _f), ("rotations", _f), ("cov3D_precomp", _f), ("viewmatrix", _f),
                 ("projmatrix", _f), ("campos", _f), ("scale_modifier", C.c_float), ("tanfovx", C.c_float),
-                ("tanfovy", C.c_float), ("indices", _i), ("parent_indices", _i), ("ts", _f), ("kids", _i)]
+                ("tanfovy", C.c_float), ("indices", _i), ("parent_indices", _i), ("ts", _f), ("kids", _i),
+                ("dc", _f), ("antialiasing", C.c_int), ("alt", C.c_int)]
 
 
 class _Geom(C.Structure):
@@ -45,12 +46,13 @@ class _Geom(C.Structure):
 
 
 class _Img(C.Structure):
-    _fields_ = [("final_T", _f), ("n_contrib", _u), ("ranges", _u), ("point_list", _u)]
+    _fields_ = [("final_T", _f), ("n_contrib", _u), ("ranges", _u), ("point_list", _u), ("pixel_colors", _f),
+                ("pixel_invdepths", _f)]
 
 
 class _Grads(C.Structure):
     _fields_ = [("dmean2D", _f), ("dconic", _f), ("dopacity", _f), ("dcolor", _f), ("dinvdepth", _f),
-                ("dmean3D", _f), ("dcov3D", _f), ("dsh", _f), ("dscale", _f), ("drot", _f)]
+                ("dmean3D", _f), ("dcov3D", _f), ("dsh", _f), ("dscale", _f), ("drot", _f), ("ddc", _f)]
 
 
 _lib = None
@@ -107,8 +109,11 @@ class Frame:
 
 
 def _make_args(scene, cam, keep):
-    """scene: dict of numpy arrays; cam: dict(W,H,tanfovx,tanfovy,viewmatrix,projmatrix,campos,bg)."""
-    d = {k: (_f32(v) if k not in ("indices", "parent_indices", "kids") else _i32(v)) for k, v in scene.items()}
+    """scene: dict of numpy arrays; cam: dict(W,H,tanfovx,tanfovy,viewmatrix,projmatrix,campos,bg).
+    scene["alt"] = True selects the alt-rasterizer variant: scene["dc"] (P,1,3) holds the degree-0
+    coefficient, scene["shs"] (P,M,3) the M higher ones, scene["antialiasing"] the AA flag."""
+    d = {k: (_f32(v) if k not in ("indices", "parent_indices", "kids") else _i32(v)) for k, v in scene.items()
+         if not isinstance(v, (bool, int, float))}
     cd = {k: _f32(v) for k, v in cam.items() if k in ("viewmatrix", "projmatrix", "campos", "bg")}
     keep.extend(list(d.values()) + list(cd.values()))
     shs = d.get("shs")
@@ -122,7 +127,9 @@ def _make_args(scene, cam, keep):
               projmatrix=_p(cd["projmatrix"]), campos=_p(cd["campos"]),
               scale_modifier=float(scene.get("scale_modifier", 1.0)), tanfovx=float(cam["tanfovx"]),
               tanfovy=float(cam["tanfovy"]), indices=_p(d.get("indices"), _i),
-              parent_indices=_p(d.get("parent_indices"), _i), ts=_p(d.get("ts")), kids=_p(d.get("kids"), _i))
+              parent_indices=_p(d.get("parent_indices"), _i), ts=_p(d.get("ts")), kids=_p(d.get("kids"), _i),
+              dc=_p(d.get("dc")), antialiasing=int(bool(scene.get("antialiasing", True))),
+              alt=int(bool(scene.get("alt", False))))
     return a, P
 
 
@@ -156,9 +163,11 @@ def forward(scene, cam, do_depth=True):
     fr.n_contrib = np.zeros(W * H, np.uint32)
     fr.ranges = np.zeros((gx * gy, 2), np.uint32)
     fr.point_list = np.zeros(max(R, 1), np.uint32)
-    fr.img = _Img(_p(fr.final_T), _p(fr.n_contrib, _u), _p(fr.ranges, _u), _p(fr.point_list, _u))
     fr.color = np.zeros((3, H, W), np.float32)
+    do_depth = do_depth or bool(a.alt)  # the alt rasterizer always renders inverse depth
     fr.invdepth = np.zeros((1, H, W), np.float32) if do_depth else np.zeros((0, H, W), np.float32)
+    fr.img = _Img(_p(fr.final_T), _p(fr.n_contrib, _u), _p(fr.ranges, _u), _p(fr.point_list, _u), _p(fr.color),
+                  _p(fr.invdepth) if do_depth else C.cast(None, _f))
     fr.seen = np.zeros(P, np.int32)
     if P:
         L.orc_forward_render(C.byref(a), C.byref(fr.geom), C.byref(fr.img), R, _p(fr.color),
@@ -174,10 +183,10 @@ def backward(fr, scene, dL_dcolor, dL_dinvdepth=None):
     M = fr.args.M
     g = {k: np.zeros(s, np.float32) for k, s in dict(
         dmean2D=(Pf, 3), dconic=(Pf, 4), dopacity=(Pf, 1), dcolor=(Pf, 3), dmean3D=(Pf, 3), dcov3D=(Pf, 6),
-        dsh=(Pf, max(M, 0), 3), dscale=(Pf, 3), drot=(Pf, 4)).items()}
+        dsh=(Pf, max(M, 0), 3), dscale=(Pf, 3), drot=(Pf, 4), ddc=(Pf, 1, 3)).items()}
     g["dinvdepth"] = np.zeros((Pf, 1), np.float32) if dL_dinvdepth is not None else None
     gr = _Grads(*[_p(g[k]) for k in ("dmean2D", "dconic", "dopacity", "dcolor", "dinvdepth", "dmean3D", "dcov3D",
-                                    "dsh", "dscale", "drot")])
+                                    "dsh", "dscale", "drot", "ddc")])
     dpix = _f32(dL_dcolor)
     dinv = _f32(dL_dinvdepth) if dL_dinvdepth is not None else None
     if fr.P:

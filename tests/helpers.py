@@ -90,6 +90,8 @@ def oracle_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_c
 def rel_err(a, b):
     """max |a-b| / max |b| (per tensor) -- the 1e-3 gradient criterion of BASELINE.json north_star."""
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    if b.size == 0:
+        return 0.0 if a.size == 0 else float("inf")
     den = max(np.abs(b).max(), 1e-12)
     return float(np.abs(a - b).max() / den)
 

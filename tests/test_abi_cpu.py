@@ -28,9 +28,31 @@ def test_buffer_sizes_are_monotone_and_aligned():
     assert lib.hlgs_binning_buffer_size(2_500_000) >= 2_500_000 * 20
     assert lib.hlgs_backward_scratch_size(1000, 5000) >= 5000 * 40
     assert lib.hlgs_lod_scratch_size(10) > 0 and lib.hlgs_spt_work_size(10) > 0
-    # struct layouts the binding passes match the header (pointer-sized fields after six ints)
-    assert C.sizeof(L.RasterArgs) == 6 * 4 + 11 * 8 + 3 * 4 + 4 + 4 * 8 + 2 * 4
-    assert C.sizeof(L.Grads) == 8 * 8
+
+
+def _c_layout(struct, fields):
+    """sizeof and field offsets of a header struct, as gcc lays it out from include/hlgs.h itself."""
+    import os
+    import subprocess
+    import tempfile
+    body = "".join(f'printf("%zu\\n", offsetof({struct}, {f}));' for f in fields)
+    src = ('#include <stdio.h>\n#include <stddef.h>\n#include "hlgs.h"\n'
+           f'int main(void) {{ printf("%zu\\n", sizeof({struct})); {body} return 0; }}\n')
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "t.c"), os.path.join(d, "t")
+        open(c, "w").write(src)
+        subprocess.check_call(["gcc", "-I", os.path.dirname(L.HEADER), c, "-o", exe])
+        vals = [int(v) for v in subprocess.check_output([exe]).split()]
+    return vals[0], vals[1:]
+
+
+@pytest.mark.parametrize("cls,struct", [(L.RasterArgs, "hlgs_raster_args"), (L.Grads, "hlgs_grads"),
+                                        (L.FrameInfo, "hlgs_frame_info")])
+def test_ctypes_structs_match_header_layout(cls, struct):
+    names = [f[0] for f in cls._fields_]
+    size, offs = _c_layout(struct, names)
+    assert C.sizeof(cls) == size
+    assert [getattr(cls, n).offset for n in names] == offs
 
 
 def test_stage_names():

@@ -88,14 +88,35 @@ class _AAScale(torch.autograd.Function):
         return w * (w * y + y * y + z * z) * den, -2.0 * w * z * (w + x + y) * den, w * (w * x + x * x + z * z) * den
 
 
-def torch_render(sc, cam, fr, deg):
+class _ClampST(torch.autograd.Function):
+    """min(alpha, 0.99) whose gradient passes straight through: the alt rasterizer's backward has no
+    o * G > 0.99 => dL/dalpha = 0 rule (alt-rasterizer/cuda_rasterizer/backward.cu:596-624)."""
+
+    @staticmethod
+    def forward(ctx, a):
+        return torch.clamp(a, max=0.99)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+def torch_render(sc, cam, fr, deg, alt=False, aa=True):
     """Differentiable float64 forward with the reference's semantics; the per-tile sorted lists come from
-    the oracle frame (the sort itself has no gradient)."""
+    the oracle frame (the sort itself has no gradient).  alt=True: the alt rasterizer's forward (AA scaling
+    only when `aa`) with its backward's two departures from autograd modelled explicitly -- the clamp
+    gradient passes through, and the T_final * bg term enters dL/dalpha twice (backward.cu:608, 619)."""
     dt = torch.float64
     leaf = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=dt, requires_grad=True)  # noqa: E731
     P = sc["means3D"].shape[0]
     means, scales, rots = leaf(sc["means3D"]), leaf(sc["scales"]), leaf(sc["rotations"])
     opac, shs = leaf(sc["opacities"]), leaf(sc["shs"])
+    if alt:  # dc + rest as separate leaves, concatenated for the SH polynomial
+        dc_l = leaf(sc["dc"])
+        shs = leaf(sc["shs"])
+        sh_all = torch.cat([dc_l, shs], 1)
+    else:
+        sh_all = shs
     W, H = cam["W"], cam["H"]
     view = torch.tensor(cam["viewmatrix"].numpy().reshape(4, 4), dtype=dt)
     proj = torch.tensor(cam["projmatrix"].numpy().reshape(4, 4), dtype=dt)
@@ -126,13 +147,13 @@ def torch_render(sc, cam, fr, deg):
     JA = J @ A
     cov2 = JA @ Sig @ JA.transpose(1, 2)
     a, b, c = cov2[:, 0, 0], cov2[:, 0, 1], cov2[:, 1, 1]
-    hs = _AAScale.apply(a, b, c)
+    hs = _AAScale.apply(a, b, c) if aa else torch.ones_like(a)
     a, c = a + 0.3, c + 0.3
     det = a * c - b * b
     conic = torch.stack([c / det, -b / det, a / det], -1)
     o2 = opac[:, 0] * hs
     d = means - campos
-    rgb = _sh_rgb(deg, shs, d / d.norm(dim=1, keepdim=True))
+    rgb = _sh_rgb(deg, sh_all, d / d.norm(dim=1, keepdim=True))
     invz = 1.0 / tz
     bg = torch.tensor(cam["bg"].numpy(), dtype=dt)
     gx = (W + 15) // 16
@@ -150,7 +171,8 @@ def torch_render(sc, cam, fr, deg):
             dy = pix[ids, 1][None] - py
             cn = conic[ids]
             power = -0.5 * (cn[None, :, 0] * dx * dx + cn[None, :, 2] * dy * dy) - cn[None, :, 1] * dx * dy
-            alpha = torch.clamp(o2[ids][None] * torch.exp(power), max=0.99)
+            raw = o2[ids][None] * torch.exp(power)
+            alpha = _ClampST.apply(raw) if alt else torch.clamp(raw, max=0.99)
             keep = (power <= 0) & (alpha >= 1.0 / 255.0)
             alpha = torch.where(keep, alpha, torch.zeros_like(alpha))
             one_m = 1 - alpha
@@ -162,6 +184,8 @@ def torch_render(sc, cam, fr, deg):
             w = alpha * Tb
             Tf = Tb[:, -1] * (1 - alpha[:, -1])
             col = w @ rgb[ids] + Tf[:, None] * bg[None]
+            if alt:
+                col = col + (Tf - Tf.detach())[:, None] * bg[None]
             dep = w @ invz[ids]
         else:
             col = bg[None].expand(px.shape[0], 3)
@@ -169,7 +193,10 @@ def torch_render(sc, cam, fr, deg):
         hh, ww = len(ys), len(xs)
         color[:, ty0:ty0 + hh, tx0:tx0 + ww] = col.T.reshape(3, hh, ww)
         inv[0, ty0:ty0 + hh, tx0:tx0 + ww] = dep.reshape(hh, ww)
-    return dict(color=color, invdepth=inv, means=means, scales=scales, rots=rots, opac=opac, shs=shs, ndc=ndc)
+    out = dict(color=color, invdepth=inv, means=means, scales=scales, rots=rots, opac=opac, shs=shs, ndc=ndc)
+    if alt:
+        out["dc"] = dc_l
+    return out
 
 
 def _rel(a, b):
@@ -223,3 +250,55 @@ def test_oracle_point_list_is_stable_tile_depth_order():
         ids = fr.point_list[s:e]
         keys = [(fr.depths[i], i) for i in ids]
         assert keys == sorted(keys)
+
+
+def alt_scene(sc, antialiasing=True):
+    """The same Gaussians in the alt rasterizer's layout: dc (P,1,3) + the remaining coefficients."""
+    out = dict(sc)
+    out["dc"] = np.ascontiguousarray(sc["shs"][:, :1])
+    out["shs"] = np.ascontiguousarray(sc["shs"][:, 1:])
+    out["alt"] = True
+    out["antialiasing"] = antialiasing
+    return out
+
+
+@pytest.mark.parametrize("P,deg,W,H,bg,aa", [(250, 3, 64, 48, (0.0, 0.0, 0.0), True),
+                                             (300, 2, 48, 40, (0.2, 0.5, 0.8), False),
+                                             (200, 1, 40, 40, (0.3, 0.1, 0.6), True)])
+def test_alt_oracle_matches_float64_autograd(P, deg, W, H, bg, aa):
+    """alt-rasterizer restatement (dc/rest split, optional AA, per-tile culling, its own backward)."""
+    cam = S.make_camera(W, H, bg=bg)
+    sc = alt_scene(S.make_gaussians(P, deg, cam, seed=P + 7), aa)
+    sc["opacities"][: P // 10] = 0.999  # some splats reach the 0.99 clamp
+    fr = O.forward(sc, S.cam_numpy(cam))
+    assert fr.invdepth.shape == (1, H, W)
+    g, gd = S.upstream_grads(W, H)
+    gr = O.backward(fr, sc, g, gd)
+    tr = torch_render(sc, cam, fr, deg, alt=True, aa=aa)
+    assert _rel(fr.color, tr["color"].detach().numpy()) < 1e-5
+    assert _rel(fr.invdepth, tr["invdepth"].detach().numpy()) < 1e-5
+    loss = (tr["color"] * torch.tensor(g, dtype=torch.float64)).sum() + \
+        (tr["invdepth"] * torch.tensor(gd, dtype=torch.float64)).sum()
+    loss.backward()
+    vis = fr.radii > 0
+    checks = [("dmean3D", tr["means"].grad), ("dscale", tr["scales"].grad), ("drot", tr["rots"].grad),
+              ("dopacity", tr["opac"].grad), ("dsh", tr["shs"].grad), ("ddc", tr["dc"].grad)]
+    for name, ref in checks:
+        e = _rel(gr[name][vis], ref.numpy()[vis])
+        assert e < 2e-3, f"{name}: alt oracle vs autograd rel err {e}"
+    e = _rel(gr["dmean2D"][vis, :2], tr["ndc"].grad.numpy()[vis])
+    assert e < 2e-3, f"dmean2D: {e}"
+
+
+def test_alt_oracle_culls_tiles_and_renders_bg_when_empty():
+    cam = S.make_camera(64, 64, bg=(0.5, 0.25, 0.75))
+    sc = alt_scene(S.make_gaussians(400, 1, cam, seed=3))
+    fr = O.forward(sc, S.cam_numpy(cam))
+    kept = int((fr.ranges[:, 1] - fr.ranges[:, 0]).sum())
+    assert 0 < kept < fr.R  # some rect tiles are culled; num_rendered still counts them (sentinels)
+    assert np.all(fr.point_list[kept:] == 0xFFFFFFFF)
+    # every Gaussian/tile pair culled away contributes nothing: no pixel of that tile reaches alpha >= 1/255
+    sc["means3D"][:, 2] = -3.0  # everything behind the camera: R == 0, the alt rasterizer still renders bg
+    fr = O.forward(sc, S.cam_numpy(cam))
+    assert fr.R == 0
+    np.testing.assert_array_equal(fr.color, np.broadcast_to(np.float32([0.5, 0.25, 0.75])[:, None, None], (3, 64, 64)))
