@@ -32,6 +32,7 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
 void launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t s);
 void launch_relocation(int P, const float* oo, const float* so, const int* N, const float* binoms, int n_max,
                        float* on, float* sn, hipStream_t s);
+void launch_morton(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, hipStream_t s);
 void launch_adam(float* param, const float* grad, float* m, float* v, const uint8_t* vis, float lr, float b1, float b2,
                  float eps, uint32_t N, uint32_t M, hipStream_t s);
 void launch_expand_dynamic(int N, float target, const int* nodes, const float* pos, const float* scales,
@@ -130,6 +131,8 @@ static int fail(int code, const std::string& msg)
     g_err = msg;
     return code;
 }
+
+int fail_msg(int code, const std::string& msg) { return fail(code, msg); }  // hier_io.cpp
 
 #define HLGS_TRY_HIP(expr)                                                                            \
     do {                                                                                              \
@@ -508,6 +511,17 @@ int hlgs_adam_update(float* param, const float* grad, float* exp_avg, float* exp
     hipGetLastError();
     launch_adam(param, grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps, N, M, s);
     return check_stage(s, false, "adam_update");
+}
+
+int hlgs_morton_codes(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, void* stream)
+{
+    if (P < 0) return fail(HLGS_ERR_ARG, "P < 0");
+    if (P == 0) return HLGS_OK;
+    if (!xyz || !mn || !mx || !codes) return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_morton(P, xyz, mn, mx, codes, s);
+    return check_stage(s, false, "morton_codes");
 }
 
 // ---------------------------------------------------------------- LOD

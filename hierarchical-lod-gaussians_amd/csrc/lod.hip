@@ -409,4 +409,32 @@ void launch_lod_interp_bwd(int S, int n, int M3, const int* ridx, const int* pid
                        gop, gsh, dm, dsc, drot, dop, dsh);
 }
 
+// get_morton_indices (gaussianhierarchy/morton.cu:9-42, bound at torch_interface.cpp:246-260): 63-bit Morton
+// code of each position normalised to the [min, max] box and scaled by 2^21; the float -> int64 conversion
+// truncates and only bits 0..20 of each coordinate are interleaved, as the reference does.
+__global__ void __launch_bounds__(256) k_morton(int P, const float* __restrict__ xyz, const float* __restrict__ mn,
+                                                const float* __restrict__ mx, int64_t* __restrict__ codes)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    const float bx = mx[0] - mn[0], by = mx[1] - mn[1], bz = mx[2] - mn[2];
+    const float px = (xyz[3 * i] - mn[0]) / bx * (float)(1 << 21);
+    const float py = (xyz[3 * i + 1] - mn[1]) / by * (float)(1 << 21);
+    const float pz = (xyz[3 * i + 2] - mn[2]) / bz * (float)(1 << 21);
+    const int64_t q[3] = {(int64_t)px, (int64_t)py, (int64_t)pz};
+    int64_t code = 0;
+#pragma unroll
+    for (int b = 0; b < 21; ++b) {
+        code |= (q[0] >> b & 1) << (3 * b);
+        code |= (q[1] >> b & 1) << (3 * b + 1);
+        code |= (q[2] >> b & 1) << (3 * b + 2);
+    }
+    codes[i] = code;
+}
+
+void launch_morton(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_morton, g256(P), dim3(256), 0, s, P, xyz, mn, mx, codes);
+}
+
 }  // namespace hlgs

@@ -11,6 +11,14 @@ Signatures follow submodules/gaussianhierarchy/torch/torch_interface.h:36-95 as 
                                       num_kids) -> None
     get_spt_cut_cuda(number_of_SPTs, gaussian_indices, SPT_starts, SPT_max, SPT_min, SPT_indices,
                      SPT_distances) -> (cut, counts_prefix)
+    get_morton_indices(xyz, min, max, codes) -> None          (codes: int64, written in place)
+    load_hierarchy(filename) -> (pos, shs (P,16,3), alpha (P,1), log-scales, rotations, nodes (N,7), boxes (N,2,4))
+    load_dynamic_hierarchy(filename) -> (pos, shs (P,(deg+1)^2,3), alpha (P,1), log-scales, rotations, nodes (P,6))
+    write_hierarchy(filename, pos, shs, opacities, log_scales, rotations, nodes, boxes) -> None
+    write_dynamic_hierarchy(filename, pos, shs, opacities, log_scales, rotations, nodes, SH_degree) -> None
+    expand_to_target(nodes, target) -> int32 indices
+
+The file functions run in libhlgs.so's host code (no Eigen) and return CPU tensors, as the reference does.
 
 Output buffers are caller-allocated, full-size and written in place; only the first `count` entries are
 valid (render_hierarchy.py:36-40, 68-69).  The reference reads `viewdir` on the host for
@@ -168,3 +176,90 @@ def lod_interp_backward(S, ridx, pidx, w, rots, P, g_m, g_s, g_r, g_o, g_sh, sh_
                                          L.ptr(g_sh) if M3 else None, L.ptr(d_m), L.ptr(d_s), L.ptr(d_r), L.ptr(d_o),
                                          L.ptr(d_sh) if M3 else None, L.stream()))
     return d_m, d_s, d_r, d_o, d_sh
+
+
+def get_morton_indices(xyz, min, max, codes):  # noqa: A002  (the reference's parameter names)
+    """Morton code per position inside the [min, max] box, written into the int64 tensor `codes`
+    (morton.cu:9-58)."""
+    lib = L.load()
+    p = _f32(xyz)
+    mn = min.detach().reshape(-1)[:3].to(device=p.device, dtype=torch.float32).contiguous()
+    mx = max.detach().reshape(-1)[:3].to(device=p.device, dtype=torch.float32).contiguous()
+    if codes.dtype != torch.int64 or not codes.is_contiguous():
+        raise RuntimeError("codes must be a contiguous int64 tensor")
+    L.require_gpu(p, mn, mx, codes)
+    L.check(lib.hlgs_morton_codes(p.size(0), L.ptr(p), L.ptr(mn), L.ptr(mx), L.ptr(codes), L.stream()))
+
+
+def _info(filename, dynamic):
+    info = L.HierInfo()
+    L.check(L.load().hlgs_hier_info_read(str(filename).encode(), int(dynamic), C.byref(info)))
+    return info
+
+
+def _host_f32(t, *shape):
+    return t.detach().to("cpu", torch.float32).contiguous().reshape(*shape)
+
+
+def load_hierarchy(filename):
+    """LoadHierarchy (torch_interface.cpp:9-40): full or binary16 .hier -> CPU tensors
+    (pos (P,3), shs (P,16,3), alpha (P,1), log-scales (P,3), rotations (P,4), nodes (N,7) int32, boxes (N,2,4))."""
+    info = _info(filename, False)
+    P, N = info.G, info.N
+    f = lambda *sh: torch.empty(sh, dtype=torch.float32)  # noqa: E731
+    pos, shs, alpha, scales, rot, boxes = f(P, 3), f(P, 16, 3), f(P, 1), f(P, 3), f(P, 4), f(N, 2, 4)
+    nodes = torch.empty((N, 7), dtype=torch.int32)
+    L.check(L.load().hlgs_hier_load(str(filename).encode(), L.ptr(pos), L.ptr(rot), L.ptr(scales), L.ptr(alpha),
+                                    L.ptr(shs), L.ptr(nodes), L.ptr(boxes)))
+    return pos, shs, alpha, scales, rot, nodes, boxes
+
+
+def load_dynamic_hierarchy(filename):
+    """LoadDynamicHierarchy (torch_interface.cpp:43-74): .dhier -> CPU tensors (pos (P,3), shs (P,(deg+1)^2,3),
+    alpha (P,1), log-scales (P,3), rotations (P,4), nodes (P,6) int32 HierarchyNode rows)."""
+    info = _info(filename, True)
+    P = info.G
+    f = lambda *sh: torch.empty(sh, dtype=torch.float32)  # noqa: E731
+    pos, shs, alpha, scales, rot = f(P, 3), f(P, (info.sh_degree + 1) ** 2, 3), f(P, 1), f(P, 3), f(P, 4)
+    nodes = torch.empty((P, 6), dtype=torch.int32)
+    L.check(L.load().hlgs_dhier_load(str(filename).encode(), L.ptr(pos), L.ptr(rot), L.ptr(scales), L.ptr(alpha),
+                                     L.ptr(shs), L.ptr(nodes)))
+    return pos, shs, alpha, scales, rot, nodes
+
+
+def write_hierarchy(filename, pos, shs, opacities, log_scales, rotations, nodes, boxes):
+    """WriteHierarchy (torch_interface.cpp:77-104): the binary16 .hier layout (the reference writer's default)."""
+    P, N = pos.size(0), nodes.size(0)
+    a = [_host_f32(pos, P, 3), _host_f32(shs, P, 48), _host_f32(opacities, P), _host_f32(log_scales, P, 3),
+         _host_f32(rotations, P, 4)]
+    nd = nodes.detach().to("cpu", torch.int32).contiguous().reshape(N, 7)
+    bx = _host_f32(boxes, N, 8)
+    L.check(L.load().hlgs_hier_write(str(filename).encode(), P, N, *[L.ptr(x) for x in a], L.ptr(nd), L.ptr(bx), 1))
+
+
+def write_dynamic_hierarchy(filename, pos, shs, opacities, log_scales, rotations, nodes, SH_degree):
+    """WriteDynamicHierarchy (torch_interface.cpp:107-133): the first (deg+1)^2 x 3 floats of every SH row of
+    the contiguous `shs` are written (hierarchy_writer.cpp:133-150 writes that many bytes from its start)."""
+    P, N = pos.size(0), nodes.size(0)
+    deg = int(SH_degree)
+    flat = shs.detach().to("cpu", torch.float32).contiguous().reshape(-1)
+    need = P * 3 * (deg + 1) ** 2
+    if flat.numel() < need:
+        raise RuntimeError("shs holds fewer coefficients than SH_degree needs")
+    a = [_host_f32(pos, P, 3), flat[:need].contiguous(), _host_f32(opacities, P), _host_f32(log_scales, P, 3),
+         _host_f32(rotations, P, 4)]
+    nd = nodes.detach().to("cpu", torch.int32).contiguous().reshape(N, 6)
+    L.check(L.load().hlgs_dhier_write(str(filename).encode(), P, N, *[L.ptr(x) for x in a], L.ptr(nd), deg))
+
+
+def expand_to_target(nodes, target):
+    """ExpandToTarget (torch_interface.cpp:136-146): Gaussian indices of the static hierarchy cut at depth
+    `target` (traversal.cpp:15-39) as a CPU int32 tensor."""
+    lib = L.load()
+    nd = nodes.detach().to("cpu", torch.int32).contiguous()
+    N = nd.size(0)
+    count = C.c_int(0)
+    L.check(lib.hlgs_expand_to_target(N, L.ptr(nd), int(target), None, 0, C.byref(count)))
+    out = torch.empty((count.value,), dtype=torch.int32)
+    L.check(lib.hlgs_expand_to_target(N, L.ptr(nd), int(target), L.ptr(out), count.value, C.byref(count)))
+    return out

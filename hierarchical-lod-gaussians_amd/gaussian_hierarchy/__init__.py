@@ -1,15 +1,18 @@
-"""Drop-in `gaussian_hierarchy` for MI355X: the runtime LOD functions of `gaussian_hierarchy._C`
-(submodules/gaussianhierarchy/ext.cpp:15-27) plus `interpolate_lod`, a HIP replacement for the
+"""Drop-in `gaussian_hierarchy` for MI355X: every function of `gaussian_hierarchy._C`
+(submodules/gaussianhierarchy/ext.cpp:15-27: file I/O, traversal, runtime LOD cuts, Morton codes) plus
+`interpolate_lod`, a HIP replacement for the
 child/parent lerp `render_post` performs in Python (gaussian_renderer/__init__.py:304-339).
 """
 import torch
 
 from . import _C
-from ._C import (expand_to_size, expand_to_size_dynamic, get_interpolation_weights,  # noqa: F401
-                 get_interpolation_weights_dynamic, get_spt_cut_cuda)
+from ._C import (expand_to_size, expand_to_size_dynamic, expand_to_target, get_interpolation_weights,  # noqa: F401
+                 get_interpolation_weights_dynamic, get_morton_indices, get_spt_cut_cuda, load_dynamic_hierarchy,
+                 load_hierarchy, write_dynamic_hierarchy, write_hierarchy)
 
-__all__ = ["_C", "expand_to_size", "expand_to_size_dynamic", "get_interpolation_weights",
-           "get_interpolation_weights_dynamic", "get_spt_cut_cuda", "interpolate_lod"]
+__all__ = ["_C", "expand_to_size", "expand_to_size_dynamic", "expand_to_target", "get_interpolation_weights",
+           "get_interpolation_weights_dynamic", "get_morton_indices", "get_spt_cut_cuda", "interpolate_lod",
+           "load_dynamic_hierarchy", "load_hierarchy", "write_dynamic_hierarchy", "write_hierarchy"]
 
 
 class _InterpolateLOD(torch.autograd.Function):

@@ -37,6 +37,10 @@ class Grads(C.Structure):
                 ("dsh", _vp), ("dscale", _vp), ("drot", _vp), ("ddc", _vp)]
 
 
+class HierInfo(C.Structure):
+    _fields_ = [("format", _i), ("G", _i), ("N", _i), ("sh_degree", _i)]
+
+
 class FrameInfo(C.Structure):
     _fields_ = [("num_rendered", _i), ("max_tile_count", _i), ("rendered", _i), ("num_binned", _i)]
 
@@ -58,6 +62,13 @@ _SIGS = {
     "hlgs_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "hlgs_compute_relocation": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "hlgs_adam_update": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, C.c_uint32, C.c_uint32, _vp]),
+    "hlgs_morton_codes": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "hlgs_hier_info_read": (_i, [C.c_char_p, _i, C.POINTER(HierInfo)]),
+    "hlgs_hier_load": (_i, [C.c_char_p] + [_vp] * 7),
+    "hlgs_hier_write": (_i, [C.c_char_p, _i, _i] + [_vp] * 7 + [_i]),
+    "hlgs_dhier_load": (_i, [C.c_char_p] + [_vp] * 6),
+    "hlgs_dhier_write": (_i, [C.c_char_p, _i, _i] + [_vp] * 6 + [_i]),
+    "hlgs_expand_to_target": (_i, [_i, _vp, _i, _vp, _i, C.POINTER(_i)]),
     "hlgs_lod_scratch_size": (_sz, [_i]),
     "hlgs_expand_to_size_dynamic": (_i, [_i, _f, _vp, _vp, _vp, _vp, C.POINTER(_f), _vp, _vp, _vp, _vp,
                                          C.POINTER(_i), _vp]),

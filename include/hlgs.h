@@ -207,6 +207,43 @@ int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* p
                              const float* g_opac, const float* g_shs, float* d_means, float* d_scales,
                              float* d_rots, float* d_opac, float* d_shs, void* stream);
 
+/* Morton codes of P positions in the [mn, mx] box (device float3 each): get_morton_indices,
+ * gaussianhierarchy/morton.cu:9-58 via torch_interface.cpp:246-260 (used by GaussianModel.sort_morton,
+ * scene/gaussian_model.py:570-589). */
+int hlgs_morton_codes(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, void* stream);
+
+/* ---- hierarchy files and traversal (host code, host buffers; gaussianhierarchy/hierarchy_loader.cpp,
+ *      hierarchy_writer.cpp, traversal.cpp -- bound there as load_hierarchy, load_dynamic_hierarchy,
+ *      write_hierarchy, write_dynamic_hierarchy, expand_to_target: ext.cpp:16-20) ---- */
+#define HLGS_HIER_FULL 0    /* .hier, float32 (hierarchy_writer.cpp:33-57) */
+#define HLGS_HIER_HALF 1    /* .hier, binary16 attributes (the default of WriteHierarchy, :58-110) */
+#define HLGS_HIER_DYNAMIC 2 /* .dhier (HierarchyNode rows, :113-155) */
+typedef struct hlgs_hier_info {
+    int format;     /* HLGS_HIER_* */
+    int G;          /* Gaussians */
+    int N;          /* nodes (.dhier: == G, hierarchy_loader.cpp:185) */
+    int sh_degree;  /* .dhier: stored degree (SH rows hold (deg+1)^2 coefficients); .hier: 3 (48 floats) */
+} hlgs_hier_info;
+/* Sizes of a hierarchy file; dynamic != 0 reads the .dhier header. */
+int hlgs_hier_info_read(const char* path, int dynamic, hlgs_hier_info* info);
+/* LoadHierarchy (torch_interface.cpp:9-40): pos G x 3, rot G x 4, log_scales G x 3, opacities G, shs G x 48,
+ * nodes N x 7 int32 (Node), boxes N x 8 (minn xyzw, maxx xyzw); both the full and the half layout. */
+int hlgs_hier_load(const char* path, float* pos, float* rot, float* log_scales, float* opacities, float* shs,
+                   int* nodes, float* boxes);
+/* WriteHierarchy (torch_interface.cpp:77-104); compressed != 0 writes the binary16 layout (the reference's
+ * default) and fails with "Would lose information!" when a node count exceeds 32000. */
+int hlgs_hier_write(const char* path, int G, int N, const float* pos, const float* shs, const float* opacities,
+                    const float* log_scales, const float* rot, const int* nodes, const float* boxes, int compressed);
+/* LoadDynamicHierarchy (torch_interface.cpp:43-74): shs G x (deg+1)^2 x 3, nodes G x 6 int32 (HierarchyNode). */
+int hlgs_dhier_load(const char* path, float* pos, float* rot, float* log_scales, float* opacities, float* shs,
+                    int* nodes);
+/* WriteDynamicHierarchy (torch_interface.cpp:107-133): shs G x (deg+1)^2 x 3, nodes N x 6. */
+int hlgs_dhier_write(const char* path, int G, int N, const float* pos, const float* shs, const float* opacities,
+                     const float* log_scales, const float* rot, const int* nodes, int sh_degree);
+/* ExpandToTarget (torch_interface.cpp:136-146, traversal.cpp:15-39): Gaussian indices of the cut at node depth
+ * `target` over N static Nodes (host).  Writes min(count, capacity) entries to out (may be NULL to query). */
+int hlgs_expand_to_target(int N, const int* nodes, int target, int* out, int capacity, int* count);
+
 /* ---- inspection (tests): byte offsets of fields inside the caller's buffers, counted from the
  * buffer's first 256-byte-aligned address ---- */
 size_t hlgs_binning_point_list_offset(int R);  /* uint32 point_list[R] */

@@ -213,3 +213,20 @@ def test_in_kernel_hierarchy_mode_matches_oracle():
     for name, leaf_t in (("dmean3D", m), ("dopacity", o), ("dscale", s), ("drot", r), ("dsh", sh), ("dmean2D", m2)):
         e = rel_err(leaf_t.grad.cpu().numpy(), gr[name])
         assert e <= 1e-3, (name, e)
+
+
+def test_morton_codes_bit_exact():
+    """get_morton_indices (morton.cu:9-42) against the float32 numpy restatement, plus sort_morton's
+    permutation (gaussian_model.py:570-589) keeping the root first."""
+    import gaussian_hierarchy as GH
+    from hlgs_core import scene
+    from oracle import hier_format as HF
+    rng = np.random.default_rng(12)
+    xyz = rng.normal(0, 20, (50000, 3)).astype(np.float32)
+    mn, mx = xyz.min(0), xyz.max(0)
+    codes = torch.zeros(len(xyz), dtype=torch.int64, device=DEV)
+    GH.get_morton_indices(torch.tensor(xyz, device=DEV), torch.tensor(mn, device=DEV), torch.tensor(mx, device=DEV),
+                          codes)
+    np.testing.assert_array_equal(codes.cpu().numpy(), HF.morton_codes(xyz, mn, mx))
+    idx = scene.morton_order(torch.tensor(xyz, device=DEV), skybox_points=5).cpu().numpy()
+    assert idx[0] == 5 and sorted(idx.tolist()) == list(range(5, 50000))
