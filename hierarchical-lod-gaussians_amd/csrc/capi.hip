@@ -32,6 +32,16 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
 void launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t s);
 void launch_relocation(int P, const float* oo, const float* so, const int* N, const float* binoms, int n_max,
                        float* on, float* sn, hipStream_t s);
+size_t ssim_partials(int C, int H, int W);
+void launch_ssim_forward(int C, int H, int W, const float* img1, const float* img2, int valid, float* abc,
+                         float* partial, float* out, hipStream_t s);
+void launch_ssim_backward(int C, int H, int W, const float* img1, const float* img2, const float* abc,
+                          const float* coef, float* grad1, hipStream_t s);
+int depth_l1_blocks(long n);
+void launch_depth_l1_forward(long n, const float* inv, const float* mono, const float* mask, float* partial,
+                             float* out, hipStream_t s);
+void launch_depth_l1_backward(long n, const float* inv, const float* mono, const float* mask, const float* coef,
+                              float* grad, hipStream_t s);
 void launch_morton(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, hipStream_t s);
 void launch_adam(float* param, const float* grad, float* m, float* v, const uint8_t* vis, float lr, float b1, float b2,
                  float eps, uint32_t N, uint32_t M, hipStream_t s);
@@ -522,6 +532,63 @@ int hlgs_morton_codes(int P, const float* xyz, const float* mn, const float* mx,
     hipGetLastError();
     launch_morton(P, xyz, mn, mx, codes, s);
     return check_stage(s, false, "morton_codes");
+}
+
+// ---------------------------------------------------------------- losses
+size_t hlgs_ssim_scratch_size(int C, int H, int W)
+{
+    if (C <= 0 || H <= 0 || W <= 0) return kAlign;
+    return align_up(2 * sizeof(float) * ssim_partials(C, H, W)) + kAlign;
+}
+
+int hlgs_ssim_forward(int C, int H, int W, const float* img1, const float* img2, int valid, float* dmaps,
+                      void* scratch, float* out, void* stream)
+{
+    if (C <= 0 || H <= 0 || W <= 0) return fail(HLGS_ERR_ARG, "empty image");
+    if (valid && (H <= 10 || W <= 10)) return fail(HLGS_ERR_ARG, "padding='valid' needs images larger than 10x10");
+    if (!img1 || !img2 || !scratch || !out) return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_ssim_forward(C, H, W, img1, img2, valid, dmaps, static_cast<float*>(aligned(scratch)), out, s);
+    return check_stage(s, false, "ssim_forward");
+}
+
+int hlgs_ssim_backward(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
+                       const float* coef, float* grad_img1, void* stream)
+{
+    if (C <= 0 || H <= 0 || W <= 0) return fail(HLGS_ERR_ARG, "empty image");
+    if (!img1 || !img2 || !dmaps || !coef || !grad_img1) return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_ssim_backward(C, H, W, img1, img2, dmaps, coef, grad_img1, s);
+    return check_stage(s, false, "ssim_backward");
+}
+
+size_t hlgs_depth_l1_scratch_size(int64_t n)
+{
+    return align_up(sizeof(float) * (size_t)depth_l1_blocks(n > 0 ? n : 1)) + kAlign;
+}
+
+int hlgs_depth_l1_forward(int64_t n, const float* invdepth, const float* mono, const float* mask, void* scratch,
+                          float* out, void* stream)
+{
+    if (n <= 0) return fail(HLGS_ERR_ARG, "empty depth map");
+    if (!invdepth || !mono || !scratch || !out) return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_depth_l1_forward(n, invdepth, mono, mask, static_cast<float*>(aligned(scratch)), out, s);
+    return check_stage(s, false, "depth_l1_forward");
+}
+
+int hlgs_depth_l1_backward(int64_t n, const float* invdepth, const float* mono, const float* mask, const float* coef,
+                           float* grad, void* stream)
+{
+    if (n <= 0) return fail(HLGS_ERR_ARG, "empty depth map");
+    if (!invdepth || !mono || !coef || !grad) return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_depth_l1_backward(n, invdepth, mono, mask, coef, grad, s);
+    return check_stage(s, false, "depth_l1_backward");
 }
 
 // ---------------------------------------------------------------- LOD

@@ -63,6 +63,12 @@ _SIGS = {
     "hlgs_compute_relocation": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "hlgs_adam_update": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, C.c_uint32, C.c_uint32, _vp]),
     "hlgs_morton_codes": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "hlgs_ssim_scratch_size": (_sz, [_i, _i, _i]),
+    "hlgs_ssim_forward": (_i, [_i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
+    "hlgs_ssim_backward": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "hlgs_depth_l1_scratch_size": (_sz, [C.c_int64]),
+    "hlgs_depth_l1_forward": (_i, [C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "hlgs_depth_l1_backward": (_i, [C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hlgs_hier_info_read": (_i, [C.c_char_p, _i, C.POINTER(HierInfo)]),
     "hlgs_hier_load": (_i, [C.c_char_p] + [_vp] * 7),
     "hlgs_hier_write": (_i, [C.c_char_p, _i, _i] + [_vp] * 7 + [_i]),

@@ -212,6 +212,28 @@ int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* p
  * scene/gaussian_model.py:570-589). */
 int hlgs_morton_codes(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, void* stream);
 
+/* ---- photometric losses of the training step (utils/loss_utils.py:17-63, train_single.py:106-121,
+ *      train_post.py:558-559 with the un-vendored fused_ssim) ---- */
+/* SSIM of C planes of H x W (11x11 Gaussian window, sigma 1.5, zero padding, C1 = 0.01^2, C2 = 0.03^2:
+ * _ssim, loss_utils.py:44-63).  out (device, 2 floats) = (mean of the SSIM map -- over the interior
+ * [5, H-5) x [5, W-5) when valid != 0, fused_ssim padding="valid" --, mean |img1 - img2| = l1_loss).
+ * dmaps (C x 3 x H x W, or NULL when no gradient is needed) receives the map's derivatives with respect to the
+ * window moments for hlgs_ssim_backward.  scratch: hlgs_ssim_scratch_size bytes. */
+size_t hlgs_ssim_scratch_size(int C, int H, int W);
+int hlgs_ssim_forward(int C, int H, int W, const float* img1, const float* img2, int valid, float* dmaps,
+                      void* scratch, float* out, void* stream);
+/* grad_img1 = coef[0] * d(sum of the SSIM map)/d img1 + coef[1] * sign(img1 - img2); coef is a device array so
+ * the upstream gradient never needs a host read. */
+int hlgs_ssim_backward(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
+                       const float* coef, float* grad_img1, void* stream);
+/* Depth term of train_single.py:111-118: out[0] = mean |(invdepth - mono) * mask| over n values (mask may be
+ * NULL); backward grad = coef[0] * sign((invdepth - mono) * mask) * mask. */
+size_t hlgs_depth_l1_scratch_size(int64_t n);
+int hlgs_depth_l1_forward(int64_t n, const float* invdepth, const float* mono, const float* mask, void* scratch,
+                          float* out, void* stream);
+int hlgs_depth_l1_backward(int64_t n, const float* invdepth, const float* mono, const float* mask, const float* coef,
+                           float* grad, void* stream);
+
 /* ---- hierarchy files and traversal (host code, host buffers; gaussianhierarchy/hierarchy_loader.cpp,
  *      hierarchy_writer.cpp, traversal.cpp -- bound there as load_hierarchy, load_dynamic_hierarchy,
  *      write_hierarchy, write_dynamic_hierarchy, expand_to_target: ext.cpp:16-20) ---- */

@@ -7,6 +7,9 @@ where /root/reference exists; the fixtures are committed so tests never need the
                      (forward.cu:25-76), incl. the +0.5 and clamp_min(0).
   golden_camera.npz  world_view_transform / full_proj_transform / camera_center built with
                      utils/graphics_utils.getWorld2View2 + getProjectionMatrix as scene/cameras.py:102-107 does.
+  golden_loss.npz    utils/loss_utils.l1_loss / ssim values and their autograd gradients w.r.t. the rendered image,
+                     and the full training loss of train_single.py:106-118 (L1, D-SSIM and the masked inverse-depth
+                     L1) with its gradients w.r.t. image and inverse depth, in float32 on the CPU.
 
 Only data (inputs and expected outputs) is written; no reference source is copied.
 """
@@ -67,7 +70,39 @@ def main():
         cams[f"R_{i}"], cams[f"T_{i}"], cams[f"WH_{i}"] = R, T, np.array([W, H])
         cams[f"view_{i}"], cams[f"proj_{i}"], cams[f"campos_{i}"] = wv.numpy(), full.numpy(), cc.numpy()
     np.savez_compressed(os.path.join(OUT, "golden_camera.npz"), **cams)
-    print("wrote golden_sh.npz, golden_camera.npz")
+
+    # ---- losses: the reference's own l1_loss / ssim and the train_single.py loss expression
+    from utils.loss_utils import l1_loss, ssim
+    loss = {}
+    for i, (C, H, W) in enumerate([(3, 37, 53), (3, 64, 48), (1, 20, 31)]):
+        img = rng.uniform(0, 1, (C, H, W)).astype(np.float32)
+        gt = np.clip(img + rng.normal(0, 0.15, (C, H, W)), 0, 1).astype(np.float32)
+        gt[:, :3, :5] = img[:, :3, :5]  # exact ties: |x - y| = 0 has gradient 0
+        inv = rng.uniform(0.05, 0.5, (1, H, W)).astype(np.float32)
+        mono = (inv + rng.normal(0, 0.05, (1, H, W))).astype(np.float32)
+        mask = (rng.uniform(0, 1, (1, H, W)) < 0.8).astype(np.float32)
+        lam, dw = 0.2, 0.5
+        ti = torch.tensor(img, requires_grad=True)
+        s_val = ssim(ti, torch.tensor(gt))
+        (g_ssim,) = torch.autograd.grad(s_val, ti)
+        ti = torch.tensor(img, requires_grad=True)
+        l_val = l1_loss(ti, torch.tensor(gt))
+        (g_l1,) = torch.autograd.grad(l_val, ti)
+        ti = torch.tensor(img, requires_grad=True)
+        tinv = torch.tensor(inv, requires_grad=True)
+        Ll1 = l1_loss(ti, torch.tensor(gt))
+        Lssim = (1.0 - ssim(ti, torch.tensor(gt)))
+        total = (1.0 - lam) * Ll1 + lam * Lssim
+        Ld = torch.abs((tinv - torch.tensor(mono)) * torch.tensor(mask)).mean()
+        total = total + dw * Ld
+        g_img, g_inv = torch.autograd.grad(total, (ti, tinv))
+        for k, v in dict(img=img, gt=gt, inv=inv, mono=mono, mask=mask, ssim=s_val.detach().numpy(),
+                         g_ssim=g_ssim.numpy(), l1=l_val.detach().numpy(), g_l1=g_l1.numpy(),
+                         loss=total.detach().numpy(), depth_l1=Ld.detach().numpy(), g_img=g_img.numpy(),
+                         g_inv=g_inv.numpy(), lam=np.float32(lam), dw=np.float32(dw)).items():
+            loss[f"{k}_{i}"] = v
+    np.savez_compressed(os.path.join(OUT, "golden_loss.npz"), **loss)
+    print("wrote golden_sh.npz, golden_camera.npz, golden_loss.npz")
 
 
 if __name__ == "__main__":
