@@ -63,9 +63,11 @@ void launch_spt_finish(int s_, int E, int n, const int* gidx, const int* starts,
 void launch_lod_interp_fwd(int S, int n, int M3, const int* ridx, const int* pidx, const float* w, const float* means,
                            const float* scales, const float* rots, const float* opac, const float* shs, float* om,
                            float* osc, float* orot, float* oop, float* osh, hipStream_t s);
-void launch_lod_interp_bwd(int S, int n, int M3, const int* ridx, const int* pidx, const float* w, const float* rots,
-                           const float* gm, const float* gsc, const float* grot, const float* gop, const float* gsh,
-                           float* dm, float* dsc, float* drot, float* dop, float* dsh, hipStream_t s);
+size_t lerp_bwd_scratch_elems(int P, int n);
+void launch_lod_interp_bwd(int P, int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
+                           const float* rots, const float* gm, const float* gsc, const float* grot, const float* gop,
+                           const float* gsh, float* dm, float* dsc, float* drot, float* dop, float* dsh, void* scratch,
+                           hipStream_t s);
 
 // ---------------------------------------------------------------- buffer carving
 template <typename T>
@@ -781,17 +783,25 @@ int hlgs_lod_interp_forward(int S, int n, int M3, const int* ridx, const int* pi
     return check_stage(s, false, "lod_interp_forward");
 }
 
-int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
+size_t hlgs_lod_interp_scratch_size(int P, int n)
+{
+    return 4 * lerp_bwd_scratch_elems(P < 0 ? 0 : P, n < 0 ? 0 : n) + kAlign;
+}
+
+int hlgs_lod_interp_backward(int P, int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
                              const float* rots, const float* g_means, const float* g_scales, const float* g_rots,
                              const float* g_opac, const float* g_shs, float* d_means, float* d_scales,
-                             float* d_rots, float* d_opac, float* d_shs, void* stream)
+                             float* d_rots, float* d_opac, float* d_shs, void* scratch, void* stream)
 {
-    if (S < 0 || n < 0 || M3 < 0) return fail(HLGS_ERR_ARG, "negative size");
-    if (S + n == 0) return HLGS_OK;
+    if (P < 0 || S < 0 || n < 0 || M3 < 0) return fail(HLGS_ERR_ARG, "negative size");
+    if (M3 > 64) return fail(HLGS_ERR_ARG, "SH rows of more than 64 floats");
+    if (S > P) return fail(HLGS_ERR_ARG, "skybox prefix longer than the gradient rows");
+    if (P == 0) return HLGS_OK;
+    if (!scratch) return fail(HLGS_ERR_ARG, "missing scratch");
     hipStream_t s = (hipStream_t)stream;
     hipGetLastError();
-    launch_lod_interp_bwd(S, n, M3, ridx, pidx, w, rots, g_means, g_scales, g_rots, g_opac, M3 ? g_shs : nullptr,
-                          d_means, d_scales, d_rots, d_opac, M3 ? d_shs : nullptr, s);
+    launch_lod_interp_bwd(P, S, n, M3, ridx, pidx, w, rots, g_means, g_scales, g_rots, g_opac, M3 ? g_shs : nullptr,
+                          d_means, d_scales, d_rots, d_opac, M3 ? d_shs : nullptr, aligned(scratch), s);
     return check_stage(s, false, "lod_interp_backward");
 }
 

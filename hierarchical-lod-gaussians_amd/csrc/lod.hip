@@ -252,6 +252,35 @@ __global__ void __launch_bounds__(256) k_excl_from_incl(int s, const uint32_t* _
 }
 
 // ---- render_post lerp: one thread per output row
+// render_post lerp, one row per 16-lane group (four rows per wave): the group's lanes walk the row's SH floats
+// with unit stride, so every load / store / atomic instruction covers a contiguous 64-byte segment of one row
+// instead of one float in each of 64 rows.  Lanes 0-2 also do the mean, 3-5 the scale, 6-9 the rotation (the
+// sign of <q_child, q_parent> from the whole quaternions), 10 the opacity.  Rows [0, S) are the uninterpolated
+// skybox prefix.
+struct LerpRow {
+    int o, c, p;
+    float t, u;
+    bool skip;
+};
+__device__ __forceinline__ LerpRow lerp_row(int S, int n, const int* __restrict__ ridx, const int* __restrict__ pidx,
+                                            const float* __restrict__ w)
+{
+    LerpRow r;
+    r.o = blockIdx.x * 16 + (threadIdx.x >> 4);
+    r.skip = r.o >= S + n;
+    r.c = r.p = r.o;
+    r.t = 1.f;
+    r.u = 0.f;
+    if (!r.skip && r.o >= S) {
+        const int i = r.o - S;
+        r.c = ridx[i];
+        r.p = pidx[i];
+        r.t = w[i];
+        r.u = 1 - w[i];
+    }
+    return r;
+}
+
 __global__ void __launch_bounds__(256) k_lod_interp_fwd(int S, int n, int M3, const int* __restrict__ ridx,
                                                         const int* __restrict__ pidx, const float* __restrict__ w,
                                                         const float* __restrict__ means, const float* __restrict__ scales,
@@ -260,79 +289,166 @@ __global__ void __launch_bounds__(256) k_lod_interp_fwd(int S, int n, int M3, co
                                                         float* __restrict__ osc, float* __restrict__ orot,
                                                         float* __restrict__ oop, float* __restrict__ osh)
 {
-    const int o = blockIdx.x * 256 + threadIdx.x;
-    if (o >= S + n) return;
-    if (o < S) {
-        for (int k = 0; k < 3; k++) { om[3 * o + k] = means[3 * o + k]; osc[3 * o + k] = scales[3 * o + k]; }
-        reinterpret_cast<float4*>(orot)[o] = reinterpret_cast<const float4*>(rots)[o];
-        oop[o] = opac[o];
-        if (shs)
-            for (int k = 0; k < M3; k++) osh[(size_t)M3 * o + k] = shs[(size_t)M3 * o + k];
-        return;
+    const LerpRow r = lerp_row(S, n, ridx, pidx, w);
+    if (r.skip) return;
+    const int l = threadIdx.x & 15;
+    const bool sky = r.o < S;
+    if (shs) {
+        const float* sc = shs + (size_t)M3 * r.c;
+        const float* sp = shs + (size_t)M3 * r.p;
+        float* so = osh + (size_t)M3 * r.o;
+        for (int k = l; k < M3; k += 16) so[k] = sky ? sc[k] : r.t * sc[k] + r.u * sp[k];
     }
-    const int i = o - S, c = ridx[i], p = pidx[i];
-    const float t = w[i], u = 1 - w[i];
-    for (int k = 0; k < 3; k++) om[3 * o + k] = t * means[3 * c + k] + u * means[3 * p + k];
-    for (int k = 0; k < 3; k++) osc[3 * o + k] = t * scales[3 * c + k] + u * scales[3 * p + k];
-    if (shs)
-        for (int k = 0; k < M3; k++) osh[(size_t)M3 * o + k] = t * shs[(size_t)M3 * c + k] + u * shs[(size_t)M3 * p + k];
-    const float4 rc = reinterpret_cast<const float4*>(rots)[c];
-    float4 rp = reinterpret_cast<const float4*>(rots)[p];
-    float dotv = 0.f;
-    dotv += rc.x * rp.x;
-    dotv += rc.y * rp.y;
-    dotv += rc.z * rp.z;
-    dotv += rc.w * rp.w;
-    if (dotv < 0) { rp.x = -rp.x; rp.y = -rp.y; rp.z = -rp.z; rp.w = -rp.w; }
-    reinterpret_cast<float4*>(orot)[o] =
-        make_float4(t * rc.x + u * rp.x, t * rc.y + u * rp.y, t * rc.z + u * rp.z, t * rc.w + u * rp.w);
-    oop[o] = t * opac[c] + u * opac[p];
+    if (l < 3) {
+        om[3 * r.o + l] = sky ? means[3 * r.c + l] : r.t * means[3 * r.c + l] + r.u * means[3 * r.p + l];
+    } else if (l < 6) {
+        const int k = l - 3;
+        osc[3 * r.o + k] = sky ? scales[3 * r.c + k] : r.t * scales[3 * r.c + k] + r.u * scales[3 * r.p + k];
+    } else if (l < 10) {
+        const int k = l - 6;
+        const float4 rc = reinterpret_cast<const float4*>(rots)[r.c];
+        float v = (&rc.x)[k];
+        if (!sky) {
+            const float4 rp = reinterpret_cast<const float4*>(rots)[r.p];
+            float dotv = 0.f;
+            dotv += rc.x * rp.x;
+            dotv += rc.y * rp.y;
+            dotv += rc.z * rp.z;
+            dotv += rc.w * rp.w;
+            const float pk = dotv < 0 ? -(&rp.x)[k] : (&rp.x)[k];
+            v = r.t * v + r.u * pk;
+        }
+        orot[4 * r.o + k] = v;
+    } else if (l == 10) {
+        oop[r.o] = sky ? opac[r.c] : r.t * opac[r.c] + r.u * opac[r.p];
+    }
 }
 
-__global__ void __launch_bounds__(256) k_lod_interp_bwd(int S, int n, int M3, const int* __restrict__ ridx,
-                                                        const int* __restrict__ pidx, const float* __restrict__ w,
-                                                        const float* __restrict__ rots, const float* __restrict__ gm,
-                                                        const float* __restrict__ gsc, const float* __restrict__ grot,
-                                                        const float* __restrict__ gop, const float* __restrict__ gsh,
-                                                        float* dm, float* dsc, float* drot, float* dop, float* dsh)
+// Autograd of the lerp: d_child += t g, d_parent += (1 - t) g (the parent's rotation gradient negated where the
+// forward flipped its sign), d_sky = g for the prefix rows.  A node can be a selected child, the parent of
+// several selected nodes and, with non-monotone sizes, both.  Instead of float atomics on zero-initialised
+// gradients (torch's index_add in the reference's autograd), every node's contributions are gathered: the 2n
+// (node, row, role) entries are bucketed by node (counting sort: k_lerp_count, scan, k_lerp_fill), and
+// k_lerp_gather walks each node's bucket in (row, role) order and writes all of its gradient row -- untouched
+// nodes get zeros, so no memset is needed and the result is bitwise deterministic.
+__global__ void __launch_bounds__(256) k_lerp_count(int n, const int* __restrict__ ridx, const int* __restrict__ pidx,
+                                                    uint32_t* __restrict__ cnt)
 {
-    const int o = blockIdx.x * 256 + threadIdx.x;
-    if (o >= S + n) return;
-    if (o < S) {
-        for (int k = 0; k < 3; k++) { atomicAdd(&dm[3 * o + k], gm[3 * o + k]); atomicAdd(&dsc[3 * o + k], gsc[3 * o + k]); }
-        for (int k = 0; k < 4; k++) atomicAdd(&drot[4 * o + k], grot[4 * o + k]);
-        atomicAdd(&dop[o], gop[o]);
-        if (gsh)
-            for (int k = 0; k < M3; k++) atomicAdd(&dsh[(size_t)M3 * o + k], gsh[(size_t)M3 * o + k]);
-        return;
-    }
-    const int i = o - S, c = ridx[i], p = pidx[i];
-    const float t = w[i], u = 1 - w[i];
-    for (int k = 0; k < 3; k++) {
-        atomicAdd(&dm[3 * c + k], t * gm[3 * o + k]);
-        atomicAdd(&dm[3 * p + k], u * gm[3 * o + k]);
-        atomicAdd(&dsc[3 * c + k], t * gsc[3 * o + k]);
-        atomicAdd(&dsc[3 * p + k], u * gsc[3 * o + k]);
-    }
-    const float4 rc = reinterpret_cast<const float4*>(rots)[c];
-    const float4 rp = reinterpret_cast<const float4*>(rots)[p];
-    float dotv = 0.f;
-    dotv += rc.x * rp.x;
-    dotv += rc.y * rp.y;
-    dotv += rc.z * rp.z;
-    dotv += rc.w * rp.w;
-    const float sg = dotv < 0 ? -1.0f : 1.0f;
-    for (int k = 0; k < 4; k++) {
-        atomicAdd(&drot[4 * c + k], t * grot[4 * o + k]);
-        atomicAdd(&drot[4 * p + k], sg * (u * grot[4 * o + k]));
-    }
-    atomicAdd(&dop[c], t * gop[o]);
-    atomicAdd(&dop[p], u * gop[o]);
-    if (gsh)
-        for (int k = 0; k < M3; k++) {
-            atomicAdd(&dsh[(size_t)M3 * c + k], t * gsh[(size_t)M3 * o + k]);
-            atomicAdd(&dsh[(size_t)M3 * p + k], u * gsh[(size_t)M3 * o + k]);
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    atomicAdd(&cnt[ridx[i]], 1u);
+    atomicAdd(&cnt[pidx[i]], 1u);
+}
+
+__global__ void __launch_bounds__(256) k_lerp_fill(int n, const int* __restrict__ ridx, const int* __restrict__ pidx,
+                                                   const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ incl,
+                                                   uint32_t* __restrict__ cur, uint32_t* __restrict__ list)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int c = ridx[i], p = pidx[i];
+    list[incl[c] - cnt[c] + atomicAdd(&cur[c], 1u)] = 2u * (uint32_t)i;       // child role
+    list[incl[p] - cnt[p] + atomicAdd(&cur[p], 1u)] = 2u * (uint32_t)i + 1u;  // parent role
+}
+
+// One wave per 64 consecutive nodes: the wave first stores zero rows for all of them with full-wave coalesced
+// stores, then its four 16-lane groups take the touched nodes (bucket non-empty or skybox) four at a time, walk
+// each bucket in (row, role) order and overwrite the node's row.
+template <int KSH>  // SH floats handled per lane: ceil(M3 / 16) <= KSH
+__global__ void __launch_bounds__(64) k_lerp_gather(int P, int S, int M3, const int* __restrict__ ridx,
+                                                    const float* __restrict__ w, const float* __restrict__ rots,
+                                                    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ incl,
+                                                    const uint32_t* __restrict__ list, const float* __restrict__ gm,
+                                                    const float* __restrict__ gsc, const float* __restrict__ grot,
+                                                    const float* __restrict__ gop, const float* __restrict__ gsh,
+                                                    float* __restrict__ dm, float* __restrict__ dsc,
+                                                    float* __restrict__ drot, float* __restrict__ dop,
+                                                    float* __restrict__ dsh)
+{
+    const int lane = threadIdx.x;
+    const int v0 = blockIdx.x * 64;
+    const int nv = min(64, P - v0);
+    // zero rows (every output row is written by this kernel)
+    for (int e = lane; e < 3 * nv; e += 64) { dm[3 * (size_t)v0 + e] = 0.f; dsc[3 * (size_t)v0 + e] = 0.f; }
+    for (int e = lane; e < 4 * nv; e += 64) drot[4 * (size_t)v0 + e] = 0.f;
+    if (lane < nv) dop[v0 + lane] = 0.f;
+    if (dsh)
+        for (int e = lane; e < M3 * nv; e += 64) dsh[(size_t)M3 * v0 + e] = 0.f;
+    const int my_v = v0 + lane;
+    const uint32_t my_k = lane < nv ? cnt[my_v] : 0u;
+    const uint32_t my_start = lane < nv ? incl[my_v] - my_k : 0u;
+    uint64_t todo = __ballot(lane < nv && (my_k > 0 || my_v < S));
+    // make the zero stores visible before the overwrites (same wave, same addresses: program order suffices for
+    // a single lane, but rows are overwritten by other lanes)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0);
+    const int grp = lane >> 4, l = lane & 15;
+    while (todo) {
+        // the group's node: the grp-th remaining set bit
+        uint64_t m = todo;
+        for (int q = 0; q < grp && m; q++) m &= m - 1;
+        const bool have = m != 0;
+        const int src = have ? __builtin_ctzll(m) : 0;
+        // consume four bits
+        for (int q = 0; q < 4 && todo; q++) todo &= todo - 1;
+        const uint32_t k = __shfl(my_k, src, 64), start = __shfl(my_start, src, 64);
+        if (!have) continue;
+        const int v = v0 + src;
+        float acc_sh[KSH];
+#pragma unroll
+        for (int j = 0; j < KSH; j++) acc_sh[j] = 0.f;
+        float acc = 0.f;  // lane 0-2 mean, 3-5 scale, 6-9 rotation, 10 opacity
+        auto small_grad = [&](int o) -> float {
+            if (l < 3) return gm[3 * o + l];
+            if (l < 6) return gsc[3 * o + l - 3];
+            if (l < 10) return grot[4 * o + l - 6];
+            if (l == 10) return gop[o];
+            return 0.f;
+        };
+        if (v < S) {  // skybox prefix: identity
+            acc += small_grad(v);
+#pragma unroll
+            for (int j = 0; j < KSH; j++)
+                if (gsh && l + 16 * j < M3) acc_sh[j] += gsh[(size_t)M3 * v + l + 16 * j];
         }
+        uint32_t prev = 0xffffffffu;
+        for (uint32_t e = 0; e < k; e++) {
+            uint32_t best = 0xffffffffu;  // next entry in (row, role) order: buckets hold a handful of entries
+            for (uint32_t q = 0; q < k; q++) {
+                const uint32_t x = list[start + q];
+                if ((prev == 0xffffffffu || x > prev) && x < best) best = x;
+            }
+            prev = best;
+            const int row = (int)(best >> 1);
+            const bool parent = best & 1u;
+            const int o = S + row;
+            const float t = w[row];
+            const float f = parent ? 1 - t : t;
+            const float g = small_grad(o);
+            if (parent && l >= 6 && l < 10) {
+                const float4 rc = reinterpret_cast<const float4*>(rots)[ridx[row]];
+                const float4 rp = reinterpret_cast<const float4*>(rots)[v];
+                float dotv = 0.f;
+                dotv += rc.x * rp.x;
+                dotv += rc.y * rp.y;
+                dotv += rc.z * rp.z;
+                dotv += rc.w * rp.w;
+                acc += (dotv < 0 ? -1.0f : 1.0f) * (f * g);
+            } else {
+                acc += f * g;
+            }
+#pragma unroll
+            for (int j = 0; j < KSH; j++)
+                if (gsh && l + 16 * j < M3) acc_sh[j] += f * gsh[(size_t)M3 * o + l + 16 * j];
+        }
+        if (l < 3) dm[3 * v + l] = acc;
+        else if (l < 6) dsc[3 * v + l - 3] = acc;
+        else if (l < 10) drot[4 * v + l - 6] = acc;
+        else if (l == 10) dop[v] = acc;
+#pragma unroll
+        for (int j = 0; j < KSH; j++)
+            if (dsh && l + 16 * j < M3) dsh[(size_t)M3 * v + l + 16 * j] = acc_sh[j];
+    }
 }
 
 // ---- host launchers
@@ -397,16 +513,47 @@ void launch_lod_interp_fwd(int S, int n, int M3, const int* ridx, const int* pid
                            const float* scales, const float* rots, const float* opac, const float* shs, float* om,
                            float* osc, float* orot, float* oop, float* osh, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_lod_interp_fwd, g256((long)S + n), dim3(256), 0, s, S, n, M3, ridx, pidx, w, means, scales,
+    hipLaunchKernelGGL(k_lod_interp_fwd, dim3((unsigned)(((long)S + n + 15) / 16)), dim3(256), 0, s, S, n, M3, ridx,
+                       pidx, w, means, scales,
                        rots, opac, shs, om, osc, orot, oop, osh);
 }
 
-void launch_lod_interp_bwd(int S, int n, int M3, const int* ridx, const int* pidx, const float* w, const float* rots,
-                           const float* gm, const float* gsc, const float* grot, const float* gop, const float* gsh,
-                           float* dm, float* dsc, float* drot, float* dop, float* dsh, hipStream_t s)
+size_t lerp_bwd_scratch_elems(int P, int n)
 {
-    hipLaunchKernelGGL(k_lod_interp_bwd, g256((long)S + n), dim3(256), 0, s, S, n, M3, ridx, pidx, w, rots, gm, gsc, grot,
-                       gop, gsh, dm, dsc, drot, dop, dsh);
+    return 4 * align_up(sizeof(uint32_t) * (size_t)P) / 4 + align_up(sizeof(uint32_t) * scan_scratch_elems(P)) / 4 +
+           align_up(sizeof(uint32_t) * 2 * (size_t)n) / 4;
+}
+
+void launch_lod_interp_bwd(int P, int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
+                           const float* rots, const float* gm, const float* gsc, const float* grot, const float* gop,
+                           const float* gsh, float* dm, float* dsc, float* drot, float* dop, float* dsh, void* scratch,
+                           hipStream_t s)
+{
+    char* p = static_cast<char*>(scratch);
+    auto take = [&](size_t count) {
+        uint32_t* r = reinterpret_cast<uint32_t*>(p);
+        p += align_up(count * sizeof(uint32_t));
+        return r;
+    };
+    uint32_t* cnt = take(P);
+    uint32_t* cur = take(P);
+    uint32_t* incl = take(P);
+    take(P);  // reserved
+    uint32_t* tmp = take(scan_scratch_elems(P));
+    uint32_t* list = take(2 * (size_t)n);
+    hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (size_t)P, s);
+    hipMemsetAsync(cur, 0, sizeof(uint32_t) * (size_t)P, s);
+    if (n > 0) hipLaunchKernelGGL(k_lerp_count, g256(n), dim3(256), 0, s, n, ridx, pidx, cnt);
+    scan_inclusive_u32(cnt, incl, (size_t)P, tmp, s);
+    if (n > 0) hipLaunchKernelGGL(k_lerp_fill, g256(n), dim3(256), 0, s, n, ridx, pidx, cnt, incl, cur, list);
+    const dim3 grid((unsigned)(((long)P + 63) / 64));
+#define HLGS_LG(K) hipLaunchKernelGGL((k_lerp_gather<K>), grid, dim3(64), 0, s, P, S, M3, ridx, w, rots, cnt, incl, list, \
+                                      gm, gsc, grot, gop, gsh, dm, dsc, drot, dop, dsh)
+    if (M3 <= 16) HLGS_LG(1);
+    else if (M3 <= 32) HLGS_LG(2);
+    else if (M3 <= 48) HLGS_LG(3);
+    else HLGS_LG(4);
+#undef HLGS_LG
 }
 
 // get_morton_indices (gaussianhierarchy/morton.cu:9-42, bound at torch_interface.cpp:246-260): 63-bit Morton

@@ -162,19 +162,20 @@ def lod_interp_backward(S, ridx, pidx, w, rots, P, g_m, g_s, g_r, g_o, g_sh, sh_
     n = int(ridx.size(0))
     dev = rots.device
     f32 = dict(dtype=torch.float32, device=dev)
-    d_m = torch.zeros((P, 3), **f32)
-    d_s = torch.zeros((P, 3), **f32)
-    d_r = torch.zeros((P, 4), **f32)
-    d_o = torch.zeros((P, 1), **f32)
+    d_m = torch.empty((P, 3), **f32)  # written completely by the kernel
+    d_s = torch.empty((P, 3), **f32)
+    d_r = torch.empty((P, 4), **f32)
+    d_o = torch.empty((P, 1), **f32)
     M3 = 0
     d_sh = None
     if sh_shape is not None:
-        d_sh = torch.zeros((P,) + tuple(sh_shape[1:]), **f32)
+        d_sh = torch.empty((P,) + tuple(sh_shape[1:]), **f32)
         M3 = int(d_sh[0].numel()) if P else 0
-    L.check(lib.hlgs_lod_interp_backward(int(S), n, M3, L.ptr(ridx), L.ptr(pidx), L.ptr(w), L.ptr(rots),
+    scratch = _scratch(lib.hlgs_lod_interp_scratch_size(int(P), n), dev)
+    L.check(lib.hlgs_lod_interp_backward(int(P), int(S), n, M3, L.ptr(ridx), L.ptr(pidx), L.ptr(w), L.ptr(rots),
                                          L.ptr(g_m), L.ptr(g_s), L.ptr(g_r), L.ptr(g_o),
                                          L.ptr(g_sh) if M3 else None, L.ptr(d_m), L.ptr(d_s), L.ptr(d_r), L.ptr(d_o),
-                                         L.ptr(d_sh) if M3 else None, L.stream()))
+                                         L.ptr(d_sh) if M3 else None, L.ptr(scratch), L.stream()))
     return d_m, d_s, d_r, d_o, d_sh
 
 

@@ -87,7 +87,8 @@ _SIGS = {
     "hlgs_spt_cut_prepare": (_i, [_i, _vp, _vp, _vp, _vp, _vp, C.POINTER(_i), _vp]),
     "hlgs_spt_cut_finish": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, C.POINTER(_i), _vp]),
     "hlgs_lod_interp_forward": (_i, [_i, _i, _i] + [_vp] * 14),
-    "hlgs_lod_interp_backward": (_i, [_i, _i, _i] + [_vp] * 15),
+    "hlgs_lod_interp_scratch_size": (_sz, [_i, _i]),
+    "hlgs_lod_interp_backward": (_i, [_i, _i, _i, _i] + [_vp] * 16),
     "hlgs_binning_point_list_offset": (_sz, [_i]),
     "hlgs_image_ranges_offset": (_sz, [_i, _i]),
     "hlgs_geom_splat_offset": (_sz, [_i]),

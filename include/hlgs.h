@@ -201,11 +201,15 @@ int hlgs_lod_interp_forward(int S, int n, int M3, const int* ridx, const int* pi
                             const float* means, const float* scales, const float* rots, const float* opac,
                             const float* shs, float* o_means, float* o_scales, float* o_rots, float* o_opac,
                             float* o_shs, void* stream);
-/* Gradient of the lerp: accumulates into P-row d_* arrays, which the caller zero-initialises. */
-int hlgs_lod_interp_backward(int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
+/* Gradient of the lerp (the autograd of render_post's block, gaussian_renderer/__init__.py:304-339) into the
+ * P-row gradient arrays d_*: every row is written (zeros where no output row depends on it), so no
+ * initialisation is needed; contributions are gathered per node in a fixed order (bitwise deterministic).
+ * scratch: hlgs_lod_interp_scratch_size(P, n) bytes.  M3 <= 64. */
+size_t hlgs_lod_interp_scratch_size(int P, int n);
+int hlgs_lod_interp_backward(int P, int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
                              const float* rots, const float* g_means, const float* g_scales, const float* g_rots,
                              const float* g_opac, const float* g_shs, float* d_means, float* d_scales,
-                             float* d_rots, float* d_opac, float* d_shs, void* stream);
+                             float* d_rots, float* d_opac, float* d_shs, void* scratch, void* stream);
 
 /* Morton codes of P positions in the [mn, mx] box (device float3 each): get_morton_indices,
  * gaussianhierarchy/morton.cu:9-58 via torch_interface.cpp:246-260 (used by GaussianModel.sort_morton,

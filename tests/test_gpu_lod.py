@@ -179,6 +179,15 @@ def test_lod_interpolation_forward_backward():
                               dict(means=gs[0], scales=gs[1], rots=gs[2], opac=gs[3], shs=gs[4]))
     for leaf_t, key in zip((m, s, r, o, sh), ("means", "scales", "rots", "opac", "shs")):
         np.testing.assert_allclose(leaf_t.grad.cpu().numpy().reshape(d[key].shape), d[key], rtol=1e-5, atol=1e-5)
+    # the gather backward is bitwise deterministic and writes every row (no pre-zeroed buffers)
+    first = [t.grad.clone() for t in (m, s, r, o, sh)]
+    for t in (m, s, r, o, sh):
+        t.grad = None
+    outs = GH.interpolate_lod(m, s, r, o, sh, torch.tensor(ri[:n], device=DEV), torch.tensor(pi, device=DEV),
+                              torch.tensor(np.pad(ts, (0, N - n)), device=DEV), Sk)
+    sum((x * torch.tensor(g, device=DEV)).sum() for x, g in zip(outs, gs)).backward()
+    for a, t in zip(first, (m, s, r, o, sh)):
+        assert torch.equal(a, t.grad)
 
 
 def test_in_kernel_hierarchy_mode_matches_oracle():

@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Measurements of the rows around the rasterizer hot path, on one GPU:
+
+  lod       config #3: a synthetic binary hierarchy over config #2's 1M leaves (~2M nodes), cut with
+            expand_to_size_dynamic at tau = 2 (6 + 0.5) tanfovx / (0.5 W) (render_hierarchy.py:56), interpolation
+            weights, the render_post lerp (interpolate_lod), then rasterizer forward + backward at 1080p and the
+            lerp's backward: each stage separately and the whole step inclusive.
+  alt       the alt rasterizer (train_post.py's default) on config #2: forward + backward Mpix/s.
+  loss      photometric_loss (L1 + D-SSIM + masked inverse-depth L1) forward + backward on a 1080p view.
+  adam      SparseGaussianAdam.step over 1M Gaussians (59 floats each, six parameter groups), half visible.
+  morton    get_morton_indices over the hierarchy's nodes.
+
+Times are medians of CUDA-event spans on torch's current stream (the library launches there).  Inputs are
+synthetic (seeded) and resident on the device.  Prints one JSON object.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hierarchical-lod-gaussians_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from hlgs_core import synthetic as S  # noqa: E402
+
+DEV = "cuda"
+HBM = 8000.0
+
+
+def timed(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
+def settings(cam, deg, do_depth=True, alt=False):
+    e_i = torch.empty(0, dtype=torch.int32, device=DEV)
+    e_f = torch.empty(0, dtype=torch.float32, device=DEV)
+    common = dict(image_height=cam["H"], image_width=cam["W"], tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
+                  bg=torch.zeros(3, device=DEV), scale_modifier=1.0, viewmatrix=cam["viewmatrix"].to(DEV),
+                  projmatrix=cam["projmatrix"].to(DEV), sh_degree=deg, campos=cam["campos"].to(DEV),
+                  prefiltered=False, debug=False)
+    if alt:
+        from alt_gaussian_rasterization import GaussianRasterizationSettings
+        return GaussianRasterizationSettings(antialiasing=True, **common)
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    return GaussianRasterizationSettings(render_indices=e_i, parent_indices=e_i, interpolation_weights=e_f,
+                                         num_node_kids=e_i, do_depth=do_depth, **common)
+
+
+def bench_alt(P, W, H, deg):
+    from alt_gaussian_rasterization import GaussianRasterizer
+    cam = S.make_camera(W, H)
+    h = S.make_gaussians(P, deg, cam, seed=0)
+    t = lambda a: torch.tensor(np.ascontiguousarray(a), device=DEV, requires_grad=True)  # noqa: E731
+    m, sc, r, o = t(h["means3D"]), t(h["scales"]), t(h["rotations"]), t(h["opacities"])
+    dc, rest = t(h["shs"][:, :1]), t(h["shs"][:, 1:])
+    g_np, gd_np = S.upstream_grads(W, H, seed=1)
+    g, gd = torch.tensor(g_np, device=DEV), torch.tensor(gd_np, device=DEV)
+    rast = GaussianRasterizer(settings(cam, deg, alt=True))
+
+    def step():
+        m2 = torch.zeros_like(m, requires_grad=True)
+        c, _, inv = rast(means3D=m, means2D=m2, opacities=o, dc=dc, shs=rest, scales=sc, rotations=r)
+        torch.autograd.backward([c, inv], [g, gd])
+
+    ms = timed(step)
+    return dict(workload=f"alt rasterizer, {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd (antialiasing)",
+                ms=round(ms, 4), Mpix_s=round(W * H / ms / 1e3, 1))
+
+
+def bench_loss(W, H):
+    from hlgs_core import loss
+    rng = np.random.default_rng(0)
+    img = torch.tensor(rng.uniform(0, 1, (3, H, W)).astype(np.float32), device=DEV, requires_grad=True)
+    gt = torch.tensor(rng.uniform(0, 1, (3, H, W)).astype(np.float32), device=DEV)
+    inv = torch.tensor(rng.uniform(0.05, 0.5, (1, H, W)).astype(np.float32), device=DEV, requires_grad=True)
+    mono = torch.tensor(rng.uniform(0.05, 0.5, (1, H, W)).astype(np.float32), device=DEV)
+    mask = torch.ones((1, H, W), device=DEV)
+
+    def step():
+        tot = loss.photometric_loss(img, gt, 0.2, inv, mono, mask, 0.5)[0]
+        tot.backward()
+
+    ms = timed(step)
+    N = W * H
+    # algorithmic HBM bytes: fwd reads both images (24 B/px) and writes 3 derivative maps per channel (36 B/px);
+    # bwd reads the maps and both images (60 B/px) and writes the image gradient (12 B/px); depth term
+    # reads 12 B/px twice and writes 4 B/px
+    alg = N * (24 + 36 + 60 + 12) + N * (12 + 12 + 4)
+    return dict(workload=f"photometric loss (L1 + D-SSIM + depth L1), 3x{H}x{W}, fwd+bwd", ms=round(ms, 4),
+                alg_GBs=round(alg / (ms * 1e-3) / 1e9, 1), hbm_frac=round(alg / (ms * 1e-3) / 1e9 / HBM, 3))
+
+
+def bench_adam(P):
+    from alt_gaussian_rasterization import SparseGaussianAdam
+    widths = dict(xyz=3, f_dc=3, f_rest=45, opacity=1, scaling=3, rotation=4)
+    params = {k: torch.nn.Parameter(torch.randn(P, w, device=DEV)) for k, w in widths.items()}
+    opt = SparseGaussianAdam([{"params": [p], "lr": 1e-3, "name": k} for k, p in params.items()], lr=0.0, eps=1e-15)
+    for p in params.values():
+        p.grad = torch.randn_like(p)
+    vis = torch.rand(P, device=DEV) < 0.5
+    ms = timed(lambda: opt.step(vis, P))
+    alg = 0.5 * P * 59 * 28 + P  # visible elements: 16 B read + 12 B written; one visibility byte per Gaussian
+    return dict(workload=f"SparseGaussianAdam.step, {P} Gaussians x 59 floats, 50% visible", ms=round(ms, 4),
+                alg_GBs=round(alg / (ms * 1e-3) / 1e9, 1), hbm_frac=round(alg / (ms * 1e-3) / 1e9 / HBM, 3))
+
+
+def bench_lod(P, W, H, deg):
+    import gaussian_hierarchy as GH
+    from diff_gaussian_rasterization import GaussianRasterizer
+    cam = S.make_camera(W, H)
+    t0 = time.perf_counter()
+    hier = S.make_dynamic_hierarchy(S.make_gaussians(P, deg, cam, seed=0), seed=0)
+    build_s = time.perf_counter() - t0
+    N = hier["nodes"].shape[0]
+    d = lambda a, **kw: torch.tensor(np.ascontiguousarray(a), device=DEV, **kw)  # noqa: E731
+    nodes, xyz, scales = d(hier["nodes"]), d(hier["means3D"], requires_grad=True), d(hier["scales"], requires_grad=True)
+    rots, opac, shs = (d(hier["rotations"], requires_grad=True), d(hier["opacities"], requires_grad=True),
+                       d(hier["shs"], requires_grad=True))
+    tau = (2 * (6 + 0.5)) * cam["tanfovx"] / (0.5 * W)
+    vp = cam["campos"].to(DEV)
+    vd = torch.tensor([0.0, 0.0, 1.0])
+    ri = torch.zeros(N, dtype=torch.int32, device=DEV)
+    pi = torch.zeros(N, dtype=torch.int32, device=DEV)
+    ni = torch.zeros(N, dtype=torch.int32, device=DEV)
+    ts = torch.zeros(N, device=DEV)
+    kids = torch.zeros(N, dtype=torch.int32, device=DEV)
+    rast = GaussianRasterizer(settings(cam, deg, do_depth=True))
+    g_np, gd_np = S.upstream_grads(W, H, seed=1)
+    g, gd = torch.tensor(g_np, device=DEV), torch.tensor(gd_np, device=DEV)
+    state = {}
+
+    def cut():
+        state["n"] = GH.expand_to_size_dynamic(nodes, xyz.detach(), scales.detach(), tau, vp, vd, ri, pi, ni)
+
+    def weights():
+        n = state["n"]
+        GH.get_interpolation_weights_dynamic(ni[:n], tau, nodes, xyz.detach(), scales.detach(), vp.cpu(), vd, ts, kids)
+
+    def lerp():
+        n = state["n"]
+        state["outs"] = GH.interpolate_lod(xyz, scales, rots, opac, shs, ri[:n], pi, ts, 0)
+
+    def raster():
+        m, s_, r_, o_, sh_ = state["outs"]
+        m2 = torch.zeros_like(m, requires_grad=True)
+        c, _, inv = rast(means3D=m, means2D=m2, opacities=o_, shs=sh_, scales=s_, rotations=r_)
+        state["graph"] = (c, inv)
+
+    def backward():
+        c, inv = state["graph"]
+        torch.autograd.backward([c, inv], [g, gd])
+        for p in (xyz, scales, rots, opac, shs):
+            p.grad = None
+
+    def full():
+        cut(); weights(); lerp(); raster(); backward()  # noqa: E702
+
+    full()
+    stages = {}
+    for name, fn in (("expand_to_size_dynamic", cut), ("get_interpolation_weights_dynamic", weights),
+                     ("interpolate_lod_fwd", lerp)):
+        stages[name] = round(timed(fn), 4)
+    stages["rasterizer_fwd"] = round(timed(raster), 4)
+
+    def raster_bwd():
+        lerp(); raster()  # noqa: E702
+        backward()
+
+    stages["rasterizer_bwd+lerp_bwd"] = round(timed(raster_bwd) - stages["interpolate_lod_fwd"] -
+                                              stages["rasterizer_fwd"], 4)
+    incl = timed(full)
+    n = state["n"]
+    return dict(workload=f"config #3: synthetic binary hierarchy over {P} leaves ({N} nodes), SH deg {deg}, {W}x{H}, "
+                         f"tau={tau:.3e}, cut -> weights -> lerp -> rasterize fwd+bwd -> lerp bwd",
+                nodes=N, selected=n, hierarchy_build_s=round(build_s, 1), stages_ms=stages,
+                inclusive_ms=round(incl, 4), lod_cut_and_interp_ms=round(sum(stages[k] for k in (
+                    "expand_to_size_dynamic", "get_interpolation_weights_dynamic", "interpolate_lod_fwd")), 4),
+                Mpix_s=round(W * H / incl / 1e3, 1)), (xyz.detach(), N)
+
+
+def bench_morton(xyz):
+    import gaussian_hierarchy as GH
+    codes = torch.zeros(xyz.shape[0], dtype=torch.int64, device=DEV)
+    mn, mx = xyz.min(0)[0], xyz.max(0)[0]
+    ms = timed(lambda: GH.get_morton_indices(xyz, mn, mx, codes))
+    alg = xyz.shape[0] * (12 + 8)
+    return dict(workload=f"get_morton_indices, {xyz.shape[0]} points", ms=round(ms, 4),
+                alg_GBs=round(alg / (ms * 1e-3) / 1e9, 1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--only", default="alt,loss,adam,lod")
+    args = ap.parse_args()
+    only = set(args.only.split(","))
+    out = dict(device=torch.cuda.get_device_name(0), data="synthetic (seeded PCG64)")
+    if "alt" in only:
+        out["alt"] = bench_alt(args.P, args.W, args.H, 3)
+    if "loss" in only:
+        out["loss"] = bench_loss(args.W, args.H)
+    if "adam" in only:
+        out["adam"] = bench_adam(args.P)
+    if "lod" in only:
+        out["lod"], (xyz, _) = bench_lod(args.P, args.W, args.H, 3)
+        out["morton"] = bench_morton(xyz)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
