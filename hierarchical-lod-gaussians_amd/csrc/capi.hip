@@ -42,6 +42,8 @@ void launch_depth_l1_forward(long n, const float* inv, const float* mono, const 
                              float* out, hipStream_t s);
 void launch_depth_l1_backward(long n, const float* inv, const float* mono, const float* mask, const float* coef,
                               float* grad, hipStream_t s);
+void launch_upper_cut(const CutArgs& a, hipStream_t s);
+void launch_rows(bool gather, long n, int row_bytes, const int64_t* idx, const void* src, void* dst, hipStream_t s);
 void launch_morton(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, hipStream_t s);
 void launch_adam(float* param, const float* grad, float* m, float* v, const uint8_t* vis, float lr, float b1, float b2,
                  float eps, uint32_t N, uint32_t M, hipStream_t s);
@@ -534,6 +536,63 @@ int hlgs_morton_codes(int P, const float* xyz, const float* mn, const float* mx,
     hipGetLastError();
     launch_morton(P, xyz, mn, mx, codes, s);
     return check_stage(s, false, "morton_codes");
+}
+
+// ---------------------------------------------------------------- SPT streaming (stream.hip)
+size_t hlgs_upper_cut_scratch_size(int N)
+{
+    const size_t cap = 2 * (size_t)(N > 0 ? N : 0) + 2;
+    return 2 * align_up(sizeof(int) * cap) + align_up(2 * sizeof(int)) + kAlign;
+}
+
+int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
+                        const float* planes, const float* campos, float distance_multiplier, int use_frustum,
+                        int use_lod, void* scratch, int* cut, int* count, void* stream)
+{
+    *count = 0;
+    if (N < 0) return fail(HLGS_ERR_ARG, "N < 0");
+    if (N == 0) return HLGS_OK;
+    if (!nodes || !xyz || !cut || !scratch || (use_frustum && (!bounds || !planes)) ||
+        (use_lod && (!min_dist2 || !campos)))
+        return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    const int cap = 2 * N + 2;
+    char* p = static_cast<char*>(aligned(scratch));
+    CutArgs a{N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum, use_lod,
+              take<int>(p, cap), take<int>(p, cap), N, cut, nullptr};
+    a.count = take<int>(p, 2);
+    launch_upper_cut(a, s);
+    int rc = check_stage(s, false, "upper_tree_cut");
+    if (rc) return rc;
+    int host[2];
+    HLGS_TRY_HIP(hipMemcpyAsync(host, a.count, sizeof(host), hipMemcpyDeviceToHost, s));
+    HLGS_TRY_HIP(hipStreamSynchronize(s));
+    if (host[1]) return fail(HLGS_ERR_ARG, "upper-tree cut outgrew the node count (not a tree?)");
+    *count = host[0];
+    return HLGS_OK;
+}
+
+int hlgs_gather_rows(int64_t n, int row_bytes, const int64_t* idx, const void* src, void* dst, void* stream)
+{
+    if (n < 0 || row_bytes < 0 || row_bytes % 4) return fail(HLGS_ERR_ARG, "row size must be a multiple of 4 bytes");
+    if (n == 0 || row_bytes == 0) return HLGS_OK;
+    if (!idx || !src || !dst) return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_rows(true, n, row_bytes, idx, src, dst, s);
+    return check_stage(s, false, "gather_rows");
+}
+
+int hlgs_scatter_rows(int64_t n, int row_bytes, const int64_t* idx, const void* src, void* dst, void* stream)
+{
+    if (n < 0 || row_bytes < 0 || row_bytes % 4) return fail(HLGS_ERR_ARG, "row size must be a multiple of 4 bytes");
+    if (n == 0 || row_bytes == 0) return HLGS_OK;
+    if (!idx || !src || !dst) return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_rows(false, n, row_bytes, idx, src, dst, s);
+    return check_stage(s, false, "scatter_rows");
 }
 
 // ---------------------------------------------------------------- losses

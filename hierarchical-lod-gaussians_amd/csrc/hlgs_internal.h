@@ -82,6 +82,27 @@ __device__ __forceinline__ bool guard_fail(const Guard& gd)
     return gd.misc && (gd.misc[0] > gd.cap_R || gd.misc[1] > gd.cap_n);
 }
 
+// Upper-tree cut (stream.hip).  Per level the frontier (the reference's `stack`) is filtered by the cull;
+// leaves go to the cut, then the non-leaves whose LOD condition is false, each group in frontier order; the
+// next frontier is the first children of the expanded nodes in order, then their first children's next
+// siblings in order (scene/gaussian_model.py:364-404).
+struct CutArgs {
+    int N;
+    const int* nodes;      // N x 6 HierarchyNode rows: 2 child_count, 3 first_child, 4 next_sibling
+    const float* xyz;
+    const float* bounds;
+    const float* min_dist2;
+    const float* planes;   // 4 x (nx, ny, nz, d), normalised as extract_frustum_planes does
+    const float* campos;
+    float dmul;
+    int use_frustum, use_lod;
+    int* front_a;
+    int* front_b;
+    int capacity;          // entries of cut
+    int* cut;
+    int* count;            // [0] = cut size, [1] = overflow flag
+};
+
 // scan.hip
 void scan_inclusive_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp, hipStream_t s);
 

@@ -63,6 +63,14 @@ _SIGS = {
     "hlgs_compute_relocation": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "hlgs_adam_update": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, C.c_uint32, C.c_uint32, _vp]),
     "hlgs_morton_codes": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "hlgs_upper_cut_scratch_size": (_sz, [_i]),
+    "hlgs_upper_tree_cut": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, C.POINTER(_i), _vp]),
+    "hlgs_gather_rows": (_i, [C.c_int64, _i, _vp, _vp, _vp, _vp]),
+    "hlgs_spt_build": (_i, [_i, _vp, _vp, _vp, _i, _f, _f, _i, _i, C.POINTER(_vp)]),
+    "hlgs_spt_result_sizes": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),
+    "hlgs_spt_result_copy": (_i, [_vp] * 11),
+    "hlgs_spt_result_free": (None, [_vp]),
+    "hlgs_scatter_rows": (_i, [C.c_int64, _i, _vp, _vp, _vp, _vp]),
     "hlgs_ssim_scratch_size": (_sz, [_i, _i, _i]),
     "hlgs_ssim_forward": (_i, [_i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "hlgs_ssim_backward": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),

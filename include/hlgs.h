@@ -216,6 +216,39 @@ int hlgs_lod_interp_backward(int P, int S, int n, int M3, const int* ridx, const
  * scene/gaussian_model.py:570-589). */
 int hlgs_morton_codes(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, void* stream);
 
+/* ---- SPT streaming around the SPT cut (train_post.py:323-491) ---- */
+/* Coarse cut of the upper tree (GaussianModel.cut_hierarchy_on_condition with root 0, no upper-tree output,
+ * leave_out_of_cut_condition = frustum_cull_spheres: scene/gaussian_model.py:364-404, 67-100, as train_post.py
+ * :326-343 calls it).  nodes: N x 6 int32 upper-tree HierarchyNode rows; xyz N x 3; bounds N (sphere radii);
+ * min_dist2 N; planes: 4 x 4 floats (nx, ny, nz, d) from extract_frustum_planes; campos 3.  A node survives the
+ * cull unless n.p + d + r < 0 for one plane (use_frustum); it is cut if it is a leaf or (use_lod) if not
+ * min_dist2 > |campos - p|^2 * distance_multiplier, else its first child and that child's next sibling are
+ * visited.  cut (device, N entries) receives the nodes in the reference's order; *count (host) their number.
+ * scratch: hlgs_upper_cut_scratch_size(N) bytes.  One host synchronisation (the reference's len()). */
+size_t hlgs_upper_cut_scratch_size(int N);
+int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
+                        const float* planes, const float* campos, float distance_multiplier, int use_frustum,
+                        int use_lod, void* scratch, int* cut, int* count, void* stream);
+/* SPT construction (GaussianModel.build_hierarchical_SPT + get_min_distance, scene/gaussian_model.py:184-352), host
+ * code over host arrays: nodes G x 6 (HierarchyNode), xyz G x 3, log_scales G x 3 (unactivated, as _scaling);
+ * root = the hierarchy root (the reference's default root_node 100000 is its skybox size).  The result is an
+ * opaque handle: query the sizes, copy into caller buffers (any pointer may be NULL), free.
+ *   starts (n_spt + 1), smax / smin / gidx (n_entries): the SPT arrays get_spt_cut_cuda takes;
+ *   roots (n_spt): hierarchy ids of the SPT roots; up_nodes (n_upper x 6), up_xyz, up_scaling (n_upper x 3),
+ *   min_d2, radii (n_upper): the upper tree (radii only with use_bounding_spheres). */
+typedef struct hlgs_spt_result hlgs_spt_result;
+int hlgs_spt_build(int G, const int* nodes, const float* xyz, const float* log_scales, int root, float spt_root_volume,
+                   float target_granularity, int min_spt_size, int use_bounding_spheres, hlgs_spt_result** out);
+int hlgs_spt_result_sizes(const hlgs_spt_result* r, int* n_spt, int* n_entries, int* n_upper);
+int hlgs_spt_result_copy(const hlgs_spt_result* r, int* starts, float* smax, float* smin, int* gidx, int* roots,
+                         int* up_nodes, float* up_xyz, float* up_scaling, float* min_d2, float* radii);
+void hlgs_spt_result_free(hlgs_spt_result* r);
+/* Row gather dst[i] = src[idx[i]] and scatter dst[idx[i]] = src[i] for n rows of row_bytes (a multiple of 4):
+ * the streaming cache's storage[idx].cuda() loads and write-backs (train_post.py:439-488).  src / dst may be
+ * pinned host memory (read and written by the GPU over the host link). */
+int hlgs_gather_rows(int64_t n, int row_bytes, const int64_t* idx, const void* src, void* dst, void* stream);
+int hlgs_scatter_rows(int64_t n, int row_bytes, const int64_t* idx, const void* src, void* dst, void* stream);
+
 /* ---- photometric losses of the training step (utils/loss_utils.py:17-63, train_single.py:106-121,
  *      train_post.py:558-559 with the un-vendored fused_ssim) ---- */
 /* SSIM of C planes of H x W (11x11 Gaussian window, sigma 1.5, zero padding, C1 = 0.01^2, C2 = 0.03^2:

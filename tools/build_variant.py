@@ -21,7 +21,7 @@ def main(name, variant, replaces="raster_bwd.hip"):
     try:
         obj = os.path.join(PKG, "build", "var", name + ".o")
         os.makedirs(os.path.dirname(obj), exist_ok=True)
-        subprocess.run([B.HIPCC] + B.FLAGS + ["-c", tmp, "-o", obj], check=True)
+        subprocess.run([B.HIPCC] + B.FLAGS + B.PER_FILE.get(replaces, []) + ["-c", tmp, "-o", obj], check=True)
     finally:
         os.remove(tmp)
     objs = [os.path.join(B.OBJDIR, os.path.splitext(s)[0] + ".o") for s in B.SOURCES if s != replaces] + [obj]
