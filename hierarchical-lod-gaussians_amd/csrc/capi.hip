@@ -6,6 +6,7 @@
 // Re-entrancy: no device memory is allocated here and no scratch is static; every buffer is passed
 // in.  The only process-wide state is the opt-in stage-timing instrumentation used by bench.py.
 #include <algorithm>
+#include <cmath>
 #include <stdio.h>
 #include <string.h>
 
@@ -593,6 +594,131 @@ int hlgs_scatter_rows(int64_t n, int row_bytes, const int64_t* idx, const void* 
     hipGetLastError();
     launch_rows(false, n, row_bytes, idx, src, dst, s);
     return check_stage(s, false, "scatter_rows");
+}
+
+size_t hlgs_spt_cache_scratch_size(int n_cut, int m, int R, int num_spts)
+{
+    const size_t c = n_cut > 0 ? n_cut : 0, r = R > 0 ? R : 0, ns = num_spts > 0 ? num_spts : 0;
+    (void)m;
+    return align_up(4 * ns) + 2 * align_up(4 * c) + 2 * align_up(4 * (r + 1)) + 2 * align_up(4 * r) +
+           align_up(4 * scan_scratch_elems(r + 1)) + align_up(4 * 8) + kAlign;
+}
+
+int hlgs_spt_cache_plan(const hlgs_cache_args* a, hlgs_cache_plan* pl, void* scratch, void* stream)
+{
+    if (!a || !pl) return fail(HLGS_ERR_ARG, "missing argument");
+    pl->n_kept = pl->n_load = pl->n_upper = pl->n_keep_rows = pl->prefix = 0;
+    if (a->n_cut < 0 || a->m < 0 || a->R < 0 || a->num_spts < 0) return fail(HLGS_ERR_ARG, "negative size");
+    if (!scratch || (a->n_cut && (!a->cut || !a->upper_nodes || !a->upper_xyz || !a->campos)) ||
+        (a->m && (!a->prev_spt_indices || !a->prev_spt_distances || !a->prev_spt_counts)) ||
+        (a->R && !a->render_indices))
+        return fail(HLGS_ERR_ARG, "missing tensor");
+    if ((a->m && (!pl->keep_spt_indices || !pl->keep_spt_distances || !pl->keep_spt_counts)) ||
+        (a->n_cut && (!pl->load_spt_indices || !pl->load_spt_distances || !pl->upper_render)) ||
+        (a->R && (!pl->keep_rows || !pl->render_kept || !pl->write_back_rows || !pl->write_back_indices)))
+        return fail(HLGS_ERR_ARG, "missing output");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    const int R = a->R;
+    char* p = static_cast<char*>(aligned(scratch));
+    CacheArgs c{};
+    c.n_cut = a->n_cut;
+    c.cut = a->cut;
+    c.nodes = a->upper_nodes;
+    c.xyz = a->upper_xyz;
+    c.campos = a->campos;
+    c.dmul = a->distance_multiplier;
+    c.num_spts = a->num_spts;
+    c.m = a->m;
+    c.prev_idx = a->prev_spt_indices;
+    c.prev_dist = a->prev_spt_distances;
+    c.prev_counts = a->prev_spt_counts;
+    c.R = R;
+    c.tail_end = R - a->n_loaded_prev;
+    c.rtol = a->rtol;
+    c.atol = a->atol;
+    c.flag = take<int>(p, a->num_spts);
+    c.spt_idx = take<int>(p, a->n_cut);
+    c.spt_dist = take<float>(p, a->n_cut);
+    c.diff = take<int>(p, (size_t)R + 1);
+    uint32_t* diff_incl = take<uint32_t>(p, (size_t)R + 1);
+    uint32_t* keep = take<uint32_t>(p, R);
+    uint32_t* keep_incl = take<uint32_t>(p, R);
+    uint32_t* tmp = take<uint32_t>(p, scan_scratch_elems((size_t)R + 1));
+    c.sizes = take<int>(p, 8);
+    c.keep_idx = pl->keep_spt_indices;
+    c.keep_dist = pl->keep_spt_distances;
+    c.keep_counts = pl->keep_spt_counts;
+    c.load_idx = pl->load_spt_indices;
+    c.load_dist = pl->load_spt_distances;
+    c.upper = pl->upper_render;
+    if (a->num_spts) HLGS_TRY_HIP(hipMemsetAsync(c.flag, 0, sizeof(int) * a->num_spts, s));
+    HLGS_TRY_HIP(hipMemsetAsync(c.diff, 0, sizeof(int) * ((size_t)R + 1), s));
+    HLGS_TRY_HIP(hipMemsetAsync(c.sizes, 0, sizeof(int) * 8, s));
+    launch_cache_lists(c, s);
+    if (R > 0) {
+        scan_inclusive_u32(reinterpret_cast<const uint32_t*>(c.diff), diff_incl, R, tmp, s);
+        launch_cache_keep(R, a->skybox_points, diff_incl, keep, s);
+        scan_inclusive_u32(keep, keep_incl, R, tmp, s);
+        launch_cache_split(R, a->render_indices, keep_incl, pl->keep_rows, pl->render_kept, pl->write_back_rows,
+                           pl->write_back_indices, s);
+        HLGS_TRY_HIP(hipMemcpyAsync(c.sizes + 4, keep_incl + (R - 1), sizeof(int), hipMemcpyDeviceToDevice, s));
+    }
+    int rc = check_stage(s, false, "spt_cache_plan");
+    if (rc) return rc;
+    int host[5];
+    HLGS_TRY_HIP(hipMemcpyAsync(host, c.sizes, sizeof(host), hipMemcpyDeviceToHost, s));
+    HLGS_TRY_HIP(hipStreamSynchronize(s));
+    pl->n_kept = host[0];
+    pl->n_load = host[1];
+    pl->n_upper = host[2];
+    pl->prefix = host[3];
+    pl->n_keep_rows = host[4];
+    return HLGS_OK;
+}
+
+int hlgs_copy_rows(int T, const hlgs_row_copy* tables, int64_t n, const int* src_rows, const int* dst_rows,
+                   void* stream)
+{
+    if (T < 0 || T > kMaxRowTables) return fail(HLGS_ERR_ARG, "at most 32 tables");
+    if (n < 0) return fail(HLGS_ERR_ARG, "n < 0");
+    if (T == 0 || n == 0) return HLGS_OK;
+    if (!tables) return fail(HLGS_ERR_ARG, "missing tables");
+    RowCopy rc_[kMaxRowTables];
+    for (int t = 0; t < T; t++) {
+        if (tables[t].row_bytes < 0 || tables[t].row_bytes % 4) return fail(HLGS_ERR_ARG, "row size must be a multiple of 4 bytes");
+        if (tables[t].row_bytes && (!tables[t].src || !tables[t].dst)) return fail(HLGS_ERR_ARG, "missing tensor");
+        rc_[t] = RowCopy{tables[t].src, tables[t].dst, tables[t].row_bytes};
+    }
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_rows_multi(T, rc_, n, src_rows, dst_rows, s);
+    return check_stage(s, false, "copy_rows");
+}
+
+int hlgs_adam_step(int T, const hlgs_adam_tensor* tensors, int64_t step, int skybox_rows, double beta1, double beta2,
+                   double eps, void* stream)
+{
+    if (T < 0 || T > kMaxRowTables) return fail(HLGS_ERR_ARG, "at most 32 tensors");
+    if (T == 0) return HLGS_OK;
+    if (!tensors) return fail(HLGS_ERR_ARG, "missing tensors");
+    if (step < 1) return fail(HLGS_ERR_ARG, "step must be >= 1");
+    // Python-float scalars as _single_tensor_adam2 forms them (OurAdam.py:425-432), each rounded to float32
+    // where torch hands it to a float32 kernel
+    const double bc1 = 1.0 - std::pow(beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(beta2, (double)step);
+    AdamTensor at[kMaxRowTables];
+    for (int t = 0; t < T; t++) {
+        const hlgs_adam_tensor& x = tensors[t];
+        if (x.numel < 0 || x.row_elems < 0) return fail(HLGS_ERR_ARG, "negative size");
+        if (x.numel && (!x.param || !x.grad || !x.exp_avg || !x.exp_avg_sq)) return fail(HLGS_ERR_ARG, "missing tensor");
+        at[t] = AdamTensor{x.param, x.grad, x.exp_avg, x.exp_avg_sq, x.numel, x.row_elems, (float)(-(x.lr / bc1))};
+    }
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_adam_multi(T, at, skybox_rows < 0 ? 0 : skybox_rows, (float)beta1, (float)(1.0 - beta1), (float)beta2,
+                      (float)(1.0 - beta2), (float)std::sqrt(bc2), (float)eps, s);
+    return check_stage(s, false, "adam_step");
 }
 
 // ---------------------------------------------------------------- losses

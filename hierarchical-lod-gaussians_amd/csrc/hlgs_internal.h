@@ -103,6 +103,61 @@ struct CutArgs {
     int* count;            // [0] = cut size, [1] = overflow flag
 };
 
+// SPT cache bookkeeping of one streaming step (stream.hip, train_post.py:346-430)
+struct CacheArgs {
+    int n_cut;
+    const int* cut;           // coarse cut of the upper tree
+    const int* nodes;         // upper-tree HierarchyNode rows
+    const float* xyz;
+    const float* campos;
+    float dmul;
+    int num_spts;
+    int m;                    // previous step's SPTs
+    const int* prev_idx;
+    const float* prev_dist;
+    const int* prev_counts;
+    int R;                    // len(render_indices)
+    int tail_end;             // len(render_indices) - len(load_from_disk_indices)
+    float rtol, atol;
+    // scratch
+    int* flag;                // num_spts, zero on entry
+    int* spt_idx;             // n_cut
+    float* spt_dist;          // n_cut
+    int* diff;                // R + 1, zero on entry
+    int* sizes;               // device: n_kept, n_load, n_upper, prefix
+    // outputs
+    int* keep_idx;
+    float* keep_dist;
+    int* keep_counts;
+    int* load_idx;
+    float* load_dist;
+    int* upper;
+};
+void launch_cache_lists(const CacheArgs& a, hipStream_t s);
+void launch_cache_keep(int R, int sky, const uint32_t* diff_incl, uint32_t* keep, hipStream_t s);
+void launch_cache_split(int R, const int* render, const uint32_t* keep_incl, int* keep_rows, int* render_kept,
+                        int* wb_rows, int* wb_indices, hipStream_t s);
+struct RowCopy {
+    const void* src;
+    void* dst;
+    int64_t row_bytes;
+};
+constexpr int kMaxRowTables = 32;
+void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_rows, const int* dst_rows,
+                       hipStream_t s);
+// optim.hip: one dense Adam step over up to kMaxRowTables tensors (OurAdam._single_tensor_adam2)
+struct AdamTensor {
+    float* param;
+    float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+    int64_t row_elems;        // elements per Gaussian row (skybox rows have their gradient zeroed)
+    float neg_step_size;      // -lr / (1 - beta1^step)
+};
+void launch_adam_multi(int T, const AdamTensor* t, int sky, float b1, float a1, float b2, float a2, float bc2_sqrt,
+                       float eps, hipStream_t s);
+
 // scan.hip
 void scan_inclusive_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp, hipStream_t s);
 

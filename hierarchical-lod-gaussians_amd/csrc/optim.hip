@@ -9,6 +9,12 @@
 // visibility byte per Gaussian.  Each thread owns four consecutive elements and moves them as float4 when
 // all four are visible; invisible elements are neither read nor written, so a sparse step only pays for
 // the visible rows.
+//
+// k_adam_multi: the dense per-step Adam of train_post.py:793-812 (OurAdam._single_tensor_adam2,
+// scene/OurAdam.py:357-448) over all six parameter tensors of the resident Gaussians in one launch, with the
+// skybox gradient rows zeroed first (train_post.py:786-791).  HBM-bound: 28 bytes per element.
+#include <algorithm>
+
 #include "hlgs_internal.h"
 
 namespace hlgs {
@@ -71,6 +77,76 @@ void launch_adam(float* param, const float* grad, float* m, float* v, const uint
     const int vec = ((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) & 15u) == 0) ? 1 : 0;
     hipLaunchKernelGGL(k_adam, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, param, grad, m, v, vis, lr, b1,
                        b2, eps, N, M, vec);
+}
+
+// torch's float32 sequence: exp_avg.mul_(b1).add_(g, alpha=1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, value=1-b2);
+// denom = (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps); param.addcdiv_(exp_avg, denom, value=-step_size).  The two
+// multiply-adds are fused as the GPU build of those torch kernels fuses them.
+__device__ __forceinline__ void adam_dense(float& p, float g, float& m, float& v, float ns, float b1, float a1, float b2,
+                                           float a2, float bc2s, float eps)
+{
+#pragma clang fp contract(off)
+    m = fmaf(a1, g, m * b1);
+    v = fmaf(a2 * g, g, v * b2);
+    const float den = sqrtf(v) / bc2s + eps;
+    p = (ns * m) / den + p;
+}
+
+struct AdamTabs {
+    AdamTensor t[kMaxRowTables];
+};
+
+__global__ void __launch_bounds__(256) k_adam_multi(AdamTabs tabs, int sky, float b1, float a1, float b2, float a2,
+                                                    float bc2s, float eps)
+{
+    const AdamTensor& t = tabs.t[blockIdx.y];
+    const int64_t n = t.numel, zero_end = std::min<int64_t>((int64_t)sky * t.row_elems, n);
+    const bool vec = ((((uintptr_t)t.param | (uintptr_t)t.grad | (uintptr_t)t.exp_avg | (uintptr_t)t.exp_avg_sq) & 15u) == 0);
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    for (; e < n; e += stride * 4) {
+        if (vec && e + 4 <= n && e >= zero_end) {
+            float4 p = *reinterpret_cast<const float4*>(t.param + e);
+            const float4 g = *reinterpret_cast<const float4*>(t.grad + e);
+            float4 m = *reinterpret_cast<const float4*>(t.exp_avg + e);
+            float4 v = *reinterpret_cast<const float4*>(t.exp_avg_sq + e);
+            adam_dense(p.x, g.x, m.x, v.x, t.neg_step_size, b1, a1, b2, a2, bc2s, eps);
+            adam_dense(p.y, g.y, m.y, v.y, t.neg_step_size, b1, a1, b2, a2, bc2s, eps);
+            adam_dense(p.z, g.z, m.z, v.z, t.neg_step_size, b1, a1, b2, a2, bc2s, eps);
+            adam_dense(p.w, g.w, m.w, v.w, t.neg_step_size, b1, a1, b2, a2, bc2s, eps);
+            *reinterpret_cast<float4*>(t.param + e) = p;
+            *reinterpret_cast<float4*>(t.exp_avg + e) = m;
+            *reinterpret_cast<float4*>(t.exp_avg_sq + e) = v;
+            continue;
+        }
+        for (int64_t k = e; k < std::min<int64_t>(e + 4, n); k++) {
+            float g = t.grad[k];
+            if (k < zero_end) {
+                g = 0.f;
+                t.grad[k] = 0.f;
+            }
+            float p = t.param[k], m = t.exp_avg[k], v = t.exp_avg_sq[k];
+            adam_dense(p, g, m, v, t.neg_step_size, b1, a1, b2, a2, bc2s, eps);
+            t.param[k] = p;
+            t.exp_avg[k] = m;
+            t.exp_avg_sq[k] = v;
+        }
+    }
+}
+
+void launch_adam_multi(int T, const AdamTensor* t, int sky, float b1, float a1, float b2, float a2, float bc2_sqrt,
+                       float eps, hipStream_t s)
+{
+    AdamTabs at{};
+    int64_t most = 0;
+    for (int i = 0; i < T; i++) {
+        at.t[i] = t[i];
+        most = std::max<int64_t>(most, t[i].numel);
+    }
+    const int64_t blocks = std::min<int64_t>((most + 1023) / 1024, 8192);
+    if (blocks > 0)
+        hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)blocks, T), dim3(256), 0, s, at, sky, b1, a1, b2, a2, bc2_sqrt,
+                           eps);
 }
 
 }  // namespace hlgs

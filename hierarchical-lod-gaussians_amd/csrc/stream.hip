@@ -8,6 +8,15 @@
 //                      storage[idx] = values.to(storage) write-backs (train_post.py:439-488).  Either side
 //                      may be pinned host memory: the GPU reads and writes it directly over the host link
 //                      instead of a CPU gather/scatter plus a copy.
+//   k_rows_multi    <- the same traffic for all of a step's tensors (parameters and Adam moments) in one launch
+//   k_cache_lists / k_cache_keep / k_cache_split
+//                   <- the SPT cache's bookkeeping (train_post.py:346-430): which of the previous view's SPTs
+//                      are reused, which are loaded, the new SPT_counts prefix, and which cached Gaussians stay
+//                      resident or are written back.  The reference does this with per-SPT Python loops and a
+//                      host read per kept SPT; here it is one single-workgroup pass over the SPT lists plus two
+//                      scans over the resident Gaussians, with one host read for all the sizes.
+#include <algorithm>
+
 #include "hlgs_internal.h"
 
 namespace hlgs {
@@ -162,6 +171,228 @@ void launch_rows(bool gather, long n, int row_bytes, const int64_t* idx, const v
             hipLaunchKernelGGL(k_rows_scatter<uint32_t>, grid, dim3(256), 0, s, n, row_bytes / 4, idx,
                                (const uint32_t*)src, (uint32_t*)dst);
     }
+}
+
+// ---------------------------------------------------------------- multi-tensor row copy
+// dst_t[dst_rows[i]] = src_t[src_rows[i]] for every table t (blockIdx.y); a NULL row list is the identity.  One
+// thread per 4-byte word: consecutive threads walk a row and then the next, so the identity side is contiguous.
+struct RowTabs {
+    RowCopy t[kMaxRowTables];
+};
+
+__global__ void __launch_bounds__(256) k_rows_multi(RowTabs tabs, int64_t n, const int* __restrict__ src_rows,
+                                                    const int* __restrict__ dst_rows)
+{
+    const RowCopy& tb = tabs.t[blockIdx.y];
+    const int64_t words = tb.row_bytes >> 2;
+    const int64_t total = n * words;
+    const uint32_t* __restrict__ src = static_cast<const uint32_t*>(tb.src);
+    uint32_t* __restrict__ dst = static_cast<uint32_t*>(tb.dst);
+    for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < total; w += (int64_t)gridDim.x * 256) {
+        const int64_t r = w / words, k = w - r * words;
+        const int64_t sr = src_rows ? src_rows[r] : r;
+        const int64_t dr = dst_rows ? dst_rows[r] : r;
+        dst[dr * words + k] = src[sr * words + k];
+    }
+}
+
+void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_rows, const int* dst_rows, hipStream_t s)
+{
+    RowTabs rt{};
+    int64_t most = 0;
+    for (int t = 0; t < T; t++) {
+        rt.t[t] = tabs[t];
+        most = std::max<int64_t>(most, n * (tabs[t].row_bytes >> 2));
+    }
+    const int64_t blocks = std::min<int64_t>((most + 255) / 256, 16384);
+    if (blocks > 0) hipLaunchKernelGGL(k_rows_multi, dim3((unsigned)blocks, T), dim3(256), 0, s, rt, n, src_rows, dst_rows);
+}
+
+// ---------------------------------------------------------------- SPT cache bookkeeping
+// exclusive prefix of an int over the 1024-thread block
+__device__ __forceinline__ int block_excl_sum(int v, int* s_w, int* total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    __syncthreads();
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    int before = 0, t = 0;
+    for (int i = 0; i < 16; i++) {
+        const int c = s_w[i];
+        if (i < w) before += c;
+        t += c;
+    }
+    *total = t;
+    return before + x - v;
+}
+
+// a Python slice bound against a sequence of length R (step 1)
+__device__ __forceinline__ int py_bound(int x, int R)
+{
+    if (x < 0) {
+        x += R;
+        return x < 0 ? 0 : x;
+    }
+    return x > R ? R : x;
+}
+
+// torch.isclose on float32 (allowed = atol + |rtol * b|; finite |a - b| <= allowed, or a == b)
+__device__ __forceinline__ bool is_close(float a, float b, float rtol, float atol)
+{
+#pragma clang fp contract(off)
+    if (a == b) return true;
+    const float err = fabsf(a - b);
+    const float allowed = atol + fabsf(rtol * b);
+    return isfinite(err) && err <= allowed;
+}
+
+__global__ void __launch_bounds__(1024) k_cache_lists(CacheArgs a)
+{
+#pragma clang fp contract(off)
+    __shared__ int s_w[16];
+    // 1. leaves of the cut, in cut order: SPT leaves (first_child >= 0, with their camera distance) and
+    //    upper-tree Gaussians to render (first_child <= 0; a leaf holding SPT 0 is in both lists, as in the
+    //    reference's two masks)
+    int ns = 0, nu = 0;
+    for (int c0 = 0; c0 < a.n_cut; c0 += 1024) {
+        const int i = c0 + threadIdx.x;
+        int v = 0, fc = -1;
+        bool leaf = false;
+        if (i < a.n_cut) {
+            v = a.cut[i];
+            leaf = a.nodes[6 * v + 2] == 0;
+            fc = a.nodes[6 * v + 3];
+        }
+        const bool is_s = leaf && fc >= 0, is_u = leaf && fc <= 0;
+        int ts, tu;
+        const int ps = block_excl(is_s, s_w, &ts);
+        const int pu = block_excl(is_u, s_w, &tu);
+        if (is_s) {
+            const float dx = a.xyz[3 * v] - a.campos[0], dy = a.xyz[3 * v + 1] - a.campos[1],
+                        dz = a.xyz[3 * v + 2] - a.campos[2];
+            a.spt_idx[ns + ps] = fc;
+            a.spt_dist[ns + ps] = sqrtf(dx * dx + dy * dy + dz * dz) * a.dmul;
+        }
+        if (is_u) a.upper[nu + pu] = a.nodes[6 * v + 5];
+        ns += ts;
+        nu += tu;
+    }
+    __syncthreads();
+    // 2. previous SPTs: torch.searchsorted (lower bound; the list is in cut order, not sorted, and the search
+    //    runs on it as it is), equal id and isclose distance -> kept, with the reference's segment bounds
+    int nk = 0, prefix = 0;
+    for (int c0 = 0; c0 < a.m; c0 += 1024) {
+        const int j = c0 + threadIdx.x;
+        bool keep = false;
+        int pv = 0, d = 0, start = 0, to = 0;
+        if (j < a.m) {
+            pv = a.prev_idx[j];
+            int lo = 0, hi = ns;
+            while (lo < hi) {
+                const int mid = lo + ((hi - lo) >> 1);
+                if (!(a.spt_idx[mid] >= pv)) lo = mid + 1;
+                else hi = mid;
+            }
+            keep = lo < ns && a.spt_idx[lo] == pv && is_close(a.spt_dist[lo], a.prev_dist[j], a.rtol, a.atol);
+            if (keep) {
+                start = a.prev_counts[j];
+                to = j == a.m - 1 ? a.tail_end : a.prev_counts[j + 1];
+                d = to - start;
+            }
+        }
+        int tk, td;
+        const int pk = block_excl(keep, s_w, &tk);
+        const int pd = block_excl_sum(d, s_w, &td);
+        if (keep) {
+            a.keep_idx[nk + pk] = pv;
+            a.keep_dist[nk + pk] = a.prev_dist[j];
+            a.keep_counts[nk + pk] = prefix + pd;
+            if (pv >= 0 && pv < a.num_spts) a.flag[pv] = 1;
+            const int lo = py_bound(start, a.R), hi = py_bound(to, a.R);
+            if (hi > lo) {
+                atomicAdd(a.diff + lo, 1);
+                atomicAdd(a.diff + hi, -1);
+            }
+        }
+        nk += tk;
+        prefix += td;
+    }
+    __syncthreads();
+    // 3. the cut's SPTs whose id was not kept (torch.isin) are loaded, in cut order
+    int nl = 0;
+    for (int c0 = 0; c0 < ns; c0 += 1024) {
+        const int k = c0 + threadIdx.x;
+        bool load = false;
+        int v = 0;
+        if (k < ns) {
+            v = a.spt_idx[k];
+            load = !(v >= 0 && v < a.num_spts && a.flag[v]);
+        }
+        int tl;
+        const int pl = block_excl(load, s_w, &tl);
+        if (load) {
+            a.load_idx[nl + pl] = v;
+            a.load_dist[nl + pl] = a.spt_dist[k];
+        }
+        nl += tl;
+    }
+    if (threadIdx.x == 0) {
+        a.sizes[0] = nk;
+        a.sizes[1] = nl;
+        a.sizes[2] = nu;
+        a.sizes[3] = prefix;
+    }
+}
+
+void launch_cache_lists(const CacheArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_cache_lists, dim3(1), dim3(1024), 0, s, a);
+}
+
+// keep_gaussians_mask: the skybox prefix, or covered by a kept SPT's segment (running sum of the +1/-1 marks)
+__global__ void __launch_bounds__(256) k_cache_keep(int R, int sky, const uint32_t* __restrict__ diff_incl,
+                                                    uint32_t* __restrict__ keep)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < R) keep[i] = (i < sky || (int)diff_incl[i] > 0) ? 1u : 0u;
+}
+
+void launch_cache_keep(int R, int sky, const uint32_t* diff_incl, uint32_t* keep, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_cache_keep, dim3((R + 255) / 256), dim3(256), 0, s, R, sky, diff_incl, keep);
+}
+
+// render_indices[keep] / nonzero(keep) and render_indices[~keep] / nonzero(~keep), both in order
+__global__ void __launch_bounds__(256) k_cache_split(int R, const int* __restrict__ render,
+                                                     const uint32_t* __restrict__ keep_incl, int* __restrict__ keep_rows,
+                                                     int* __restrict__ render_kept, int* __restrict__ wb_rows,
+                                                     int* __restrict__ wb_indices)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= R) return;
+    const int incl = (int)keep_incl[i];
+    const int prev = i ? (int)keep_incl[i - 1] : 0;
+    if (incl != prev) {
+        keep_rows[incl - 1] = i;
+        render_kept[incl - 1] = render[i];
+    } else {
+        const int w = i - incl;
+        wb_rows[w] = i;
+        wb_indices[w] = render[i];
+    }
+}
+
+void launch_cache_split(int R, const int* render, const uint32_t* keep_incl, int* keep_rows, int* render_kept,
+                        int* wb_rows, int* wb_indices, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_cache_split, dim3((R + 255) / 256), dim3(256), 0, s, R, render, keep_incl, keep_rows,
+                       render_kept, wb_rows, wb_indices);
 }
 
 }  // namespace hlgs

@@ -45,6 +45,29 @@ class FrameInfo(C.Structure):
     _fields_ = [("num_rendered", _i), ("max_tile_count", _i), ("rendered", _i), ("num_binned", _i)]
 
 
+class CacheArgs(C.Structure):
+    _fields_ = [("n_cut", _i), ("cut", _vp), ("upper_nodes", _vp), ("upper_xyz", _vp), ("campos", _vp),
+                ("distance_multiplier", _f), ("num_spts", _i), ("m", _i), ("prev_spt_indices", _vp),
+                ("prev_spt_distances", _vp), ("prev_spt_counts", _vp), ("R", _i), ("render_indices", _vp),
+                ("n_loaded_prev", _i), ("skybox_points", _i), ("rtol", _f), ("atol", _f)]
+
+
+class CachePlan(C.Structure):
+    _fields_ = [("keep_spt_indices", _vp), ("keep_spt_distances", _vp), ("keep_spt_counts", _vp),
+                ("load_spt_indices", _vp), ("load_spt_distances", _vp), ("upper_render", _vp), ("keep_rows", _vp),
+                ("render_kept", _vp), ("write_back_rows", _vp), ("write_back_indices", _vp), ("n_kept", _i),
+                ("n_load", _i), ("n_upper", _i), ("n_keep_rows", _i), ("prefix", _i)]
+
+
+class RowCopy(C.Structure):
+    _fields_ = [("src", _vp), ("dst", _vp), ("row_bytes", C.c_int64)]
+
+
+class AdamTensor(C.Structure):
+    _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("numel", C.c_int64),
+                ("row_elems", C.c_int64), ("lr", C.c_double)]
+
+
 _SIGS = {
     "hlgs_last_error": (C.c_char_p, []),
     "hlgs_version": (C.c_char_p, []),
@@ -66,6 +89,10 @@ _SIGS = {
     "hlgs_upper_cut_scratch_size": (_sz, [_i]),
     "hlgs_upper_tree_cut": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, C.POINTER(_i), _vp]),
     "hlgs_gather_rows": (_i, [C.c_int64, _i, _vp, _vp, _vp, _vp]),
+    "hlgs_spt_cache_scratch_size": (_sz, [_i, _i, _i, _i]),
+    "hlgs_spt_cache_plan": (_i, [C.POINTER(CacheArgs), C.POINTER(CachePlan), _vp, _vp]),
+    "hlgs_copy_rows": (_i, [_i, C.POINTER(RowCopy), C.c_int64, _vp, _vp, _vp]),
+    "hlgs_adam_step": (_i, [_i, C.POINTER(AdamTensor), C.c_int64, _i, C.c_double, C.c_double, C.c_double, _vp]),
     "hlgs_spt_build": (_i, [_i, _vp, _vp, _vp, _i, _f, _f, _i, _i, C.POINTER(_vp)]),
     "hlgs_spt_result_sizes": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),
     "hlgs_spt_result_copy": (_i, [_vp] * 11),

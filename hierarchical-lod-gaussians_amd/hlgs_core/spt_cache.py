@@ -1,0 +1,217 @@
+"""train_post.py's SPT cache (Cache_SPTs=True) on the HIP path.
+
+The reference keeps every Gaussian in host storage (GaussianModel.move_storage_to, scene/gaussian_model.py
+:430-460) and, per training view, keeps on the GPU only the Gaussians of the SPTs the view cuts:
+
+  setup                  train_post.py:208-231  (skybox resident, empty SPT state)
+  coarse cut             :326-343  -> spt.upper_tree_cut (one workgroup, k_upper_cut)
+  bookkeeping            :346-430  -> hlgs_spt_cache_plan (k_cache_lists + two scans + k_cache_split), with
+                                      get_spt_cut_cuda on the SPTs to load
+  write-back and load    :439-479  -> hlgs_copy_rows: three launches move all six parameters and their twelve
+                                      Adam moments (write-back, resident compaction, load); the host side is
+                                      pinned memory the GPU reads and writes directly
+  optimizer step         :786-812  -> hlgs_adam_step (one launch over the six tensors, skybox gradients zeroed)
+
+Differences from the reference: when the Gaussian budget forces a second pass, each pass
+starts again from the step's initial state with the larger distance multiplier (the reference's second pass
+reads state its first pass already replaced and then fails on mismatched masks); occlusion culling (a render
+inside the cut) is not provided.
+"""
+import ctypes as C
+import math
+
+import torch
+
+from hlgs_core import _lib as L
+from hlgs_core import spt as _spt
+
+NAMES = ("xyz", "f_dc", "opacity", "scaling", "rotation", "f_rest")
+
+
+def _p(t):
+    return t.data_ptr() if t is not None and t.numel() else None
+
+
+def _row_bytes(t):
+    return t.element_size() * math.prod(t.shape[1:])
+
+
+def copy_rows(pairs, n, src_rows=None, dst_rows=None):
+    """dst[dst_rows[i]] = src[src_rows[i]] for every (src, dst) pair, one launch (hlgs_copy_rows)."""
+    lib = L.load()
+    if n == 0 or not pairs:
+        return
+    tabs = (L.RowCopy * len(pairs))()
+    for k, (src, dst) in enumerate(pairs):
+        for t in (src, dst):
+            if not t.is_contiguous():
+                raise RuntimeError("row storage must be contiguous")
+            if t.device.type == "cpu" and not t.is_pinned():
+                raise RuntimeError("host storage must be pinned (tensor.pin_memory()) for direct GPU access")
+        rb = _row_bytes(src)
+        if rb != _row_bytes(dst) or src.dtype != dst.dtype:
+            raise RuntimeError("source and destination rows differ")
+        tabs[k] = L.RowCopy(src.data_ptr(), dst.data_ptr(), rb)
+    L.check(lib.hlgs_copy_rows(len(pairs), tabs, int(n), _p(src_rows), _p(dst_rows), L.stream()))
+
+
+def adam_step(params, grads, exp_avgs, exp_avg_sqs, lrs, step, skybox_points=0, beta1=0.9, beta2=0.999, eps=1e-8):
+    """The dense Adam of train_post.py:786-812 over a list of float32 tensors (in place, one launch): grads of
+    the first skybox_points rows are zeroed, then OurAdam._single_tensor_adam2 with state step `step` (the
+    reference passes torch.tensor(iteration) and increments it, so step = iteration + 1)."""
+    lib = L.load()
+    ts = (L.AdamTensor * len(params))()
+    for k, (p, g, m, v, lr) in enumerate(zip(params, grads, exp_avgs, exp_avg_sqs, lrs)):
+        for t in (p, g, m, v):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != p.numel():
+                raise RuntimeError("Adam tensors must be contiguous float32 of the parameter's size")
+        L.require_gpu(p, g, m, v)
+        rows = p.size(0) if p.dim() else 1
+        ts[k] = L.AdamTensor(_p(p), _p(g), _p(m), _p(v), p.numel(), p.numel() // rows if rows else 0, float(lr))
+    L.check(lib.hlgs_adam_step(len(params), ts, int(step), int(skybox_points), float(beta1), float(beta2), float(eps),
+                               L.stream()))
+
+
+class SPTCache:
+    """Resident set of a cached training run.  storage: dict name -> host tensor of all Gaussians (rows), for
+    the names in NAMES; opt_storage: dict name -> {"exp_avgs", "exp_avgs_sqs"} of the same shapes (zero-filled
+    when None).  Host tensors are pinned here if they are not already.  spt: build_hierarchical_spt's dict.
+
+    After step(), `params`, `exp_avgs` and `exp_avg_sqs` (dicts of device tensors) hold the resident rows in
+    render_indices order, as the reference's parameter list does."""
+
+    def __init__(self, storage, spt, skybox_points, opt_storage=None, reuse_tolerance=0.9,
+                 max_gaussian_budget=100_000_000, distance_multiplier_until_budget=1.5, use_frustum_culling=True,
+                 use_bounding_spheres=True, device="cuda"):
+        pin = lambda t: t if t.device.type != "cpu" or t.is_pinned() else t.contiguous().pin_memory()  # noqa: E731
+        self.storage = {k: pin(storage[k].contiguous()) for k in NAMES}
+        if opt_storage is None:
+            opt_storage = {k: {"exp_avgs": torch.zeros_like(self.storage[k]),
+                               "exp_avgs_sqs": torch.zeros_like(self.storage[k])} for k in NAMES}
+        self.opt_storage = {k: {s: pin(opt_storage[k][s].contiguous()) for s in ("exp_avgs", "exp_avgs_sqs")}
+                            for k in NAMES}
+        self.device = torch.device(device)
+        dev = self.device
+        self.nodes = spt["upper_tree_nodes"].to(dev, torch.int32).contiguous()
+        self.xyz = spt["upper_tree_xyz"].to(dev, torch.float32).contiguous()
+        self.min_distance_squared = spt["min_distance_squared"].to(dev, torch.float32).contiguous()
+        if use_bounding_spheres:
+            self.bounds = spt["bounding_sphere_radii"].to(dev, torch.float32).contiguous()
+        else:  # scaling_activation(max(upper_tree_scaling)) * 3.0 (train_post.py:330)
+            self.bounds = (torch.exp(torch.max(spt["upper_tree_scaling"].to(dev, torch.float32), dim=-1)[0]) * 3.0)
+        self.spt_starts = spt["SPT_starts"].to(dev, torch.int32).contiguous()
+        self.spt_max = spt["SPT_max"].to(dev, torch.float32).contiguous()
+        self.spt_min = spt["SPT_min"].to(dev, torch.float32).contiguous()
+        self.spt_gidx = spt["SPT_gaussian_indices"].to(dev, torch.int32).contiguous()
+        self.num_spts = int(self.spt_starts.numel()) - 1
+        self.sky = int(skybox_points)
+        self.rtol, self.atol = float(reuse_tolerance), 0.05
+        self.budget = max_gaussian_budget
+        self.dm_step = distance_multiplier_until_budget
+        self.use_frustum = use_frustum_culling
+        # setup, train_post.py:208-231
+        self.render_indices = torch.arange(0, self.sky, device=dev, dtype=torch.int32)
+        head = torch.arange(0, self.sky, device=dev, dtype=torch.int32)
+        self.params = {k: self._alloc(k, self.sky) for k in NAMES}
+        copy_rows([(self.storage[k], self.params[k]) for k in NAMES], self.sky, head, None)
+        self.exp_avgs = {k: torch.zeros_like(self.params[k]) for k in NAMES}
+        self.exp_avg_sqs = {k: torch.zeros_like(self.params[k]) for k in NAMES}
+        self.prev_SPT_indices = torch.empty(0, dtype=torch.int32, device=dev)
+        self.prev_SPT_distances = torch.empty(0, dtype=torch.float32, device=dev)
+        self.prev_SPT_counts = torch.empty(0, dtype=torch.int32, device=dev)
+        self.n_loaded = 0
+        self.last_plan = None
+
+    def _alloc(self, k, rows):
+        return torch.empty((rows,) + tuple(self.storage[k].shape[1:]), dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------ bookkeeping (:326-430)
+    def plan(self, full_proj_transform, camera_center, distance_multiplier=1.0):
+        """One bookkeeping pass for a view; no parameter moves.  Returns the reference's per-pass variables."""
+        lib = L.load()
+        dev = self.device
+        cam = camera_center.detach().reshape(-1)[:3].to(dev, torch.float32).contiguous()
+        planes = _spt.extract_frustum_planes(full_proj_transform.to(dev, torch.float32)) if self.use_frustum else None
+        coarse = _spt.upper_tree_cut(self.nodes, self.xyz, self.bounds, self.min_distance_squared, planes, cam,
+                                     distance_multiplier, self.use_frustum, True)
+        n_cut, m, R = coarse.numel(), self.prev_SPT_indices.numel(), self.render_indices.numel()
+        i32 = lambda n: torch.empty(max(n, 1), dtype=torch.int32, device=dev)  # noqa: E731
+        f32 = lambda n: torch.empty(max(n, 1), dtype=torch.float32, device=dev)  # noqa: E731
+        out = dict(keep_spt_indices=i32(m), keep_spt_distances=f32(m), keep_spt_counts=i32(m),
+                   load_spt_indices=i32(n_cut), load_spt_distances=f32(n_cut), upper_render=i32(n_cut),
+                   keep_rows=i32(R), render_kept=i32(R), write_back_rows=i32(R), write_back_indices=i32(R))
+        a = L.CacheArgs(n_cut, _p(coarse), _p(self.nodes), _p(self.xyz), _p(cam), float(distance_multiplier),
+                        self.num_spts, m, _p(self.prev_SPT_indices), _p(self.prev_SPT_distances),
+                        _p(self.prev_SPT_counts), R, _p(self.render_indices), int(self.n_loaded), self.sky,
+                        self.rtol, self.atol)
+        pl = L.CachePlan(*[out[f].data_ptr() for f, _ in L.CachePlan._fields_[:10]])
+        scratch = torch.empty(lib.hlgs_spt_cache_scratch_size(n_cut, m, R, self.num_spts), dtype=torch.uint8,
+                              device=dev)
+        L.check(lib.hlgs_spt_cache_plan(C.byref(a), C.byref(pl), scratch.data_ptr(), L.stream()))
+        nk, nl, nu, nkr, prefix = pl.n_kept, pl.n_load, pl.n_upper, pl.n_keep_rows, pl.prefix
+        load_idx, load_dist = out["load_spt_indices"][:nl], out["load_spt_distances"][:nl]
+        if nl > 0:
+            import gaussian_hierarchy._C as GHC
+            cut_spts, spt_counts = GHC.get_spt_cut_cuda(nl, self.spt_gidx, self.spt_starts, self.spt_max,
+                                                        self.spt_min, load_idx, load_dist)
+        else:
+            cut_spts = torch.empty(0, dtype=torch.int32, device=dev)
+            spt_counts = torch.empty(0, dtype=torch.int32, device=dev)
+        load_from_disk = torch.cat([cut_spts, out["upper_render"][:nu]])
+        return dict(
+            SPT_indices=torch.cat([out["keep_spt_indices"][:nk], load_idx]),
+            SPT_distances=torch.cat([out["keep_spt_distances"][:nk], load_dist]),
+            SPT_counts=torch.cat([out["keep_spt_counts"][:nk], spt_counts + (self.sky + prefix)]),
+            keep_rows=out["keep_rows"][:nkr], write_back_rows=out["write_back_rows"][:R - nkr],
+            write_back_indices=out["write_back_indices"][:R - nkr], load_from_disk_indices=load_from_disk,
+            render_indices=torch.cat([out["render_kept"][:nkr], load_from_disk]), n_kept=nk,
+            load_SPT_indices=load_idx, upper_tree_nodes_to_render=out["upper_render"][:nu], prefix=prefix,
+            distance_multiplier=distance_multiplier)
+
+    # ------------------------------------------------------------ one view (:326-483)
+    def step(self, full_proj_transform, camera_center):
+        dm = 1.0
+        while True:
+            pl = self.plan(full_proj_transform, camera_center, dm)
+            if pl["render_indices"].numel() <= self.budget:
+                break
+            dm *= self.dm_step
+        self._move(pl)
+        self.prev_SPT_indices = pl["SPT_indices"]
+        self.prev_SPT_distances = pl["SPT_distances"]
+        self.prev_SPT_counts = pl["SPT_counts"]
+        self.render_indices = pl["render_indices"]
+        self.n_loaded = pl["load_from_disk_indices"].numel()
+        self.last_plan = pl
+        return self.render_indices
+
+    def _move(self, pl):
+        dev_t = [self.params[k] for k in NAMES] + [self.exp_avgs[k] for k in NAMES] + \
+                [self.exp_avg_sqs[k] for k in NAMES]
+        host_t = [self.storage[k] for k in NAMES] + [self.opt_storage[k]["exp_avgs"] for k in NAMES] + \
+                 [self.opt_storage[k]["exp_avgs_sqs"] for k in NAMES]
+        wb = pl["write_back_rows"]
+        # write the evicted rows back to storage (:439-444, :473-474)
+        copy_rows([(d.detach(), h) for d, h in zip(dev_t, host_t)], wb.numel(), wb, pl["write_back_indices"])
+        nk = pl["keep_rows"].numel()
+        load = pl["load_from_disk_indices"]
+        rows = nk + load.numel()
+        new_t = [torch.empty((rows,) + tuple(d.shape[1:]), dtype=d.dtype, device=self.device) for d in dev_t]
+        # resident rows that stay, then the loaded rows (:446-479)
+        copy_rows([(d.detach(), n) for d, n in zip(dev_t, new_t)], nk, pl["keep_rows"], None)
+        copy_rows([(h, n[nk:]) for h, n in zip(host_t, new_t)], load.numel(), load, None)
+        k6 = len(NAMES)
+        self.params = {k: new_t[i].requires_grad_(True) for i, k in enumerate(NAMES)}
+        self.exp_avgs = {k: new_t[k6 + i] for i, k in enumerate(NAMES)}
+        self.exp_avg_sqs = {k: new_t[2 * k6 + i] for i, k in enumerate(NAMES)}
+
+    # ------------------------------------------------------------ optimizer step (:786-812)
+    def optimizer_step(self, iteration, lrs):
+        """lrs: dict name -> learning rate.  Uses the gradients autograd left on self.params."""
+        ps = [self.params[k] for k in NAMES]
+        for p in ps:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        with torch.no_grad():
+            adam_step([p.data for p in ps], [p.grad for p in ps], [self.exp_avgs[k] for k in NAMES],
+                      [self.exp_avg_sqs[k] for k in NAMES], [lrs[k] for k in NAMES], int(iteration) + 1, self.sky)

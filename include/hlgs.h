@@ -22,6 +22,10 @@
  *        reference's candidate-count sync, runtime_switching.cu:926-931)
  *   hlgs_lod_interp_forward/_backward       <- the Python child/parent lerp of render_post,
  *        gaussian_renderer/__init__.py:304-339 (interp_python=True), and its autograd
+ *   hlgs_upper_tree_cut, hlgs_spt_cache_plan, hlgs_copy_rows, hlgs_adam_step, hlgs_spt_build
+ *                                           <- the SPT streaming step of train_post.py:323-491, 786-812 and
+ *        GaussianModel.build_hierarchical_SPT (scene/gaussian_model.py:184-352), which the reference runs as
+ *        Python loops over torch ops
  *   hlgs_adam_update                        <- adamUpdate, submodules/alt-rasterizer/rasterize_points.cu:255-281
  *        (kernel cuda_rasterizer/adam.cu:9-36), bound as _C.adamUpdate (ext.cpp:19)
  *
@@ -248,6 +252,71 @@ void hlgs_spt_result_free(hlgs_spt_result* r);
  * pinned host memory (read and written by the GPU over the host link). */
 int hlgs_gather_rows(int64_t n, int row_bytes, const int64_t* idx, const void* src, void* dst, void* stream);
 int hlgs_scatter_rows(int64_t n, int row_bytes, const int64_t* idx, const void* src, void* dst, void* stream);
+
+/* One bookkeeping pass of train_post.py's SPT cache (the body of the budget loop, :346-430): given the view's
+ * coarse cut and the previous step's SPT state, decide which SPTs are reused, which are loaded, and which
+ * resident Gaussians stay or are written back.  All arrays are device int32/float32 unless noted. */
+typedef struct hlgs_cache_args {
+    int n_cut;                         /* coarse cut (hlgs_upper_tree_cut) */
+    const int* cut;
+    const int* upper_nodes;            /* upper tree, n_upper x 6 */
+    const float* upper_xyz;            /* n_upper x 3 */
+    const float* campos;               /* 3 */
+    float distance_multiplier;         /* SPT distances are |xyz - campos| * distance_multiplier */
+    int num_spts;                      /* SPT ids are in [0, num_spts) */
+    int m;                             /* prev_SPT_indices / _distances / _counts, m each */
+    const int* prev_spt_indices;
+    const float* prev_spt_distances;
+    const int* prev_spt_counts;
+    int R;                             /* len(render_indices) */
+    const int* render_indices;
+    int n_loaded_prev;                 /* len(load_from_disk_indices) of the previous pass */
+    int skybox_points;
+    float rtol, atol;                  /* isclose of the reused distances (Reuse_SPT_Tolerarance, 0.05) */
+} hlgs_cache_args;
+typedef struct hlgs_cache_plan {
+    int* keep_spt_indices;             /* m: keep_SPT_indices */
+    float* keep_spt_distances;         /* m: prev_SPT_distances[SPT_keep_counts_indices] */
+    int* keep_spt_counts;              /* m: SPT_counts_new[:n_kept] */
+    int* load_spt_indices;             /* n_cut: load_SPT_indices (for hlgs_spt_cut_*) */
+    float* load_spt_distances;         /* n_cut */
+    int* upper_render;                 /* n_cut: upper_tree_nodes_to_render */
+    int* keep_rows;                    /* R: nonzero(keep_gaussians_mask) */
+    int* render_kept;                  /* R: render_indices[keep_gaussians_mask] */
+    int* write_back_rows;              /* R: nonzero(write_back_mask) */
+    int* write_back_indices;           /* R: render_indices[write_back_mask] */
+    int n_kept, n_load, n_upper;       /* host outputs: list lengths */
+    int n_keep_rows;                   /* R - n_keep_rows rows are written back */
+    int prefix;                        /* the prefix the loaded SPTs' counts are shifted by (plus skybox_points) */
+} hlgs_cache_plan;
+/* scratch: hlgs_spt_cache_scratch_size bytes; one host synchronisation for all the sizes. */
+size_t hlgs_spt_cache_scratch_size(int n_cut, int m, int R, int num_spts);
+int hlgs_spt_cache_plan(const hlgs_cache_args* a, hlgs_cache_plan* plan, void* scratch, void* stream);
+/* dst_t[dst_rows[i]] = src_t[src_rows[i]] for i < n and every table t < T (at most 32); a NULL row list is the
+ * identity.  row_bytes a multiple of 4; src / dst may be pinned host memory.  All of a cache step's parameter
+ * and Adam-moment traffic (train_post.py:439-479) in one launch per direction. */
+typedef struct hlgs_row_copy {
+    const void* src;
+    void* dst;
+    int64_t row_bytes;
+} hlgs_row_copy;
+int hlgs_copy_rows(int T, const hlgs_row_copy* tables, int64_t n, const int* src_rows, const int* dst_rows,
+                   void* stream);
+/* Dense Adam step of the cached training loop (train_post.py:786-812: skybox gradient rows zeroed, then
+ * OurAdam._single_tensor_adam2, scene/OurAdam.py:357-448, with state step = step) over T (at most 32) tensors in
+ * one launch.  The scalars follow torch: lr, betas and eps are the caller's doubles; step_size =
+ * lr / (1 - beta1^step) and sqrt(1 - beta2^step) are formed in double, then every tensor op runs in float32. */
+typedef struct hlgs_adam_tensor {
+    float* param;
+    float* grad;                       /* rows < skybox_rows are set to 0 before the update */
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+    int64_t row_elems;                 /* elements per Gaussian row */
+    double lr;
+} hlgs_adam_tensor;
+int hlgs_adam_step(int T, const hlgs_adam_tensor* tensors, int64_t step, int skybox_rows, double beta1, double beta2,
+                   double eps, void* stream);
 
 /* ---- photometric losses of the training step (utils/loss_utils.py:17-63, train_single.py:106-121,
  *      train_post.py:558-559 with the un-vendored fused_ssim) ---- */

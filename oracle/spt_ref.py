@@ -6,6 +6,13 @@ a leave_out_of_cut_condition (scene/gaussian_model.py:364-404), the frustum_cull
 (:80-100) and the LOD distance condition of train_post.py:336: a level-by-level walk of a `stack` that is
 filtered by the cull, sends leaves and then condition-false nodes to the cut, and continues with the first
 children followed by the first children's next siblings.  float32 arithmetic in the reference's order.
+
+Also restated here (same status: checkers of csrc/stream.hip and csrc/optim.hip, never the product path):
+  cache_pass   one pass of train_post.py's SPT-cache bookkeeping (:346-430) -- searchsorted of the previous
+               SPTs in the (unsorted) new list, isclose reuse test, Python-slice segment marks, isin, the
+               SPT_counts prefix, and the keep / write-back split of render_indices
+  adam_dense   OurAdam._single_tensor_adam2 (scene/OurAdam.py:357-448) with the skybox gradient rows zeroed
+               (train_post.py:786-791), as float32 torch ops on the CPU
 """
 import numpy as np
 
@@ -171,3 +178,95 @@ def build_spt(nodes, xyz, scaling, root, volume, tg, min_size=100, use_bounding_
                 SPT_min=cat(smin, torch.float32), SPT_gaussian_indices=cat(gidx, torch.int32),
                 SPT_root_hierarchy_indices=torch.tensor(roots, dtype=torch.int32), upper_tree_nodes=un.to(torch.int32),
                 upper_tree_xyz=uxyz, upper_tree_scaling=uscale, min_distance_squared=md2, bounding_sphere_radii=radii)
+
+
+# ---------------------------------------------------------------- SPT cache (train_post.py:346-430)
+def lower_bound(arr, v):
+    """torch.searchsorted(arr, v) (right=False): a plain lower-bound binary search over arr as it is given."""
+    lo, hi = 0, len(arr)
+    while lo < hi:
+        mid = lo + ((hi - lo) >> 1)
+        if not arr[mid] >= v:
+            lo = mid + 1
+        else:
+            hi = mid
+    return lo
+
+
+def isclose32(a, b, rtol, atol):
+    """torch.isclose on float32 scalars: a == b, or finite |a - b| <= atol + |rtol * b| (scalars in float32)."""
+    f = np.float32
+    a, b = f(a), f(b)
+    if a == b:
+        return True
+    err = f(abs(f(a - b)))
+    allowed = f(f(atol) + f(abs(f(f(rtol) * b))))
+    return bool(np.isfinite(err) and err <= allowed)
+
+
+def spt_distances(xyz, cam, dmul):
+    """(upper_tree_xyz[i] - camera_position).pow(2).sum(1).sqrt() * distance_multiplier, float32."""
+    d = (np.asarray(xyz, np.float32) - np.asarray(cam, np.float32)).astype(np.float32)
+    q = (d * d).astype(np.float32)
+    s = ((q[:, 0] + q[:, 1]).astype(np.float32) + q[:, 2]).astype(np.float32)
+    return (np.sqrt(s).astype(np.float32) * np.float32(dmul)).astype(np.float32)
+
+
+def cache_pass(nodes, xyz, coarse, cam, dmul, prev_idx, prev_dist, prev_counts, render, n_loaded_prev, sky, rtol,
+               atol, spt_cut):
+    """One pass of the SPT cache bookkeeping.  spt_cut(load_idx, load_dist) -> (cut, counts_prefix) is
+    get_spt_cut_cuda's restatement.  Returns a dict of numpy arrays named after the reference's variables."""
+    nodes = np.asarray(nodes)
+    coarse = np.asarray(coarse, np.int64)
+    leaf_nodes = coarse[nodes[coarse, 2] == 0]
+    fc = nodes[leaf_nodes, 3]
+    spt_idx = fc[fc >= 0].astype(np.int32)
+    spt_nodes = leaf_nodes[fc >= 0]
+    upper = nodes[leaf_nodes[fc <= 0], 5].astype(np.int32)
+    dist = spt_distances(np.asarray(xyz)[spt_nodes].reshape(-1, 3), cam, dmul)
+    m, R = len(prev_idx), len(render)
+    tail_end = R - n_loaded_prev
+    kept = []
+    for j in range(m):
+        pos = lower_bound(spt_idx, prev_idx[j])
+        if pos < len(spt_idx) and spt_idx[pos] == prev_idx[j] and isclose32(dist[pos], prev_dist[j], rtol, atol):
+            kept.append(j)
+    seg_end = lambda j: int(prev_counts[j + 1]) if j + 1 < m else tail_end  # noqa: E731
+    keep = np.zeros(R, bool)
+    for j in kept:
+        keep[int(prev_counts[j]):seg_end(j)] = True
+    keep[:sky] = True
+    keep_idx = np.asarray([prev_idx[j] for j in kept], np.int32)
+    keep_dist = np.asarray([prev_dist[j] for j in kept], np.float32)
+    load = ~np.isin(spt_idx, keep_idx)
+    load_idx, load_dist = spt_idx[load], dist[load]
+    if len(load_idx):
+        cut, counts = spt_cut(load_idx, load_dist)
+    else:
+        cut, counts = np.zeros(0, np.int32), np.zeros(0, np.int32)
+    counts = np.asarray(counts, np.int64) + sky
+    prefix, keep_counts = 0, []
+    for j in kept:
+        keep_counts.append(prefix)
+        prefix += seg_end(j) - int(prev_counts[j])
+    render = np.asarray(render, np.int32)
+    load_from_disk = np.concatenate([np.asarray(cut, np.int32), upper]).astype(np.int32)
+    return dict(SPT_indices=np.concatenate([keep_idx, load_idx]).astype(np.int32),
+                SPT_distances=np.concatenate([keep_dist, load_dist]).astype(np.float32),
+                SPT_counts=np.concatenate([np.asarray(keep_counts, np.int64), counts + prefix]).astype(np.int32),
+                keep_mask=keep, write_back_indices=render[~keep], load_from_disk_indices=load_from_disk,
+                render_indices=np.concatenate([render[keep], load_from_disk]).astype(np.int32),
+                n_kept=len(kept), load_SPT_indices=load_idx, upper_tree_nodes_to_render=upper, prefix=prefix)
+
+
+# ---------------------------------------------------------------- dense Adam (train_post.py:786-812)
+def adam_dense(param, grad, exp_avg, exp_avg_sq, lr, step, sky, beta1=0.9, beta2=0.999, eps=1e-8):
+    """In-place float32 torch CPU ops of OurAdam._single_tensor_adam2 (maximize=False, weight_decay=0,
+    amsgrad=False, capturable=False) after grad[:sky] = 0; step is the incremented state step."""
+    import math
+    grad[:sky] = 0
+    exp_avg.mul_(beta1).add_(grad, alpha=1 - beta1)
+    exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
+    step_size = lr / (1 - beta1 ** step)
+    denom = (exp_avg_sq.sqrt() / math.sqrt(1 - beta2 ** step)).add_(eps)
+    param.addcdiv_(exp_avg, denom, value=-step_size)

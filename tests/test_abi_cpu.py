@@ -47,7 +47,9 @@ def _c_layout(struct, fields):
 
 
 @pytest.mark.parametrize("cls,struct", [(L.RasterArgs, "hlgs_raster_args"), (L.Grads, "hlgs_grads"),
-                                        (L.FrameInfo, "hlgs_frame_info")])
+                                        (L.FrameInfo, "hlgs_frame_info"), (L.HierInfo, "hlgs_hier_info"),
+                                        (L.CacheArgs, "hlgs_cache_args"), (L.CachePlan, "hlgs_cache_plan"),
+                                        (L.RowCopy, "hlgs_row_copy"), (L.AdamTensor, "hlgs_adam_tensor")])
 def test_ctypes_structs_match_header_layout(cls, struct):
     names = [f[0] for f in cls._fields_]
     size, offs = _c_layout(struct, names)

@@ -1,0 +1,165 @@
+"""train_post.py's SPT cache on the HIP path (hlgs_core/spt_cache.py over csrc/stream.hip and csrc/optim.hip)
+against the CPU restatement (oracle/spt_ref.py cache_pass, upper_tree_cut, adam_dense; oracle spt_cut):
+several views in a row, with the resident parameters changed between views as training would, so the
+write-back is observable.  Lists, counts and moved rows are bit-exact; Adam is within float32 rounding."""
+import numpy as np
+import pytest
+import torch
+
+from hlgs_core import synthetic as S
+from oracle import oracle as O
+from oracle import spt_ref as SR
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+NAMES = ("xyz", "f_dc", "opacity", "scaling", "rotation", "f_rest")
+SHAPES = {"xyz": (3,), "f_dc": (1, 3), "opacity": (1,), "scaling": (3,), "rotation": (4,), "f_rest": (15, 3)}
+
+
+def _scene(sky=4, n=6000, seed=8):
+    from hlgs_core import spt
+    cam0 = S.make_camera(256, 192)
+    h = S.make_dynamic_hierarchy(S.make_gaussians(n, 0, cam0, seed=seed), skybox_points=sky, seed=seed)
+    nodes = torch.tensor(h["nodes"])
+    nodes[:, 3] = torch.where(nodes[:, 2] == 2, nodes[:, 3], torch.zeros_like(nodes[:, 3]))
+    b = spt.build_hierarchical_spt(nodes, torch.tensor(h["means3D"]), torch.log(torch.tensor(h["scales"])), sky, 3.0,
+                                   0.02, 20)
+    G = nodes.shape[0]
+    rng = np.random.default_rng(seed)
+    storage = {k: torch.tensor(rng.normal(size=(G,) + SHAPES[k]).astype(np.float32)) for k in NAMES}
+    return b, storage
+
+
+def _cameras():
+    cams = [S.make_camera(320, 240, T=np.array([0.04 * k, 0.0, 0.3 + 0.02 * k])) for k in range(4)]
+    a = 0.5  # turn away: part of the upper tree leaves the frustum
+    R = np.array([[np.cos(a), 0.0, np.sin(a)], [0.0, 1.0, 0.0], [-np.sin(a), 0.0, np.cos(a)]])
+    cams.append(S.make_camera(320, 240, R=R, T=np.array([-0.5, 0.1, 1.0])))
+    cams.append(cams[0])
+    return cams
+
+
+class _Oracle:
+    """The same run on the CPU restatement."""
+
+    def __init__(self, b, storage, sky, rtol, budget):
+        self.b = {k: (v.numpy() if v is not None else None) for k, v in b.items()}
+        self.sky, self.rtol, self.budget = sky, rtol, budget
+        tens = [storage[k].numpy().copy() for k in NAMES]
+        self.host = tens + [np.zeros_like(t) for t in tens] + [np.zeros_like(t) for t in tens]
+        self.dev = [h[:sky].copy() for h in self.host]
+        self.render, self.n_loaded = np.arange(sky, dtype=np.int32), 0
+        self.prev = (np.zeros(0, np.int32), np.zeros(0, np.float32), np.zeros(0, np.int32))
+
+    def step(self, cam):
+        from hlgs_core import spt
+        b = self.b
+        planes = spt.extract_frustum_planes(cam["projmatrix"]).numpy()
+        campos = cam["campos"].numpy()
+        cut_fn = lambda i, d: O.spt_cut(b["SPT_gaussian_indices"], b["SPT_starts"], b["SPT_max"],  # noqa: E731
+                                        b["SPT_min"], i, d, compat=True)
+        dm = 1.0
+        while True:
+            coarse = SR.upper_tree_cut(b["upper_tree_nodes"], b["upper_tree_xyz"], b["bounding_sphere_radii"],
+                                       b["min_distance_squared"], planes, campos, dm, True, True)
+            r = SR.cache_pass(b["upper_tree_nodes"], b["upper_tree_xyz"], coarse, campos, dm, *self.prev,
+                              self.render, self.n_loaded, self.sky, self.rtol, 0.05, cut_fn)
+            if len(r["render_indices"]) <= self.budget:
+                break
+            dm *= 1.5
+        keep, wb, lfd = r["keep_mask"], r["write_back_indices"], r["load_from_disk_indices"]
+        for k in range(len(self.host)):
+            self.host[k][wb] = self.dev[k][~keep]
+            self.dev[k] = np.concatenate([self.dev[k][keep], self.host[k][lfd]])
+        self.prev = (r["SPT_indices"], r["SPT_distances"], r["SPT_counts"])
+        self.render, self.n_loaded = r["render_indices"], len(lfd)
+        r["distance_multiplier"] = dm
+        return r
+
+
+def _dev_list(c):
+    return [c.params[k] for k in NAMES] + [c.exp_avgs[k] for k in NAMES] + [c.exp_avg_sqs[k] for k in NAMES]
+
+
+@pytest.mark.parametrize("rtol,budget", [(0.9, None), (0.02, None), (0.9, "tight")])
+def test_spt_cache_views_match_restatement(rtol, budget):
+    from hlgs_core.spt_cache import SPTCache
+    sky = 4
+    b, storage = _scene(sky)
+    cams = _cameras()
+    if budget == "tight":  # a budget just under the first view's size forces the distance-multiplier loop
+        probe = _Oracle(b, storage, sky, rtol, 10 ** 9)
+        budget = len(probe.step(cams[0])["render_indices"]) - 1
+    else:
+        budget = 10 ** 9
+    cache = SPTCache(storage, b, sky, reuse_tolerance=rtol, max_gaussian_budget=budget)
+    orc = _Oracle(b, storage, sky, rtol, budget)
+    reused = 0
+    for step, cam in enumerate(cams):
+        got = cache.step(cam["projmatrix"], cam["campos"])
+        want = orc.step(cam)
+        pl = cache.last_plan
+        assert pl["distance_multiplier"] == want["distance_multiplier"]
+        for k in ("SPT_indices", "SPT_distances", "SPT_counts", "load_from_disk_indices"):
+            np.testing.assert_array_equal(pl[k].cpu().numpy(), want[k], err_msg=f"{k} view {step}")
+        np.testing.assert_array_equal(got.cpu().numpy(), want["render_indices"])
+        np.testing.assert_array_equal(pl["write_back_indices"].cpu().numpy(), want["write_back_indices"])
+        for t, (g, w) in enumerate(zip(_dev_list(cache), orc.dev)):
+            np.testing.assert_array_equal(g.detach().cpu().numpy(), w, err_msg=f"tensor {t} view {step}")
+        reused += want["n_kept"]
+        # training changes the resident rows between views
+        with torch.no_grad():
+            for t, g in enumerate(_dev_list(cache)):
+                g.add_(0.001 * (step + 1) * (t + 1))
+        for t in range(len(orc.dev)):
+            orc.dev[t] = (orc.dev[t] + np.float32(0.001 * (step + 1) * (t + 1))).astype(np.float32)
+    assert reused > 0 or rtol < 0.1
+    host = [cache.storage[k] for k in NAMES] + [cache.opt_storage[k]["exp_avgs"] for k in NAMES] + \
+           [cache.opt_storage[k]["exp_avgs_sqs"] for k in NAMES]
+    for t, (h, w) in enumerate(zip(host, orc.host)):
+        np.testing.assert_array_equal(h.numpy(), w, err_msg=f"host tensor {t}")
+
+
+def test_copy_rows_tables_and_identity():
+    from hlgs_core.spt_cache import copy_rows
+    rng = np.random.default_rng(3)
+    host = [torch.tensor(rng.normal(size=(500,) + SHAPES[k]).astype(np.float32)).pin_memory() for k in NAMES]
+    dev = [torch.tensor(rng.normal(size=(60,) + SHAPES[k]).astype(np.float32), device=DEV) for k in NAMES]
+    src = torch.tensor(rng.permutation(60)[:40].astype(np.int32), device=DEV)
+    dst = torch.tensor(rng.permutation(500)[:40].astype(np.int32), device=DEV)
+    want = [h.clone() for h in host]
+    for w, d in zip(want, dev):
+        w[dst.cpu().long()] = d.cpu()[src.cpu().long()]
+    copy_rows(list(zip(dev, host)), 40, src, dst)
+    torch.cuda.synchronize()
+    for h, w in zip(host, want):
+        assert torch.equal(h, w)
+    out = [torch.empty((40,) + SHAPES[k], device=DEV) for k in NAMES]
+    copy_rows(list(zip(host, out)), 40, dst, None)
+    for o, h in zip(out, host):
+        assert torch.equal(o.cpu(), h[dst.cpu().long()])
+    with pytest.raises(RuntimeError):
+        copy_rows([(torch.zeros(4, 3), dev[0])], 4, None, None)  # unpinned host memory is refused
+
+
+def test_adam_step_matches_restatement():
+    from hlgs_core.spt_cache import adam_step
+    g = torch.Generator().manual_seed(5)
+    sky = 3
+    ps = [torch.randn((70,) + SHAPES[k], generator=g) for k in NAMES]
+    ms = [torch.zeros_like(p) for p in ps]
+    vs = [torch.zeros_like(p) for p in ps]
+    lrs = [1.6e-4, 2.5e-3, 5e-2, 5e-3, 1e-3, 2.5e-3 / 20]
+    dp = [p.to(DEV) for p in ps]
+    dm = [m.to(DEV) for m in ms]
+    dv = [v.to(DEV) for v in vs]
+    for it in range(4):
+        grads = [torch.randn(p.shape, generator=g) for p in ps]
+        dg = [x.to(DEV) for x in grads]
+        adam_step(dp, dg, dm, dv, lrs, it + 1, sky)
+        for p, gr, m, v, lr in zip(ps, grads, ms, vs, lrs):
+            SR.adam_dense(p, gr, m, v, lr, it + 1, sky)
+        for x, y in zip(dg, grads):
+            assert torch.equal(x.cpu(), y)  # skybox rows zeroed, the rest untouched
+    for a, b in zip(dp + dm + dv, ps + ms + vs):
+        torch.testing.assert_close(a.cpu(), b, rtol=2e-6, atol=1e-7)
