@@ -677,6 +677,16 @@ int hlgs_spt_cache_plan(const hlgs_cache_args* a, hlgs_cache_plan* pl, void* scr
     return HLGS_OK;
 }
 
+static bool is_device_memory(const void* p)
+{
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice;
+}
+
 int hlgs_copy_rows(int T, const hlgs_row_copy* tables, int64_t n, const int* src_rows, const int* dst_rows,
                    void* stream)
 {
@@ -688,7 +698,8 @@ int hlgs_copy_rows(int T, const hlgs_row_copy* tables, int64_t n, const int* src
     for (int t = 0; t < T; t++) {
         if (tables[t].row_bytes < 0 || tables[t].row_bytes % 4) return fail(HLGS_ERR_ARG, "row size must be a multiple of 4 bytes");
         if (tables[t].row_bytes && (!tables[t].src || !tables[t].dst)) return fail(HLGS_ERR_ARG, "missing tensor");
-        rc_[t] = RowCopy{tables[t].src, tables[t].dst, tables[t].row_bytes};
+        rc_[t] = RowCopy{tables[t].src, tables[t].dst, tables[t].row_bytes, is_device_memory(tables[t].src) &&
+                                                                             is_device_memory(tables[t].dst)};
     }
     hipStream_t s = (hipStream_t)stream;
     hipGetLastError();

@@ -141,6 +141,7 @@ struct RowCopy {
     const void* src;
     void* dst;
     int64_t row_bytes;
+    int device_only;          // both sides in device memory: 16-byte accesses at 4-byte alignment are used
 };
 constexpr int kMaxRowTables = 32;
 void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_rows, const int* dst_rows,

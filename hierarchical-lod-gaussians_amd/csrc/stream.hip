@@ -67,35 +67,48 @@ __device__ __forceinline__ int block_excl(int flag, int* s_w, int* total)
     return before + in_wave;
 }
 
+// Pass 1 classifies the level once (the states go to LDS when the level fits, so pass 2 does not reload the nodes)
+// and counts with wave ballots and LDS atomics, without block barriers, so the waves' node loads overlap.
+constexpr int kCutLds = 48 * 1024;
+
 __global__ void __launch_bounds__(1024) k_upper_cut(CutArgs a)
 {
     __shared__ int s_w[16];
+    __shared__ int s_n[3];
+    __shared__ uint8_t s_st[kCutLds];
     int* front = a.front_a;
     int* next = a.front_b;
     int size = a.N > 0 ? 1 : 0;
     if (threadIdx.x == 0) front[0] = 0;  // root_node = 0
     int total = 0;
     bool overflow = false;
+    const int lane = threadIdx.x & 63;
     __syncthreads();
     while (size > 0 && !overflow) {
-        // pass 1: level totals of the three outcomes
-        int n1 = 0, n2 = 0, n3 = 0;
+        // pass 1: classify, level totals of the three outcomes
+        if (threadIdx.x < 3) s_n[threadIdx.x] = 0;
+        __syncthreads();
+        const bool cached = size <= kCutLds;
         for (int c0 = 0; c0 < size; c0 += 1024) {
             const int i = c0 + threadIdx.x;
             const int st = i < size ? cut_state(a, front[i]) : 0;
-            int t1, t2, t3;
-            block_excl(st == 1, s_w, &t1);
-            block_excl(st == 2, s_w, &t2);
-            block_excl(st == 3, s_w, &t3);
-            n1 += t1; n2 += t2; n3 += t3;
+            if (cached && i < size) s_st[i] = (uint8_t)st;
+            const uint64_t b1 = __ballot(st == 1), b2 = __ballot(st == 2), b3 = __ballot(st == 3);
+            if (lane == 0) {
+                if (b1) atomicAdd(&s_n[0], __popcll(b1));
+                if (b2) atomicAdd(&s_n[1], __popcll(b2));
+                if (b3) atomicAdd(&s_n[2], __popcll(b3));
+            }
         }
+        __syncthreads();
+        const int n1 = s_n[0], n2 = s_n[1], n3 = s_n[2];
         if (total + n1 + n2 > a.capacity || 2 * n3 > a.capacity) { overflow = true; break; }
         // pass 2: write the cut and the next frontier in the reference's order
         int o1 = 0, o2 = 0, o3 = 0;
         for (int c0 = 0; c0 < size; c0 += 1024) {
             const int i = c0 + threadIdx.x;
             const int v = i < size ? front[i] : 0;
-            const int st = i < size ? cut_state(a, v) : 0;
+            const int st = i < size ? (cached ? (int)s_st[i] : cut_state(a, v)) : 0;
             int t1, t2, t3;
             const int p1 = block_excl(st == 1, s_w, &t1);
             const int p2 = block_excl(st == 2, s_w, &t2);
@@ -175,24 +188,51 @@ void launch_rows(bool gather, long n, int row_bytes, const int64_t* idx, const v
 
 // ---------------------------------------------------------------- multi-tensor row copy
 // dst_t[dst_rows[i]] = src_t[src_rows[i]] for every table t (blockIdx.y); a NULL row list is the identity.  One
-// thread per 4-byte word: consecutive threads walk a row and then the next, so the identity side is contiguous.
+// lane per 4-byte word, words numbered row after row, so every wave touches one contiguous span of the identity
+// side with all lanes busy; a lane's (row, word) advances by the grid stride without dividing in the loop.
 struct RowTabs {
     RowCopy t[kMaxRowTables];
 };
+
+typedef uint4 __attribute__((aligned(4))) uint4_a4;  // 16-byte access at 4-byte alignment (global_load_dwordx4)
 
 __global__ void __launch_bounds__(256) k_rows_multi(RowTabs tabs, int64_t n, const int* __restrict__ src_rows,
                                                     const int* __restrict__ dst_rows)
 {
     const RowCopy& tb = tabs.t[blockIdx.y];
     const int64_t words = tb.row_bytes >> 2;
-    const int64_t total = n * words;
+    if (words == 0) return;
     const uint32_t* __restrict__ src = static_cast<const uint32_t*>(tb.src);
     uint32_t* __restrict__ dst = static_cast<uint32_t*>(tb.dst);
-    for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < total; w += (int64_t)gridDim.x * 256) {
-        const int64_t r = w / words, k = w - r * words;
-        const int64_t sr = src_rows ? src_rows[r] : r;
-        const int64_t dr = dst_rows ? dst_rows[r] : r;
-        dst[dr * words + k] = src[sr * words + k];
+    // lanes own U consecutive words (U = 4 for device-only tables, whose interior row chunks move as one 16-byte
+    // access; 1 otherwise, since a 16-byte access to host memory may straddle a page)
+    const int U = tb.device_only ? 4 : 1;
+    const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * U, S = (int64_t)gridDim.x * 256 * U;
+    int64_t r = w0 / words, k = w0 - r * words;
+    const int64_t dr = S / words, dk = S - dr * words;
+    while (r < n) {
+        int64_t rr = r, kk = k;
+        if (U == 4 && k + 4 <= words) {
+            const int64_t sr = src_rows ? src_rows[r] : r;
+            const int64_t drow = dst_rows ? dst_rows[r] : r;
+            *reinterpret_cast<uint4_a4*>(dst + drow * words + k) = *reinterpret_cast<const uint4_a4*>(src + sr * words + k);
+        } else {
+            for (int u = 0; u < U && rr < n; u++) {
+                const int64_t sr = src_rows ? src_rows[rr] : rr;
+                const int64_t drow = dst_rows ? dst_rows[rr] : rr;
+                dst[drow * words + kk] = src[sr * words + kk];
+                if (++kk == words) {
+                    kk = 0;
+                    rr++;
+                }
+            }
+        }
+        r += dr;
+        k += dk;
+        while (k >= words) {
+            k -= words;
+            r++;
+        }
     }
 }
 
@@ -202,9 +242,9 @@ void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_row
     int64_t most = 0;
     for (int t = 0; t < T; t++) {
         rt.t[t] = tabs[t];
-        most = std::max<int64_t>(most, n * (tabs[t].row_bytes >> 2));
+        most = std::max<int64_t>(most, (n * (tabs[t].row_bytes >> 2) + 3) / (tabs[t].device_only ? 4 : 1));
     }
-    const int64_t blocks = std::min<int64_t>((most + 255) / 256, 16384);
+    const int64_t blocks = std::min<int64_t>((most + 255) / 256, 4096);
     if (blocks > 0) hipLaunchKernelGGL(k_rows_multi, dim3((unsigned)blocks, T), dim3(256), 0, s, rt, n, src_rows, dst_rows);
 }
 

@@ -9,6 +9,10 @@
   loss      photometric_loss (L1 + D-SSIM + masked inverse-depth L1) forward + backward on a 1080p view.
   adam      SparseGaussianAdam.step over 1M Gaussians (59 floats each, six parameter groups), half visible.
   morton    get_morton_indices over the hierarchy's nodes.
+  stream    train_post.py's SPT cache over the same hierarchy: SPT construction (host code), then a camera path
+            of views through SPTCache.step (coarse cut, cache bookkeeping, SPT cut, write-back and load of the
+            six parameters and twelve Adam moments to and from pinned host storage) and the dense Adam step of
+            the resident set; per-stage times and the host-link bytes moved per view.
 
 Times are medians of CUDA-event spans on torch's current stream (the library launches there).  Inputs are
 synthetic (seeded) and resident on the device.  Prints one JSON object.
@@ -204,6 +208,59 @@ def bench_morton(xyz):
                 alg_GBs=round(alg / (ms * 1e-3) / 1e9, 1))
 
 
+def bench_stream(P, views=12):
+    from hlgs_core import spt
+    from hlgs_core.spt_cache import NAMES, SPTCache
+    cam = S.make_camera(1920, 1080)
+    h = S.make_dynamic_hierarchy(S.make_gaussians(P, 0, cam, seed=0), seed=0)
+    nodes = torch.tensor(h["nodes"])
+    nodes[:, 3] = torch.where(nodes[:, 2] == 2, nodes[:, 3], torch.zeros_like(nodes[:, 3]))
+    xyz, log_s = torch.tensor(h["means3D"]), torch.log(torch.tensor(h["scales"]))
+    G = nodes.shape[0]
+    vol, tg, mn = 0.5, 0.00228, 256  # train_post.py:89-91 (granularity and minimum size; volume for this scene scale)
+    t0 = time.perf_counter()
+    b = spt.build_hierarchical_spt(nodes, xyz, log_s, 0, vol, tg, mn)
+    build_s = time.perf_counter() - t0
+    widths = dict(xyz=(3,), f_dc=(1, 3), opacity=(1,), scaling=(3,), rotation=(4,), f_rest=(15, 3))
+    g = torch.Generator().manual_seed(0)
+    storage = {k: torch.randn((G,) + widths[k], generator=g) for k in NAMES}
+    t0 = time.perf_counter()
+    cache = SPTCache(storage, b, 0, reuse_tolerance=0.05)
+    setup_s = time.perf_counter() - t0
+    path = [S.make_camera(1920, 1080, T=np.array([0.03 * k, 0.01 * k, 0.2 * math.sin(0.3 * k)])) for k in range(views)]
+    step_ms, plan_ms, rows_moved, resident = [], [], [], []
+    for k, c in enumerate(path):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ri = cache.step(c["projmatrix"], c["campos"])
+        torch.cuda.synchronize()
+        step_ms.append((time.perf_counter() - t0) * 1e3)
+        pl = cache.last_plan
+        rows_moved.append(pl["write_back_indices"].numel() + pl["load_from_disk_indices"].numel())
+        resident.append(ri.numel())
+        t0 = time.perf_counter()
+        cache.plan(c["projmatrix"], c["campos"])
+        torch.cuda.synchronize()
+        plan_ms.append((time.perf_counter() - t0) * 1e3)
+    row_bytes = 4 * 59 * 3  # parameters + two moments per Gaussian
+    moved = float(np.median(rows_moved[1:])) * row_bytes
+    ms = float(np.median(step_ms[1:]))
+    # dense Adam over the resident set (train_post.py:786-812)
+    for p in cache.params.values():
+        p.grad = torch.randn_like(p)
+    R = resident[-1]
+    adam_ms = timed(lambda: cache.optimizer_step(100, {k: 1e-3 for k in NAMES}))
+    adam_alg = R * 59 * 28
+    return dict(workload=f"SPT cache over a {G}-node hierarchy ({P} leaves), {views}-view camera path",
+                spt_build_s=round(build_s, 3), n_spt=len(b["SPT_starts"]) - 1, spt_entries=len(b["SPT_max"]),
+                upper_tree_nodes=int(b["upper_tree_nodes"].shape[0]), setup_s=round(setup_s, 3),
+                resident_median=int(np.median(resident)), view_step_ms=round(ms, 3),
+                view_plan_ms=round(float(np.median(plan_ms[1:])), 3), rows_moved_median=int(np.median(rows_moved[1:])),
+                host_link_GBs=round(moved / (ms * 1e-3) / 1e9, 2),
+                adam=dict(ms=round(adam_ms, 4), alg_GBs=round(adam_alg / (adam_ms * 1e-3) / 1e9, 1),
+                          hbm_frac=round(adam_alg / (adam_ms * 1e-3) / 1e9 / HBM, 3), rows=R))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--P", type=int, default=1_000_000)
@@ -222,6 +279,8 @@ def main():
     if "lod" in only:
         out["lod"], (xyz, _) = bench_lod(args.P, args.W, args.H, 3)
         out["morton"] = bench_morton(xyz)
+    if "stream" in only:
+        out["stream"] = bench_stream(args.P)
     print(json.dumps(out))
 
 
