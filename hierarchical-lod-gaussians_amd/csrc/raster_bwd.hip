@@ -260,10 +260,65 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
                                                    BwdScratch rec, hlgs_grads o, float fx, float fy, int has_depth)
 {
     const int t_idx = blockIdx.x * 256 + threadIdx.x;
+    const bool vis = t_idx < a.P && radii[t_idx] > 0;
+    // Gaussians with more than kWide record slots (rects over many tiles) are summed by their whole wave, lane-
+    // strided, with a fixed butterfly at the end -- deterministic, and one wide splat no longer serialises a lane
+    // over thousands of slots.  Done before any lane leaves, so every lane of the wave takes part.
+    constexpr uint32_t kWide = 32;
+    uint32_t r_end = 0, r_start = 0;
+    if (vis) {
+        r_end = g.point_offsets[t_idx];
+        r_start = r_end - g.tiles_touched[t_idx];
+    }
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f, s8 = 0.f, s9 = 0.f;
+    {
+        uint64_t wide = __ballot(vis && r_end - r_start > kWide);
+        const int lane = threadIdx.x & 63;
+        while (wide) {
+            const int src = __ffsll((long long)wide) - 1;
+            wide &= wide - 1;
+            const uint32_t ws = (uint32_t)__shfl((int)r_start, src, 64), we = (uint32_t)__shfl((int)r_end, src, 64);
+            const int sidx = t_idx - lane + src;  // the wide Gaussian's rasterised index
+            float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
+            float kx = 0.f, ky = 0.f, kthr = 0.f;
+            int kx0 = 0, ky0 = 0, kw = 1;
+            if (ALT) {
+                const float4 r0 = g.splat[4 * (size_t)sidx], r1 = g.splat[4 * (size_t)sidx + 1];
+                const float4 r3 = g.splat[4 * (size_t)sidx + 3];
+                kx = r0.x; ky = r0.y;
+                kco = make_float4(r0.z, r0.w, r1.x, r1.y);
+                kthr = alt_keep_threshold(kco.w);
+                kx0 = __float_as_int(r3.y) & 0xffff;
+                ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
+                kw = __float_as_int(r3.z);
+            }
+            float p[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (uint32_t r = ws + lane; r < we; r += 64) {
+                if (ALT) {
+                    const int k = (int)(r - ws);
+                    if (!alt_tile_keep(kx, ky, kco, kthr, kx0 + k % kw, ky0 + k / kw)) continue;
+                }
+                const float4 A = rec.recA[r];
+                const float4 B = rec.recB[r];
+                const float2 Cc = rec.recC[r];
+                p[0] += A.x; p[1] += A.y; p[2] += A.z; p[3] += A.w;
+                p[4] += B.x; p[5] += B.y; p[6] += B.z; p[7] += B.w;
+                p[8] += Cc.x; p[9] += Cc.y;
+            }
+#pragma unroll
+            for (int v = 0; v < 10; v++)
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) p[v] += __shfl_xor(p[v], off, 64);
+            if (lane == src) {
+                s0 = p[0]; s1 = p[1]; s2 = p[2]; s3 = p[3]; s4 = p[4];
+                s5 = p[5]; s6 = p[6]; s7 = p[7]; s8 = p[8]; s9 = p[9];
+            }
+        }
+    }
     if (t_idx >= a.P) return;
     const int idx = HIER ? a.indices[t_idx] : t_idx;
     const int M3 = a.M * 3;
-    if (!(radii[t_idx] > 0)) {
+    if (!vis) {
         if (!HIER) {
             o.dmean2D[3 * idx] = 0.f; o.dmean2D[3 * idx + 1] = 0.f; o.dmean2D[3 * idx + 2] = 0.f;
             o.dcolor[3 * idx] = 0.f; o.dcolor[3 * idx + 1] = 0.f; o.dcolor[3 * idx + 2] = 0.f;
@@ -278,8 +333,8 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
         }
         return;
     }
-    // ---- per-Gaussian sum of the blend records (fixed order => deterministic)
-    const uint32_t end = g.point_offsets[t_idx], start = end - g.tiles_touched[t_idx];
+    // ---- per-Gaussian sum of the blend records (fixed order => deterministic); wide ones were summed above
+    const uint32_t end = r_end - r_start > kWide ? r_start : r_end, start = r_start;
     constexpr bool alt = ALT;
     float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
     float kx = 0.f, ky = 0.f, kthr = 0.f;
@@ -294,7 +349,6 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
         ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
         kw = __float_as_int(r3.z);
     }
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f, s8 = 0.f, s9 = 0.f;
     for (uint32_t r = start; r < end; r++) {
         if (alt) {
             const int k = (int)(r - start);

@@ -175,29 +175,116 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
 // instances are counted per tile in LDS and each non-empty bin costs one coalesced device atomic,
 // instead of one lane-scattered atomic per (Gaussian, tile) instance.
 // ------------------------------------------------------------------------------------------------
-// Calls f(idx, tile) for every binned instance of the block's Gaussians: every tile of the rect, or for the
-// alt rasterizer the tiles alt_tile_keep leaves (rasterizer_impl.cu:147-179 of alt-rasterizer).
-template <typename F>
-__device__ __forceinline__ void for_each_instance(int P, const int* __restrict__ radii, const Geom& g, int gx, int gy,
-                                                  bool alt, F&& f)
+// s_pre[k] = exclusive prefix of tiles_touched over the block's kBinGauss Gaussians (0 past P), s_pre[kBinGauss] =
+// the block's total: thread t scans its four consecutive entries, then the 1024 thread totals are scanned.
+__device__ __forceinline__ void block_rect_prefix(int P, const Geom& g, uint32_t* s_pre, uint32_t* s_w)
 {
-    const int g0 = blockIdx.x * kBinGauss, g1 = min(P, g0 + kBinGauss);
-    for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += kBinThreads) {
-        if (radii[idx] <= 0) continue;
+    static_assert(kBinGauss == 4 * kBinThreads, "four Gaussians per thread");
+    const int g0 = blockIdx.x * kBinGauss, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t a[4], sum = 0, mx = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = g0 + 4 * t + k;
+        a[k] = idx < P ? g.tiles_touched[idx] : 0u;
+        sum += a[k];
+        mx = max(mx, a[k]);
+    }
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    if (lane == 0) atomicMax(&s_w[kBinThreads / 64], mx);
+    uint32_t x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+    for (int i = 0; i < kBinThreads / 64; i++) {
+        const uint32_t c = s_w[i];
+        if (i < w) base += c;
+        total += c;
+    }
+    uint32_t run = base + x - sum;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        s_pre[4 * t + k] = run;
+        run += a[k];
+    }
+    if (t == 0) s_pre[kBinGauss] = total;
+    __syncthreads();
+}
+
+// the block's longest rect (s_w[kBinThreads / 64], zeroed before block_rect_prefix)
+constexpr uint32_t kNarrowRect = 64;
+
+// Calls f(idx, tile) for every binned instance of the block's Gaussians: every tile of the rect, or for the
+// alt rasterizer the tiles alt_tile_keep leaves (rasterizer_impl.cu:147-179 of alt-rasterizer).  The block's
+// instances are numbered Gaussian by Gaussian (s_pre) and each thread takes one contiguous run of them, so a
+// Gaussian whose rect spans thousands of tiles is spread over the whole block instead of serialising one thread.
+template <typename F>
+__device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy, bool alt, const uint32_t* s_pre,
+                                                  const uint32_t* s_w, F&& f)
+{
+    const int g0 = blockIdx.x * kBinGauss;
+    if (s_w[kBinThreads / 64] <= kNarrowRect) {  // no wide rect in this block: one thread per Gaussian
+        for (int k = threadIdx.x; k < kBinGauss; k += kBinThreads) {
+            if (s_pre[k + 1] == s_pre[k]) continue;
+            const int idx = g0 + k;
+            const float2 xy = g.means2D[idx];
+            const int2 ext = g.rects[idx];
+            int x0, y0, x1, y1;
+            tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
+            if (alt) {
+                const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
+                const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
+                const float thr = alt_keep_threshold(co.w);
+                for (int y = y0; y < y1; y++)
+                    for (int x = x0; x < x1; x++)
+                        if (alt_tile_keep(xy.x, xy.y, co, thr, x, y)) f(idx, y * gx + x);
+            } else {
+                for (int y = y0; y < y1; y++)
+                    for (int x = x0; x < x1; x++) f(idx, y * gx + x);
+            }
+        }
+        return;
+    }
+    const uint32_t total = s_pre[kBinGauss];
+    const uint32_t chunk = (total + kBinThreads - 1) / kBinThreads;
+    uint32_t i = threadIdx.x * chunk;
+    const uint32_t iend = min(total, i + chunk);
+    if (i >= iend) return;
+    int lo = 0, hi = kBinGauss - 1;  // last k with s_pre[k] <= i: the Gaussian holding instance i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_pre[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    for (int k = lo; i < iend; k++) {
+        const uint32_t b = s_pre[k], e = s_pre[k + 1];
+        if (e == b) continue;
+        const int idx = g0 + k;
         const float2 xy = g.means2D[idx];
         const int2 ext = g.rects[idx];
         int x0, y0, x1, y1;
         tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
+        const int w = x1 - x0;
+        const uint32_t local = i - b;
+        int ty = (int)(local / (uint32_t)w), tx = (int)local - ty * w;
+        const uint32_t stop = min(iend, e);
         if (alt) {
             const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
             const float thr = alt_keep_threshold(co.w);
-            for (int y = y0; y < y1; y++)
-                for (int x = x0; x < x1; x++)
-                    if (alt_tile_keep(xy.x, xy.y, co, thr, x, y)) f(idx, y * gx + x);
+            for (; i < stop; i++) {
+                if (alt_tile_keep(xy.x, xy.y, co, thr, x0 + tx, y0 + ty)) f(idx, (y0 + ty) * gx + x0 + tx);
+                if (++tx == w) { tx = 0; ty++; }
+            }
         } else {
-            for (int y = y0; y < y1; y++)
-                for (int x = x0; x < x1; x++) f(idx, y * gx + x);
+            for (; i < stop; i++) {
+                f(idx, (y0 + ty) * gx + x0 + tx);
+                if (++tx == w) { tx = 0; ty++; }
+            }
         }
     }
 }
@@ -206,10 +293,14 @@ __global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* _
                                                              uint32_t* __restrict__ tile_count, int gx, int gy, int alt)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+    __shared__ uint32_t s_pre[kBinGauss + 1];
+    __shared__ uint32_t s_w[kBinThreads / 64 + 1];
     const int T = gx * gy;
     for (int t = threadIdx.x; t < T; t += kBinThreads) s_hist[t] = 0;
+    if (threadIdx.x == 0) s_w[kBinThreads / 64] = 0;
     __syncthreads();
-    for_each_instance(P, radii, g, gx, gy, alt, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
+    block_rect_prefix(P, g, s_pre, s_w);
+    for_each_instance(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += kBinThreads) {
         const uint32_t c = s_hist[t];
@@ -227,10 +318,13 @@ __global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const i
 {
     if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+    __shared__ uint32_t s_pre[kBinGauss + 1];
+    __shared__ uint32_t s_w[kBinThreads / 64 + 1];
     const int T = gx * gy;
     uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
     uint32_t* s_rank = s_hist + T; // per-tile running rank
     for (int t = threadIdx.x; t < T; t += kBinThreads) { s_cnt[t] = 0; s_rank[t] = 0; }
+    if (threadIdx.x == 0) s_w[kBinThreads / 64] = 0;
     {
         const int g0 = blockIdx.x * kBinGauss, g1 = min(P, g0 + kBinGauss);
         for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += kBinThreads)
@@ -238,14 +332,15 @@ __global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const i
                 g.splat[4 * (size_t)idx + 3].x = __uint_as_float(g.point_offsets[idx] - g.tiles_touched[idx]);
     }
     __syncthreads();
-    for_each_instance(P, radii, g, gx, gy, alt, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
+    block_rect_prefix(P, g, s_pre, s_w);
+    for_each_instance(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += kBinThreads) {
         const uint32_t c = s_cnt[t];
         s_cnt[t] = c ? ranges[t].x + atomicAdd(&cursor[t], c) : 0u;
     }
     __syncthreads();
-    for_each_instance(P, radii, g, gx, gy, alt, [&](int idx, int tile) {
+    for_each_instance(g, gx, gy, alt, s_pre, s_w, [&](int idx, int tile) {
         const uint32_t r = atomicAdd(&s_rank[tile], 1u);
         keys[s_cnt[tile] + r] = ((uint64_t)__float_as_uint(g.depths[idx]) << 32) | (uint32_t)idx;
     });
@@ -572,8 +667,11 @@ static void allow_big_lds()
 {
     static bool done = false;
     if (done) return;
-    hipFuncSetAttribute((const void*)k_count_tiles, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)k_scatter_keys_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    // the kernels' static LDS (the block's rect prefix, ~16 KiB) comes out of the same 160 KiB
+    const int dyn = 2 * (int)sizeof(uint32_t) * kBinMaxTiles;
+    hipFuncSetAttribute((const void*)k_count_tiles, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_scatter_keys_lds, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipGetLastError();
     done = true;
 }
 

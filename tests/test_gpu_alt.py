@@ -222,3 +222,13 @@ def test_sparse_gaussian_adam_step():
     assert torch.equal(moved, vis)
     st = opt.state[x]
     np.testing.assert_allclose(st["exp_avg"][vis].cpu().numpy(), (0.1 * x.grad[vis]).cpu().numpy(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("aa", [True, False])
+def test_alt_wide_splats_balanced_binning(aa):
+    """A few splats whose rects cover most of a 512x384 frame (hundreds of tiles): the binning spreads their
+    instances over the block and the record sums go through the wave-wide path (> 32 slots)."""
+    sc, cam = _alt_scene(3000, 1, 512, 384, seed=31, aa=aa)
+    sc["scales"][:6] *= 40.0
+    sc["opacities"][:6] = np.float32(0.3)
+    _compare(sc, cam)

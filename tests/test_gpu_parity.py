@@ -174,3 +174,11 @@ def test_mark_visible_and_relocation():
     o_r, s_r = O.compute_relocation(op, scl, N, binoms, n_max)
     np.testing.assert_allclose(o_g.cpu().numpy(), o_r, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(s_g.cpu().numpy(), s_r, rtol=1e-4, atol=1e-6)
+
+
+def test_wide_splats_balanced_binning():
+    """As test_alt_wide_splats_balanced_binning, for the hierarchy rasterizer (every rect tile is binned)."""
+    sc, cam = _scene(3000, 2, 512, 384, seed=33)
+    sc["scales"][:6] *= 40.0
+    sc["opacities"][:6] = np.float32(0.3)
+    _compare(sc, cam)
