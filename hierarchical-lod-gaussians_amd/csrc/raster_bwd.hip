@@ -99,18 +99,17 @@ struct BwdArgs {
     int W, H, gx, gy, T;
     Geom g;
     const float* final_Ts;
-    const uint32_t* n_contrib;  // bit 31: the forward's exact pass rendered this pixel
+    const uint32_t* n_contrib;
     const float* bg;
     const float* dL_dpixels;
     const float* dL_dinvdepths;
     BwdScratch rec;
 };
 
-// Exact replay of a tile some of whose pixels the forward rendered with exact alpha-band decisions (rare):
-// one quadrant at a time, one pixel per lane (little register state next to the double-precision test),
-// each pass adding its per-(tile, Gaussian) records to the slots the first pass stored.  Records are
-// linear in the moments, so the sum equals the one-pass record up to float rounding.
-// One wave per tile, back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant.
+// One wave per tile, back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant.  Each 64-splat
+// batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel whose
+// n_contrib lies behind it) run bwd_pair, the ten moments are folded over the wave, and one record per
+// (tile, splat) is stored after the batch.
 template <bool INTERP, bool DEPTH, bool ALT>
 __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
 {
