@@ -350,6 +350,60 @@ __device__ __forceinline__ void sh_rows_copy(float* gbase, float* lds, const int
     }
 }
 
+// Global -> LDS copy of n rows like sh_rows_copy<.., true>, with every global load of the wave issued before
+// its first LDS store (registers hold the rows in flight), so a wave waits for HBM once, not once per float4.
+// live (optional, LDS): rows r with live[r] == 0 are not read and land in LDS as zeros.
+template <int M3T>
+__device__ __forceinline__ void sh_rows_load(const float* gbase, float* lds, const int* rows, int n, int lane, int m3,
+                                             const int* live = nullptr)
+{
+    if constexpr (M3T > 0 && M3T % 4 == 0) {
+        constexpr int Q = M3T / 4;
+        float4 v[Q];
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const int f = lane + 64 * k;
+            v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (f < n * Q) {
+                const int r = f / Q, q = f - r * Q;
+                if (!live || live[r]) v[k] = reinterpret_cast<const float4*>(gbase + (size_t)rows[r] * M3T)[q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const int f = lane + 64 * k;
+            if (f < n * Q) {
+                const int r = f / Q, q = f - r * Q;
+                float* lp = lds + r * kShStride + 4 * q;
+                lp[0] = v[k].x; lp[1] = v[k].y; lp[2] = v[k].z; lp[3] = v[k].w;
+            }
+        }
+    } else {
+        const int M3 = M3T ? M3T : m3;
+        constexpr int B = 12;
+        for (int f0 = 0; f0 < n * M3; f0 += 64 * B) {
+            float v[B];
+#pragma unroll
+            for (int k = 0; k < B; k++) {
+                const int f = f0 + lane + 64 * k;
+                v[k] = 0.f;
+                if (f < n * M3) {
+                    const int r = f / M3, q = f - r * M3;
+                    if (!live || live[r]) v[k] = gbase[(size_t)rows[r] * M3 + q];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < B; k++) {
+                const int f = f0 + lane + 64 * k;
+                if (f < n * M3) {
+                    const int r = f / M3, q = f - r * M3;
+                    lds[r * kShStride + q] = v[k];
+                }
+            }
+        }
+    }
+}
+
 // Bijective XCD-aware block remap (cdna_hip_programming.md section 5): consecutive logical blocks
 // land on the same XCD so neighbouring tiles share that XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg)

@@ -561,24 +561,24 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
     const int M3 = 3 * M;
     __shared__ float s_rows[64 * kShStride];
     __shared__ int s_idx[64];
+    __shared__ int s_vis[64];
     const int lane = threadIdx.x;
     const int t0 = blockIdx.x * 64;
     const int n = min(64, a.P - t0);
     const int t_idx = t0 + lane;
     const bool active = lane < n;
     const int idx = active ? (HIER ? a.indices[t_idx] : t_idx) : 0;
+    const bool vis = active && radii[t_idx] > 0;
     s_idx[lane] = idx;
+    s_vis[lane] = vis;
     __syncthreads();
-    sh_rows_copy<3 * MT, true>(const_cast<float*>(a.shs), s_rows, s_idx, n, lane, M3);
+    // rows of invisible Gaussians are not read: they arrive as zeros, which is their dsh row
+    sh_rows_load<3 * MT>(a.shs, s_rows, s_idx, n, lane, M3, s_vis);
     __syncthreads();
     float* row = s_rows + lane * kShStride;
     if (active) {
-        const bool vis = radii[t_idx] > 0;
         const bool dropped = HIER && a.parent_indices && a.parent_indices[t_idx] != -1;
         if (!vis) {
-#pragma unroll
-            for (int i = 0; i < 3 * MC; i++)
-                if (i < M3) row[i] = 0.f;
             if (ALT) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
         } else {
             const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);

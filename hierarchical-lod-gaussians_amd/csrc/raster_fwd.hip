@@ -171,6 +171,130 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Preprocess, common path (no hierarchy indices, SH coefficients given): one wave per 64 Gaussians.
+// The geometry is per thread as in k_preprocess; then the rows of the Gaussians that survived culling
+// are compacted (ballot + mbcnt) and copied into LDS with all 64 lanes on consecutive float4s, so the
+// 192-byte SH rows (M = 16) stream from HBM in whole lines instead of 48 strided 4-byte loads per thread.
+// Every per-Gaussian output is bit-identical to k_preprocess (same arithmetic, same order).
+// ------------------------------------------------------------------------------------------------
+struct PreGeom {
+    float pix_x, pix_y, depth, conic_x, conic_y, conic_z, h_scale, radius;
+    int x0, y0, x1, y1;
+};
+
+// forward.cu:218-403 up to the colour: writes the zero defaults, cov3D and rects; false = culled.
+template <bool ALT>
+__device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const Geom& g, int* radii, int t_idx,
+                                                int gx, int gy, float fx, float fy, PreGeom& o)
+{
+    radii[t_idx] = 0;
+    g.tiles_touched[t_idx] = 0;
+    g.rects[t_idx] = make_int2(0, 0);
+    g.clamped[t_idx] = 0;
+    const f3 p_orig = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
+    const float* proj = a.projmatrix;
+    const float* view = a.viewmatrix;
+    const float hx = proj[0] * p_orig.x + proj[4] * p_orig.y + proj[8] * p_orig.z + proj[12];
+    const float hy = proj[1] * p_orig.x + proj[5] * p_orig.y + proj[9] * p_orig.z + proj[13];
+    const float hw = xform44w(p_orig, proj);
+    const float p_w = 1.0f / (hw + 0.0000001f);
+    const float ppx = hx * p_w, ppy = hy * p_w;
+    const f3 p_view = xform43(p_orig, view);
+    if (p_view.z <= 0.2f) return false;
+    float c3[6];
+    if (a.cov3D_precomp == nullptr) {
+        const f3 scale = mk(a.scales[3 * t_idx], a.scales[3 * t_idx + 1], a.scales[3 * t_idx + 2]);
+        const float4 rq = reinterpret_cast<const float4*>(a.rotations)[t_idx];
+        const float rot[4] = {rq.x, rq.y, rq.z, rq.w};
+        cov3d_fwd(scale, a.scale_modifier, rot, c3);
+    } else {
+        for (int i = 0; i < 6; i++) c3[i] = a.cov3D_precomp[6 * t_idx + i];
+    }
+    float2* c3o = reinterpret_cast<float2*>(g.cov3D + 6 * (size_t)t_idx);
+    c3o[0] = make_float2(c3[0], c3[1]);
+    c3o[1] = make_float2(c3[2], c3[3]);
+    c3o[2] = make_float2(c3[4], c3[5]);
+    Cov2D k;
+    cov2d_eval(p_orig, fx, fy, a.tanfovx, a.tanfovy, c3, view, k);
+    float cx = k.cov.m[0][0], cy = k.cov.m[0][1], cz = k.cov.m[1][1];
+    const float h_var = 0.3f;
+    const float det_cov = cx * cz - cy * cy;
+    cx += h_var;
+    cz += h_var;
+    const float det_h = cx * cz - cy * cy;
+    o.h_scale = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    if (ALT && !a.antialiasing) o.h_scale = 1.0f;
+    const float det = det_h;
+    if (det == 0.0f) return false;
+    const float det_inv = 1.f / det;
+    o.conic_x = cz * det_inv;
+    o.conic_y = -cy * det_inv;
+    o.conic_z = cx * det_inv;
+    const float mid = 0.5f * (cx + cz);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    o.radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    o.pix_x = ndc2pix(ppx, a.W);
+    o.pix_y = ndc2pix(ppy, a.H);
+    const int ex = ALT ? (int)o.radius : (int)ceilf(3.f * sqrtf(cx));
+    const int ey = ALT ? (int)o.radius : (int)ceilf(3.f * sqrtf(cz));
+    g.rects[t_idx] = make_int2(ex, ey);
+    tile_rect(o.pix_x, o.pix_y, ex, ey, gx, gy, o.x0, o.y0, o.x1, o.y1);
+    o.depth = p_view.z;
+    return (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0) != 0;
+}
+
+template <bool ALT, int M3T>
+__global__ void __launch_bounds__(64) k_preprocess_sh(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
+                                                      int gy, float fx, float fy)
+{
+    __shared__ float s_rows[64 * kShStride];
+    __shared__ int s_idx[64];
+    const int lane = threadIdx.x;
+    const int t_idx = blockIdx.x * 64 + lane;
+    PreGeom o;
+    const bool need = t_idx < a.P && preprocess_geom<ALT>(a, g, radii, t_idx, gx, gy, fx, fy, o);
+    const uint64_t bal = __ballot(need);
+    if (bal == 0) return;  // wave-uniform: nothing of this block reaches the screen
+    const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    const int n = __popcll(bal);
+    if (need) s_idx[slot] = t_idx;
+    __syncthreads();
+    sh_rows_load<M3T>(a.shs, s_rows, s_idx, n, lane, 3 * a.M);
+    __syncthreads();
+    if (!need) return;
+    const float* row = s_rows + slot * kShStride;
+    const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+    const f3 mean_r = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
+    uint32_t cb = 0;
+    f3 col;
+    if (ALT) {
+        const float* d0 = a.dc + 3 * (size_t)t_idx;
+        col = sh_to_rgb(a.D, [&](int c) {
+            return c == 0 ? mk(d0[0], d0[1], d0[2]) : mk(row[3 * c - 3], row[3 * c - 2], row[3 * c - 1]);
+        }, mean_r, campos, cb);
+    } else {
+        col = sh_to_rgb(a.D, [&](int c) { return mk(row[3 * c], row[3 * c + 1], row[3 * c + 2]); }, mean_r, campos,
+                        cb);
+    }
+    g.clamped[t_idx] = cb;
+    g.depths[t_idx] = o.depth;
+    radii[t_idx] = (int)o.radius;
+    g.means2D[t_idx] = make_float2(o.pix_x, o.pix_y);
+    const float opacity = a.opacities[t_idx];
+    g.tiles_touched[t_idx] = (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0);
+    const bool interp = a.ts && a.kids;
+    float4* rec = g.splat + 4 * (size_t)t_idx;
+    rec[0] = make_float4(o.pix_x, o.pix_y, o.conic_x, o.conic_y);
+    rec[1] = make_float4(o.conic_z, opacity * o.h_scale, col.x, col.y);
+    const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+    rec[2] = make_float4(col.z, 1.f / o.depth, tt, fr);
+    rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0),
+                         alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr));
+}
+
+// ------------------------------------------------------------------------------------------------
 // Tile binning with block-level LDS histograms.  A block owns kBinGauss consecutive Gaussians; its
 // instances are counted per tile in LDS and each non-empty bin costs one coalesced device atomic,
 // instead of one lane-scattered atomic per (Gaussian, tile) instance.
@@ -690,6 +814,29 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
     const float fy = a.H / (2.0f * a.tanfovy);
     const float fx = a.W / (2.0f * a.tanfovx);
     const dim3 grid((a.P + 255) / 256);
+    const bool alt = a.variant == HLGS_VARIANT_ALT;
+    if (!a.indices && !a.colors_precomp && a.shs && a.M > 0 && !tile_count && a.M <= 16) {
+        const dim3 g64((a.P + 63) / 64);
+#define HLGS_PSH(AL, M3) hipLaunchKernelGGL((k_preprocess_sh<AL, M3>), g64, dim3(64), 0, s, a, g, radii, gx, gy, fx, fy)
+        if (alt) {
+            switch (a.M) {
+            case 3: HLGS_PSH(true, 9); break;
+            case 8: HLGS_PSH(true, 24); break;
+            case 15: HLGS_PSH(true, 45); break;
+            default: HLGS_PSH(true, 0); break;
+            }
+        } else {
+            switch (a.M) {
+            case 1: HLGS_PSH(false, 3); break;
+            case 4: HLGS_PSH(false, 12); break;
+            case 9: HLGS_PSH(false, 27); break;
+            case 16: HLGS_PSH(false, 48); break;
+            default: HLGS_PSH(false, 0); break;
+            }
+        }
+#undef HLGS_PSH
+        return;
+    }
     if (a.indices)
         hipLaunchKernelGGL((k_preprocess<true, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
     else if (a.variant == HLGS_VARIANT_ALT)
