@@ -17,9 +17,11 @@
 
 namespace hlgs {
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
+                       const ZeroJob& z,
                        hipStream_t s);
 void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s);
-bool lds_binning(int gx, int gy);
+void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, hipStream_t s);
+bool lds_binning(int P, int gx, int gy);
 void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
                         hipStream_t s);
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
@@ -280,26 +282,38 @@ size_t hlgs_image_ranges_offset(int W, int H)
 }
 
 namespace hlgs {
-// Phase 1 without the host read-back: preprocess, tile counts, scans, tile ranges (misc = R, longest list).
-static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int* radii, hipStream_t s)
+// Phase 1: preprocess, tile counts, scans, tile ranges (misc = R, longest list, record slots).  With LDS-histogram
+// binning the preprocess also clears tile_count and `seen`, and one k_plan block does both scans and the ranges and
+// mirrors misc into `host` (pinned, may be null); otherwise the generic path runs device-wide scans.
+static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int* radii, int* seen, uint32_t* host,
+                          hipStream_t s)
 {
     const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16, T = gx * gy;
     Geom g = carve_geom(aligned(geom), a->P, nullptr);
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     hipGetLastError();
-    HLGS_TRY_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
-    HLGS_TRY_HIP(hipMemsetAsync(im.misc, 0, sizeof(uint32_t) * 16, s));
-    const bool lds_bins = lds_binning(gx, gy);
+    const bool lds_bins = lds_binning(a->P, gx, gy);
     const bool alt = a->variant == HLGS_VARIANT_ALT;
-    stage_mark(s, ST_PRE, true);
-    launch_preprocess(*a, g, radii, lds_bins ? nullptr : im.tile_count, gx, gy, s);
-    stage_mark(s, ST_PRE, false);
+    int rc;
     if (lds_bins) {
+        stage_mark(s, ST_PRE, true);
+        launch_preprocess(*a, g, radii, nullptr, gx, gy, ZeroJob{im.tile_count, T, seen, a->P}, s);
+        stage_mark(s, ST_PRE, false);
         stage_mark(s, ST_COUNT_TILES, true);
         launch_count_tiles(a->P, radii, g, im.tile_count, gx, gy, alt, s);
         stage_mark(s, ST_COUNT_TILES, false);
+        if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
+        stage_mark(s, ST_SCAN, true);
+        launch_plan(a->P, g, im, T, host, s);
+        stage_mark(s, ST_SCAN, false);
+        return check_stage(s, a->debug, "scan");
     }
-    int rc;
+    if (seen) HLGS_TRY_HIP(hipMemsetAsync(seen, 0, sizeof(int) * (size_t)a->P, s));
+    HLGS_TRY_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
+    HLGS_TRY_HIP(hipMemsetAsync(im.misc, 0, sizeof(uint32_t) * 16, s));
+    stage_mark(s, ST_PRE, true);
+    launch_preprocess(*a, g, radii, im.tile_count, gx, gy, ZeroJob{nullptr, 0, nullptr, 0}, s);
+    stage_mark(s, ST_PRE, false);
     if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
     stage_mark(s, ST_SCAN, true);
     scan_inclusive_u32(g.tiles_touched, g.point_offsets, (size_t)a->P, g.scan_tmp, s);
@@ -308,7 +322,9 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
     scan_inclusive_u32(im.tile_count, im.tile_cursor, (size_t)T, im.scan_tmp, s);
     launch_tile_ranges(im, T, g.point_offsets, a->P, s);
     stage_mark(s, ST_RANGES, false);
-    return check_stage(s, a->debug, "scan");
+    if ((rc = check_stage(s, a->debug, "scan"))) return rc;
+    if (host) HLGS_TRY_HIP(hipMemcpyAsync(host, im.misc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    return HLGS_OK;
 }
 
 static int render_launch(const hlgs_raster_args* a, const int* radii, void* geom, void* img, void* binning, int R_carve,
@@ -350,7 +366,7 @@ static int readback_for(hipStream_t s, Readback** out)
     HLGS_TRY_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return fail(HLGS_ERR_DEVICE, "device index out of range");
     Readback& r = rb[dev];
-    if (!r.host) HLGS_TRY_HIP(hipHostMalloc((void**)&r.host, 16 * sizeof(uint32_t), hipHostMallocDefault));
+    if (!r.host) HLGS_TRY_HIP(hipHostMalloc((void**)&r.host, 16 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
     if (!r.ev) HLGS_TRY_HIP(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
     (void)s;
     *out = &r;
@@ -369,7 +385,7 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     info->num_binned = 0;
     if (a->P == 0) return HLGS_OK;
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = prepare_launch(a, geom, img, radii, s))) return rc;
+    if ((rc = prepare_launch(a, geom, img, radii, nullptr, nullptr, s))) return rc;
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     uint32_t misc[3];
     HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
@@ -414,12 +430,10 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
         info->rendered = 1;
         return HLGS_OK;
     }
-    if (seen) HLGS_TRY_HIP(hipMemsetAsync(seen, 0, sizeof(int) * (size_t)a->P, s));
-    if ((rc = prepare_launch(a, geom, img, radii, s))) return rc;
     Readback* rb;
     if ((rc = readback_for(s, &rb))) return rc;
+    if ((rc = prepare_launch(a, geom, img, radii, seen, rb->host, s))) return rc;
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
-    HLGS_TRY_HIP(hipMemcpyAsync(rb->host, im.misc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipEventRecord(rb->ev, s));
     // Queue the render before knowing R: it is sized for the caller's buffer and for lists the one-wave and
     // block sorts handle; the kernels exit at once if the frame exceeds either (Guard).

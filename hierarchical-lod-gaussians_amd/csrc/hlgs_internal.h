@@ -71,6 +71,22 @@ struct BwdScratch {
 };
 BwdScratch carve_bwd(void* base, int P, int R, size_t* total);
 
+// Buffers the preprocess clears on its way (instead of separate memsets before it): the per-tile counts the
+// binning adds into and the caller's `seen` flags.  Null members are skipped.
+struct ZeroJob {
+    uint32_t* tile_count;
+    int T;
+    int* seen;
+    int P;
+};
+__device__ __forceinline__ void zero_prelude(const ZeroJob& z, int tid, int nthreads)
+{
+    if (z.seen)
+        for (int i = tid; i < z.P; i += nthreads) z.seen[i] = 0;
+    if (z.tile_count)
+        for (int i = tid; i < z.T; i += nthreads) z.tile_count[i] = 0;
+}
+
 // Speculative render (hlgs_rasterize_forward): the render kernels are queued before the host has read
 // R and the longest tile list; each exits at once when they exceed what the launch was sized for.
 struct Guard {

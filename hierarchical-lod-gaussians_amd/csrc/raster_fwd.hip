@@ -23,9 +23,10 @@ namespace hlgs {
 template <bool HIER, bool ALT>
 __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, int* __restrict__ radii,
                                                     uint32_t* __restrict__ tile_count, int gx, int gy, float fx,
-                                                    float fy)
+                                                    float fy, ZeroJob z)
 {
     const int t_idx = blockIdx.x * 256 + threadIdx.x;
+    zero_prelude(z, t_idx, gridDim.x * 256);
     if (t_idx >= a.P) return;
     const int r_idx = HIER ? a.indices[t_idx] : t_idx;
     radii[t_idx] = 0;
@@ -246,12 +247,13 @@ __device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const
 
 template <bool ALT, int M3T>
 __global__ void __launch_bounds__(64) k_preprocess_sh(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
-                                                      int gy, float fx, float fy)
+                                                      int gy, float fx, float fy, ZeroJob z)
 {
     __shared__ float s_rows[64 * kShStride];
     __shared__ int s_idx[64];
     const int lane = threadIdx.x;
     const int t_idx = blockIdx.x * 64 + lane;
+    zero_prelude(z, t_idx, gridDim.x * 64);
     PreGeom o;
     const bool need = t_idx < a.P && preprocess_geom<ALT>(a, g, radii, t_idx, gx, gy, fx, fy, o);
     const uint64_t bal = __ballot(need);
@@ -414,7 +416,8 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
 }
 
 __global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
-                                                             uint32_t* __restrict__ tile_count, int gx, int gy, int alt)
+                                                             uint32_t* __restrict__ tile_count, int gx, int gy, int alt,
+                                                             uint32_t* __restrict__ block_tot)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_pre[kBinGauss + 1];
@@ -424,6 +427,7 @@ __global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* _
     if (threadIdx.x == 0) s_w[kBinThreads / 64] = 0;
     __syncthreads();
     block_rect_prefix(P, g, s_pre, s_w);
+    if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[kBinGauss];
     for_each_instance(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += kBinThreads) {
@@ -438,7 +442,7 @@ __global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* _
 __global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
                                                                   uint64_t* __restrict__ keys, int gx, int gy, int alt,
-                                                                  Guard gd)
+                                                                  Guard gd, const uint32_t* __restrict__ block_base)
 {
     if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
@@ -449,14 +453,17 @@ __global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const i
     uint32_t* s_rank = s_hist + T; // per-tile running rank
     for (int t = threadIdx.x; t < T; t += kBinThreads) { s_cnt[t] = 0; s_rank[t] = 0; }
     if (threadIdx.x == 0) s_w[kBinThreads / 64] = 0;
-    {
-        const int g0 = blockIdx.x * kBinGauss, g1 = min(P, g0 + kBinGauss);
-        for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += kBinThreads)
-            if (radii[idx] > 0)
-                g.splat[4 * (size_t)idx + 3].x = __uint_as_float(g.point_offsets[idx] - g.tiles_touched[idx]);
-    }
     __syncthreads();
     block_rect_prefix(P, g, s_pre, s_w);
+    {  // point_offsets (the inclusive scan of tiles_touched) = the block's base (k_plan) + the block-local prefix
+        const int g0 = blockIdx.x * kBinGauss, g1 = min(P, g0 + kBinGauss);
+        const uint32_t base = block_base[blockIdx.x];
+        for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += kBinThreads) {
+            const int k = idx - g0;
+            g.point_offsets[idx] = base + s_pre[k + 1];
+            if (radii[idx] > 0) g.splat[4 * (size_t)idx + 3].x = __uint_as_float(base + s_pre[k]);
+        }
+    }
     for_each_instance(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += kBinThreads) {
@@ -486,6 +493,89 @@ __global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict_
         misc[2] = P > 0 ? point_offsets[P - 1] : 0u;
     }
     if (c) atomicMax(&misc[1], c);
+}
+
+// Binning plan of the LDS-histogram path, one 1024-thread block: the exclusive scan of the count blocks'
+// instance totals (block_tot -> block bases, in place; k_scatter_keys_lds adds its local prefix to form
+// point_offsets), the tile ranges from the per-tile counts, cursor reset, and misc[0..2] = R, longest list,
+// record slots -- mirrored into the caller's pinned host words, so the host reads R without a copy.
+// Replaces two device-wide scans, k_tile_ranges and the read-back copy (seven launches).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t& total)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    uint32_t woff = 0;
+    total = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+        const uint32_t c = s_w[w];
+        if (w < wid) woff += c;
+        total += c;
+    }
+    __syncthreads();
+    return woff + x - v;
+}
+
+// Scan of n counts by one 1024-thread block, each thread over a contiguous run of up to kPlanRun entries with
+// all its loads issued at once (one block-wide scan of the run totals instead of a loop of them).
+constexpr int kPlanRun = 16;  // 16 x 1024 >= kBinMaxTiles
+template <typename F>
+__device__ __forceinline__ uint32_t plan_scan(const uint32_t* in, int n, uint32_t* s_w, uint32_t& mx, F&& emit)
+{
+    const int run = (n + 1023) / 1024;  // <= kPlanRun (checked by the launcher)
+    const int i0 = (int)threadIdx.x * run;
+    uint32_t v[kPlanRun];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanRun; k++) {
+        v[k] = (k < run && i0 + k < n) ? in[i0 + k] : 0u;
+        sum += v[k];
+        mx = max(mx, v[k]);
+    }
+    uint32_t total;
+    uint32_t ex = block_excl_scan(sum, s_w, total);
+#pragma unroll
+    for (int k = 0; k < kPlanRun; k++) {
+        if (k < run && i0 + k < n) emit(i0 + k, ex, v[k]);
+        ex += v[k];
+    }
+    return total;
+}
+
+__global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot, int nb,
+                                               const uint32_t* __restrict__ count, uint32_t* __restrict__ cursor,
+                                               uint2* __restrict__ ranges, int T, uint32_t* __restrict__ misc,
+                                               uint32_t* host)
+{
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_max;
+    if (threadIdx.x == 0) s_max = 0;
+    uint32_t mx = 0, unused = 0;
+    const uint32_t slots = plan_scan(block_tot, nb, s_w, unused, [&](int i, uint32_t ex, uint32_t) { block_tot[i] = ex; });
+    const uint32_t R = plan_scan(count, T, s_w, mx, [&](int t, uint32_t ex, uint32_t c) {
+        ranges[t] = make_uint2(ex, ex + c);
+        cursor[t] = 0;
+    });
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(&s_max, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        misc[0] = R;
+        misc[1] = s_max;
+        misc[2] = slots;
+        if (host) {
+            host[0] = R;
+            host[1] = s_max;
+            host[2] = slots;
+            __threadfence_system();
+        }
+    }
 }
 
 // One thread per Gaussian: drop (depth, index) keys into each touched tile's segment.
@@ -784,7 +874,12 @@ __global__ void __launch_bounds__(256) k_relocation(int P, const float* __restri
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
-bool lds_binning(int gx, int gy) { return gx * gy <= kBinMaxTiles; }
+// LDS-histogram binning with the one-block plan: tile grids up to kBinMaxTiles and up to kPlanRun * 1024 blocks of
+// kBinGauss Gaussians (67M); anything larger takes the generic per-Gaussian path.
+bool lds_binning(int P, int gx, int gy)
+{
+    return gx * gy <= kBinMaxTiles && (long)(P + kBinGauss - 1) / kBinGauss <= (long)kPlanRun * 1024;
+}
 
 // Dynamic LDS above 64 KiB must be opted into per kernel (idempotent; done once per process).
 static void allow_big_lds()
@@ -805,11 +900,19 @@ void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_c
     const size_t lds = sizeof(uint32_t) * (size_t)gx * gy;
     allow_big_lds();
     hipLaunchKernelGGL(k_count_tiles, dim3((P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads), lds, s, P, radii, g,
-                       tile_count, gx, gy, (int)alt);
+                       tile_count, gx, gy, (int)alt, g.scan_tmp);
+}
+
+void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, hipStream_t s)
+{
+    static_assert(kPlanRun * 1024 >= kBinMaxTiles, "one k_plan block covers every LDS-binned tile grid");
+
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, (P + kBinGauss - 1) / kBinGauss, im.tile_count,
+                       im.tile_cursor, im.ranges, T, im.misc, host);
 }
 
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
-                       hipStream_t s)
+                       const ZeroJob& z, hipStream_t s)
 {
     const float fy = a.H / (2.0f * a.tanfovy);
     const float fx = a.W / (2.0f * a.tanfovx);
@@ -817,7 +920,7 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
     const bool alt = a.variant == HLGS_VARIANT_ALT;
     if (!a.indices && !a.colors_precomp && a.shs && a.M > 0 && !tile_count && a.M <= 16) {
         const dim3 g64((a.P + 63) / 64);
-#define HLGS_PSH(AL, M3) hipLaunchKernelGGL((k_preprocess_sh<AL, M3>), g64, dim3(64), 0, s, a, g, radii, gx, gy, fx, fy)
+#define HLGS_PSH(AL, M3) hipLaunchKernelGGL((k_preprocess_sh<AL, M3>), g64, dim3(64), 0, s, a, g, radii, gx, gy, fx, fy, z)
         if (alt) {
             switch (a.M) {
             case 3: HLGS_PSH(true, 9); break;
@@ -838,11 +941,11 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
         return;
     }
     if (a.indices)
-        hipLaunchKernelGGL((k_preprocess<true, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
+        hipLaunchKernelGGL((k_preprocess<true, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy, z);
     else if (a.variant == HLGS_VARIANT_ALT)
-        hipLaunchKernelGGL((k_preprocess<false, true>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
+        hipLaunchKernelGGL((k_preprocess<false, true>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy, z);
     else
-        hipLaunchKernelGGL((k_preprocess<false, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy);
+        hipLaunchKernelGGL((k_preprocess<false, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy, z);
 }
 
 void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s)
@@ -857,11 +960,11 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
     const int T = gx * gy;
     const int alt = a.variant == HLGS_VARIANT_ALT;
     if (timing) stage_mark(s, 3, true);
-    if (lds_binning(gx, gy)) {
+    if (lds_binning(a.P, gx, gy)) {
         allow_big_lds();
         hipLaunchKernelGGL(k_scatter_keys_lds, dim3((a.P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads),
                            2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy,
-                           alt, gd);
+                           alt, gd, g.scan_tmp);
     } else
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
                            im.tile_cursor, b.keys, gx, gy, alt, gd);
