@@ -15,10 +15,18 @@ import ctypes as C
 import torch
 
 from hlgs_core import _lib as L
+from hlgs_core.dp import direct_grad
 
 
 def _dev_f32(t, device):
     return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+def _dest(src, shape, f32):
+    """Gradient output for input `src`: the view hlgs_core.dp.direct_grad offers (a view-DP exchange's flat buffer)
+    when its shape matches, else a fresh tensor.  Every kernel output row is written, so no zero-fill either way."""
+    d = direct_grad(src) if src is not None else None
+    return d if d is not None and tuple(d.shape) == tuple(shape) else torch.empty(shape, **f32)
 
 
 def _opt(t):
@@ -107,10 +115,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     P = means3D.size(0)
     M = sh.size(1) if (sh is not None and sh.size(0) != 0 and sh.dim() > 1) else 0
     out = dict(dmean2D=torch.empty((P, 3), **f32), dcolor=torch.empty((P, 3), **f32),
-               dopacity=torch.empty((P, 1), **f32), dmean3D=torch.empty((P, 3), **f32),
-               dcov3D=torch.empty((P, 6), **f32), ddc=torch.empty((P, 1, 3), **f32),
-               dsh=torch.empty((P, M, 3), **f32), dscale=torch.empty((P, 3), **f32),
-               drot=torch.empty((P, 4), **f32))
+               dopacity=_dest(opacities, (P, 1), f32), dmean3D=_dest(means3D, (P, 3), f32),
+               dcov3D=torch.empty((P, 6), **f32), ddc=_dest(dc, (P, 1, 3), f32),
+               dsh=_dest(sh, (P, M, 3), f32), dscale=_dest(scales, (P, 3), f32),
+               drot=_dest(rotations, (P, 4), f32))
     order = ("dmean2D", "dcolor", "dopacity", "dmean3D", "dcov3D", "ddc", "dsh", "dscale", "drot")
     if P == 0:
         return tuple(out[k] for k in order)

@@ -813,8 +813,9 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             }
             const float test_T = Tt * (1 - alpha);
             const bool valid = !done && !(e2 > 0.0f) && !(e2 < xy.w);  // alpha >= 1/255 (alpha_e2_threshold)
-            const bool stop = valid && test_T < 0.0001f;
-            const bool blended = valid && !stop;
+            const bool tlow = test_T < 0.0001f;  // one compare; stop / blended split it with scalar mask ops
+            const bool stop = valid && tlow;
+            const bool blended = valid && !tlow;
             const float wgt = blended ? alpha * Tt : 0.f;
             C0 = fmaf(c.x, wgt, C0);
             C1 = fmaf(c.y, wgt, C1);
@@ -823,7 +824,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             Tt = blended ? test_T : Tt;
             last = blended ? base - range.x + (uint32_t)j + 1 : last;
             done = done || stop;
-            if (__ballot(blended)) seen_mask |= 1ull << j;
+            if (__builtin_amdgcn_ballot_w64(wgt > 0.f)) seen_mask |= 1ull << j;  // wgt > 0 <=> blended (alpha >= 1/255, T >= 1e-4)
         }
         if (A.seen && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
         __syncthreads();

@@ -11,12 +11,20 @@ import ctypes as C
 import torch
 
 from hlgs_core import _lib as L
+from hlgs_core.dp import direct_grad
 
 
 def _dev_f32(t, device):
     """Small per-call tensors (bg, view/proj matrices, campos) must live on the device: the kernels
     dereference them (rasterize_points.cu:109-125)."""
     return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+def _dest(src, shape, f32):
+    """Gradient output for input `src`: the view hlgs_core.dp.direct_grad offers (a view-DP exchange's flat buffer)
+    when its shape matches, else a fresh tensor.  Every kernel output row is written, so no zero-fill either way."""
+    d = direct_grad(src) if src is not None else None
+    return d if d is not None and tuple(d.shape) == tuple(shape) else torch.empty(shape, **f32)
 
 
 def _opt(t, dtype=None):
@@ -113,9 +121,9 @@ def rasterize_gaussians_backward(bg, render_indices, parent_indices, ts, kids, m
     dev = means3D.device
     f32 = dict(dtype=torch.float32, device=dev)
     out = dict(dmean2D=torch.empty((P_full, 3), **f32), dcolor=torch.empty((P_full, 3), **f32),
-               dopacity=torch.empty((P_full, 1), **f32), dmean3D=torch.empty((P_full, 3), **f32),
-               dcov3D=torch.empty((P_full, 6), **f32), dsh=torch.empty((P_full, M, 3), **f32),
-               dscale=torch.empty((P_full, 3), **f32), drot=torch.empty((P_full, 4), **f32))
+               dopacity=_dest(opacities, (P_full, 1), f32), dmean3D=_dest(means3D, (P_full, 3), f32),
+               dcov3D=torch.empty((P_full, 6), **f32), dsh=_dest(sh, (P_full, M, 3), f32),
+               dscale=_dest(scales, (P_full, 3), f32), drot=_dest(rotations, (P_full, 4), f32))
     g = L.Grads(**{k: L.ptr(v) for k, v in out.items()})
     dpix = dL_dout_color.contiguous().float()
     dinv = None

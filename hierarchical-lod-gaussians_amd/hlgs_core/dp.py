@@ -12,6 +12,28 @@ import torch.distributed as dist
 
 _AVG_OK = [True]  # ReduceOp.AVG accepted by the backend (flips once if it is not)
 
+# Parameters whose gradient the rasterizer backward may write straight into an exchange's flat buffer:
+# data_ptr -> (parameter, flat buffer, offset).  The view is made per call: autograd adopts a returned gradient
+# only while nothing else holds a reference to that tensor.
+_DIRECT = {}
+
+
+def direct_grad(t):
+    """Destination for the gradient of input tensor `t`, or None.
+
+    Used by the rasterizer backward (diff_gaussian_rasterization._C, alt_gaussian_rasterization._C): when `t` is a
+    parameter registered by a FlatGradExchange(direct=True) and its .grad is unset, the backward writes the
+    gradient into the exchange's flat buffer, autograd adopts that tensor as .grad (it steals a fresh leaf
+    gradient instead of copying it), and the all-reduce finds it already packed.  With .grad set (accumulation)
+    a fresh tensor is returned as usual, so an in-place `.grad +=` never aliases its own input."""
+    e = _DIRECT.get(t.data_ptr()) if t is not None and t.numel() else None
+    if e is None:
+        return None
+    p, flat, off = e
+    if p.grad is not None or p.shape != t.shape or p.dtype != t.dtype or flat.device != t.device:
+        return None
+    return flat[off:off + p.numel()].view_as(p)
+
 
 class FlatGradExchange:
     """Pack -> all-reduce -> hand back, for a fixed list of parameter tensors.
@@ -23,7 +45,7 @@ class FlatGradExchange:
     leaving several buckets to pipeline for a 1M-Gaussian model (236 MB of fp32 gradients).
     """
 
-    def __init__(self, params, bucket_bytes=64 << 20, average=True, group=None):
+    def __init__(self, params, bucket_bytes=64 << 20, average=True, group=None, direct=True):
         self.params = list(params)
         self.numels = [p.numel() for p in self.params]
         self.offsets = []
@@ -38,6 +60,18 @@ class FlatGradExchange:
         self.group = group
         per = max(1, bucket_bytes // 4)
         self.buckets = [(s, min(s + per, total)) for s in range(0, total, per)]
+        self.direct = []
+        if direct:
+            for p, off, n in zip(self.params, self.offsets, self.numels):
+                if p.is_contiguous() and p.dtype == torch.float32:
+                    _DIRECT[p.data_ptr()] = (p, self.flat, off)
+                    self.direct.append(p.data_ptr())
+
+    def close(self):
+        """Stop offering the flat buffer to the rasterizer backward."""
+        for k in self.direct:
+            _DIRECT.pop(k, None)
+        self.direct = []
 
     def _pack_range(self, a, b):
         for p, off, n in zip(self.params, self.offsets, self.numels):

@@ -57,3 +57,59 @@ def test_view_dp_allreduce_gloo(tmp_path):
     for k, e in zip(r0.files, expect):
         np.testing.assert_array_equal(r0[k], r1[k])
         np.testing.assert_allclose(r0[k], e, rtol=1e-6, atol=1e-7)
+
+
+def _direct_worker(rank, world, port, out_dir):
+    """The rasterizer backward's direct path: gradients written into the exchange's flat buffer (direct_grad),
+    adopted by autograd as .grad, all-reduced without packing; a second backward on top of a set .grad must
+    accumulate into fresh memory (no aliasing)."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hierarchical-lod-gaussians_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hlgs_core.dp import FlatGradExchange, direct_grad
+    grads = [torch.tensor(g) for g in _rank_grads(rank, world)]
+    params = [torch.zeros(g.shape, requires_grad=True) for g in grads]
+
+    class Render(torch.autograd.Function):  # stands in for _RasterizeGaussians: grads land where direct_grad says
+        @staticmethod
+        def forward(ctx, *ps):
+            ctx.ps = ps
+            return sum((p * 0).sum() for p in ps)
+
+        @staticmethod
+        def backward(ctx, _):
+            outs = []
+            for p, g in zip(ctx.ps, grads):
+                d = direct_grad(p)
+                d = torch.empty_like(g) if d is None else d
+                d.copy_(g)
+                outs.append(d)
+            return tuple(outs)
+
+    ex = FlatGradExchange(params, bucket_bytes=4096)
+    Render.apply(*params).backward()
+    lo, hi = ex.flat.data_ptr(), ex.flat.data_ptr() + 4 * ex.flat.numel()
+    aliased = all(lo <= p.grad.data_ptr() < hi for p in params)
+    Render.apply(*params).backward()  # .grad set: accumulate, 2 x local gradient
+    doubled = all(torch.equal(p.grad, 2 * g) for p, g in zip(params, grads))
+    for p in params:
+        p.grad = None
+    Render.apply(*params).backward()
+    ex.allreduce()
+    ex.close()
+    np.savez(os.path.join(out_dir, f"d{rank}.npz"), *[p.grad.numpy() for p in params],
+             flags=np.array([aliased, doubled]))
+    dist.destroy_process_group()
+
+
+def test_view_dp_direct_gradients_gloo(tmp_path):
+    world = 2
+    port = _free_port()
+    mp.spawn(_direct_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    r0, r1 = np.load(tmp_path / "d0.npz"), np.load(tmp_path / "d1.npz")
+    assert r0["flags"].all() and r1["flags"].all()
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hierarchical-lod-gaussians_amd")]
+    expect = [(a + b) / 2 for a, b in zip(_rank_grads(0, world), _rank_grads(1, world))]
+    for k, e in zip([f for f in r0.files if f != "flags"], expect):
+        np.testing.assert_array_equal(r0[k], r1[k])
+        np.testing.assert_allclose(r0[k], e, rtol=1e-6, atol=1e-7)
