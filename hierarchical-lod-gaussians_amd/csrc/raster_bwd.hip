@@ -348,17 +348,38 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
         ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
         kw = __float_as_int(r3.z);
     }
-    for (uint32_t r = start; r < end; r++) {
-        if (alt) {
-            const int k = (int)(r - start);
-            if (!alt_tile_keep(kx, ky, kco, kthr, kx0 + k % kw, ky0 + k / kw)) continue;
+    // per-Gaussian inputs of the covariance / projection backward, loaded before the record sum so their
+    // latency overlaps it
+    const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
+    float c3[6];
+    for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
+    const f3 mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    // records four at a time: all loads of a group are in flight together, the sums stay in slot order
+    for (uint32_t r0 = start; r0 < end; r0 += 4) {
+        float4 A[4], B[4];
+        float2 Cc[4];
+        bool use[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r = r0 + k;
+            use[k] = r < end;
+            if (alt && use[k]) {
+                const int kk = (int)(r - start);
+                use[k] = alt_tile_keep(kx, ky, kco, kthr, kx0 + kk % kw, ky0 + kk / kw);
+            }
+            if (use[k]) {
+                A[k] = rec.recA[r];
+                B[k] = rec.recB[r];
+                Cc[k] = rec.recC[r];
+            }
         }
-        const float4 A = rec.recA[r];
-        const float4 B = rec.recB[r];
-        const float2 Cc = rec.recC[r];
-        s0 += A.x; s1 += A.y; s2 += A.z; s3 += A.w;
-        s4 += B.x; s5 += B.y; s6 += B.z; s7 += B.w;
-        s8 += Cc.x; s9 += Cc.y;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!use[k]) continue;
+            s0 += A[k].x; s1 += A[k].y; s2 += A[k].z; s3 += A[k].w;
+            s4 += B[k].x; s5 += B[k].y; s6 += B[k].z; s7 += B[k].w;
+            s8 += Cc[k].x; s9 += Cc[k].y;
+        }
     }
     o.dmean2D[3 * idx] = s0;
     o.dmean2D[3 * idx + 1] = s1;
@@ -368,10 +389,6 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     o.dcolor[3 * idx + 2] = s8;
 
     // ---- computeCov2DCUDA (backward.cu:147-326)
-    const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
-    float c3[6];
-    for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
-    const f3 mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     Cov2D k;
     cov2d_eval(mean, fx, fy, a.tanfovx, a.tanfovy, c3, a.viewmatrix, k);
     const float xg = k.txtz < -k.limx || k.txtz > k.limx ? 0.f : 1.f;
@@ -571,6 +588,14 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
     const bool vis = active && radii[t_idx] > 0;
     s_idx[lane] = idx;
     s_vis[lane] = vis;
+    // the visible Gaussian's own inputs, issued before the row copy so both latencies overlap
+    f3 m = mk(0.f, 0.f, 0.f), dcol = mk(0.f, 0.f, 0.f);
+    uint32_t cl = 0;
+    if (vis) {
+        m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+        dcol = mk(o.dcolor[3 * idx], o.dcolor[3 * idx + 1], o.dcolor[3 * idx + 2]);
+        cl = g.clamped[t_idx];
+    }
     __syncthreads();
     // rows of invisible Gaussians are not read: they arrive as zeros, which is their dsh row
     sh_rows_load<3 * MT>(a.shs, s_rows, s_idx, n, lane, M3, s_vis);
@@ -582,14 +607,12 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
             if (ALT) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
         } else {
             const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
-            const f3 m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
             const f3 dir_orig = sub(m, campos);
             const float len = sqrtf(dot(dir_orig, dir_orig));
             const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
-            const uint32_t cl = g.clamped[t_idx];
-            const float dR = (cl & 1u) ? 0.f : o.dcolor[3 * idx];
-            const float dG = (cl & 2u) ? 0.f : o.dcolor[3 * idx + 1];
-            const float dB = (cl & 4u) ? 0.f : o.dcolor[3 * idx + 2];
+            const float dR = (cl & 1u) ? 0.f : dcol.x;
+            const float dG = (cl & 2u) ? 0.f : dcol.y;
+            const float dB = (cl & 4u) ? 0.f : dcol.z;
             const int ncoef = (a.D + 1) * (a.D + 1);
             float vx = 0.f, vy = 0.f, vz = 0.f;
             float basis[MC + OFF];

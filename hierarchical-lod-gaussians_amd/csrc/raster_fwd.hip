@@ -193,6 +193,13 @@ __device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const
     g.rects[t_idx] = make_int2(0, 0);
     g.clamped[t_idx] = 0;
     const f3 p_orig = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
+    // scale and rotation issued with the mean (before the near-plane cull) so their latency overlaps
+    f3 scale = mk(0.f, 0.f, 0.f);
+    float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.cov3D_precomp == nullptr) {
+        scale = mk(a.scales[3 * t_idx], a.scales[3 * t_idx + 1], a.scales[3 * t_idx + 2]);
+        rq = reinterpret_cast<const float4*>(a.rotations)[t_idx];
+    }
     const float* proj = a.projmatrix;
     const float* view = a.viewmatrix;
     const float hx = proj[0] * p_orig.x + proj[4] * p_orig.y + proj[8] * p_orig.z + proj[12];
@@ -204,8 +211,6 @@ __device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const
     if (p_view.z <= 0.2f) return false;
     float c3[6];
     if (a.cov3D_precomp == nullptr) {
-        const f3 scale = mk(a.scales[3 * t_idx], a.scales[3 * t_idx + 1], a.scales[3 * t_idx + 2]);
-        const float4 rq = reinterpret_cast<const float4*>(a.rotations)[t_idx];
         const float rot[4] = {rq.x, rq.y, rq.z, rq.w};
         cov3d_fwd(scale, a.scale_modifier, rot, c3);
     } else {
