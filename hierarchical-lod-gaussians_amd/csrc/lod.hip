@@ -324,6 +324,65 @@ __global__ void __launch_bounds__(256) k_lod_interp_fwd(int S, int n, int M3, co
     }
 }
 
+// Degree-3 rows (M3 = 48) with every load of the row issued at once: lanes 0-11 of the group take one float4 of the
+// child's and the parent's SH row each, lane 12 the mean, 13 the scale, 14 the rotation, 15 the opacity, so the
+// group waits for one gather latency instead of one per loop step.  Same arithmetic as k_lod_interp_fwd.
+__global__ void __launch_bounds__(256) k_lod_interp_fwd48(int S, int n, const int* __restrict__ ridx,
+                                                          const int* __restrict__ pidx, const float* __restrict__ w,
+                                                          const float* __restrict__ means,
+                                                          const float* __restrict__ scales,
+                                                          const float* __restrict__ rots, const float* __restrict__ opac,
+                                                          const float* __restrict__ shs, float* __restrict__ om,
+                                                          float* __restrict__ osc, float* __restrict__ orot,
+                                                          float* __restrict__ oop, float* __restrict__ osh)
+{
+    const LerpRow r = lerp_row(S, n, ridx, pidx, w);
+    if (r.skip) return;
+    const int l = threadIdx.x & 15;
+    const bool sky = r.o < S;
+    const float t = r.t, u = r.u;
+    // every lane issues the same four dword loads for the child and four for the parent, at lane-specific addresses
+    // (lanes 0-11 a float4 of the SH row, 12 the mean, 13 the scale, 14 the rotation, 15 the opacity; short fields
+    // repeat their last element): no divergent load paths, so one gather latency per row
+    const float* base = l < 12 ? shs + 48 * (size_t)r.c + 4 * l
+                      : l == 12 ? means + 3 * (size_t)r.c
+                      : l == 13 ? scales + 3 * (size_t)r.c
+                      : l == 14 ? rots + 4 * (size_t)r.c : opac + r.c;
+    const float* pbase = l < 12 ? shs + 48 * (size_t)r.p + 4 * l
+                       : l == 12 ? means + 3 * (size_t)r.p
+                       : l == 13 ? scales + 3 * (size_t)r.p
+                       : l == 14 ? rots + 4 * (size_t)r.p : opac + r.p;
+    const int kmax = (l < 12 || l == 14) ? 3 : (l == 15 ? 0 : 2);
+    float cv[4], pv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cv[k] = base[min(k, kmax)];
+#pragma unroll
+    for (int k = 0; k < 4; k++) pv[k] = sky ? 0.f : pbase[min(k, kmax)];
+    const float4 c = make_float4(cv[0], cv[1], cv[2], cv[3]);
+    float4 p = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    float4 v = c;
+    if (!sky) {
+        if (l == 14) {
+            float dotv = 0.f;
+            dotv += c.x * p.x;
+            dotv += c.y * p.y;
+            dotv += c.z * p.z;
+            dotv += c.w * p.w;
+            if (dotv < 0) p = make_float4(-p.x, -p.y, -p.z, -p.w);
+        }
+        v = make_float4(t * c.x + u * p.x, t * c.y + u * p.y, t * c.z + u * p.z, t * c.w + u * p.w);
+    }
+    if (l < 12) reinterpret_cast<float4*>(osh + (size_t)48 * r.o)[l] = v;
+    else if (l == 14) reinterpret_cast<float4*>(orot)[r.o] = v;
+    else if (l == 15) oop[r.o] = v.x;
+    else {
+        float* dst = l == 12 ? om : osc;
+        dst[3 * r.o] = v.x;
+        dst[3 * r.o + 1] = v.y;
+        dst[3 * r.o + 2] = v.z;
+    }
+}
+
 // Autograd of the lerp: d_child += t g, d_parent += (1 - t) g (the parent's rotation gradient negated where the
 // forward flipped its sign), d_sky = g for the prefix rows.  A node can be a selected child, the parent of
 // several selected nodes and, with non-monotone sizes, both.  Instead of float atomics on zero-initialised
@@ -342,11 +401,21 @@ __global__ void __launch_bounds__(256) k_lerp_count(int n, const int* __restrict
 
 __global__ void __launch_bounds__(256) k_lerp_fill(int n, const int* __restrict__ ridx, const int* __restrict__ pidx,
                                                    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ incl,
-                                                   uint32_t* __restrict__ cur, uint32_t* __restrict__ list)
+                                                   uint32_t* __restrict__ cur, uint32_t* __restrict__ list,
+                                                   const float* __restrict__ rots, uint32_t* __restrict__ flip)
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const int c = ridx[i], p = pidx[i];
+    if (flip) {  // the forward's rotation sign flip of row i (<q_child, q_parent> < 0), for the gather kernels
+        const float4 rc = reinterpret_cast<const float4*>(rots)[c], rp = reinterpret_cast<const float4*>(rots)[p];
+        float dotv = 0.f;
+        dotv += rc.x * rp.x;
+        dotv += rc.y * rp.y;
+        dotv += rc.z * rp.z;
+        dotv += rc.w * rp.w;
+        flip[i] = dotv < 0 ? 1u : 0u;
+    }
     list[incl[c] - cnt[c] + atomicAdd(&cur[c], 1u)] = 2u * (uint32_t)i;       // child role
     list[incl[p] - cnt[p] + atomicAdd(&cur[p], 1u)] = 2u * (uint32_t)i + 1u;  // parent role
 }
@@ -451,6 +520,145 @@ __global__ void __launch_bounds__(64) k_lerp_gather(int P, int S, int M3, const 
     }
 }
 
+// Degree-3 rows (M3 = 48).  The small upstream gradients of each interpolated row (mean 3, scale 3, rotation 4,
+// opacity 1) are first packed into one 12-float row (k_lerp_pack), so every lane of a 16-lane group issues the same single
+// float4 load per entry: lanes 0-11 one float4 of the SH row, lanes 12-14 the packed small row (lane 15 idles).
+// A group owns four consecutive nodes; their bucket bounds, then their bucket entries (up to kLerpUnroll each, put in
+// (row, role) order in registers), then every weight, sign flag and gradient load of every entry are issued as three
+// rounds; a longer bucket takes the serial next-minimum walk.  Untouched nodes store zero rows.  Sums run in the
+// (sky, then (row, role) ascending) order of k_lerp_gather; a parent entry's rotation sign comes from k_lerp_fill.
+constexpr int kLerpUnroll = 3;
+constexpr int kLerpNodes = 4;
+__global__ void __launch_bounds__(256) k_lerp_pack(int n, int S, const float* __restrict__ gm,
+                                                   const float* __restrict__ gsc, const float* __restrict__ grot,
+                                                   const float* __restrict__ gop, float4* __restrict__ packed)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int o = S + i;
+    const float4 r = reinterpret_cast<const float4*>(grot)[o];
+    packed[3 * i] = make_float4(gm[3 * o], gm[3 * o + 1], gm[3 * o + 2], gsc[3 * o]);
+    packed[3 * i + 1] = make_float4(gsc[3 * o + 1], gsc[3 * o + 2], r.x, r.y);
+    packed[3 * i + 2] = make_float4(r.z, r.w, gop[o], 0.f);
+}
+// gradient of interpolated row `row` (output row S + row) in the lane's packed layout
+__device__ __forceinline__ const float4* lerp_src(int l, int S, int row, const float* __restrict__ gsh,
+                                                  const float4* __restrict__ packed)
+{
+    return l < 12 ? reinterpret_cast<const float4*>(gsh + (size_t)48 * (S + row)) + l
+                  : packed + 3 * (size_t)row + min(l - 12, 2);
+}
+// skybox output row v (< S) in the same lane layout, read field by field (a short prefix)
+__device__ __forceinline__ float4 lerp_sky(int l, int v, const float* __restrict__ gm, const float* __restrict__ gsc,
+                                           const float* __restrict__ grot, const float* __restrict__ gop,
+                                           const float* __restrict__ gsh)
+{
+    if (l < 12) return reinterpret_cast<const float4*>(gsh + (size_t)48 * v)[l];
+    if (l == 12) return make_float4(gm[3 * v], gm[3 * v + 1], gm[3 * v + 2], gsc[3 * v]);
+    if (l == 13) return make_float4(gsc[3 * v + 1], gsc[3 * v + 2], grot[4 * v], grot[4 * v + 1]);
+    if (l == 14) return make_float4(grot[4 * v + 2], grot[4 * v + 3], gop[v], 0.f);
+    return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// rotation components in the packed layout: lane 13 .z .w, lane 14 .x .y
+__device__ __forceinline__ void lerp_acc(float4& acc, float f, float4 g, bool neg, int l)
+{
+    const float sx = (neg && l == 14) ? -1.0f : 1.0f, sy = sx;
+    const float sz = (neg && l == 13) ? -1.0f : 1.0f, sw = sz;
+    acc.x += sx * (f * g.x);
+    acc.y += sy * (f * g.y);
+    acc.z += sz * (f * g.z);
+    acc.w += sw * (f * g.w);
+}
+
+__global__ void __launch_bounds__(256) k_lerp_gather48(int P, int S, const float* __restrict__ w,
+                                                       const uint32_t* __restrict__ flip,
+                                                       const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ incl,
+                                                       const uint32_t* __restrict__ list, const float4* __restrict__ packed,
+                                                       const float* __restrict__ gm, const float* __restrict__ gsc,
+                                                       const float* __restrict__ grot, const float* __restrict__ gop,
+                                                       const float* __restrict__ gsh, float* __restrict__ dm,
+                                                       float* __restrict__ dsc, float* __restrict__ drot,
+                                                       float* __restrict__ dop, float* __restrict__ dsh)
+{
+    const int v0 = (blockIdx.x * 16 + (threadIdx.x >> 4)) * kLerpNodes;
+    if (v0 >= P) return;
+    const int l = threadIdx.x & 15;
+    uint32_t k[kLerpNodes], st[kLerpNodes];
+#pragma unroll
+    for (int j = 0; j < kLerpNodes; j++) {
+        const int v = v0 + j;
+        k[j] = v < P ? cnt[v] : 0u;
+        st[j] = v < P ? incl[v] - k[j] : 0u;
+    }
+    uint32_t e[kLerpNodes][kLerpUnroll];
+#pragma unroll
+    for (int j = 0; j < kLerpNodes; j++)
+#pragma unroll
+        for (int q = 0; q < kLerpUnroll; q++) e[j][q] = (q < (int)k[j] && k[j] <= kLerpUnroll) ? list[st[j] + q] : ~0u;
+    float4 acc[kLerpNodes];
+#pragma unroll
+    for (int j = 0; j < kLerpNodes; j++) {
+        acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (v0 + j < S) acc[j] = lerp_sky(l, v0 + j, gm, gsc, grot, gop, gsh);  // skybox prefix: identity
+#pragma unroll
+        for (int i = 1; i < kLerpUnroll; i++)  // insertion sort in registers (entries are distinct; ~0 pads last)
+#pragma unroll
+            for (int q = i; q > 0; q--) {
+                const uint32_t x = e[j][q - 1], y = e[j][q];
+                e[j][q - 1] = min(x, y);
+                e[j][q] = max(x, y);
+            }
+    }
+    float4 g[kLerpNodes][kLerpUnroll];
+    float f[kLerpNodes][kLerpUnroll];
+    bool neg[kLerpNodes][kLerpUnroll];
+#pragma unroll
+    for (int j = 0; j < kLerpNodes; j++)
+#pragma unroll
+        for (int q = 0; q < kLerpUnroll; q++) {
+            f[j][q] = 0.f;
+            neg[j][q] = false;
+            g[j][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e[j][q] != ~0u) {
+                const int row = (int)(e[j][q] >> 1);
+                const bool par = e[j][q] & 1u;
+                const float t = w[row];
+                f[j][q] = par ? 1 - t : t;
+                neg[j][q] = par && flip[row];
+                g[j][q] = *lerp_src(l, S, row, gsh, packed);
+            }
+        }
+#pragma unroll
+    for (int j = 0; j < kLerpNodes; j++) {
+        const int v = v0 + j;
+        if (v >= P) break;
+        if (k[j] <= kLerpUnroll) {
+#pragma unroll
+            for (int q = 0; q < kLerpUnroll; q++)
+                if (e[j][q] != ~0u) lerp_acc(acc[j], f[j][q], g[j][q], neg[j][q], l);
+        } else {
+            uint32_t prev = ~0u;
+            for (uint32_t q = 0; q < k[j]; q++) {
+                uint32_t best = ~0u;
+                for (uint32_t x = 0; x < k[j]; x++) {
+                    const uint32_t y = list[st[j] + x];
+                    if ((prev == ~0u || y > prev) && y < best) best = y;
+                }
+                prev = best;
+                const int row = (int)(best >> 1);
+                const bool par = best & 1u;
+                const float t = w[row];
+                lerp_acc(acc[j], par ? 1 - t : t, *lerp_src(l, S, row, gsh, packed), par && flip[row], l);
+            }
+        }
+        const float4 a = acc[j];
+        if (l < 12) reinterpret_cast<float4*>(dsh + (size_t)48 * v)[l] = a;
+        else if (l == 12) { dm[3 * v] = a.x; dm[3 * v + 1] = a.y; dm[3 * v + 2] = a.z; dsc[3 * v] = a.w; }
+        else if (l == 13) { dsc[3 * v + 1] = a.x; dsc[3 * v + 2] = a.y; drot[4 * v] = a.z; drot[4 * v + 1] = a.w; }
+        else if (l == 14) { drot[4 * v + 2] = a.x; drot[4 * v + 3] = a.y; dop[v] = a.z; }
+    }
+}
+
 // ---- host launchers
 static inline dim3 g256(long n) { return dim3((unsigned)((n + 255) / 256)); }
 
@@ -513,6 +721,11 @@ void launch_lod_interp_fwd(int S, int n, int M3, const int* ridx, const int* pid
                            const float* scales, const float* rots, const float* opac, const float* shs, float* om,
                            float* osc, float* orot, float* oop, float* osh, hipStream_t s)
 {
+    if (M3 == 48 && shs) {
+        hipLaunchKernelGGL(k_lod_interp_fwd48, dim3((unsigned)(((long)S + n + 15) / 16)), dim3(256), 0, s, S, n, ridx,
+                           pidx, w, means, scales, rots, opac, shs, om, osc, orot, oop, osh);
+        return;
+    }
     hipLaunchKernelGGL(k_lod_interp_fwd, dim3((unsigned)(((long)S + n + 15) / 16)), dim3(256), 0, s, S, n, M3, ridx,
                        pidx, w, means, scales,
                        rots, opac, shs, om, osc, orot, oop, osh);
@@ -521,7 +734,7 @@ void launch_lod_interp_fwd(int S, int n, int M3, const int* ridx, const int* pid
 size_t lerp_bwd_scratch_elems(int P, int n)
 {
     return 4 * align_up(sizeof(uint32_t) * (size_t)P) / 4 + align_up(sizeof(uint32_t) * scan_scratch_elems(P)) / 4 +
-           align_up(sizeof(uint32_t) * 2 * (size_t)n) / 4;
+           align_up(sizeof(uint32_t) * 2 * (size_t)n) / 4 + align_up(sizeof(float) * 12 * (size_t)n) / 4;
 }
 
 void launch_lod_interp_bwd(int P, int S, int n, int M3, const int* ridx, const int* pidx, const float* w,
@@ -538,14 +751,25 @@ void launch_lod_interp_bwd(int P, int S, int n, int M3, const int* ridx, const i
     uint32_t* cnt = take(P);
     uint32_t* cur = take(P);
     uint32_t* incl = take(P);
-    take(P);  // reserved
+    uint32_t* flip = take(P);  // per-row rotation sign flip (n <= P)
     uint32_t* tmp = take(scan_scratch_elems(P));
     uint32_t* list = take(2 * (size_t)n);
+    float4* packed = reinterpret_cast<float4*>(take(12 * (size_t)n));  // k_lerp_pack rows (degree-3 path)
     hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (size_t)P, s);
     hipMemsetAsync(cur, 0, sizeof(uint32_t) * (size_t)P, s);
     if (n > 0) hipLaunchKernelGGL(k_lerp_count, g256(n), dim3(256), 0, s, n, ridx, pidx, cnt);
     scan_inclusive_u32(cnt, incl, (size_t)P, tmp, s);
-    if (n > 0) hipLaunchKernelGGL(k_lerp_fill, g256(n), dim3(256), 0, s, n, ridx, pidx, cnt, incl, cur, list);
+    const bool fast = M3 == 48 && gsh && dsh;
+    if (n > 0)
+        hipLaunchKernelGGL(k_lerp_fill, g256(n), dim3(256), 0, s, n, ridx, pidx, cnt, incl, cur, list, rots,
+                           fast ? flip : nullptr);
+    if (fast) {
+        if (n > 0) hipLaunchKernelGGL(k_lerp_pack, g256(n), dim3(256), 0, s, n, S, gm, gsc, grot, gop, packed);
+        const long groups = ((long)P + kLerpNodes - 1) / kLerpNodes;
+        hipLaunchKernelGGL(k_lerp_gather48, dim3((unsigned)((groups + 15) / 16)), dim3(256), 0, s, P, S, w, flip, cnt,
+                           incl, list, packed, gm, gsc, grot, gop, gsh, dm, dsc, drot, dop, dsh);
+        return;
+    }
     const dim3 grid((unsigned)(((long)P + 63) / 64));
 #define HLGS_LG(K) hipLaunchKernelGGL((k_lerp_gather<K>), grid, dim3(64), 0, s, P, S, M3, ridx, w, rots, cnt, incl, list, \
                                       gm, gsc, grot, gop, gsh, dm, dsc, drot, dop, dsh)

@@ -239,3 +239,31 @@ def test_morton_codes_bit_exact():
     np.testing.assert_array_equal(codes.cpu().numpy(), HF.morton_codes(xyz, mn, mx))
     idx = scene.morton_order(torch.tensor(xyz, device=DEV), skybox_points=5).cpu().numpy()
     assert idx[0] == 5 and sorted(idx.tolist()) == list(range(5, 50000))
+
+
+@pytest.mark.parametrize("deg", [3, 1])
+def test_lod_interpolation_backward_wide_buckets(deg):
+    """Parents shared by many selected rows (buckets far longer than a binary tree's), nodes that are both a child
+    and a parent, a skybox prefix: the gather backward against the oracle restatement of the lerp's autograd."""
+    import gaussian_hierarchy as GH
+    rng = np.random.default_rng(7)
+    N, n, Sk, M = 5000, 1500, 5, (deg + 1) ** 2
+    ri = rng.choice(np.arange(Sk, N), n, replace=False).astype(np.int32)
+    pi = rng.choice(np.arange(Sk, 40), n).astype(np.int32)          # ~40 rows per parent
+    pi[::7] = ri[(np.arange(len(pi[::7])) * 3) % n]                  # parents that are selected children too
+    ts = rng.uniform(0, 1, n).astype(np.float32)
+    h = dict(means3D=rng.normal(size=(N, 3)), scales=rng.uniform(0.01, 1, (N, 3)), rotations=rng.normal(size=(N, 4)),
+             opacities=rng.uniform(0, 1, (N, 1)), shs=rng.normal(size=(N, M, 3)))
+    h = {k: v.astype(np.float32) for k, v in h.items()}
+    leaf = lambda a: torch.tensor(a, device=DEV, requires_grad=True)  # noqa: E731
+    m, s, r, o, sh = leaf(h["means3D"]), leaf(h["scales"]), leaf(h["rotations"]), leaf(h["opacities"]), leaf(h["shs"])
+    pfull = np.zeros(N, np.int32)
+    pfull[:n] = pi
+    outs = GH.interpolate_lod(m, s, r, o, sh, torch.tensor(ri, device=DEV), torch.tensor(pfull, device=DEV),
+                              torch.tensor(np.pad(ts, (0, N - n)), device=DEV), Sk)
+    gs = [rng.normal(size=tuple(x.shape)).astype(np.float32) for x in outs]
+    sum((x * torch.tensor(g, device=DEV)).sum() for x, g in zip(outs, gs)).backward()
+    d = O.lod_interp_backward(Sk, ri, pi, ts, h["rotations"], N,
+                              dict(means=gs[0], scales=gs[1], rots=gs[2], opac=gs[3], shs=gs[4]))
+    for leaf_t, key in zip((m, s, r, o, sh), ("means", "scales", "rots", "opac", "shs")):
+        np.testing.assert_allclose(leaf_t.grad.cpu().numpy().reshape(d[key].shape), d[key], rtol=1e-5, atol=1e-4)
