@@ -523,12 +523,12 @@ __global__ void __launch_bounds__(64) k_lerp_gather(int P, int S, int M3, const 
 // Degree-3 rows (M3 = 48).  The small upstream gradients of each interpolated row (mean 3, scale 3, rotation 4,
 // opacity 1) are first packed into one 12-float row (k_lerp_pack), so every lane of a 16-lane group issues the same single
 // float4 load per entry: lanes 0-11 one float4 of the SH row, lanes 12-14 the packed small row (lane 15 idles).
-// A group owns four consecutive nodes; their bucket bounds, then their bucket entries (up to kLerpUnroll each, put in
+// A group owns two consecutive nodes; their bucket bounds, then their bucket entries (up to kLerpUnroll each, put in
 // (row, role) order in registers), then every weight, sign flag and gradient load of every entry are issued as three
 // rounds; a longer bucket takes the serial next-minimum walk.  Untouched nodes store zero rows.  Sums run in the
 // (sky, then (row, role) ascending) order of k_lerp_gather; a parent entry's rotation sign comes from k_lerp_fill.
 constexpr int kLerpUnroll = 3;
-constexpr int kLerpNodes = 4;
+constexpr int kLerpNodes = 2;
 __global__ void __launch_bounds__(256) k_lerp_pack(int n, int S, const float* __restrict__ gm,
                                                    const float* __restrict__ gsc, const float* __restrict__ grot,
                                                    const float* __restrict__ gop, float4* __restrict__ packed)
