@@ -134,10 +134,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # HLGS_DIST_BACKEND=gloo with more ranks than GPUs rehearses the multi-rank path on a one-GPU box (ranks share
+    # the card); the driver's N-GPU runs use the default, RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("HLGS_DIST_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count()) if world > 1 else 0
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
 
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from hlgs_core import _lib as L
@@ -261,7 +268,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded PCG64 scene and upstream gradients; no dataset)",
             "config": {"workload": f"configs[1]: {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd with depth, "
-                                   f"one view per GPU" + (", RCCL grad all-reduce" if world > 1 else ""),
+                                   f"one view per GPU" + ((", RCCL" if backend == "nccl" else ", " + backend) + " grad all-reduce"
+                                                          if world > 1 else ""),
                        "num_rendered": nr, "visible": V, "tiles": T,
                        "parallelism": f"view-dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
