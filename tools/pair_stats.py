@@ -26,7 +26,7 @@ from diff_gaussian_rasterization import GaussianRasterizer  # noqa: E402
 rast = GaussianRasterizer(settings(cam, 3))
 lib = L.load()
 lib.hlgs_pair_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-out = (C.c_ulonglong * 4)()
+out = (C.c_ulonglong * 8)()
 m2 = torch.zeros_like(m, requires_grad=True)
 c, _, inv = rast(means3D=m, means2D=m2, opacities=o, shs=sh, scales=sc, rotations=r)
 torch.cuda.synchronize()
@@ -34,6 +34,6 @@ lib.hlgs_pair_stats(out, 1)
 torch.autograd.backward([c, inv], [torch.tensor(g_np, device="cuda"), torch.tensor(gd_np, device="cuda")])
 torch.cuda.synchronize()
 lib.hlgs_pair_stats(out, 1)
-quads, valid, iters, skipped = list(out)
-print(dict(quad_evals=quads, valid_lanes=valid, lane_util=valid / (64 * quads), gauss_iters=iters, skipped=skipped,
-           quads_per_iter=quads / iters))
+quads, valid, empty_quads, iters, no_reduce = list(out)[:5]
+print(dict(quad_evals=quads, valid_lanes=valid, lane_util=valid / (64 * quads), empty_quad_evals=empty_quads,
+           splat_iters=iters, splat_iters_without_valid_lane=no_reduce, quads_per_iter=quads / iters))
