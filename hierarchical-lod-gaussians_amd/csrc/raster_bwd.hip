@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
     const float* __restrict__ dL_dpixels = A.dL_dpixels;
     const float* __restrict__ dL_dinvdepths = A.dL_dinvdepths;
     const BwdScratch& rec = A.rec;
-    __shared__ float4 s_xy[64];   // x, y, 1/depth, quadrant mask bits
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, unused
     __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
     __shared__ float4 s_col[64];  // r, g, b, alpha threshold on e2
     __shared__ float2 s_tf[64];   // interpolation t, 1/kids
@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
         const int n = (int)min(64u, cnt - b0);
         const uint32_t li_top = cnt - 1 - b0;
         const bool lane_valid = lane < n;
-        uint32_t slot = 0;
+        uint32_t slot = 0, qm = 0;
         float4 my_co = make_float4(0.f, 0.f, 0.f, 0.f);
         if (lane_valid) {
             const uint32_t pos = range.x + li_top - lane;
@@ -182,8 +182,8 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
             const float4* sr = g.splat + 4 * (size_t)id;
             const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            const uint32_t qm = quad_mask(r0.x, r0.y, co, tx0, ty0);
-            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, __uint_as_float(qm));
+            qm = quad_mask(r0.x, r0.y, co, tx0, ty0);
+            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
             s_q[lane] = conic_q(co);
             my_co = co;
             s_col[lane] = make_float4(r1.z, r1.w, r2.x, r3.w);
@@ -198,14 +198,27 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
         // a batch entirely behind every pixel's last contributor leaves its records zero
         const uint32_t li_bot = li_top - (uint32_t)(n - 1);
         if (li_bot < maxlast) {
-            for (int j = 0; j < n; j++) {
-                const uint32_t li = li_top - (uint32_t)j;
-                const float4 xy = s_xy[j];
-                uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(xy.w));
+            // per quadrant, the wave-uniform set of the batch's splats to visit: footprint reaches the quadrant
+            // (quad_mask) and the splat lies in front of the quadrant's furthest contributor (li < qlast[k],
+            // i.e. j > li_top - qlast[k]); the loop then visits set bits only, with no LDS read to decide
+            uint64_t qv[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if (li >= qlast[k]) qm &= ~(1u << k);
-                if (qm == 0) continue;
+            for (int k = 0; k < 4; k++) {
+                uint64_t m = __ballot((qm >> k) & 1u);
+                if (li_top >= qlast[k]) {
+                    const uint32_t d = li_top - qlast[k];  // splats 0..d are behind every pixel of quadrant k
+                    m = d >= 63 ? 0ull : m & (~0ull << (d + 1));
+                }
+                qv[k] = m;
+            }
+            uint64_t todo = qv[0] | qv[1] | qv[2] | qv[3];
+            while (todo) {
+                const int j = __builtin_ctzll(todo);
+                todo &= todo - 1;
+                const uint32_t li = li_top - (uint32_t)j;
+                const uint32_t qm = (uint32_t)((qv[0] >> j) & 1u) | ((uint32_t)((qv[1] >> j) & 1u) << 1) |
+                                    ((uint32_t)((qv[2] >> j) & 1u) << 2) | ((uint32_t)((qv[3] >> j) & 1u) << 3);
+                const float4 xy = s_xy[j];
                 const float4 co = s_q[j];
                 const float4 col = s_col[j];
                 const float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
