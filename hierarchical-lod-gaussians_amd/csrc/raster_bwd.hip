@@ -212,16 +212,16 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
                 qv[k] = m;
             }
             uint64_t todo = qv[0] | qv[1] | qv[2] | qv[3];
+            // the next visited splat's LDS reads are issued after this splat's pixel steps and before its
+            // reduction, which covers their latency (the splat data is dead by then, so no extra registers)
+            int j = todo ? __builtin_ctzll(todo) : 0;
+            float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
+            float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
             while (todo) {
-                const int j = __builtin_ctzll(todo);
                 todo &= todo - 1;
                 const uint32_t li = li_top - (uint32_t)j;
                 const uint32_t qm = (uint32_t)((qv[0] >> j) & 1u) | ((uint32_t)((qv[1] >> j) & 1u) << 1) |
                                     ((uint32_t)((qv[2] >> j) & 1u) << 2) | ((uint32_t)((qv[3] >> j) & 1u) << 3);
-                const float4 xy = s_xy[j];
-                const float4 co = s_q[j];
-                const float4 col = s_col[j];
-                const float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
                 float acc[10];
 #pragma unroll
                 for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
@@ -236,14 +236,22 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
                     if ((qm >> k) & 1u)  // uniform branch
                         any |= bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), co, col,
                                                        xy.z, tf.x, tf.y, col.w, acc);
+                const int jc = j;
+                if (todo) {
+                    j = __builtin_ctzll(todo);
+                    xy = s_xy[j];
+                    co = s_q[j];
+                    col = s_col[j];
+                    if (INTERP) tf = s_tf[j];
+                }
                 if (__ballot(any)) {
                     float r0, r1, r2;
                     wave_reduce10(acc, r0, r1, r2);
                     if ((lane & 15) == 0) {
                         const int row = lane >> 4, c = ((row & 1) << 1) | (row >> 1);
-                        s_m[64 * c + j] = r0;
-                        s_m[64 * (4 + c) + j] = r1;
-                        if (!(row & 1)) s_m[64 * (8 + (row >> 1)) + j] = r2;
+                        s_m[64 * c + jc] = r0;
+                        s_m[64 * (4 + c) + jc] = r1;
+                        if (!(row & 1)) s_m[64 * (8 + (row >> 1)) + jc] = r2;
                     }
                 }
             }
