@@ -782,9 +782,11 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     uint32_t last = 0;
-    bool done = !(px < A.W && py < A.H);
+    // per-lane predicates are kept as wave masks (the wave is always full): compares are ballots of one v_cmp
+    // each, their combinations scalar mask operations, and selects read them back with inverse_ballot
+    uint64_t done = __builtin_amdgcn_ballot_w64(!(px < A.W && py < A.H));
     for (uint32_t base = range.x; base < range.y; base += 64) {
-        if (__all(done)) break;
+        if (done == ~0ull) break;
         const uint32_t pos = base + lane;
         uint32_t my_id = 0;
         bool hit = false;
@@ -817,19 +819,20 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
                 alpha = tt * my_alpha + (1.0f - tt) * (1.0f - __powf(1.0f - my_alpha, c.w));
             }
             const float test_T = Tt * (1 - alpha);
-            const bool valid = !done && !(e2 > 0.0f) && !(e2 < xy.w);  // alpha >= 1/255 (alpha_e2_threshold)
-            const bool tlow = test_T < 0.0001f;  // one compare; stop / blended split it with scalar mask ops
-            const bool stop = valid && tlow;
-            const bool blended = valid && !tlow;
-            const float wgt = blended ? alpha * Tt : 0.f;
+            // alpha >= 1/255 (alpha_e2_threshold); a NaN e2 passes both tests, as in the reference
+            const uint64_t valid = ~done & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < xy.w);
+            const uint64_t tlow = __builtin_amdgcn_ballot_w64(test_T < 0.0001f);
+            const uint64_t blended = valid & ~tlow;
+            done |= valid & tlow;  // the pixel stops; this splat is not blended into it
+            const bool bl = __builtin_amdgcn_inverse_ballot_w64(blended);
+            const float wgt = bl ? alpha * Tt : 0.f;
             C0 = fmaf(c.x, wgt, C0);
             C1 = fmaf(c.y, wgt, C1);
             C2 = fmaf(c.z, wgt, C2);
             if (DEPTH) D = fmaf(xy.z, wgt, D);
-            Tt = blended ? test_T : Tt;
-            last = blended ? base - range.x + (uint32_t)j + 1 : last;
-            done = done || stop;
-            if (__builtin_amdgcn_ballot_w64(wgt > 0.f)) seen_mask |= 1ull << j;  // wgt > 0 <=> blended (alpha >= 1/255, T >= 1e-4)
+            Tt = bl ? test_T : Tt;
+            last = bl ? base - range.x + (uint32_t)j + 1 : last;
+            if (blended) seen_mask |= 1ull << j;
         }
         if (A.seen && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
         __syncthreads();
