@@ -39,8 +39,8 @@ struct PixB {
 // ALT: the alt rasterizer's backward (alt-rasterizer/cuda_rasterizer/backward.cu:596-624) has no
 // o * G > 0.99 => dL/dalpha = 0 rule; its doubled background term is folded into p.TB by the caller.
 template <bool INTERP, bool DEPTH, bool ALT>
-__device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& q, const float4& col,
-                                         float invz, float tt, float fr, float thr, float (&acc)[10])
+__device__ __forceinline__ uint64_t bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& q, const float4& col,
+                                             float invz, float tt, float fr, float thr, float (&acc)[10])
 {
     const float e2 = splat_e2(q, dx, dy);  // power * log2(e)
     const float G = __builtin_amdgcn_exp2f(e2);
@@ -48,8 +48,10 @@ __device__ __forceinline__ bool bwd_pair(PixB& p, uint32_t li, float dx, float d
     const float my_alpha = fminf(0.99f, test_alpha);
     float alpha = my_alpha;
     if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
-    const bool valid = li < p.last && !(e2 > 0.0f) && !(e2 < thr);  // alpha >= 1/255 (alpha_e2_threshold)
-    if (valid) {
+    // alpha >= 1/255 (alpha_e2_threshold), as a wave mask: one v_cmp per test, combined in SALU (the wave is full)
+    const uint64_t valid = __builtin_amdgcn_ballot_w64(li < p.last) & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) &
+                           ~__builtin_amdgcn_ballot_w64(e2 < thr);
+    if (__builtin_amdgcn_inverse_ballot_w64(valid)) {
         const float r1m = __builtin_amdgcn_rcpf(1.f - alpha);  // 1/(1-alpha), alpha <= 0.99
         p.T = p.T * r1m;
         const float weight = alpha * p.T;
@@ -230,7 +232,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
                     acc[v] = __uint_as_float((uint32_t)z);
                     acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
                 }
-                bool any = false;
+                uint64_t any = 0;  // lanes with a valid pair (wave mask)
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     if ((qm >> k) & 1u)  // uniform branch
@@ -244,7 +246,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
                     col = s_col[j];
                     if (INTERP) tf = s_tf[j];
                 }
-                if (__ballot(any)) {
+                if (any) {
                     float r0, r1, r2;
                     wave_reduce10(acc, r0, r1, r2);
                     if ((lane & 15) == 0) {
