@@ -14,6 +14,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/write -o run -
 echo "write ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES -d $O/sq -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-stage-timing > $O/sq.log 2>&1
 echo "sq ok"
+# refresh the committed PMC summary on the box first, so the plain bench line reports this run's traffic and
+# instruction counts (the summary is written again locally from the merged gpurun_out/round)
+python3 tools/summarize_profile.py $O $O/summary > /dev/null && cp $O/summary/pmc_traffic.json profiles/r01/pmc_traffic.json
 timeout -k 10 300 python3 bench.py > $O/bench_plain.log 2>&1
 echo "plain ok"
 tail -1 $O/bench_plain.log

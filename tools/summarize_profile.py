@@ -32,9 +32,11 @@ def main(src, dst):
     dom = os.path.join(src, "trace", "run_domain_stats.csv")
     if os.path.exists(dom):
         shutil.copy(dom, os.path.join(dst, "bench_domain_stats.csv"))
-    line = open(os.path.join(src, "bench_plain.log")).read().strip().splitlines()[-1]
-    json.loads(line)
-    open(os.path.join(dst, "bench_line.json"), "w").write(line + "\n")
+    plain = os.path.join(src, "bench_plain.log")
+    if os.path.exists(plain):  # absent when called on the box before the plain bench run
+        line = open(plain).read().strip().splitlines()[-1]
+        json.loads(line)
+        open(os.path.join(dst, "bench_line.json"), "w").write(line + "\n")
     traced = open(os.path.join(src, "bench_line.log")).read().strip().splitlines()[-1]
     open(os.path.join(dst, "bench_line_under_rocprof.json"), "w").write(traced + "\n")
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
