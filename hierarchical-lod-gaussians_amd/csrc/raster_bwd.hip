@@ -275,6 +275,39 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
 }
 
 
+// cov3d_fwd (forward.cu:181-215) with every product and sum rounded on its own, as in the preprocess, which is
+// compiled without FMA contraction (this file is not): the recomputed covariance is bit-identical to the one the
+// forward used, so the forward need not store it (24 bytes per Gaussian written there and read here).
+__device__ __forceinline__ void cov3d_exact(f3 scale, float mod, float4 q, float out[6])
+{
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    auto M_ = [](float u, float v) { return __fmul_rn(u, v); };
+    auto A_ = [](float u, float v) { return __fadd_rn(u, v); };
+    auto S_ = [](float u, float v) { return __fsub_rn(u, v); };
+    const m3 R = mcols(S_(1.f, M_(2.f, A_(M_(y, y), M_(z, z)))), M_(2.f, S_(M_(x, y), M_(r, z))),
+                       M_(2.f, A_(M_(x, z), M_(r, y))), M_(2.f, A_(M_(x, y), M_(r, z))),
+                       S_(1.f, M_(2.f, A_(M_(x, x), M_(z, z)))), M_(2.f, S_(M_(y, z), M_(r, x))),
+                       M_(2.f, S_(M_(x, z), M_(r, y))), M_(2.f, A_(M_(y, z), M_(r, x))),
+                       S_(1.f, M_(2.f, A_(M_(x, x), M_(y, y)))));
+    m3 Sm = mcols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    Sm.m[0][0] = M_(mod, scale.x);
+    Sm.m[1][1] = M_(mod, scale.y);
+    Sm.m[2][2] = M_(mod, scale.z);
+    m3 Mm, Sig;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int row = 0; row < 3; row++)  // mmul(S, R)
+            Mm.m[c][row] = A_(A_(M_(Sm.m[0][row], R.m[c][0]), M_(Sm.m[1][row], R.m[c][1])), M_(Sm.m[2][row], R.m[c][2]));
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int row = 0; row < 3; row++)  // mmul(mtrans(M), M)
+            Sig.m[c][row] = A_(A_(M_(Mm.m[row][0], Mm.m[c][0]), M_(Mm.m[row][1], Mm.m[c][1])), M_(Mm.m[row][2], Mm.m[c][2]));
+    out[0] = Sig.m[0][0]; out[1] = Sig.m[0][1]; out[2] = Sig.m[0][2];
+    out[3] = Sig.m[1][1]; out[4] = Sig.m[1][2]; out[5] = Sig.m[2][2];
+}
+
 // One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
 // backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
 template <bool HIER, bool ALT>
@@ -373,9 +406,14 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     }
     // per-Gaussian inputs of the covariance / projection backward, loaded before the record sum so their
     // latency overlaps it
-    const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
     float c3[6];
-    for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
+    if (a.cov3D_precomp || HIER) {
+        const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
+        for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
+    } else {  // not stored by the forward: recomputed from the scale and rotation the forward used
+        cov3d_exact(mk(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]), a.scale_modifier,
+                    reinterpret_cast<const float4*>(a.rotations)[idx], c3);
+    }
     const f3 mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     // records four at a time: all loads of a group are in flight together, the sums stay in slot order
     for (uint32_t r0 = start; r0 < end; r0 += 4) {

@@ -81,10 +81,12 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
         for (int i = 0; i < 6; i++) c3[i] = a.cov3D_precomp[6 * t_idx + i];
         cov3D = c3;
     }
-    float2* c3o = reinterpret_cast<float2*>(g.cov3D + 6 * (size_t)t_idx);
-    c3o[0] = make_float2(c3[0], c3[1]);
-    c3o[1] = make_float2(c3[2], c3[3]);
-    c3o[2] = make_float2(c3[4], c3[5]);
+    if (HIER) {  // the hierarchy-mode backward reads the lerped covariance; otherwise k_gauss_bwd recomputes it
+        float2* c3o = reinterpret_cast<float2*>(g.cov3D + 6 * (size_t)t_idx);
+        c3o[0] = make_float2(c3[0], c3[1]);
+        c3o[1] = make_float2(c3[2], c3[3]);
+        c3o[2] = make_float2(c3[4], c3[5]);
+    }
 
     Cov2D k;
     cov2d_eval(p_orig, fx, fy, a.tanfovx, a.tanfovy, cov3D, view, k);
@@ -183,7 +185,7 @@ struct PreGeom {
     int x0, y0, x1, y1;
 };
 
-// forward.cu:218-403 up to the colour: writes the zero defaults, cov3D and rects; false = culled.
+// forward.cu:218-403 up to the colour: writes the zero defaults and rects; false = culled.
 template <bool ALT>
 __device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const Geom& g, int* radii, int t_idx,
                                                 int gx, int gy, float fx, float fy, PreGeom& o)
@@ -216,10 +218,8 @@ __device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const
     } else {
         for (int i = 0; i < 6; i++) c3[i] = a.cov3D_precomp[6 * t_idx + i];
     }
-    float2* c3o = reinterpret_cast<float2*>(g.cov3D + 6 * (size_t)t_idx);
-    c3o[0] = make_float2(c3[0], c3[1]);
-    c3o[1] = make_float2(c3[2], c3[3]);
-    c3o[2] = make_float2(c3[4], c3[5]);
+    // cov3D is not stored: k_gauss_bwd recomputes it bit-identically (cov3d_exact), 24 bytes per Gaussian saved
+    // on each side
     Cov2D k;
     cov2d_eval(p_orig, fx, fy, a.tanfovx, a.tanfovy, c3, view, k);
     float cx = k.cov.m[0][0], cy = k.cov.m[0][1], cz = k.cov.m[1][1];
