@@ -28,17 +28,21 @@ def per_kernel(path, counter):
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
-    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "bench_kernel_stats.csv"))
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):  # absent when called on the box before the trace run
+        shutil.copy(stats, os.path.join(dst, "bench_kernel_stats.csv"))
     dom = os.path.join(src, "trace", "run_domain_stats.csv")
     if os.path.exists(dom):
         shutil.copy(dom, os.path.join(dst, "bench_domain_stats.csv"))
     plain = os.path.join(src, "bench_plain.log")
     if os.path.exists(plain):  # absent when called on the box before the plain bench run
-        line = open(plain).read().strip().splitlines()[-1]
+        line = [l for l in open(plain).read().splitlines() if l.startswith("{")][-1]
         json.loads(line)
         open(os.path.join(dst, "bench_line.json"), "w").write(line + "\n")
-    traced = open(os.path.join(src, "bench_line.log")).read().strip().splitlines()[-1]
-    open(os.path.join(dst, "bench_line_under_rocprof.json"), "w").write(traced + "\n")
+    traced = os.path.join(src, "bench_line.log")
+    if os.path.exists(traced):
+        line = [l for l in open(traced).read().splitlines() if l.startswith("{")][-1]
+        open(os.path.join(dst, "bench_line_under_rocprof.json"), "w").write(line + "\n")
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     sqp = os.path.join(src, "sq", "run_counter_collection.csv")
