@@ -38,8 +38,10 @@ def direct_grad(t):
 class FlatGradExchange:
     """Pack -> all-reduce -> hand back, for a fixed list of parameter tensors.
 
-    The flat buffer is cut into buckets; each bucket's all-reduce is launched (async) as soon as its slice is
-    packed, so packing bucket k+1 overlaps the transfer of bucket k.  RCCL averages in the collective
+    When the rasterizer backward has written the gradients straight into the flat buffer (direct_grad), there is
+    nothing to pack and one collective covers the whole buffer.  Otherwise the buffer is cut into buckets; each
+    bucket's all-reduce is launched (async) as soon as its slice is packed, so packing bucket k+1 overlaps the
+    transfer of bucket k.  RCCL averages in the collective
     (ReduceOp.AVG), and afterwards every parameter's .grad is a view into the reduced buffer -- no unpack copy
     and no separate scaling pass.  64 MB buckets keep each ring well above its bandwidth knee on xGMI while
     leaving several buckets to pipeline for a 1M-Gaussian model (236 MB of fp32 gradients).
@@ -100,7 +102,14 @@ class FlatGradExchange:
         world = dist.get_world_size(self.group)
         native_avg = self.average and dist.get_backend(self.group) == "nccl" and _AVG_OK[0]
         works = []
-        for a, b in self.buckets:
+        # gradients the backward already wrote into the flat buffer need no packing, so there is nothing for the
+        # buckets to overlap with: one collective over the whole buffer saves the per-call startup of the others
+        base = self.flat.data_ptr()
+        in_place = all(p.grad is not None and p.grad.data_ptr() == base + 4 * off
+                       for p, off in zip(self.params, self.offsets))
+        spans = [(0, self.flat.numel())] if in_place else self.buckets
+        self.last_collectives = len(spans)
+        for a, b in spans:
             self._pack_range(a, b)
             if native_avg:
                 try:

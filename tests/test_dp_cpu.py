@@ -42,7 +42,9 @@ def _worker(rank, world, port, out_dir):
     params = [torch.zeros(g.shape, requires_grad=True) for g in grads]
     for p, g in zip(params, grads):
         p.grad = torch.tensor(g)
-    FlatGradExchange(params, bucket_bytes=4096).allreduce()
+    ex = FlatGradExchange(params, bucket_bytes=4096)
+    ex.allreduce()
+    assert ex.last_collectives > 1  # packed gradients: bucketed, pack and transfer pipelined
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), *[p.grad.numpy() for p in params])
     dist.destroy_process_group()
 
@@ -96,6 +98,7 @@ def _direct_worker(rank, world, port, out_dir):
         p.grad = None
     Render.apply(*params).backward()
     ex.allreduce()
+    assert ex.last_collectives == 1  # gradients already in the flat buffer: one collective over all of it
     ex.close()
     np.savez(os.path.join(out_dir, f"d{rank}.npz"), *[p.grad.numpy() for p in params],
              flags=np.array([aliased, doubled]))
