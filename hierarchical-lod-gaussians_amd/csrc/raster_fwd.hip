@@ -769,7 +769,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
     if (guard_fail(gd)) return;
     __shared__ float4 s_xy[64];   // x, y, 1/depth, alpha threshold on e2
     __shared__ float4 s_co[64];   // conic_q, opacity
-    __shared__ float4 s_col[64];  // r, g, b, 1/kids
+    __shared__ float4 s_col[64];  // r, g, b, 1/kids (hierarchy mode) or 1-based list position
     __shared__ float s_t[64];     // interpolation t
     const int L = xcd_remap(blockIdx.x, 4 * A.T);
     const int tile = L >> 2, q = L & 3;
@@ -798,7 +798,8 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             hit = touches_quad(r0.x, r0.y, co, fqx, fqy);
             s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, r3.w);
             s_co[lane] = conic_q(co);
-            s_col[lane] = make_float4(r1.z, r1.w, r2.x, INTERP ? r2.w : 0.f);
+            // .w: 1/kids in hierarchy mode, otherwise the splat's 1-based position in the tile list (n_contrib value)
+            s_col[lane] = make_float4(r1.z, r1.w, r2.x, INTERP ? r2.w : __uint_as_float(base - range.x + lane + 1));
             if (INTERP) s_t[lane] = r2.z;
         }
         uint64_t todo = __ballot(hit);
@@ -831,7 +832,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             C2 = fmaf(c.z, wgt, C2);
             if (DEPTH) D = fmaf(xy.z, wgt, D);
             Tt = bl ? test_T : Tt;
-            last = bl ? base - range.x + (uint32_t)j + 1 : last;
+            last = bl ? (INTERP ? base - range.x + (uint32_t)j + 1 : __float_as_uint(c.w)) : last;
             if (blended) seen_mask |= 1ull << j;
         }
         if (A.seen && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
