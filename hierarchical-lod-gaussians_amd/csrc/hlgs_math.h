@@ -184,7 +184,9 @@ struct SplatFoot {
     float x, y, a, b, c, kv, ku, t;  // kv = -b/c, ku = -b/a, t = threshold on Q
     int mode;                        // 0: test, 1: always (non-finite / degenerate), 2: never
 };
-__device__ __forceinline__ SplatFoot splat_foot(float x, float y, float4 co)
+// thr = the splat's alpha threshold on e2 (alpha_e2_threshold): alpha >= 1/255 needs e2 >= thr, i.e.
+// Q <= -2 ln2 thr = 2 ln(255 o) (or the lerped bound in hierarchy mode), so the log is already in hand.
+__device__ __forceinline__ SplatFoot splat_foot(float x, float y, float4 co, float thr)
 {
     SplatFoot f;
     f.x = x; f.y = y; f.a = co.x; f.b = co.y; f.c = co.z;
@@ -195,7 +197,7 @@ __device__ __forceinline__ SplatFoot splat_foot(float x, float y, float4 co)
     if (o < (1.0f / 255.0f) * 0.999f) { f.mode = 2; return f; }
     const float det = co.x * co.z - co.y * co.y;
     if (!(det > 0.f) || !(co.x > 0.f) || !(co.z > 0.f)) { f.mode = 1; return f; }
-    f.t = fmaxf(2.0f * logf(255.0f * o), 0.f) * 1.002f + 2e-3f;
+    f.t = fmaxf(-1.3862944f * thr, 0.f) * 1.002f + 2e-3f;
     f.kv = -co.y / co.z;
     f.ku = -co.y / co.x;
     return f;
@@ -219,9 +221,9 @@ __device__ __forceinline__ bool foot_touches(const SplatFoot& f, float qx, float
                           fminf(q_edge_v(f, v0, u0, u1), q_edge_v(f, v1, u0, u1)));
     return m <= f.t;
 }
-__device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, int x0, int y0)
+__device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, float thr, int x0, int y0)
 {
-    const SplatFoot f = splat_foot(x, y, co);
+    const SplatFoot f = splat_foot(x, y, co, thr);
     uint32_t m = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++)
@@ -314,9 +316,9 @@ __device__ __forceinline__ bool alt_tile_keep(float mx, float my, float4 co, flo
 }
 
 // Does the alpha >= 1/255 footprint of a splat (see quad_mask) reach the 8x8 pixel block at (qx, qy)?
-__device__ __forceinline__ bool touches_quad(float x, float y, float4 co, float qx, float qy)
+__device__ __forceinline__ bool touches_quad(float x, float y, float4 co, float thr, float qx, float qy)
 {
-    return foot_touches(splat_foot(x, y, co), qx, qy);
+    return foot_touches(splat_foot(x, y, co, thr), qx, qy);
 }
 
 // Copy n rows of M3 floats between global memory (row r at base + rows[r] * M3) and LDS (row r at

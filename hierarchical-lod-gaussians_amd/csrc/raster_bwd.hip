@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
             const float4* sr = g.splat + 4 * (size_t)id;
             const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            qm = quad_mask(r0.x, r0.y, co, tx0, ty0);
+            qm = quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
             s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
             s_q[lane] = conic_q(co);
             my_co = co;

@@ -795,7 +795,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             const float4* rec = A.splat + 4 * (size_t)my_id;
             const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            hit = touches_quad(r0.x, r0.y, co, fqx, fqy);
+            hit = touches_quad(r0.x, r0.y, co, r3.w, fqx, fqy);
             s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, r3.w);
             s_co[lane] = conic_q(co);
             // .w: 1/kids in hierarchy mode, otherwise the splat's 1-based position in the tile list (n_contrib value)

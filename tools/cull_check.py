@@ -21,7 +21,11 @@ power = -0.5*(a[:, None]*dx*dx + cc[:, None]*dy*dy) - b[:, None]*dx*dy
 alpha = np.minimum(0.99, o[:, None]*np.exp(power))
 truth = ((power <= 0) & (alpha >= 1/255)).any(1)
 # the float32 test
-t = (np.maximum(2*np.log(f32(255)*o), 0).astype(f32)*f32(1.002) + f32(2e-3))
+# the kernels take the bound from the splat's e2 threshold: the smallest float32 at or above -log2(255 o)
+thr_exact = -np.log2(255.0 * o.astype(np.float64))
+thr = thr_exact.astype(f32)
+thr = np.where(thr.astype(np.float64) < thr_exact, np.nextafter(thr, f32(np.inf)), thr).astype(f32)
+t = (np.maximum(f32(-1.3862944)*thr, f32(0)).astype(f32)*f32(1.002) + f32(2e-3)).astype(f32)
 kv = (-b/cc).astype(f32); ku = (-b/a).astype(f32)
 u0 = (0 - x).astype(f32); u1 = u0 + f32(7); v0 = (0 - y).astype(f32); v1 = v0 + f32(7)
 def qu(U):
