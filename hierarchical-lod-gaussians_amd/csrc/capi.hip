@@ -113,6 +113,7 @@ Img carve_img(void* base, int W, int H, size_t* total)
     im.tile_cursor = take<uint32_t>(p, T);
     im.misc = take<uint32_t>(p, 16);
     im.scan_tmp = take<uint32_t>(p, scan_scratch_elems(T));
+    im.split_state = take<float>(p, (size_t)T * kBwdSplits * kSplitFloats);
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return im;
 }
@@ -132,9 +133,7 @@ BwdScratch carve_bwd(void* base, int P, int R, size_t* total)
 {
     char* p = static_cast<char*>(base);
     BwdScratch r;
-    r.recA = take<float4>(p, R);
-    r.recB = take<float4>(p, R);
-    r.recC = take<float2>(p, R);
+    r.rec = take<float4>(p, 3 * (size_t)R);
     r.parent_dmean = take<float>(p, 3 * (size_t)P);
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return r;

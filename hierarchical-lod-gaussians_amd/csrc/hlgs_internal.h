@@ -16,6 +16,26 @@ constexpr int kBinThreads = 1024;   // LDS-histogram binning: threads per block
 constexpr int kBinGauss = 4096;     // Gaussians per binning block
 constexpr int kBinMaxTiles = 16384; // tile grids up to this use LDS histograms (2 x 64 KiB)
 
+// The blend backward splits each tile's list into up to kBwdSplits + 1 chunks of bwd_chunk_len(count) entries (a
+// multiple of the 64-splat batch, at least kBwdChunk) and runs one wave per (tile, chunk), so a launch holds ~3x
+// more, shorter waves than tiles.  A chunk that is not the tile's last starts from the per-pixel state the forward
+// sampled at the chunk's end (Img::split_state): the transmittance there, and the colour and inverse depth blended
+// behind it (final - sampled), which give the back-to-front recursion's accumulators without replaying the back part.
+#ifndef HLGS_BWD_CHUNK
+#define HLGS_BWD_CHUNK 128
+#endif
+#ifndef HLGS_BWD_SPLITS
+#define HLGS_BWD_SPLITS 2
+#endif
+constexpr int kBwdChunk = HLGS_BWD_CHUNK;
+constexpr int kBwdSplits = HLGS_BWD_SPLITS;
+constexpr int kSplitFloats = 4 * 5 * 64;  // per (tile, split): [quadrant][T, dC r, g, b, dD][lane]
+__host__ __device__ inline uint32_t bwd_chunk_len(uint32_t cnt)
+{
+    const uint32_t even = ((cnt + kBwdSplits) / (kBwdSplits + 1) + 63u) & ~63u;
+    return even > (uint32_t)kBwdChunk ? even : (uint32_t)kBwdChunk;
+}
+
 inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 size_t scan_scratch_elems(size_t n);
 
@@ -50,6 +70,7 @@ struct Img {
     uint32_t* tile_cursor; // T
     uint32_t* misc;        // 16: [0] = binned instances, [1] = longest per-tile list, [2] = record slots (point_offsets[P-1])
     uint32_t* scan_tmp;
+    float* split_state;    // T x kBwdSplits x kSplitFloats (see bwd_chunk_len)
 };
 Img carve_img(void* base, int W, int H, size_t* total);
 
@@ -61,12 +82,14 @@ struct Bin {
 };
 Bin carve_bin(void* base, int R, size_t* total);
 
-// Backward scratch: one gradient record per (tile, Gaussian) instance, stored Gaussian-major at the
-// Gaussian's point_offsets slot so the per-Gaussian reduction reads contiguous rows.
+// Backward scratch: one 48-byte gradient record per (tile, Gaussian) instance, stored Gaussian-major at the
+// Gaussian's point_offsets slot so the per-Gaussian reduction reads contiguous rows; one slot is three float4s
+// (one contiguous write per instance instead of three partial lines in three arrays):
+//   rec[3 s]     dmean2D.x, dmean2D.y, dconic.x, dconic.y
+//   rec[3 s + 1] dconic.w, dopacity, dcolor.r, dcolor.g
+//   rec[3 s + 2] dcolor.b, dinvdepth, -, -
 struct BwdScratch {
-    float4* recA;   // dmean2D.x, dmean2D.y, dconic.x, dconic.y
-    float4* recB;   // dconic.w, dopacity, dcolor.r, dcolor.g
-    float2* recC;   // dcolor.b, dinvdepth
+    float4* rec;
     float* parent_dmean;  // P x 3 (hierarchy mode only)
 };
 BwdScratch carve_bwd(void* base, int P, int R, size_t* total);

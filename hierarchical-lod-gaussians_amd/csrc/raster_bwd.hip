@@ -78,6 +78,50 @@ __device__ __forceinline__ uint64_t bwd_pair(PixB& p, uint32_t li, float dx, flo
     return valid;
 }
 
+// bwd_pair without the exec-masked branch: every lane runs the step and an invalid pair is neutralised by two
+// selects (alpha -> 0 makes 1/(1 - alpha) = 1, so T, ARD and the colour moments are unchanged; w -> 0 clears the
+// geometric moments).  Valid pairs run the very same operations as bwd_pair.  Two such steps on different
+// quadrants share one basic block, so their dependency chains (exp2 -> alpha -> rcp -> T -> moments) interleave.
+template <bool INTERP, bool DEPTH, bool ALT>
+__device__ __forceinline__ uint64_t bwd_pair_pred(PixB& p, uint32_t li, float dx, float dy, const float4& q,
+                                                  const float4& col, float invz, float tt, float fr, float thr,
+                                                  float (&acc)[10])
+{
+    const float e2 = splat_e2(q, dx, dy);
+    const uint64_t valid = __builtin_amdgcn_ballot_w64(li < p.last) & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) &
+                           ~__builtin_amdgcn_ballot_w64(e2 < thr);
+    const bool vb = __builtin_amdgcn_inverse_ballot_w64(valid);
+    const float G = __builtin_amdgcn_exp2f(e2);
+    const float test_alpha = q.w * G;
+    const float my_alpha = fminf(0.99f, test_alpha);
+    float alpha = my_alpha;
+    if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
+    alpha = vb ? alpha : 0.f;
+    const float r1m = __builtin_amdgcn_rcpf(1.f - alpha);
+    p.T = p.T * r1m;
+    const float weight = alpha * p.T;
+    float cd = col.x * p.dr + col.y * p.dg + col.z * p.db;
+    if (DEPTH) cd += invz * p.dinv;
+    const float raw = cd - p.ARD;
+    p.ARD = fmaf(alpha, raw, p.ARD);
+    acc[6] += weight * p.dr;
+    acc[7] += weight * p.dg;
+    acc[8] += weight * p.db;
+    if (DEPTH) acc[9] += weight * p.dinv;
+    float dL_dalpha = raw * p.T - p.TB * r1m;
+    if (!ALT) dL_dalpha = test_alpha > 0.99f ? 0.f : dL_dalpha;
+    const float w = vb ? G * dL_dalpha : 0.f;
+    const float wdx = w * dx, wdy = w * dy;
+    acc[0] += wdx;
+    acc[1] += wdy;
+    acc[2] = fmaf(wdx, dx, acc[2]);
+    acc[3] = fmaf(wdx, dy, acc[3]);
+    acc[4] = fmaf(wdy, dy, acc[4]);
+    if (INTERP) acc[5] += (tt - powf(1.0f - my_alpha, fr - 1.0f) * (tt - 1.0f) * fr) * w;
+    else acc[5] += w;
+    return valid;
+}
+
 // Per-splat record from the reduced moments (see bwd_pair); co = conic and opacity of the splat.
 __device__ __forceinline__ void finish_record(const float* m, float4 co, float ddelx_dx, float ddely_dy, float4& ra,
                                               float4& rb, float2& rc)
@@ -102,20 +146,35 @@ struct BwdArgs {
     Geom g;
     const float* final_Ts;
     const uint32_t* n_contrib;
+    const float* split_state;
     const float* bg;
     const float* dL_dpixels;
     const float* dL_dinvdepths;
     BwdScratch rec;
 };
 
-// One wave per tile, back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant.  Each 64-splat
-// batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel whose
-// n_contrib lies behind it) run bwd_pair, the ten moments are folded over the wave, and one record per
+// One wave per (tile, chunk of the tile's list), back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8
+// quadrant.  Chunk c covers list entries [c clen, min(count, (c + 1) clen)) (bwd_chunk_len); blocks are ordered
+// chunk-major, so the front chunks, where most pixels are still live, start first.  A pixel whose last contributor
+// lies behind the chunk's end starts from the forward's sample there (transmittance, and what was blended behind
+// it), otherwise from its final state, as the reference's single back-to-front pass has it at that point.  Each
+// 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
+// whose n_contrib lies behind it) run bwd_pair, the ten moments are folded over the wave, and one record per
 // (tile, splat) is stored after the batch.
+#ifndef HLGS_BWD_PAIRS
+#define HLGS_BWD_PAIRS 0  // 1: interleave two quadrants' steps (bwd_pair_pred); measured slower (496 vs 423 us)
+#endif
+#ifndef HLGS_BWD_PREFETCH
+#define HLGS_BWD_PREFETCH (!HLGS_BWD_PAIRS)  // next splat's LDS reads ahead of this one's reduction
+#endif
+#ifndef HLGS_BWD_WAVES
+#define HLGS_BWD_WAVES 5  // waves per SIMD: 96 VGPRs
+#endif
 template <bool INTERP, bool DEPTH, bool ALT>
-__global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
+__global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
 {
-    const int tile = xcd_remap(blockIdx.x, A.T);
+    const int part = blockIdx.x / A.T;
+    const int tile = xcd_remap(blockIdx.x - part * A.T, A.T);
     const uint2* __restrict__ ranges = A.ranges;
     const uint32_t* __restrict__ point_list = A.point_list;
     const int W = A.W, H = A.H, gx = A.gx;
@@ -135,8 +194,13 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
     const int tx = tile % gx, ty = tile / gx;
     const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
     const uint2 range = ranges[tile];
-    const uint32_t cnt = range.y - range.x;
-    if (cnt == 0) return;
+    const uint32_t count = range.y - range.x;
+    const uint32_t clen = bwd_chunk_len(count);
+    const uint32_t c0 = (uint32_t)part * clen;  // chunk = local list positions [c0, cnt)
+    if (c0 >= count) return;
+    const uint32_t cnt = min(count, c0 + clen);
+    const float* __restrict__ st =
+        cnt < count ? A.split_state + (size_t)(tile * kBwdSplits + part) * kSplitFloats + lane : nullptr;
     const size_t HW = (size_t)H * W;
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
     const float lx = (float)(tx0 + (lane & 7)), ly = (float)(ty0 + (lane >> 3));
@@ -157,6 +221,14 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
         p.dr = inside ? dL_dpixels[pid] : 0.f;
         p.dg = inside ? dL_dpixels[HW + pid] : 0.f;
         p.db = inside ? dL_dpixels[2 * HW + pid] : 0.f;
+        p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
+        if (p.last > cnt) {  // still blending at the chunk's end (so the forward sampled it there, with T >= 1e-4)
+            const float* sk = st + k * 5 * 64;
+            p.T = sk[0];
+            float behind = sk[64] * p.dr + sk[128] * p.dg + sk[192] * p.db;
+            if (DEPTH) behind += sk[256] * p.dinv;
+            p.ARD = behind / p.T;  // <accum_rec, dL/dpixel> (+ depth) at the chunk's end
+        }
         float bgd = 0.f;
         bgd += bg[0] * p.dr;
         bgd += bg[1] * p.dg;
@@ -164,16 +236,15 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
         // the alt rasterizer's ar includes the final colour's T_final * bg and adds the bg term once more
         // (alt-rasterizer backward.cu:608, 619): the background enters dL/dalpha twice
         p.TB = ALT ? 2.f * (tf * bgd) : tf * bgd;
-        p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
-        uint32_t m = p.last;
+        uint32_t m = min(p.last, cnt);
         for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
         qlast[k] = __builtin_amdgcn_readfirstlane(m);
     }
     const uint32_t maxlast = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
 
-    for (uint32_t b0 = 0; b0 < cnt; b0 += 64) {
+    for (uint32_t b0 = 0; b0 < cnt - c0; b0 += 64) {
         // batch covers local positions cnt-1-b0 down to cnt-1-b0-(n-1), loaded back to front
-        const int n = (int)min(64u, cnt - b0);
+        const int n = (int)min(64u, cnt - c0 - b0);
         const uint32_t li_top = cnt - 1 - b0;
         const bool lane_valid = lane < n;
         uint32_t slot = 0, qm = 0;
@@ -217,9 +288,16 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
             // the next visited splat's LDS reads are issued after this splat's pixel steps and before its
             // reduction, which covers their latency (the splat data is dead by then, so no extra registers)
             int j = todo ? __builtin_ctzll(todo) : 0;
+#if HLGS_BWD_PREFETCH
             float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
             float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
+#endif
             while (todo) {
+#if !HLGS_BWD_PREFETCH
+                j = __builtin_ctzll(todo);
+                const float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
+                const float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
+#endif
                 todo &= todo - 1;
                 const uint32_t li = li_top - (uint32_t)j;
                 const uint32_t qm = (uint32_t)((qv[0] >> j) & 1u) | ((uint32_t)((qv[1] >> j) & 1u) << 1) |
@@ -233,12 +311,48 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
                     acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
                 }
                 uint64_t any = 0;  // lanes with a valid pair (wave mask)
+#if HLGS_BWD_PAIRS
+                // quadrants taken two at a time (predicated steps in one block: interleaved chains), a lone one
+                // with the exec-masked step; qm is wave-uniform
+#define HLGS_P1(k)                                                                                                \
+    any |= bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * ((k) & 1)), xy.y - (ly + 8.f * ((k) >> 1)), co, \
+                                        col, xy.z, tf.x, tf.y, col.w, acc)
+#define HLGS_PP(k)                                                                                                \
+    any |= bwd_pair_pred<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * ((k) & 1)),                           \
+                                             xy.y - (ly + 8.f * ((k) >> 1)), co, col, xy.z, tf.x, tf.y, col.w, acc)
+                switch (qm) {
+                case 1: HLGS_P1(0); break;
+                case 2: HLGS_P1(1); break;
+                case 4: HLGS_P1(2); break;
+                case 8: HLGS_P1(3); break;
+                case 3: HLGS_PP(0); HLGS_PP(1); break;
+                case 5: HLGS_PP(0); HLGS_PP(2); break;
+                case 6: HLGS_PP(1); HLGS_PP(2); break;
+                case 9: HLGS_PP(0); HLGS_PP(3); break;
+                case 10: HLGS_PP(1); HLGS_PP(3); break;
+                case 12: HLGS_PP(2); HLGS_PP(3); break;
+                case 7: HLGS_PP(0); HLGS_PP(1); HLGS_P1(2); break;
+                case 11: HLGS_PP(0); HLGS_PP(1); HLGS_P1(3); break;
+                case 13: HLGS_PP(0); HLGS_PP(2); HLGS_P1(3); break;
+                case 14: HLGS_PP(1); HLGS_PP(2); HLGS_P1(3); break;
+                case 15:  // two pairs; the barrier keeps the scheduler from overlapping all four chains (registers)
+                    HLGS_PP(0); HLGS_PP(1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    HLGS_PP(2); HLGS_PP(3);
+                    break;
+                default: break;
+                }
+#undef HLGS_P1
+#undef HLGS_PP
+#else
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     if ((qm >> k) & 1u)  // uniform branch
                         any |= bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), co, col,
                                                        xy.z, tf.x, tf.y, col.w, acc);
+#endif
                 const int jc = j;
+#if HLGS_BWD_PREFETCH
                 if (todo) {
                     j = __builtin_ctzll(todo);
                     xy = s_xy[j];
@@ -246,6 +360,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
                     col = s_col[j];
                     if (INTERP) tf = s_tf[j];
                 }
+#endif
                 if (any) {
                     float r0, r1, r2;
                     wave_reduce10(acc, r0, r1, r2);
@@ -266,9 +381,10 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
             float4 ra, rb;
             float2 rc;
             finish_record(m, my_co, ddelx_dx, ddely_dy, ra, rb, rc);
-            rec.recA[slot] = ra;
-            rec.recB[slot] = rb;
-            rec.recC[slot] = rc;
+            float4* r = rec.rec + 3 * (size_t)slot;
+            r[0] = ra;
+            r[1] = rb;
+            r[2] = make_float4(rc.x, rc.y, 0.f, 0.f);
         }
         __syncthreads();
     }
@@ -353,9 +469,9 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
                     const int k = (int)(r - ws);
                     if (!alt_tile_keep(kx, ky, kco, kthr, kx0 + k % kw, ky0 + k / kw)) continue;
                 }
-                const float4 A = rec.recA[r];
-                const float4 B = rec.recB[r];
-                const float2 Cc = rec.recC[r];
+                const float4 A = rec.rec[3 * (size_t)r];
+                const float4 B = rec.rec[3 * (size_t)r + 1];
+                const float4 Cc = rec.rec[3 * (size_t)r + 2];
                 p[0] += A.x; p[1] += A.y; p[2] += A.z; p[3] += A.w;
                 p[4] += B.x; p[5] += B.y; p[6] += B.z; p[7] += B.w;
                 p[8] += Cc.x; p[9] += Cc.y;
@@ -417,8 +533,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     const f3 mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     // records four at a time: all loads of a group are in flight together, the sums stay in slot order
     for (uint32_t r0 = start; r0 < end; r0 += 4) {
-        float4 A[4], B[4];
-        float2 Cc[4];
+        float4 A[4], B[4], Cc[4];
         bool use[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -429,9 +544,9 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
                 use[k] = alt_tile_keep(kx, ky, kco, kthr, kx0 + kk % kw, ky0 + kk / kw);
             }
             if (use[k]) {
-                A[k] = rec.recA[r];
-                B[k] = rec.recB[r];
-                Cc[k] = rec.recC[r];
+                A[k] = rec.rec[3 * (size_t)r];
+                B[k] = rec.rec[3 * (size_t)r + 1];
+                Cc[k] = rec.rec[3 * (size_t)r + 2];
             }
         }
 #pragma unroll
@@ -735,8 +850,9 @@ void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
 {
     const int T = gx * gy;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
-    BwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, im.final_T, im.n_contrib, a.bg, dL_dpix, dL_dinv, rs};
-#define HLGS_BB(I, Dp, Al) hipLaunchKernelGGL((k_blend_bwd<I, Dp, Al>), dim3(T), dim3(64), 0, s, A)
+    BwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, im.final_T, im.n_contrib, im.split_state, a.bg, dL_dpix,
+              dL_dinv, rs};
+#define HLGS_BB(I, Dp, Al) hipLaunchKernelGGL((k_blend_bwd<I, Dp, Al>), dim3((kBwdSplits + 1) * T), dim3(64), 0, s, A)
     if (a.variant == HLGS_VARIANT_ALT) { if (dL_dinv) HLGS_BB(false, true, true); else HLGS_BB(false, false, true); }
     else if (interp) { if (dL_dinv) HLGS_BB(true, true, false); else HLGS_BB(true, false, false); }
     else { if (dL_dinv) HLGS_BB(false, true, false); else HLGS_BB(false, false, false); }

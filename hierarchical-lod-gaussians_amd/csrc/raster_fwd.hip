@@ -754,6 +754,7 @@ struct FwdArgs {
     float* out_color;
     float* out_invdepth;
     int* seen;
+    float* split_state;  // Img::split_state (null: not sampled)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -763,7 +764,7 @@ struct FwdArgs {
 // set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
 // visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
 // ------------------------------------------------------------------------------------------------
-template <bool INTERP, bool DEPTH>
+template <bool INTERP, bool DEPTH, bool SEEN>  // SEEN: A.seen is set (the per-splat mask is only kept then)
 __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 {
     if (guard_fail(gd)) return;
@@ -782,11 +783,25 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     uint32_t last = 0;
+    // Backward chunk boundaries (bwd_chunk_len): at each, the transmittance is stored at once and the colour /
+    // inverse depth blended so far is kept, so that the end can store what was blended behind the boundary.
+    const uint32_t clen = bwd_chunk_len(range.y - range.x);
+    float* st = A.split_state ? A.split_state + (size_t)tile * kBwdSplits * kSplitFloats + q * 5 * 64 + lane : nullptr;
+    uint32_t next_split = range.x + clen, nsplit = 0;
+    float S0[kBwdSplits][4];
     // per-lane predicates are kept as wave masks (the wave is always full): compares are ballots of one v_cmp
     // each, their combinations scalar mask operations, and selects read them back with inverse_ballot
     uint64_t done = __builtin_amdgcn_ballot_w64(!(px < A.W && py < A.H));
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if (done == ~0ull) break;
+        if (base == next_split && st) {  // wave-uniform; never past kBwdSplits boundaries (bwd_chunk_len)
+            st[nsplit * kSplitFloats] = Tt;
+#pragma unroll
+            for (int k = 0; k < kBwdSplits; k++)
+                if (k == (int)nsplit) { S0[k][0] = C0; S0[k][1] = C1; S0[k][2] = C2; S0[k][3] = D; }
+            nsplit++;
+            next_split += clen;
+        }
         const uint32_t pos = base + lane;
         uint32_t my_id = 0;
         bool hit = false;
@@ -833,9 +848,9 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             if (DEPTH) D = fmaf(xy.z, wgt, D);
             Tt = bl ? test_T : Tt;
             last = bl ? (INTERP ? base - range.x + (uint32_t)j + 1 : __float_as_uint(c.w)) : last;
-            if (blended) seen_mask |= 1ull << j;
+            if (SEEN && blended) seen_mask |= 1ull << j;
         }
-        if (A.seen && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
+        if (SEEN && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
         __syncthreads();
     }
     if (px < A.W && py < A.H) {
@@ -848,6 +863,15 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
         A.out_color[2 * HW + pid] = C2 + Tt * A.bg[2];
         if (DEPTH) A.out_invdepth[pid] = D;
     }
+#pragma unroll
+    for (int k = 0; k < kBwdSplits; k++)
+        if (k < (int)nsplit) {
+            float* sk = st + k * kSplitFloats;
+            sk[64] = C0 - S0[k][0];
+            sk[128] = C1 - S0[k][1];
+            sk[192] = C2 - S0[k][2];
+            if (DEPTH) sk[256] = D - S0[k][3];
+        }
 }
 
 // rasterizer_impl.cu:54-66 with auxiliary.h:164-189 (prefiltered = false)
@@ -1002,8 +1026,12 @@ void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     const bool depth = out_invdepth != nullptr;
     FwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, T, g.splat, im.final_T, im.n_contrib, a.bg, out_color,
-              out_invdepth, seen};
-#define HLGS_BLEND(I, Dp) hipLaunchKernelGGL((k_blend_fwd<I, Dp>), dim3(4 * T), dim3(64), 0, s, A, gd)
+              out_invdepth, seen, im.split_state};
+#define HLGS_BLEND(I, Dp)                                                                                         \
+    do {                                                                                                          \
+        if (seen) hipLaunchKernelGGL((k_blend_fwd<I, Dp, true>), dim3(4 * T), dim3(64), 0, s, A, gd);           \
+        else hipLaunchKernelGGL((k_blend_fwd<I, Dp, false>), dim3(4 * T), dim3(64), 0, s, A, gd);               \
+    } while (0)
     if (interp) { if (depth) HLGS_BLEND(true, true); else HLGS_BLEND(true, false); }
     else { if (depth) HLGS_BLEND(false, true); else HLGS_BLEND(false, false); }
 #undef HLGS_BLEND

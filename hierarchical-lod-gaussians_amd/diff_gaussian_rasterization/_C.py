@@ -71,9 +71,10 @@ _binning_hint = {}
 
 def rasterize_gaussians(bg, render_indices, parent_indices, ts, kids, means3D, colors, opacity, scales, rotations,
                         scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
-                        image_width, sh, degree, campos, prefiltered, debug, do_depth):
+                        image_width, sh, degree, campos, prefiltered, debug, do_depth, *, need_seen=True):
     """-> (num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, invdepth, seen)
-    (rasterize_points.cu:36-139)."""
+    (rasterize_points.cu:36-139).  need_seen=False (used by the autograd wrapper, which drops it) returns an empty
+    `seen` and skips its per-splat stores."""
     lib = L.load()
     H, W = int(image_height), int(image_width)
     a, keep, P, _, _ = _raster_args(bg, render_indices, parent_indices, ts, kids, means3D, colors, opacity, scales,
@@ -84,7 +85,7 @@ def rasterize_gaussians(bg, render_indices, parent_indices, ts, kids, means3D, c
     color = torch.empty((3, H, W), **f32)
     invdepth = torch.empty((1 if do_depth else 0, H, W), **f32)
     radii = torch.empty((P,), dtype=torch.int32, device=dev)
-    seen = torch.empty((P,), dtype=torch.int32, device=dev)
+    seen = torch.empty((P if need_seen else 0,), dtype=torch.int32, device=dev)
     u8 = dict(dtype=torch.uint8, device=dev)
     geom = torch.empty((lib.hlgs_geom_buffer_size(P),), **u8)
     img = torch.empty((lib.hlgs_image_buffer_size(W, H),), **u8)
@@ -95,13 +96,14 @@ def rasterize_gaussians(bg, render_indices, parent_indices, ts, kids, means3D, c
     s = L.stream()
     L.check(lib.hlgs_rasterize_forward(C.byref(a), L.ptr(geom), L.ptr(img), L.ptr(radii), L.ptr(binning),
                                        binning.numel(), C.byref(info), L.ptr(color),
-                                       L.ptr(invdepth) if do_depth else None, L.ptr(seen), s))
+                                       L.ptr(invdepth) if do_depth else None, L.ptr(seen) if need_seen else None,
+                                       s))
     if not info.rendered:
         need = lib.hlgs_binning_buffer_size(info.num_binned)
         binning = torch.empty((need,), **u8)
         L.check(lib.hlgs_rasterize_forward_render(C.byref(a), L.ptr(radii), L.ptr(geom), L.ptr(img), L.ptr(binning),
                                                   C.byref(info), L.ptr(color), L.ptr(invdepth) if do_depth else None,
-                                                  L.ptr(seen), s))
+                                                  L.ptr(seen) if need_seen else None, s))
         _binning_hint[dev] = int(need * 1.15)
     del keep
     return int(info.num_rendered), color, radii, geom, binning, img, invdepth, seen
@@ -186,5 +188,7 @@ def inspect_ranges(imageBuffer, W, H):
 
 def inspect_splats(geomBuffer, P):
     """(P, 16) float32 per-Gaussian blend records held in a forward's geometry buffer:
-    x, y, conic a, b, conic c, opacity, r, g, b, 1/depth, t, 1/kids, record base, tile x0, y0, width."""
+    [0:4] x, y, conic a, b | [4:8] conic c, opacity, r, g | [8:12] b, 1/depth, t, 1/kids |
+    [12:16] record base (uint32 bits), x0 | y0 << 16 (int bits), rect width (int bits), alpha threshold on e2
+    (csrc/hlgs_internal.h, Geom::splat)."""
     return _field(geomBuffer, L.load().hlgs_geom_splat_offset(int(P)), 16 * int(P), torch.float32).view(int(P), 16)

@@ -48,7 +48,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         out = _C.rasterize_gaussians(rs.bg, *_hierarchy(rs), means3D, colors_precomp, opacities, scales, rotations,
                                      rs.scale_modifier, cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx,
                                      rs.tanfovy, rs.image_height, rs.image_width, sh, rs.sh_degree, rs.campos,
-                                     rs.prefiltered, rs.debug, rs.do_depth)
+                                     rs.prefiltered, rs.debug, rs.do_depth, need_seen=False)
+        # `seen` is not part of the public return (color, radii, invdepth): the reference's wrapper never hands it on
+        # (and cannot unpack it), so this path skips computing it
         num_rendered, color, radii, geom_buf, binning_buf, img_buf, invdepth, _seen = out
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered

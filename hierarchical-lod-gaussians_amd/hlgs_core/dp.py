@@ -6,6 +6,8 @@ CPU).  Gradients are packed into one flat fp32 buffer so RCCL moves a few large 
 one per parameter tensor, then averaged (the reference trains one view per step; G views per step is
 an effective batch of G).
 """
+import weakref
+
 import torch
 import torch.distributed as dist
 
@@ -13,9 +15,18 @@ import torch.distributed as dist
 _AVG_OK = [True]  # ReduceOp.AVG accepted by the backend (flips once if it is not)
 
 # Parameters whose gradient the rasterizer backward may write straight into an exchange's flat buffer:
-# data_ptr -> (parameter, flat buffer, offset).  The view is made per call: autograd adopts a returned gradient
-# only while nothing else holds a reference to that tensor.
+# data_ptr -> (weakref to the parameter, weakref to its exchange, index in the exchange).  Weak references, so a
+# parameter replaced by densification or by the SPT cache (new tensors every step) does not keep its old storage or
+# the exchange's flat buffer alive; an exchange that is garbage-collected drops its own entries.  The view is made
+# per call: autograd adopts a returned gradient only while nothing else holds a reference to that tensor.
 _DIRECT = {}
+
+
+def _drop_entries(keys, token):
+    for k in keys:
+        e = _DIRECT.get(k)
+        if e is not None and e[3] == token:
+            del _DIRECT[k]
 
 
 def direct_grad(t):
@@ -25,14 +36,23 @@ def direct_grad(t):
     parameter registered by a FlatGradExchange(direct=True) and its .grad is unset, the backward writes the
     gradient into the exchange's flat buffer, autograd adopts that tensor as .grad (it steals a fresh leaf
     gradient instead of copying it), and the all-reduce finds it already packed.  With .grad set (accumulation)
-    a fresh tensor is returned as usual, so an in-place `.grad +=` never aliases its own input."""
+    a fresh tensor is returned as usual, so an in-place `.grad +=` never aliases its own input.
+
+    The view is handed out at most once per exchange round (until allreduce() / unpack() / release()): two
+    rasterizer backwards of one autograd pass both see .grad unset, because AccumulateGrad runs only after both
+    finish; the second one gets None, so autograd sums two distinct tensors instead of the buffer with itself."""
     e = _DIRECT.get(t.data_ptr()) if t is not None and t.numel() else None
     if e is None:
         return None
-    p, flat, off = e
-    if p.grad is not None or p.shape != t.shape or p.dtype != t.dtype or flat.device != t.device:
+    p, ex = e[0](), e[1]()
+    if p is None or ex is None:
+        _DIRECT.pop(t.data_ptr(), None)
         return None
-    return flat[off:off + p.numel()].view_as(p)
+    i = e[2]
+    if ex.claimed[i] or p.grad is not None or p.shape != t.shape or p.dtype != t.dtype or ex.flat.device != t.device:
+        return None
+    ex.claimed[i] = True
+    return ex.flat[ex.offsets[i]:ex.offsets[i] + ex.numels[i]].view_as(p)
 
 
 class FlatGradExchange:
@@ -63,17 +83,25 @@ class FlatGradExchange:
         per = max(1, bucket_bytes // 4)
         self.buckets = [(s, min(s + per, total)) for s in range(0, total, per)]
         self.direct = []
+        self.claimed = [False] * len(self.params)
+        self._token = object()
         if direct:
-            for p, off, n in zip(self.params, self.offsets, self.numels):
+            me = weakref.ref(self)
+            for i, p in enumerate(self.params):
                 if p.is_contiguous() and p.dtype == torch.float32:
-                    _DIRECT[p.data_ptr()] = (p, self.flat, off)
+                    _DIRECT[p.data_ptr()] = (weakref.ref(p), me, i, self._token)
                     self.direct.append(p.data_ptr())
+        self._finalizer = weakref.finalize(self, _drop_entries, list(self.direct), self._token)
 
     def close(self):
-        """Stop offering the flat buffer to the rasterizer backward."""
-        for k in self.direct:
-            _DIRECT.pop(k, None)
+        """Stop offering the flat buffer to the rasterizer backward.  Rebuild the exchange (and close the old one)
+        whenever the parameter tensors are replaced: entries are keyed by storage address."""
+        self._finalizer()
         self.direct = []
+
+    def release(self):
+        """End the exchange round without a collective: the flat buffer may be handed out again."""
+        self.claimed = [False] * len(self.params)
 
     def _pack_range(self, a, b):
         for p, off, n in zip(self.params, self.offsets, self.numels):
@@ -94,10 +122,12 @@ class FlatGradExchange:
     def unpack(self):
         for p, off, n in zip(self.params, self.offsets, self.numels):
             p.grad = self.flat[off:off + n].view_as(p)
+        self.release()
 
     def allreduce(self):
         """All-reduce every parameter's .grad across the process group (mean if average, else sum)."""
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            self.release()
             return
         world = dist.get_world_size(self.group)
         native_avg = self.average and dist.get_backend(self.group) == "nccl" and _AVG_OK[0]

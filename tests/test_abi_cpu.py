@@ -75,7 +75,9 @@ def test_settings_fields_match_reference_order():
 def test_public_signatures_match_reference():
     import diff_gaussian_rasterization as D
     import gaussian_hierarchy as G
-    sig = lambda f: list(inspect.signature(f).parameters)  # noqa: E731
+    # positional parameters (keyword-only extensions such as _C.rasterize_gaussians(..., need_seen=) are ours)
+    sig = lambda f: [k for k, v in inspect.signature(f).parameters.items()  # noqa: E731
+                     if v.kind != inspect.Parameter.KEYWORD_ONLY]
     assert sig(D.GaussianRasterizer.forward) == ["self", "means3D", "means2D", "opacities", "shs", "colors_precomp",
                                                   "scales", "rotations", "cov3D_precomp"]
     assert sig(D.rasterize_gaussians) == ["means3D", "means2D", "sh", "colors_precomp", "opacities", "scales",

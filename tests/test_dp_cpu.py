@@ -74,8 +74,8 @@ def _direct_worker(rank, world, port, out_dir):
 
     class Render(torch.autograd.Function):  # stands in for _RasterizeGaussians: grads land where direct_grad says
         @staticmethod
-        def forward(ctx, *ps):
-            ctx.ps = ps
+        def forward(ctx, scale, *ps):
+            ctx.ps, ctx.scale = ps, scale
             return sum((p * 0).sum() for p in ps)
 
         @staticmethod
@@ -84,24 +84,32 @@ def _direct_worker(rank, world, port, out_dir):
             for p, g in zip(ctx.ps, grads):
                 d = direct_grad(p)
                 d = torch.empty_like(g) if d is None else d
-                d.copy_(g)
+                d.copy_(g * ctx.scale)
                 outs.append(d)
-            return tuple(outs)
+            return (None,) + tuple(outs)
 
     ex = FlatGradExchange(params, bucket_bytes=4096)
-    Render.apply(*params).backward()
+    Render.apply(1.0, *params).backward()
     lo, hi = ex.flat.data_ptr(), ex.flat.data_ptr() + 4 * ex.flat.numel()
     aliased = all(lo <= p.grad.data_ptr() < hi for p in params)
-    Render.apply(*params).backward()  # .grad set: accumulate, 2 x local gradient
+    Render.apply(1.0, *params).backward()  # .grad set: accumulate, 2 x local gradient
     doubled = all(torch.equal(p.grad, 2 * g) for p, g in zip(params, grads))
+    ex.allreduce()  # ends the round: the flat buffer may be handed out again
     for p in params:
         p.grad = None
-    Render.apply(*params).backward()
+    # two renders of the same parameters in one autograd pass: both backwards run before AccumulateGrad, so the
+    # buffer must be handed out once only (else the engine sums the buffer with itself)
+    (Render.apply(1.0, *params) + Render.apply(2.0, *params)).backward()
+    twice = all(torch.equal(p.grad, 3 * g) for p, g in zip(params, grads))
+    ex.allreduce()
+    for p in params:
+        p.grad = None
+    Render.apply(1.0, *params).backward()
     ex.allreduce()
     assert ex.last_collectives == 1  # gradients already in the flat buffer: one collective over all of it
     ex.close()
     np.savez(os.path.join(out_dir, f"d{rank}.npz"), *[p.grad.numpy() for p in params],
-             flags=np.array([aliased, doubled]))
+             flags=np.array([aliased, doubled, twice]))
     dist.destroy_process_group()
 
 

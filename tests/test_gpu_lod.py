@@ -7,7 +7,7 @@ import torch
 
 from hlgs_core import synthetic as S
 from oracle import oracle as O
-from helpers import gpu_render, oracle_render, rel_err, settings_for, image_check
+from helpers import assert_grad, gpu_render, oracle_render, rel_err, settings_for, image_check
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -220,8 +220,7 @@ def test_in_kernel_hierarchy_mode_matches_oracle():
     assert ok, (mx, nbad)
     ((color * t(g)).sum() + (invd * t(gd)).sum()).backward()
     for name, leaf_t in (("dmean3D", m), ("dopacity", o), ("dscale", s), ("drot", r), ("dsh", sh), ("dmean2D", m2)):
-        e = rel_err(leaf_t.grad.cpu().numpy(), gr[name])
-        assert e <= 1e-3, (name, e)
+        assert_grad(name, leaf_t.grad.cpu().numpy(), gr[name])
 
 
 def test_morton_codes_bit_exact():

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from hlgs_core import synthetic as S
-from helpers import gpu_render, image_check, oracle_render, rel_err
+from helpers import assert_grad, gpu_render, image_check, oracle_render, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -37,12 +37,13 @@ def _compare(sc, cam, do_depth=True, use_colors=False, use_cov=False, grads=True
     if grads:
         for k in ref:
             if k.startswith("d"):
-                e = rel_err(gpu[k][..., :ref[k].shape[-1]], ref[k])
-                assert e <= GRAD_TOL, f"{k}: rel err {e}"
+                assert_grad(k, gpu[k][..., :ref[k].shape[-1]], ref[k])
     return gpu, ref
 
 
-@pytest.mark.parametrize("P,deg,W,H", [(300, 0, 64, 64), (2000, 3, 128, 96), (1500, 1, 100, 75), (4000, 2, 256, 256)])
+# (10000, 0, 256, 256) is BASELINE configs[0] (10k Gaussians, SH degree 0, one 256x256 camera) on the GPU path
+@pytest.mark.parametrize("P,deg,W,H", [(300, 0, 64, 64), (2000, 3, 128, 96), (1500, 1, 100, 75), (4000, 2, 256, 256),
+                                       (10000, 0, 256, 256)])
 def test_forward_backward_parity(P, deg, W, H):
     sc, cam = _scene(P, deg, W, H, seed=P)
     _compare(sc, cam)
@@ -182,3 +183,28 @@ def test_wide_splats_balanced_binning():
     sc["scales"][:6] *= 40.0
     sc["opacities"][:6] = np.float32(0.3)
     _compare(sc, cam)
+
+
+def _transparent_dense(P, deg, W, H, seed, opacity=(0.01, 0.08)):
+    """Many faint splats over a small image: tile lists of several hundred entries with every pixel still live
+    hundreds of splats deep, so the backward's chunks (bwd_chunk_len) start from the forward's sampled state."""
+    sc, cam = _scene(P, deg, W, H, seed=seed)
+    rng = np.random.default_rng(seed)
+    sc["opacities"] = rng.uniform(opacity[0], opacity[1], (P, 1)).astype(np.float32)
+    return sc, cam
+
+
+@pytest.mark.parametrize("P,deg,W,H,depth,op", [(6000, 3, 96, 64, True, (0.01, 0.08)), (9000, 1, 80, 80, False, (0.01, 0.08)),
+                                                (3000, 0, 48, 32, True, (0.01, 0.08)), (8000, 2, 64, 64, True, (0.2, 0.9))])
+def test_backward_chunks_from_sampled_state(P, deg, W, H, depth, op):
+    """Chunked backward (one wave per (tile, chunk)) against the oracle's single back-to-front pass; the last case
+    has pixels that stop (T < 1e-4) inside a chunk."""
+    sc, cam = _transparent_dense(P, deg, W, H, seed=P, opacity=op)
+    gpu, ref = _compare(sc, cam, do_depth=depth)
+    # the frame really has multi-chunk tiles whose pixels are live at the chunk boundaries
+    counts = np.diff(ref["frame"].ranges.astype(np.int64), axis=1).ravel()
+    assert counts.max() > 2 * 128, counts.max()
+    nc = ref["frame"].n_contrib
+    assert nc.max() > 256, nc.max()
+    if op[1] > 0.5:  # pixels stop (T would drop below 1e-4) inside the middle chunk
+        assert 448 < np.median(nc) < 896 and nc.max() < counts.max()
