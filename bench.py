@@ -8,8 +8,20 @@ SH degree 3 (BASELINE.json configs[1]), one training view per GPU.
 
 A step = one view rendered through the public GaussianRasterizer API (forward, including its
 num_rendered host sync), full backward of fixed synthetic upstream gradients dL/dcolor and dL/dinvdepth
-(fed to autograd directly: the gradient of loss = <dL/dcolor, color> + <dL/dinvdepth, invdepth>), and -- for N > 1 -- the RCCL all-reduce of every Gaussian gradient
-(view-data parallel, weak scaling: each rank renders its own view of its own 1M-Gaussian replica).
+(fed to autograd directly: the gradient of loss = <dL/dcolor, color> + <dL/dinvdepth, invdepth>), and -- for N > 1 --
+the RCCL all-reduce of every Gaussian gradient.
+
+N = 1 measures configs[1] (1M Gaussians); the line also carries, each timed on the GPU in the same run:
+  config3            configs[2]: LOD cut -> weights -> render_post lerp -> rasterize fwd+bwd -> lerp bwd on a
+                     synthetic binary hierarchy over configs[1]'s 1M leaves (the example dataset is not available
+                     offline), stages separately and inclusive (SURVEY 8(d));
+  config4_one_gpu    configs[3]'s per-GPU work (4M Gaussians, one view) on one GPU, the N = 1 point of the
+                     multi-GPU curve;
+  cpu_baseline       the oracle on one full frame on all host threads (OpenMP) and on one thread;
+  parity             the GPU step against the oracle on the same inputs, in the shared arithmetic contract and in
+                     the reference's own float operation order.
+N > 1 measures configs[3]: view-data parallel, weak scaling, each rank renders its own view of its own
+4M-Gaussian replica (--P overrides) and the gradients are all-reduced (RCCL over xGMI).
 Inputs are synthetic (seeded), resident in HBM before timing starts.  Rank 0 prints one JSON line.
 """
 import argparse
@@ -28,8 +40,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles each, 2400 MHz max clock
-VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 4
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles on each SIMD-32 (across its
+# waves; MI355X_MICROARCH.md cycle constants, v_fma_f32 wave64), 2400 MHz max clock = 1228.8 G wave-instr/s
+VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 2
 
 
 def algorithmic_bytes(stage, P, V, R, N, T, M, D):
@@ -77,44 +90,238 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(P, deg, W, H):
-    """The oracle (C restatement of the reference algorithm, 1 thread) on one full frame: fwd + bwd.
-    Returns the timing summary and the oracle's outputs (same scene, camera and upstream gradients as
-    rank 0's GPU step) for the full-size parity check."""
+def _oracle_frame(O, sc, cam, g, gd, omp=False):
+    t0 = time.perf_counter()
+    fr = O.forward(sc, cam, do_depth=True, omp=omp)
+    gr = O.backward(fr, sc, g, gd)
+    dt = time.perf_counter() - t0
+    ref = dict(color=fr.color, invdepth=fr.invdepth, dmean3D=gr["dmean3D"], dmean2D=gr["dmean2D"],
+               dopacity=gr["dopacity"], dscale=gr["dscale"], drot=gr["drot"], dsh=gr["dsh"])
+    return dt, ref
+
+
+def cpu_baseline(P, deg, W, H, reference_order=True):
+    """The oracle (C restatement of the reference algorithm) on one full frame, fwd + bwd: on every host thread
+    OpenMP gives it (the box's CPU share: OMP_NUM_THREADS) and on one thread.  Returns the timing summary, the
+    serial oracle's outputs (same scene, camera and upstream gradients as rank 0's GPU step) for the full-size
+    parity check, and the same frame with alpha decided in the reference's own float op order."""
     from oracle import oracle as O
     from hlgs_core import synthetic as S
     cam = S.make_camera(W, H)
     sc = S.make_gaussians(P, deg, cam, seed=0)
     g, gd = S.upstream_grads(W, H, seed=1)
     O.build()
-    t0 = time.perf_counter()
-    fr = O.forward(sc, S.cam_numpy(cam), do_depth=True)
-    gr = O.backward(fr, sc, g, gd)
-    dt = time.perf_counter() - t0
-    summary = dict(value=round(W * H / dt / 1e6, 4), unit="Mpix/s", cores=1, kind="port",
-                   sample=f"one full frame: {P} Gaussians, SH deg {deg}, {W}x{H}, forward+backward, "
-                          f"{dt:.2f} s on 1 thread of {cpu_model()} (os.cpu_count()={os.cpu_count()})")
-    ref = dict(color=fr.color, invdepth=fr.invdepth, dmean3D=gr["dmean3D"], dmean2D=gr["dmean2D"],
-               dopacity=gr["dopacity"], dscale=gr["dscale"], drot=gr["drot"], dsh=gr["dsh"])
-    return summary, ref
+    cn = S.cam_numpy(cam)
+    dt1, ref = _oracle_frame(O, sc, cn, g, gd)
+    threads = O.num_threads(omp=True)
+    dtn = min(_oracle_frame(O, sc, cn, g, gd, omp=True)[0] for _ in range(2))
+    sample = (f"one full frame: {P} Gaussians, SH deg {deg}, {W}x{H}, forward+backward (preprocess, binning, "
+              f"stable sort, blend, blend backward, Gaussian backward), {cpu_model()}, os.cpu_count()={os.cpu_count()}")
+    summary = dict(value=round(W * H / dtn / 1e6, 4), unit="Mpix/s", cores=threads, kind="port",
+                   sample=f"{sample}; {dtn:.2f} s on {threads} OpenMP threads (best of 2)",
+                   single_thread=dict(value=round(W * H / dt1 / 1e6, 4), unit="Mpix/s", cores=1,
+                                      sample=f"same frame, {dt1:.2f} s on 1 thread"))
+    ref_order = None
+    if reference_order:
+        with O.reference_order():
+            ref_order = _oracle_frame(O, sc, cn, g, gd)[1]
+    return summary, ref, ref_order
 
 
-def parity_report(gpu, ref):
-    """Full-size parity of rank 0's step against the oracle: forward per-pixel L-inf and, per gradient
-    tensor, max-abs error and max-abs error relative to the oracle tensor's max-abs."""
-    out = dict(vs="oracle (C restatement of the reference), identical inputs, full configs[1] frame")
-    out["color_linf"] = float(np.abs(gpu["color"] - ref["color"]).max())
-    out["invdepth_linf"] = float(np.abs(gpu["invdepth"] - ref["invdepth"]).max())
+def parity_report(gpu, ref, vs):
+    """Full-size parity of rank 0's step against an oracle frame: forward per-pixel L-inf and the count of pixels
+    above the 1e-4 tolerance; per gradient tensor, max-abs error, max-abs error relative to the oracle tensor's
+    max-abs, and the elements violating |gpu - ref| <= 1e-3 |ref| + 1e-6 max|ref| (element-wise)."""
+    out = dict(vs=vs)
+    dc = np.abs(gpu["color"] - ref["color"])
+    di = np.abs(gpu["invdepth"] - ref["invdepth"])
+    out["color_linf"] = float(dc.max())
+    out["invdepth_linf"] = float(di.max())
+    out["pixels_above_1e-4"] = int((np.maximum(dc.max(0), di.max(0)) > 1e-4).sum())
     per = {}
     for k in ("dmean3D", "dmean2D", "dopacity", "dscale", "drot", "dsh"):
         a, b = gpu[k].reshape(ref[k].shape[0], -1), ref[k].reshape(ref[k].shape[0], -1)
         a = a[:, :b.shape[1]]
-        err = float(np.abs(a - b).max())
-        per[k] = dict(max_abs_err=err, rel=err / max(float(np.abs(b).max()), 1e-30))
+        d = np.abs(a - b)
+        mx = max(float(np.abs(b).max()), 1e-30)
+        err = float(d.max())
+        per[k] = dict(max_abs_err=err, rel=err / mx,
+                      elementwise_violations=int((d > 1e-3 * np.abs(b) + 1e-6 * mx).sum()))
     out["grad_max_abs_err"] = max(v["max_abs_err"] for v in per.values())
     out["grad_max_rel_err"] = max(v["rel"] for v in per.values())
+    out["grad_elementwise_violations"] = sum(v["elementwise_violations"] for v in per.values())
     out["grads"] = per
-    out["tolerance"] = dict(fwd_linf=1e-4, grad_rel=1e-3)
+    out["tolerance"] = dict(fwd_linf=1e-4, grad_rel=1e-3, grad_elementwise="|d| <= 1e-3 |ref| + 1e-6 max|ref|")
+    return out
+
+
+def _median_ms(fn, iters, warmup=2):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
+def settings_for(cam, deg, dev, do_depth=True):
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    e_i = torch.empty(0, dtype=torch.int32, device=dev)
+    e_f = torch.empty(0, dtype=torch.float32, device=dev)
+    return GaussianRasterizationSettings(
+        image_height=cam["H"], image_width=cam["W"], tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam["viewmatrix"].to(dev),
+        projmatrix=cam["projmatrix"].to(dev), sh_degree=deg, campos=cam["campos"].to(dev), prefiltered=False,
+        debug=False, render_indices=e_i, parent_indices=e_i, interpolation_weights=e_f, num_node_kids=e_i,
+        do_depth=do_depth)
+
+
+def bench_config3(P, W, H, deg, dev, iters=20, tau_px=6.0):
+    """configs[2]: the hierarchical-LOD training step of train_single.py / render_post
+    (gaussian_renderer/__init__.py:304-347): expand_to_size_dynamic at tau -> get_interpolation_weights_dynamic
+    -> the child/parent lerp (interpolate_lod) -> rasterize forward + backward at W x H -> lerp backward, on a
+    synthetic binary hierarchy over P leaves (hlgs_core.synthetic.make_dynamic_hierarchy).  Median event spans
+    on torch's stream; the cut and interpolation separately and the whole chain inclusive."""
+    import gaussian_hierarchy as GH
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from hlgs_core import synthetic as S
+    cam = S.make_camera(W, H)
+    t0 = time.perf_counter()
+    hier = S.make_dynamic_hierarchy(S.make_gaussians(P, deg, cam, seed=0), seed=0)
+    build_s = time.perf_counter() - t0
+    N = hier["nodes"].shape[0]
+    d = lambda a, **kw: torch.tensor(np.ascontiguousarray(a), device=dev, **kw)  # noqa: E731
+    nodes = d(hier["nodes"])
+    xyz, scales, rots, opac, shs = (d(hier[k], requires_grad=True)
+                                    for k in ("means3D", "scales", "rotations", "opacities", "shs"))
+    tau = (2 * (tau_px + 0.5)) * cam["tanfovx"] / (0.5 * W)
+    vp, vd = cam["campos"].to(dev), torch.tensor([0.0, 0.0, 1.0])
+    ri, pi, ni, kids = (torch.zeros(N, dtype=torch.int32, device=dev) for _ in range(4))
+    ts = torch.zeros(N, device=dev)
+    rast = GaussianRasterizer(settings_for(cam, deg, dev))
+    g_np, gd_np = S.upstream_grads(W, H, seed=1)
+    g, gd = torch.tensor(g_np, device=dev), torch.tensor(gd_np, device=dev)
+    st = {}
+
+    def cut():
+        st["n"] = GH.expand_to_size_dynamic(nodes, xyz.detach(), scales.detach(), tau, vp, vd, ri, pi, ni)
+
+    def weights():
+        GH.get_interpolation_weights_dynamic(ni[:st["n"]], tau, nodes, xyz.detach(), scales.detach(), vp.cpu(), vd,
+                                             ts, kids)
+
+    def lerp():
+        st["outs"] = GH.interpolate_lod(xyz, scales, rots, opac, shs, ri[:st["n"]], pi, ts, 0)
+
+    def raster():
+        m, s_, r_, o_, sh_ = st["outs"]
+        m2 = torch.zeros_like(m, requires_grad=True)
+        st["graph"] = rast(means3D=m, means2D=m2, opacities=o_, shs=sh_, scales=s_, rotations=r_)
+
+    def backward():
+        c, _, inv = st["graph"]
+        torch.autograd.backward([c, inv], [g, gd])
+        for p in (xyz, scales, rots, opac, shs):
+            p.grad = None
+
+    def full():
+        cut(); weights(); lerp(); raster(); backward()  # noqa: E702
+
+    def lerp_raster_bwd():
+        lerp(); raster(); backward()  # noqa: E702
+
+    full()
+    stages = {"expand_to_size_dynamic": _median_ms(cut, iters),
+              "get_interpolation_weights_dynamic": _median_ms(weights, iters),
+              "interpolate_lod_fwd": _median_ms(lerp, iters),
+              "rasterizer_fwd": _median_ms(raster, iters)}
+    stages["rasterizer_bwd+lerp_bwd"] = (_median_ms(lerp_raster_bwd, iters) - stages["interpolate_lod_fwd"]
+                                         - stages["rasterizer_fwd"])
+    incl = _median_ms(full, iters)
+    lod = sum(stages[k] for k in ("expand_to_size_dynamic", "get_interpolation_weights_dynamic",
+                                  "interpolate_lod_fwd"))
+    return dict(workload=f"configs[2]: synthetic binary hierarchy over {P} leaves ({N} nodes), SH deg {deg}, "
+                         f"{W}x{H}, tau={tau_px} px ({tau:.3e}), cut -> weights -> lerp -> rasterize fwd+bwd -> "
+                         f"lerp bwd", nodes=N, selected=int(st["n"]), hierarchy_build_s=round(build_s, 1),
+                stages_ms={k: round(v, 4) for k, v in stages.items()}, lod_cut_and_interp_ms=round(lod, 4),
+                inclusive_ms=round(incl, 4), value=round(W * H / incl / 1e3, 1), unit="Mpix/s",
+                timing=f"median of {iters} event spans per stage on torch's stream")
+
+
+def make_step(P, deg, W, H, dev, rank, world, exchange_on=True):
+    """One rank's training view: its scene replica, rasterizer and upstream gradients; returns step() and state."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from hlgs_core import synthetic as S
+    from hlgs_core.dp import FlatGradExchange
+    # every rank: the same scene replica, its own view (ring of cameras); rank 0 = configs[1] camera
+    cam = S.make_camera(W, H) if world == 1 else S.ring_camera(W, H, rank, world)
+    host = S.make_gaussians(P, deg, S.make_camera(W, H), seed=0)
+    to = lambda a: torch.tensor(a, device=dev, requires_grad=True)  # noqa: E731
+    params = [to(host[k]) for k in ("means3D", "scales", "rotations", "opacities", "shs")]
+    del host
+    means3D, scales, rots, opac, shs = params
+    g_np, gd_np = S.upstream_grads(W, H, seed=1 + rank)
+    g_col, g_inv = torch.tensor(g_np, device=dev), torch.tensor(gd_np, device=dev)
+    rs = settings_for(cam, deg, dev)
+    rast = GaussianRasterizer(rs)
+    exchange = FlatGradExchange(params) if (world > 1 and exchange_on) else None
+    st = dict(params=params, rs=rs, rast=rast, exchange=exchange, g_col=g_col, g_inv=g_inv, ar_events=[])
+
+    def step(time_exchange=False):
+        for p in params:
+            p.grad = None
+        means2D = torch.zeros_like(means3D, requires_grad=True)
+        color, radii, invd = rast(means3D=means3D, means2D=means2D, opacities=opac, shs=shs, scales=scales,
+                                  rotations=rots)
+        torch.autograd.backward([color, invd], [g_col, g_inv])
+        if exchange is not None:
+            if time_exchange:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                exchange.allreduce()
+                b.record()
+                st["ar_events"].append((a, b))
+            else:
+                exchange.allreduce()
+        st["means2D"], st["color"], st["invd"] = means2D, color, invd
+        return radii
+
+    return step, st
+
+
+def num_rendered(st, H, W, deg):
+    from diff_gaussian_rasterization import _C as DC
+    rs = st["rs"]
+    means3D, scales, rots, opac, shs = (p.detach() for p in st["params"])
+    e_i, e_f = rs.render_indices, rs.interpolation_weights
+    return int(DC.rasterize_gaussians(rs.bg, e_i, e_i, e_f, e_i, means3D, e_f, opac, scales, rots, 1.0, e_f,
+                                      rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, H, W, shs, deg,
+                                      rs.campos, False, False, True)[0])
+
+
+def bench_config4_one_gpu(P, deg, W, H, dev, steps, warmup):
+    """configs[3]'s per-GPU work (P Gaussians, one 1080p view, fwd+bwd) on one GPU with no exchange: the N = 1
+    point against which the driver's N > 1 lines (same per-rank work plus the all-reduce) scale."""
+    step, st = make_step(P, deg, W, H, dev, 0, 1)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = dict(workload=f"configs[3] per-GPU work on one GPU: {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd with "
+                        f"depth, one view, no exchange", value=round(W * H * steps / el / 1e6, 3), unit="Mpix/s",
+               ms_per_step=round(el / steps * 1e3, 4), steps=steps, num_rendered=num_rendered(st, H, W, deg))
+    del step, st
+    torch.cuda.empty_cache()
     return out
 
 
@@ -123,12 +330,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--P", type=int, default=None, help="Gaussians per replica (default: 1M at N = 1, 4M at N > 1)")
     ap.add_argument("--W", type=int, default=1920)
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--sh-degree", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the config3 and config4_one_gpu legs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -146,43 +354,12 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", gpu)
 
-    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from hlgs_core import _lib as L
-    from hlgs_core import synthetic as S
-    from hlgs_core.dp import FlatGradExchange
 
-    W, H, P, deg = args.W, args.H, args.P, args.sh_degree
-    # every rank: the same scene replica, its own view (ring of cameras); rank 0 = configs[1] camera
-    cam = S.make_camera(W, H) if world == 1 else S.ring_camera(W, H, rank, world)
-    host = S.make_gaussians(P, deg, S.make_camera(W, H), seed=0)
-    to = lambda a: torch.tensor(a, device=dev, requires_grad=True)  # noqa: E731
-    means3D, scales, rots, opac, shs = (to(host["means3D"]), to(host["scales"]), to(host["rotations"]),
-                                        to(host["opacities"]), to(host["shs"]))
-    g_np, gd_np = S.upstream_grads(W, H, seed=1 + rank)
-    g_col, g_inv = torch.tensor(g_np, device=dev), torch.tensor(gd_np, device=dev)
-    e_i = torch.empty(0, dtype=torch.int32, device=dev)
-    e_f = torch.empty(0, dtype=torch.float32, device=dev)
-    rs = GaussianRasterizationSettings(
-        image_height=H, image_width=W, tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
-        bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam["viewmatrix"].to(dev),
-        projmatrix=cam["projmatrix"].to(dev), sh_degree=deg, campos=cam["campos"].to(dev), prefiltered=False,
-        debug=False, render_indices=e_i, parent_indices=e_i, interpolation_weights=e_f, num_node_kids=e_i,
-        do_depth=True)
-    rast = GaussianRasterizer(rs)
-    params = [means3D, scales, rots, opac, shs]
-    exchange = FlatGradExchange(params) if world > 1 else None
-    stats = {}
-
-    def step():
-        for p in params:
-            p.grad = None
-        means2D = torch.zeros_like(means3D, requires_grad=True)
-        color, radii, invd = rast(means3D=means3D, means2D=means2D, opacities=opac, shs=shs, scales=scales,
-                                  rotations=rots)
-        torch.autograd.backward([color, invd], [g_col, g_inv])
-        if exchange is not None:
-            exchange.allreduce()
-        return radii
+    W, H, deg = args.W, args.H, args.sh_degree
+    P = args.P if args.P is not None else (1_000_000 if world == 1 else 4_000_000)
+    step, st = make_step(P, deg, W, H, dev, rank, world)
+    params, exchange = st["params"], st["exchange"]
 
     for _ in range(args.warmup):
         radii = step()
@@ -190,13 +367,10 @@ def main():
     # frame statistics for the algorithmic-byte model
     with torch.no_grad():
         V = int((radii > 0).sum().item())
-    from diff_gaussian_rasterization import _C as DC
-    nr = DC.rasterize_gaussians(rs.bg, e_i, e_i, e_f, e_i, means3D.detach(), e_f, opac.detach(), scales.detach(),
-                                rots.detach(), 1.0, e_f, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, H, W,
-                                shs.detach(), deg, rs.campos, False, False, True)[0]
+    nr = num_rendered(st, H, W, deg)
     # Per-stage breakdown from an untimed pass with events around every stage; the timed region below
     # then brackets only the dominant stage's kernel (each timed event is a queue barrier).
-    breakdown, dom = {}, None
+    breakdown, dom, stats = {}, None, {}
     if not args.no_stage_timing:
         L.set_stage_timing(True)
         for _ in range(max(3, args.steps // 2)):
@@ -211,7 +385,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(time_exchange=exchange is not None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -219,10 +393,19 @@ def main():
     if dom is not None:
         stats = L.stage_stats()
         L.set_stage_timing(False)
+    exchange_report = None
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        ar_ms = float(np.mean([a.elapsed_time(b) for a, b in st["ar_events"]])) if st["ar_events"] else 0.0
+        t = torch.tensor([elapsed, ar_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, ar_ms = float(t[0].item()), float(t[1].item())
+        nbytes = exchange.flat.numel() * 4
+        exchange_report = dict(
+            collective=f"all_reduce AVG, {backend}", bytes_per_step=nbytes, collectives_per_step=getattr(
+                exchange, "last_collectives", None), allreduce_ms=round(ar_ms, 4),
+            busbw_GBs=round(2 * (world - 1) / world * nbytes / (ar_ms * 1e-3) / 1e9, 1) if ar_ms > 0 else None,
+            note="events around FlatGradExchange.allreduce() on torch's stream in each timed step (mean; max over "
+                 "ranks); bus bandwidth = 2(N-1)/N x bytes / time")
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * W * H * args.steps / elapsed / 1e6
@@ -238,41 +421,47 @@ def main():
     if dom is not None and stats.get(dom, (0, 0))[1] > 0:
         ms = stats[dom][0]
         ach = round(algorithmic_bytes(dom, P, V, nr, W * H, T, M, 1) / (ms * 1e-3) / 1e9, 1)
-        traffic, src = pmc_traffic(dom)
+        traffic, src = pmc_traffic(dom) if P == 1_000_000 else (None, None)
         roofline = dict(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                         traffic=traffic, traffic_unit="bytes/launch", traffic_source=src, kernel=dom,
                         kernel_ms=round(ms, 4), launches=stats[dom][1])
-        valu, _ = pmc_traffic(dom, "valu_wave_instr")
+        valu, _ = pmc_traffic(dom, "valu_wave_instr") if P == 1_000_000 else (None, None)
         if valu:
             rate = valu / (ms * 1e-3) / 1e9
             roofline["valu_issue"] = dict(wave_instr_per_launch=valu, achieved_Ginstr_s=round(rate, 1),
                                           peak_Ginstr_s=VALU_PEAK_GINSTR, frac=round(rate / VALU_PEAK_GINSTR, 4))
-    cpu = parity = None
+    cpu = parity = config3 = config4 = None
+    if rank == 0 and world == 1 and not args.no_extras:
+        config3 = bench_config3(1_000_000 if args.P is None else P, deg, W, H, dev)
+        torch.cuda.empty_cache()
+        config4 = bench_config4_one_gpu(4_000_000, deg, W, H, dev, max(5, args.steps // 2), 2)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, ref = cpu_baseline(P, deg, W, H)
-        for p in params:  # one more step on the same inputs, outputs kept for the parity check
-            p.grad = None
-        means2D = torch.zeros_like(means3D, requires_grad=True)
-        color, _, invd = rast(means3D=means3D, means2D=means2D, opacities=opac, shs=shs, scales=scales,
-                              rotations=rots)
-        torch.autograd.backward([color, invd], [g_col, g_inv])
+        cpu, ref, ref_order = cpu_baseline(P, deg, W, H)
+        step()  # one more step on the same inputs, outputs kept for the parity check
         npy = lambda t: t.detach().cpu().numpy()  # noqa: E731
-        gpu = dict(color=npy(color), invdepth=npy(invd), dmean3D=npy(means3D.grad), dmean2D=npy(means2D.grad),
-                   dopacity=npy(opac.grad), dscale=npy(scales.grad), drot=npy(rots.grad), dsh=npy(shs.grad))
-        parity = parity_report(gpu, ref)
+        means3D, scales, rots, opac, shs = params
+        gpu = dict(color=npy(st["color"]), invdepth=npy(st["invd"]), dmean3D=npy(means3D.grad),
+                   dmean2D=npy(st["means2D"].grad), dopacity=npy(opac.grad), dscale=npy(scales.grad),
+                   dsh=npy(shs.grad), drot=npy(rots.grad))
+        parity = parity_report(gpu, ref, "oracle (C restatement of the reference; alpha decided in the shared "
+                                         "arithmetic contract, A-17), identical inputs, full configs[1] frame")
+        parity["reference_order"] = parity_report(
+            gpu, ref_order, "oracle with alpha decided in the reference's own float op order (power, expf, "
+                            "alpha < 1/255; forward.cu:538-560, backward.cu:614-643), same frame")
     if rank == 0:
+        wl = (f"configs[1]: {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd with depth, one view" if world == 1 else
+              f"configs[3]: {P} Gaussians per replica, SH deg {deg}, {W}x{H}, fwd+bwd with depth, one view per GPU, "
+              + ("RCCL" if backend == "nccl" else backend) + " grad all-reduce")
         line = {
             "metric": "forward+backward Mpix/s at 1080p (1M Gaussians); grad max-abs-err vs ref",
             "value": round(value, 3), "unit": "Mpix/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded PCG64 scene and upstream gradients; no dataset)",
-            "config": {"workload": f"configs[1]: {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd with depth, "
-                                   f"one view per GPU" + ((", RCCL" if backend == "nccl" else ", " + backend) + " grad all-reduce"
-                                                          if world > 1 else ""),
-                       "num_rendered": nr, "visible": V, "tiles": T,
+            "config": {"workload": wl, "num_rendered": nr, "visible": V, "tiles": T,
                        "parallelism": f"view-dp{world}"},
-            "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "exchange": exchange_report,
+            "config3": config3, "config4_one_gpu": config4,
             "stages": stage_report, "stages_note": "untimed pass with events around every stage",
         }
         print(json.dumps(line))

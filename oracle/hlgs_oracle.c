@@ -27,6 +27,39 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* The same source also builds the all-cores CPU baseline (oracle/build/libhlgs_oracle_omp.so, gcc -fopenmp):
+ * preprocess and per-Gaussian backward over Gaussians, the blend over tiles, per-tile sorts in parallel; the
+ * blend backward then accumulates its per-Gaussian sums with atomic adds (summation order, and so the last bits
+ * of the gradients, vary from run to run -- the timing leg only; every parity check uses the serial build). */
+#ifdef _OPENMP
+#define ORC_ACC(lhs, rhs) do { const float v_ = (rhs); _Pragma("omp atomic") lhs += v_; } while (0)
+#else
+#define ORC_ACC(lhs, rhs) ((lhs) += (rhs))
+#endif
+
+/* Alpha decision mode:
+ *   0 (default) -- the shared arithmetic contract (A-17): e2 = power log2(e) from the pre-scaled conic, G = exp2(e2),
+ *                  keep iff e2 >= the per-Gaussian threshold computed in double; bit-identical to the HIP kernels;
+ *   1           -- the reference's own float operation order: power = -0.5f (a dx dx + c dy dy) - b dx dy,
+ *                  G = expf(power), keep iff alpha >= 1.0f / 255.0f (HR/forward.cu:538-560,
+ *                  HR/backward.cu:614-643, AR/forward.cu:383-391, AR/backward.cu:594-600), evaluated without FMA
+ *                  contraction.  Reported beside the contract so that divergence from the reference's float
+ *                  behaviour stays visible. */
+static int g_ref_order = 0;
+void orc_set_alpha_mode(int reference_order) { g_ref_order = reference_order != 0; }
+int orc_get_alpha_mode(void) { return g_ref_order; }
+int orc_num_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
 
 #define TILE 16
 #define NCH 3
@@ -346,6 +379,7 @@ int orc_forward_preprocess(const orc_args *a, orc_geom *g)
     memset(g->clamped, 0, (size_t)a->P);
     memset(g->rgb, 0, sizeof(float) * 3 * (size_t)a->P);
     memset(g->rects, 0, sizeof(int) * 2 * (size_t)a->P);
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < a->P; i++) preprocess_one(a, g, i, gx, gy);
     uint64_t acc = 0;
     for (int i = 0; i < a->P; i++) { acc += g->tiles_touched[i]; g->point_offsets[i] = (uint32_t)acc; }
@@ -462,6 +496,37 @@ static float *alpha_thresholds(const orc_args *a, const orc_geom *g)
     return thr;
 }
 
+/* One pixel-splat pair: the falloff G and the (lerped) alpha; returns 0 when the reference skips the pair
+ * (power > 0 or alpha < 1/255), decided per g_ref_order.  fwd selects the forward's __powf = exp2(fr log2 x)
+ * for the lerped alpha (HR/forward.cu:551), otherwise powf (HR/backward.cu:632). */
+static inline int pair_alpha(const float *co, float dx, float dy, float thr, int interp, float tt, float fr, int fwd,
+                             float *G, float *my_alpha, float *alpha)
+{
+    float g, e2 = 0.0f;
+    if (g_ref_order) {
+        const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+        if (power > 0.0f) return 0;
+        g = expf(power);
+    } else {
+        float q[3];
+        conic_q(co, q);
+        e2 = splat_e2(q, dx, dy); /* power * log2(e) */
+        if (e2 > 0.0f) return 0;
+        g = exp2f(e2);
+    }
+    const float ma = fminf(0.99f, co[3] * g);
+    float al = ma;
+    if (interp) {
+        const float ka = fwd ? 1.0f - exp2f(fr * log2f(1.0f - ma)) : 1.0f - powf(1.0f - ma, fr);
+        al = tt * ma + (1.0f - tt) * ka;
+    }
+    if (g_ref_order ? al < 1.0f / 255.0f : e2 < thr) return 0; /* alpha < 1/255 */
+    *G = g;
+    *my_alpha = ma;
+    *alpha = al;
+    return 1;
+}
+
 void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R, float *out_color,
                         float *out_invdepth, int *seen)
 {
@@ -477,6 +542,7 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
     const float fltmax = FLT_MAX;
     uint32_t maxbits;
     memcpy(&maxbits, &fltmax, 4);
+#pragma omp parallel for schedule(dynamic, 1024)
     for (int i = 0; i < a->P; i++) {
         if (g->radii[i] <= 0) continue;
         uint32_t off = i == 0 ? 0 : g->point_offsets[i - 1];
@@ -500,8 +566,31 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
             buf[off].val = 0xFFFFFFFFu;
         }
     }
-    /* stable radix sort == sort by (key, input position), App. A-4 */
-    qsort(buf, (size_t)R, sizeof(kv), kv_cmp);
+    /* stable radix sort == sort by (key, input position), App. A-4: a stable counting pass on the key's tile word
+     * (the sentinel tile last), then each tile's run sorted by (depth bits, position) -- the order of one global
+     * sort by (key, position), with independent runs */
+    {
+        uint32_t *start = (uint32_t *)calloc((size_t)T + 2, sizeof(uint32_t));
+        kv *tmp = (kv *)malloc(sizeof(kv) * (size_t)(R > 0 ? R : 1));
+        for (int i = 0; i < R; i++) {
+            const uint32_t t = (uint32_t)(buf[i].key >> 32);
+            start[(t == 0xFFFFFFFFu ? (uint32_t)T : t) + 1]++;
+        }
+        for (int t = 0; t <= T; t++) start[t + 1] += start[t];
+        uint32_t *cur = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)T + 1));
+        memcpy(cur, start, sizeof(uint32_t) * ((size_t)T + 1));
+        for (int i = 0; i < R; i++) {
+            const uint32_t t = (uint32_t)(buf[i].key >> 32);
+            tmp[cur[t == 0xFFFFFFFFu ? (uint32_t)T : t]++] = buf[i];
+        }
+#pragma omp parallel for schedule(dynamic, 16)
+        for (int t = 0; t <= T; t++)
+            if (start[t + 1] - start[t] > 1) qsort(tmp + start[t], start[t + 1] - start[t], sizeof(kv), kv_cmp);
+        free(buf);
+        buf = tmp;
+        free(cur);
+        free(start);
+    }
     for (int i = 0; i < R; i++) im->point_list[i] = buf[i].val;
     /* identifyTileRanges, HR/rasterizer_impl.cu:120-142 (AR/rasterizer_impl.cu:195-220 skips the sentinel) */
     for (int i = 0; i < R; i++) {
@@ -519,6 +608,7 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
     int do_interp = (a->ts != NULL && a->kids != NULL);
     float *thr = alpha_thresholds(a, g);
     /* renderCUDA<3> per pixel, HR/forward.cu:450-596 (AR/forward.cu:282-430) */
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ty++)
         for (int tx = 0; tx < gx; tx++) {
             uint32_t rs = im->ranges[2 * (ty * gx + tx)], re = im->ranges[2 * (ty * gx + tx) + 1];
@@ -531,21 +621,17 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
                         uint32_t id = im->point_list[j];
                         float dx = g->means2D[2 * id] - (float)px, dy = g->means2D[2 * id + 1] - (float)py;
                         const float *co = g->conic_opacity + 4 * id;
-                        float q[3];
-                        conic_q(co, q);
-                        const float e2 = splat_e2(q, dx, dy); /* power * log2(e) */
-                        if (e2 > 0.0f) continue;
-                        float my_alpha = fminf(0.99f, co[3] * exp2f(e2));
-                        float alpha = my_alpha;
-                        if (do_interp && (int)id < a->P) {
-                            float tt = a->ts[id], fr = 1.0f / (float)a->kids[id];
-                            float ka = 1.0f - exp2f(fr * log2f(1.0f - my_alpha)); /* __powf */
-                            alpha = tt * my_alpha + (1.0f - tt) * ka;
-                        }
-                        if (e2 < thr[id]) continue; /* alpha < 1/255 */
+                        const int ip = do_interp && (int)id < a->P;
+                        float G, my_alpha, alpha;
+                        if (!pair_alpha(co, dx, dy, thr[id], ip, ip ? a->ts[id] : 0.0f,
+                                        ip ? 1.0f / (float)a->kids[id] : 0.0f, 1, &G, &my_alpha, &alpha))
+                            continue;
                         float test_T = Tt * (1 - alpha);
                         if (test_T < 0.0001f) break; /* done */
-                        if (seen) seen[id] = 1;
+                        if (seen) {
+#pragma omp atomic write
+                            seen[id] = 1;
+                        }
                         for (int ch = 0; ch < 3; ch++) C[ch] += feat[3 * id + ch] * alpha * Tt;
                         if (out_invdepth) inv += (1 / g->depths[id]) * alpha * Tt;
                         Tt = test_T;
@@ -586,6 +672,7 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
     const float *col = a->colors_precomp ? a->colors_precomp : g->rgb;
     int interp = (a->ts != NULL && a->kids != NULL);
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ty++)
         for (int tx = 0; tx < gx; tx++) {
             uint32_t rs = im->ranges[2 * (ty * gx + tx)], re = im->ranges[2 * (ty * gx + tx) + 1];
@@ -607,20 +694,10 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
                         uint32_t id = im->point_list[j];
                         float dx = g->means2D[2 * id] - (float)px, dy = g->means2D[2 * id + 1] - (float)py;
                         const float *co = g->conic_opacity + 4 * id;
-                        float q[3];
-                        conic_q(co, q);
-                        const float e2 = splat_e2(q, dx, dy); /* power * log2(e) */
-                        if (e2 > 0.0f) continue;
-                        float G = exp2f(e2);
-                        float test_alpha = co[3] * G;
-                        int nullalpha = test_alpha > 0.99f;
-                        float my_alpha = fminf(0.99f, test_alpha), alpha = my_alpha, tt = 0, fr = 0;
-                        if (interp) {
-                            tt = a->ts[id];
-                            fr = 1.0f / (float)a->kids[id];
-                            alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
-                        }
-                        if (e2 < thr[id]) continue; /* alpha < 1/255 */
+                        const float tt = interp ? a->ts[id] : 0.0f, fr = interp ? 1.0f / (float)a->kids[id] : 0.0f;
+                        float G, my_alpha, alpha;
+                        if (!pair_alpha(co, dx, dy, thr[id], interp, tt, fr, 0, &G, &my_alpha, &alpha)) continue;
+                        const int nullalpha = co[3] * G > 0.99f;
                         T = T / (1.f - alpha);
                         const float weight = alpha * T;
                         float dL_dalpha = 0.0f;
@@ -630,14 +707,14 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
                             acc[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * acc[ch];
                             last_color[ch] = c;
                             dL_dalpha += (c - acc[ch]) * dpix[ch];
-                            o->dcolor[3 * gid + ch] += weight * dpix[ch];
+                            ORC_ACC(o->dcolor[3 * gid + ch], weight * dpix[ch]);
                         }
                         if (dL_dinv) {
                             const float invd = 1.f / g->depths[id];
                             acc_inv = last_alpha * last_inv + (1.f - last_alpha) * acc_inv;
                             last_inv = invd;
                             dL_dalpha += (invd - acc_inv) * dinv;
-                            o->dinvdepth[gid] += weight * dinv;
+                            ORC_ACC(o->dinvdepth[gid], weight * dinv);
                         }
                         dL_dalpha *= T;
                         last_alpha = alpha;
@@ -649,14 +726,14 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
                         const float gdx = G * dx, gdy = G * dy;
                         const float dG_ddelx = -gdx * co[0] - gdy * co[1];
                         const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                        o->dmean2D[3 * gid] += dL_dG * dG_ddelx * ddelx_dx;
-                        o->dmean2D[3 * gid + 1] += dL_dG * dG_ddely * ddely_dy;
-                        o->dconic[4 * gid] += -0.5f * gdx * dx * dL_dG;
-                        o->dconic[4 * gid + 1] += -0.5f * gdx * dy * dL_dG;
-                        o->dconic[4 * gid + 3] += -0.5f * gdy * dy * dL_dG;
+                        ORC_ACC(o->dmean2D[3 * gid], dL_dG * dG_ddelx * ddelx_dx);
+                        ORC_ACC(o->dmean2D[3 * gid + 1], dL_dG * dG_ddely * ddely_dy);
+                        ORC_ACC(o->dconic[4 * gid], -0.5f * gdx * dx * dL_dG);
+                        ORC_ACC(o->dconic[4 * gid + 1], -0.5f * gdx * dy * dL_dG);
+                        ORC_ACC(o->dconic[4 * gid + 3], -0.5f * gdy * dy * dL_dG);
                         float mult = 1.0f;
                         if (interp) mult = tt - powf(1.0f - my_alpha, fr - 1.0f) * (tt - 1.0f) * fr;
-                        o->dopacity[gid] += mult * G * dL_dalpha;
+                        ORC_ACC(o->dopacity[gid], mult * G * dL_dalpha);
                     }
                 }
         }
@@ -679,6 +756,7 @@ static void blend_backward_alt(const orc_args *a, const orc_geom *g, const orc_i
     const size_t HW = (size_t)W * H;
     const float *col = a->colors_precomp ? a->colors_precomp : g->rgb;
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ty++)
         for (int tx = 0; tx < gx; tx++) {
             uint32_t rs = im->ranges[2 * (ty * gx + tx)], re = im->ranges[2 * (ty * gx + tx) + 1];
@@ -698,25 +776,20 @@ static void blend_backward_alt(const orc_args *a, const orc_geom *g, const orc_i
                         const uint32_t id = im->point_list[j];
                         const float dx = g->means2D[2 * id] - (float)px, dy = g->means2D[2 * id + 1] - (float)py;
                         const float *co = g->conic_opacity + 4 * id;
-                        float q[3];
-                        conic_q(co, q);
-                        const float e2 = splat_e2(q, dx, dy);
-                        if (e2 > 0.0f) continue;
-                        const float G = exp2f(e2);
-                        const float alpha = fminf(0.99f, co[3] * G);
-                        if (e2 < thr[id]) continue; /* alpha < 1/255 */
+                        float G, my_alpha, alpha;
+                        if (!pair_alpha(co, dx, dy, thr[id], 0, 0.0f, 0.0f, 0, &G, &my_alpha, &alpha)) continue;
                         const float weight = alpha * T;
                         float bg_dot = 0.0f, dL_dalpha = 0.0f;
                         for (int ch = 0; ch < 3; ch++) {
                             const float c = col[3 * id + ch];
                             ar[ch] += weight * c;
-                            o->dcolor[3 * id + ch] += weight * dpix[ch];
+                            ORC_ACC(o->dcolor[3 * id + ch], weight * dpix[ch]);
                             dL_dalpha += ((c * T) - (1.0f / (1.0f - alpha)) * (-ar[ch])) * dpix[ch];
                             bg_dot += a->bg[ch] * dpix[ch];
                         }
                         const float invd = 1.f / g->depths[id];
                         ard += weight * invd;
-                        if (o->dinvdepth) o->dinvdepth[id] += weight * dinv;
+                        if (o->dinvdepth) ORC_ACC(o->dinvdepth[id], weight * dinv);
                         dL_dalpha += ((invd * T) - (1.0f / (1.0f - alpha)) * (-ard)) * dinv;
                         dL_dalpha += (-T_final / (1.0f - alpha)) * bg_dot;
                         T *= (1.0f - alpha);
@@ -724,12 +797,12 @@ static void blend_backward_alt(const orc_args *a, const orc_geom *g, const orc_i
                         const float gdx = G * dx, gdy = G * dy;
                         const float dG_ddelx = -gdx * co[0] - gdy * co[1];
                         const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                        o->dmean2D[3 * id] += dL_dG * dG_ddelx * ddelx_dx;
-                        o->dmean2D[3 * id + 1] += dL_dG * dG_ddely * ddely_dy;
-                        o->dconic[4 * id] += -0.5f * gdx * dx * dL_dG;
-                        o->dconic[4 * id + 1] += -0.5f * gdx * dy * dL_dG;
-                        o->dconic[4 * id + 3] += -0.5f * gdy * dy * dL_dG;
-                        o->dopacity[id] += G * dL_dalpha;
+                        ORC_ACC(o->dmean2D[3 * id], dL_dG * dG_ddelx * ddelx_dx);
+                        ORC_ACC(o->dmean2D[3 * id + 1], dL_dG * dG_ddely * ddely_dy);
+                        ORC_ACC(o->dconic[4 * id], -0.5f * gdx * dx * dL_dG);
+                        ORC_ACC(o->dconic[4 * id + 1], -0.5f * gdx * dy * dL_dG);
+                        ORC_ACC(o->dconic[4 * id + 3], -0.5f * gdy * dy * dL_dG);
+                        ORC_ACC(o->dopacity[id], G * dL_dalpha);
                     }
                 }
         }
@@ -888,7 +961,9 @@ void orc_backward(const orc_args *a, const orc_geom *g, const orc_img *im, int R
     if (a->alt) blend_backward_alt(a, g, im, dL_dpix, dL_dinv, o);
     else if (R > 0) blend_backward(a, g, im, dL_dpix, dL_dinv, o);
     const float *cov3Ds = a->cov3D_precomp ? a->cov3D_precomp : g->cov3D;
-    /* computeCov2DCUDA */
+    /* computeCov2DCUDA (rows are per Gaussian unless render indices may repeat or write a parent's row) */
+    const int par = a->indices == NULL && a->parent_indices == NULL;
+#pragma omp parallel for schedule(static) if (par)
     for (int t_idx = 0; t_idx < a->P; t_idx++) {
         if (!(g->radii[t_idx] > 0)) continue;
         const float *c3 = cov3Ds + 6 * t_idx;
@@ -965,6 +1040,7 @@ void orc_backward(const orc_args *a, const orc_geom *g, const orc_img *im, int R
     }
     /* preprocessCUDA backward */
     const float *proj = a->projmatrix;
+#pragma omp parallel for schedule(static) if (par)
     for (int t_idx = 0; t_idx < a->P; t_idx++) {
         if (!(g->radii[t_idx] > 0)) continue;
         int idx = a->indices ? a->indices[t_idx] : t_idx;

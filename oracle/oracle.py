@@ -14,6 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _SRC = os.path.join(_HERE, "hlgs_oracle.c")
 _LIB = os.path.join(_HERE, "build", "libhlgs_oracle.so")
+_LIB_OMP = os.path.join(_HERE, "build", "libhlgs_oracle_omp.so")  # all-cores timing leg of bench.py only
 
 _f = C.POINTER(C.c_float)
 _i = C.POINTER(C.c_int)
@@ -22,12 +23,14 @@ _b = C.POINTER(C.c_uint8)
 
 
 def build(force=False):
-    """Compile the oracle with gcc (serial, no fast-math, no FMA contraction)."""
+    """Compile the oracle with gcc (serial, no fast-math, no FMA contraction), and the same source with OpenMP
+    for the all-cores CPU baseline (libhlgs_oracle_omp.so; its gradient sums use atomics, so it is never a
+    parity reference)."""
     os.makedirs(os.path.dirname(_LIB), exist_ok=True)
-    if not force and os.path.exists(_LIB) and os.path.getmtime(_LIB) >= os.path.getmtime(_SRC):
-        return _LIB
-    subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-ffp-contract=off",
-                           "-fno-fast-math", "-o", _LIB, _SRC, "-lm"])
+    base = ["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-ffp-contract=off", "-fno-fast-math"]
+    for lib_, extra in ((_LIB, []), (_LIB_OMP, ["-fopenmp"])):
+        if force or not os.path.exists(lib_) or os.path.getmtime(lib_) < os.path.getmtime(_SRC):
+            subprocess.check_call(base + extra + ["-o", lib_, _SRC, "-lm"])
     return _LIB
 
 
@@ -55,14 +58,18 @@ class _Grads(C.Structure):
                 ("dmean3D", _f), ("dcov3D", _f), ("dsh", _f), ("dscale", _f), ("drot", _f), ("ddc", _f)]
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
+def lib(omp=False):
+    """The serial oracle (omp=False, every parity check) or its OpenMP build (timing only)."""
+    L = _libs.get(omp)
+    if L is None:
         build()
-        L = C.CDLL(_LIB)
+        L = C.CDLL(_LIB_OMP if omp else _LIB)
+        L.orc_set_alpha_mode.argtypes = [C.c_int]
+        L.orc_get_alpha_mode.restype = C.c_int
+        L.orc_num_threads.restype = C.c_int
         L.orc_forward_preprocess.restype = C.c_int
         L.orc_forward_preprocess.argtypes = [C.POINTER(_Args), C.POINTER(_Geom)]
         L.orc_forward_render.restype = None
@@ -85,8 +92,34 @@ def lib():
         L.orc_lod_interp_backward.argtypes = [C.c_int, C.c_int, C.c_int, _i, _i, _f, _f, _f, _f, _f, _f,
                                               _f, _f, _f, _f, _f, _f]
         L.orc_sh_colors.argtypes = [C.c_int, C.c_int, C.c_int, _f, _f, _f, _f, _b]
-        _lib = L
-    return _lib
+        _libs[omp] = L
+    return L
+
+
+def set_reference_order(on, omp=False):
+    """Alpha decisions in the reference's own float op order (True) or the shared A-17 contract (False, the
+    default and the bit-exact gate); see orc_set_alpha_mode in hlgs_oracle.c."""
+    lib(omp).orc_set_alpha_mode(int(bool(on)))
+
+
+class reference_order:
+    """Context manager: the oracle decides alpha in the reference's float op order inside the block."""
+
+    def __init__(self, omp=False):
+        self.omp = omp
+
+    def __enter__(self):
+        self.prev = lib(self.omp).orc_get_alpha_mode()
+        set_reference_order(True, self.omp)
+        return self
+
+    def __exit__(self, *exc):
+        set_reference_order(self.prev, self.omp)
+        return False
+
+
+def num_threads(omp=True):
+    return lib(omp).orc_num_threads()
 
 
 def _p(a, t=_f):
@@ -133,9 +166,9 @@ def _make_args(scene, cam, keep):
     return a, P
 
 
-def forward(scene, cam, do_depth=True):
+def forward(scene, cam, do_depth=True, omp=False):
     """Full forward: returns a Frame with color (3,H,W), radii, invdepth, seen and all intermediates."""
-    L = lib()
+    L = lib(omp)
     keep = []
     a, P = _make_args(scene, cam, keep)
     W, H = int(cam["W"]), int(cam["H"])
@@ -173,12 +206,13 @@ def forward(scene, cam, do_depth=True):
         L.orc_forward_render(C.byref(a), C.byref(fr.geom), C.byref(fr.img), R, _p(fr.color),
                              _p(fr.invdepth) if do_depth else C.cast(None, _f), _p(fr.seen, _i))
     fr.W, fr.H = W, H
+    fr.omp = omp
     return fr
 
 
 def backward(fr, scene, dL_dcolor, dL_dinvdepth=None):
     """Gradients in the reference's return order (rasterize_points.cu:244) as a dict."""
-    L = lib()
+    L = lib(getattr(fr, "omp", False))
     Pf = int(np.asarray(scene["means3D"]).shape[0])
     M = fr.args.M
     g = {k: np.zeros(s, np.float32) for k, s in dict(

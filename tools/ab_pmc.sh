@@ -3,7 +3,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 V=hierarchical-lod-gaussians_amd/lib/variants
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stage-timing"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --no-stage-timing"
 for v in ${VARIANTS:-C}; do
   if [ $v = C ]; then L=""; else L=$V/$v.so; fi
   HLGS_LIBRARY=$L timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${PMC:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU} \

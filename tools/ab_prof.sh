@@ -11,7 +11,7 @@ for v in $VARS; do
 done
 for v in $VARS; do
   if [ $v = C ]; then L=""; else L=$V/$v.so; fi
-  HLGS_LIBRARY=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/abp_$v -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-stage-timing --steps 30 > gpurun_out/abp_$v.log 2>&1 || exit 1
+  HLGS_LIBRARY=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/abp_$v -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extras --no-stage-timing --steps 30 > gpurun_out/abp_$v.log 2>&1 || exit 1
   python3 - "$v" gpurun_out/abp_$v/run_kernel_stats.csv gpurun_out/abp_$v.log <<'PY'
 import csv, json, sys
 v, path, log = sys.argv[1:]

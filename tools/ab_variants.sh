@@ -12,6 +12,6 @@ done
 for r in 1 2; do
 for v in $VARS; do
   if [ $v = C ]; then L=""; else L=$V/$v.so; fi
-  HLGS_LIBRARY=$L timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/abc_$v$r.log 2>&1 || exit 1
+  HLGS_LIBRARY=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras > gpurun_out/abc_$v$r.log 2>&1 || exit 1
   tail -1 gpurun_out/abc_$v$r.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); s=d['stages']; print('$v', d['value'], 'fwd', s['blend_fwd']['ms'], 'bwd', s['blend_bwd']['ms'], 'gauss', s['gauss_bwd']['ms'], 'pre', s['preprocess']['ms'])"
 done; done

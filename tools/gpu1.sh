@@ -6,7 +6,7 @@ rc=$?
 echo "pytest rc=$rc"
 tail -30 gpurun_out/pytest1.log
 if [ $rc -eq 0 ] || [ $rc -eq 1 ]; then
-  timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench1.log 2>&1
+  timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/bench1.log 2>&1
   echo "bench rc=$?"
   tail -5 gpurun_out/bench1.log
 fi

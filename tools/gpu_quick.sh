@@ -7,7 +7,7 @@ rc=$?
 echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_q.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for i in 1 2 3; do
-  timeout -k 10 400 python bench.py --no-cpu-baseline "$@" > gpurun_out/bench_q$i.log 2>&1; rc=$?
+  timeout -k 10 400 python bench.py --no-cpu-baseline --no-extras "$@" > gpurun_out/bench_q$i.log 2>&1; rc=$?
   echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
   tail -1 gpurun_out/bench_q$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], round(sum(v['ms'] for v in d['stages'].values()),4))"
 done

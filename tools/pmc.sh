@@ -3,7 +3,7 @@ set -eu
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stage-timing"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --no-stage-timing"
 timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
 run() { name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d gpurun_out/pmc/$name -o run --output-format csv -- $B > gpurun_out/pmc/$name.log 2>&1
