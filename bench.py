@@ -90,6 +90,32 @@ def cpu_model():
     return "unknown"
 
 
+def _mem(tag):
+    """HLGS_BENCH_MEM=1: peak and current host RSS after each leg, on stderr (diagnostics only)."""
+    if os.environ.get("HLGS_BENCH_MEM"):
+        import resource
+        cur = int(open("/proc/self/statm").read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+        print(f"[mem] {tag}: rss {cur / 2**30:.2f} GiB, peak {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.2f} GiB",
+              file=sys.stderr, flush=True)
+
+
+def _mem_watchdog(limit_gib=40):
+    """HLGS_BENCH_MEM=1: dump every thread's stack and exit if host RSS passes limit_gib (diagnostics only)."""
+    import faulthandler
+    import threading
+
+    def watch():
+        while True:
+            time.sleep(0.05)
+            cur = int(open("/proc/self/statm").read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+            if cur > limit_gib * 2**30:
+                print(f"[mem] RSS over {limit_gib} GiB; stacks:", file=sys.stderr, flush=True)
+                faulthandler.dump_traceback(all_threads=True)
+                sys.stderr.flush()
+                os._exit(3)
+    threading.Thread(target=watch, daemon=True).start()
+
+
 def _oracle_frame(O, sc, cam, g, gd, omp=False):
     t0 = time.perf_counter()
     fr = O.forward(sc, cam, do_depth=True, omp=omp)
@@ -182,7 +208,7 @@ def settings_for(cam, deg, dev, do_depth=True):
         do_depth=do_depth)
 
 
-def bench_config3(P, W, H, deg, dev, iters=20, tau_px=6.0):
+def bench_config3(P, deg, W, H, dev, iters=20, tau_px=6.0):
     """configs[2]: the hierarchical-LOD training step of train_single.py / render_post
     (gaussian_renderer/__init__.py:304-347): expand_to_size_dynamic at tau -> get_interpolation_weights_dynamic
     -> the child/parent lerp (interpolate_lod) -> rasterize forward + backward at W x H -> lerp backward, on a
@@ -195,6 +221,7 @@ def bench_config3(P, W, H, deg, dev, iters=20, tau_px=6.0):
     t0 = time.perf_counter()
     hier = S.make_dynamic_hierarchy(S.make_gaussians(P, deg, cam, seed=0), seed=0)
     build_s = time.perf_counter() - t0
+    _mem("config3 hierarchy built")
     N = hier["nodes"].shape[0]
     d = lambda a, **kw: torch.tensor(np.ascontiguousarray(a), device=dev, **kw)  # noqa: E731
     nodes = d(hier["nodes"])
@@ -237,6 +264,7 @@ def bench_config3(P, W, H, deg, dev, iters=20, tau_px=6.0):
         lerp(); raster(); backward()  # noqa: E702
 
     full()
+    _mem("config3 first chain")
     stages = {"expand_to_size_dynamic": _median_ms(cut, iters),
               "get_interpolation_weights_dynamic": _median_ms(weights, iters),
               "interpolate_lod_fwd": _median_ms(lerp, iters),
@@ -309,8 +337,10 @@ def bench_config4_one_gpu(P, deg, W, H, dev, steps, warmup):
     """configs[3]'s per-GPU work (P Gaussians, one 1080p view, fwd+bwd) on one GPU with no exchange: the N = 1
     point against which the driver's N > 1 lines (same per-rank work plus the all-reduce) scale."""
     step, st = make_step(P, deg, W, H, dev, 0, 1)
+    _mem("config4 scene")
     for _ in range(warmup):
         step()
+        _mem("config4 warmup step")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -338,6 +368,8 @@ def main():
     ap.add_argument("--no-stage-timing", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the config3 and config4_one_gpu legs")
     args = ap.parse_args()
+    if os.environ.get("HLGS_BENCH_MEM"):
+        _mem_watchdog()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -431,10 +463,13 @@ def main():
             roofline["valu_issue"] = dict(wave_instr_per_launch=valu, achieved_Ginstr_s=round(rate, 1),
                                           peak_Ginstr_s=VALU_PEAK_GINSTR, frac=round(rate / VALU_PEAK_GINSTR, 4))
     cpu = parity = config3 = config4 = None
+    _mem("main step")
     if rank == 0 and world == 1 and not args.no_extras:
         config3 = bench_config3(1_000_000 if args.P is None else P, deg, W, H, dev)
         torch.cuda.empty_cache()
+        _mem("config3")
         config4 = bench_config4_one_gpu(4_000_000, deg, W, H, dev, max(5, args.steps // 2), 2)
+        _mem("config4")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, ref, ref_order = cpu_baseline(P, deg, W, H)
         step()  # one more step on the same inputs, outputs kept for the parity check
