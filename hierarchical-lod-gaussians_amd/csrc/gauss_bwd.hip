@@ -1,0 +1,515 @@
+// gauss_bwd.hip -- per-Gaussian backward kernels for gfx950, compiled without FMA contraction.
+//
+// Reference semantics (submodules/hierarchy-rasterizer/cuda_rasterizer):
+//   k_gauss_bwd  <- computeCov2DCUDA            backward.cu:147-326
+//                 + preprocessCUDA<3> backward  backward.cu:398-495 (cov3D :330-393)
+//   k_sh_bwd     <- computeColorFromSH backward backward.cu:23-142
+//
+// These kernels are HBM bound (one thread per Gaussian), so they are built with -ffp-contract=off like the
+// preprocess and the oracle: every product and sum is rounded on its own, in the oracle's order.  The conic ->
+// cov2D -> cov3D chain is ill-conditioned for wide, nearly axis-aligned splats ((denom - c_xx c_yy) cancels to
+// -c_xy^2), and contracting it moved scale / rotation gradients by up to 0.4% against the oracle.
+// k_gauss_bwd sums each Gaussian's contiguous per-(tile, Gaussian) records written by k_blend_bwd
+// (raster_bwd.hip) in a fixed order, so the backward has no float atomics and is bitwise reproducible.
+#include "hlgs_internal.h"
+#include "hlgs_math.h"
+
+namespace hlgs {
+// cov3d_fwd (forward.cu:181-215) with every product and sum rounded on its own, in the preprocess's order (both
+// files are compiled without FMA contraction; the explicit roundings keep it so under any flags): the recomputed
+// covariance is bit-identical to the one the forward used, so the forward need not store it (24 bytes per Gaussian written there and read here).
+__device__ __forceinline__ void cov3d_exact(f3 scale, float mod, float4 q, float out[6])
+{
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    auto M_ = [](float u, float v) { return __fmul_rn(u, v); };
+    auto A_ = [](float u, float v) { return __fadd_rn(u, v); };
+    auto S_ = [](float u, float v) { return __fsub_rn(u, v); };
+    const m3 R = mcols(S_(1.f, M_(2.f, A_(M_(y, y), M_(z, z)))), M_(2.f, S_(M_(x, y), M_(r, z))),
+                       M_(2.f, A_(M_(x, z), M_(r, y))), M_(2.f, A_(M_(x, y), M_(r, z))),
+                       S_(1.f, M_(2.f, A_(M_(x, x), M_(z, z)))), M_(2.f, S_(M_(y, z), M_(r, x))),
+                       M_(2.f, S_(M_(x, z), M_(r, y))), M_(2.f, A_(M_(y, z), M_(r, x))),
+                       S_(1.f, M_(2.f, A_(M_(x, x), M_(y, y)))));
+    m3 Sm = mcols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    Sm.m[0][0] = M_(mod, scale.x);
+    Sm.m[1][1] = M_(mod, scale.y);
+    Sm.m[2][2] = M_(mod, scale.z);
+    m3 Mm, Sig;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int row = 0; row < 3; row++)  // mmul(S, R)
+            Mm.m[c][row] = A_(A_(M_(Sm.m[0][row], R.m[c][0]), M_(Sm.m[1][row], R.m[c][1])), M_(Sm.m[2][row], R.m[c][2]));
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int row = 0; row < 3; row++)  // mmul(mtrans(M), M)
+            Sig.m[c][row] = A_(A_(M_(Mm.m[row][0], Mm.m[c][0]), M_(Mm.m[row][1], Mm.m[c][1])), M_(Mm.m[row][2], Mm.m[c][2]));
+    out[0] = Sig.m[0][0]; out[1] = Sig.m[0][1]; out[2] = Sig.m[0][2];
+    out[3] = Sig.m[1][1]; out[4] = Sig.m[1][2]; out[5] = Sig.m[2][2];
+}
+
+// One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
+// backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
+template <bool HIER, bool ALT>
+__global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
+                                                   BwdScratch rec, hlgs_grads o, float fx, float fy, int has_depth)
+{
+    const int t_idx = blockIdx.x * 256 + threadIdx.x;
+    const bool vis = t_idx < a.P && radii[t_idx] > 0;
+    // Gaussians with more than kWide record slots (rects over many tiles) are summed by their whole wave, lane-
+    // strided, with a fixed butterfly at the end -- deterministic, and one wide splat no longer serialises a lane
+    // over thousands of slots.  Done before any lane leaves, so every lane of the wave takes part.
+    constexpr uint32_t kWide = 32;
+    uint32_t r_end = 0, r_start = 0;
+    if (vis) {
+        r_end = g.point_offsets[t_idx];
+        r_start = r_end - g.tiles_touched[t_idx];
+    }
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f, s8 = 0.f, s9 = 0.f;
+    {
+        uint64_t wide = __ballot(vis && r_end - r_start > kWide);
+        const int lane = threadIdx.x & 63;
+        while (wide) {
+            const int src = __ffsll((long long)wide) - 1;
+            wide &= wide - 1;
+            const uint32_t ws = (uint32_t)__shfl((int)r_start, src, 64), we = (uint32_t)__shfl((int)r_end, src, 64);
+            const int sidx = t_idx - lane + src;  // the wide Gaussian's rasterised index
+            float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
+            float kx = 0.f, ky = 0.f, kthr = 0.f;
+            int kx0 = 0, ky0 = 0, kw = 1;
+            if (ALT) {
+                const float4 r0 = g.splat[4 * (size_t)sidx], r1 = g.splat[4 * (size_t)sidx + 1];
+                const float4 r3 = g.splat[4 * (size_t)sidx + 3];
+                kx = r0.x; ky = r0.y;
+                kco = make_float4(r0.z, r0.w, r1.x, r1.y);
+                kthr = alt_keep_threshold(kco.w);
+                kx0 = __float_as_int(r3.y) & 0xffff;
+                ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
+                kw = __float_as_int(r3.z);
+            }
+            float p[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            for (uint32_t r = ws + lane; r < we; r += 64) {
+                if (ALT) {
+                    const int k = (int)(r - ws);
+                    if (!alt_tile_keep(kx, ky, kco, kthr, kx0 + k % kw, ky0 + k / kw)) continue;
+                }
+                const float4 A = rec.rec[3 * (size_t)r];
+                const float4 B = rec.rec[3 * (size_t)r + 1];
+                const float4 Cc = rec.rec[3 * (size_t)r + 2];
+                p[0] += A.x; p[1] += A.y; p[2] += A.z; p[3] += A.w;
+                p[4] += B.x; p[5] += B.y; p[6] += B.z; p[7] += B.w;
+                p[8] += Cc.x; p[9] += Cc.y;
+            }
+#pragma unroll
+            for (int v = 0; v < 10; v++)
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) p[v] += __shfl_xor(p[v], off, 64);
+            if (lane == src) {
+                s0 = p[0]; s1 = p[1]; s2 = p[2]; s3 = p[3]; s4 = p[4];
+                s5 = p[5]; s6 = p[6]; s7 = p[7]; s8 = p[8]; s9 = p[9];
+            }
+        }
+    }
+    if (t_idx >= a.P) return;
+    const int idx = HIER ? a.indices[t_idx] : t_idx;
+    const int M3 = a.M * 3;
+    if (!vis) {
+        if (!HIER) {
+            o.dmean2D[3 * idx] = 0.f; o.dmean2D[3 * idx + 1] = 0.f; o.dmean2D[3 * idx + 2] = 0.f;
+            o.dcolor[3 * idx] = 0.f; o.dcolor[3 * idx + 1] = 0.f; o.dcolor[3 * idx + 2] = 0.f;
+            o.dopacity[idx] = 0.f;
+            o.dmean3D[3 * idx] = 0.f; o.dmean3D[3 * idx + 1] = 0.f; o.dmean3D[3 * idx + 2] = 0.f;
+            for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = 0.f;
+            if (o.dsh && !a.shs)
+                for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+            if (o.ddc && !a.shs) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
+            o.dscale[3 * idx] = 0.f; o.dscale[3 * idx + 1] = 0.f; o.dscale[3 * idx + 2] = 0.f;
+            reinterpret_cast<float4*>(o.drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        return;
+    }
+    // ---- per-Gaussian sum of the blend records (fixed order => deterministic); wide ones were summed above
+    const uint32_t end = r_end - r_start > kWide ? r_start : r_end, start = r_start;
+    constexpr bool alt = ALT;
+    float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
+    float kx = 0.f, ky = 0.f, kthr = 0.f;
+    int kx0 = 0, ky0 = 0, kw = 1;
+    if (alt) {  // slots of tiles the binning culled (alt_tile_keep) hold no record: skip them
+        const float4 r0 = g.splat[4 * (size_t)t_idx], r1 = g.splat[4 * (size_t)t_idx + 1];
+        const float4 r3 = g.splat[4 * (size_t)t_idx + 3];
+        kx = r0.x; ky = r0.y;
+        kco = make_float4(r0.z, r0.w, r1.x, r1.y);
+        kthr = alt_keep_threshold(kco.w);
+        kx0 = __float_as_int(r3.y) & 0xffff;
+        ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
+        kw = __float_as_int(r3.z);
+    }
+    // per-Gaussian inputs of the covariance / projection backward, loaded before the record sum so their
+    // latency overlaps it
+    float c3[6];
+    if (a.cov3D_precomp || HIER) {
+        const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
+        for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
+    } else {  // not stored by the forward: recomputed from the scale and rotation the forward used
+        cov3d_exact(mk(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]), a.scale_modifier,
+                    reinterpret_cast<const float4*>(a.rotations)[idx], c3);
+    }
+    const f3 mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    // records four at a time: all loads of a group are in flight together, the sums stay in slot order
+    for (uint32_t r0 = start; r0 < end; r0 += 4) {
+        float4 A[4], B[4], Cc[4];
+        bool use[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r = r0 + k;
+            use[k] = r < end;
+            if (alt && use[k]) {
+                const int kk = (int)(r - start);
+                use[k] = alt_tile_keep(kx, ky, kco, kthr, kx0 + kk % kw, ky0 + kk / kw);
+            }
+            if (use[k]) {
+                A[k] = rec.rec[3 * (size_t)r];
+                B[k] = rec.rec[3 * (size_t)r + 1];
+                Cc[k] = rec.rec[3 * (size_t)r + 2];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!use[k]) continue;
+            s0 += A[k].x; s1 += A[k].y; s2 += A[k].z; s3 += A[k].w;
+            s4 += B[k].x; s5 += B[k].y; s6 += B[k].z; s7 += B[k].w;
+            s8 += Cc[k].x; s9 += Cc[k].y;
+        }
+    }
+    o.dmean2D[3 * idx] = s0;
+    o.dmean2D[3 * idx + 1] = s1;
+    o.dmean2D[3 * idx + 2] = 0.f;
+    o.dcolor[3 * idx] = s6;
+    o.dcolor[3 * idx + 1] = s7;
+    o.dcolor[3 * idx + 2] = s8;
+
+    // ---- computeCov2DCUDA (backward.cu:147-326)
+    Cov2D k;
+    cov2d_eval(mean, fx, fy, a.tanfovx, a.tanfovy, c3, a.viewmatrix, k);
+    const float xg = k.txtz < -k.limx || k.txtz > k.limx ? 0.f : 1.f;
+    const float yg = k.tytz < -k.limy || k.tytz > k.limy ? 0.f : 1.f;
+    float c_xx = k.cov.m[0][0], c_xy = k.cov.m[0][1], c_yy = k.cov.m[1][1];
+    const float h_var = 0.3f;
+    const float det_cov = c_xx * c_yy - c_xy * c_xy;
+    c_xx += h_var;
+    c_yy += h_var;
+    const float det_h = c_xx * c_yy - c_xy * c_xy;
+    float dop = s5;
+    float dxx = 0.f, dxy = 0.f, dyy = 0.f;
+    if (!alt || a.antialiasing) {  // the alt rasterizer applies the AA term only with antialiasing (backward.cu:212-245)
+        const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+        const float d_hs = s5 * a.opacities[idx];
+        dop = s5 * hs;
+        const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
+        const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
+        const float sqv = w * w + w * (x + y) + x * y - z * z;
+        const float denom_f = d_inside / (sqv * sqv);
+        dxx = w * (w * y + y * y + z * z) * denom_f;
+        dyy = w * (w * x + x * x + z * z) * denom_f;
+        dxy = -2.f * w * z * (w + x + y) * denom_f;
+    }
+    const float dcx = s2, dcy = s3, dcz = s4;
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const m3& Tm = k.T;
+    const m3& V = k.Vrk;
+    float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#define TT(c, r) Tm.m[c][r]
+#define VK(c, r) V.m[c][r]
+    if (denom2inv != 0) {
+        dxx += denom2inv * (-c_yy * c_yy * dcx + 2 * c_xy * c_yy * dcy + (denom - c_xx * c_yy) * dcz);
+        dyy += denom2inv * (-c_xx * c_xx * dcz + 2 * c_xx * c_xy * dcy + (denom - c_xx * c_yy) * dcx);
+        dxy += denom2inv * 2 * (c_xy * c_yy * dcx - (denom + 2 * c_xy * c_xy) * dcy + c_xx * c_xy * dcz);
+        dc[0] = (TT(0, 0) * TT(0, 0) * dxx + TT(0, 0) * TT(1, 0) * dxy + TT(1, 0) * TT(1, 0) * dyy);
+        dc[3] = (TT(0, 1) * TT(0, 1) * dxx + TT(0, 1) * TT(1, 1) * dxy + TT(1, 1) * TT(1, 1) * dyy);
+        dc[5] = (TT(0, 2) * TT(0, 2) * dxx + TT(0, 2) * TT(1, 2) * dxy + TT(1, 2) * TT(1, 2) * dyy);
+        dc[1] = 2 * TT(0, 0) * TT(0, 1) * dxx + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dxy + 2 * TT(1, 0) * TT(1, 1) * dyy;
+        dc[2] = 2 * TT(0, 0) * TT(0, 2) * dxx + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dxy + 2 * TT(1, 0) * TT(1, 2) * dyy;
+        dc[4] = 2 * TT(0, 2) * TT(0, 1) * dxx + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dxy + 2 * TT(1, 1) * TT(1, 2) * dyy;
+    }
+    const float dT00 = 2 * (TT(0, 0) * VK(0, 0) + TT(0, 1) * VK(0, 1) + TT(0, 2) * VK(0, 2)) * dxx + (TT(1, 0) * VK(0, 0) + TT(1, 1) * VK(0, 1) + TT(1, 2) * VK(0, 2)) * dxy;
+    const float dT01 = 2 * (TT(0, 0) * VK(1, 0) + TT(0, 1) * VK(1, 1) + TT(0, 2) * VK(1, 2)) * dxx + (TT(1, 0) * VK(1, 0) + TT(1, 1) * VK(1, 1) + TT(1, 2) * VK(1, 2)) * dxy;
+    const float dT02 = 2 * (TT(0, 0) * VK(2, 0) + TT(0, 1) * VK(2, 1) + TT(0, 2) * VK(2, 2)) * dxx + (TT(1, 0) * VK(2, 0) + TT(1, 1) * VK(2, 1) + TT(1, 2) * VK(2, 2)) * dxy;
+    const float dT10 = 2 * (TT(1, 0) * VK(0, 0) + TT(1, 1) * VK(0, 1) + TT(1, 2) * VK(0, 2)) * dyy + (TT(0, 0) * VK(0, 0) + TT(0, 1) * VK(0, 1) + TT(0, 2) * VK(0, 2)) * dxy;
+    const float dT11 = 2 * (TT(1, 0) * VK(1, 0) + TT(1, 1) * VK(1, 1) + TT(1, 2) * VK(1, 2)) * dyy + (TT(0, 0) * VK(1, 0) + TT(0, 1) * VK(1, 1) + TT(0, 2) * VK(1, 2)) * dxy;
+    const float dT12 = 2 * (TT(1, 0) * VK(2, 0) + TT(1, 1) * VK(2, 1) + TT(1, 2) * VK(2, 2)) * dyy + (TT(0, 0) * VK(2, 0) + TT(0, 1) * VK(2, 1) + TT(0, 2) * VK(2, 2)) * dxy;
+#undef VK
+#undef TT
+    const m3& Wm = k.W;
+    const float dJ00 = Wm.m[0][0] * dT00 + Wm.m[0][1] * dT01 + Wm.m[0][2] * dT02;
+    const float dJ02 = Wm.m[2][0] * dT00 + Wm.m[2][1] * dT01 + Wm.m[2][2] * dT02;
+    const float dJ11 = Wm.m[1][0] * dT10 + Wm.m[1][1] * dT11 + Wm.m[1][2] * dT12;
+    const float dJ12 = Wm.m[2][0] * dT10 + Wm.m[2][1] * dT11 + Wm.m[2][2] * dT12;
+    const f3 t = k.t;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = xg * -fx * tz2 * dJ02;
+    const float dty = yg * -fy * tz2 * dJ12;
+    float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * t.x) * tz3 * dJ02 + (2 * fy * t.y) * tz3 * dJ12;
+    if (has_depth) dtz -= alt ? s9 * tz2 : s9 / (t.z * t.z);  // alt-rasterizer backward.cu:312
+    const float* vm = a.viewmatrix;
+    f3 dmean = mk(vm[0] * dtx + vm[1] * dty + vm[2] * dtz, vm[4] * dtx + vm[5] * dty + vm[6] * dtz,
+                  vm[8] * dtx + vm[9] * dty + vm[10] * dtz);
+
+    // ---- preprocessCUDA backward (backward.cu:398-495): screen-space mean -> world mean
+    const float* proj = a.projmatrix;
+    const f3 m = mean;
+    const float m_w = 1.0f / (xform44w(m, proj) + 0.0000001f);
+    const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+    const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+    f3 d2;
+    d2.x = (proj[0] * m_w - proj[3] * mul1) * s0 + (proj[1] * m_w - proj[3] * mul2) * s1;
+    d2.y = (proj[4] * m_w - proj[7] * mul1) * s0 + (proj[5] * m_w - proj[7] * mul2) * s1;
+    d2.z = (proj[8] * m_w - proj[11] * mul1) * s0 + (proj[9] * m_w - proj[11] * mul2) * s1;
+    dmean = add(dmean, d2);
+
+    // ---- SH backward (backward.cu:23-142) runs in k_sh_bwd, which adds its view-direction term to
+    //      dmean3D (or to the parent-deferred share) after this kernel.
+    if (!a.shs && o.dsh)
+        for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+    // alt without higher-order coefficients: the reference skips the whole SH backward (backward.cu:443),
+    // so even dc gets no gradient
+    if (!a.shs && o.ddc) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
+
+    // ---- cov3D backward (backward.cu:330-393)
+    float dscale[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.scales) {
+        const float4 q4 = reinterpret_cast<const float4*>(a.rotations)[idx];
+        const float qq[4] = {q4.x, q4.y, q4.z, q4.w};
+        const float r = qq[0], x = qq[1], y = qq[2], z = qq[3];
+        const m3 R = quat_rot(qq);
+        m3 S = mcols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        const f3 s = scl(a.scale_modifier, mk(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]));
+        S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
+        const m3 Mm = mmul(S, R);
+        const m3 dS = mcols(dc[0], 0.5f * dc[1], 0.5f * dc[2], 0.5f * dc[1], dc[3], 0.5f * dc[4], 0.5f * dc[2],
+                            0.5f * dc[4], dc[5]);
+        m3 M2 = Mm;
+        for (int c = 0; c < 3; c++)
+            for (int rr = 0; rr < 3; rr++) M2.m[c][rr] = 2.0f * Mm.m[c][rr];
+        const m3 dM = mmul(M2, dS);
+        const m3 Rt = mtrans(R);
+        m3 dMt = mtrans(dM);
+        for (int i = 0; i < 3; i++)
+            dscale[i] = Rt.m[i][0] * dMt.m[i][0] + Rt.m[i][1] * dMt.m[i][1] + Rt.m[i][2] * dMt.m[i][2];
+        for (int rr = 0; rr < 3; rr++) { dMt.m[0][rr] *= s.x; dMt.m[1][rr] *= s.y; dMt.m[2][rr] *= s.z; }
+        dq[0] = 2 * z * (dMt.m[0][1] - dMt.m[1][0]) + 2 * y * (dMt.m[2][0] - dMt.m[0][2]) + 2 * x * (dMt.m[1][2] - dMt.m[2][1]);
+        dq[1] = 2 * y * (dMt.m[1][0] + dMt.m[0][1]) + 2 * z * (dMt.m[2][0] + dMt.m[0][2]) + 2 * r * (dMt.m[1][2] - dMt.m[2][1]) - 4 * x * (dMt.m[2][2] + dMt.m[1][1]);
+        dq[2] = 2 * x * (dMt.m[1][0] + dMt.m[0][1]) + 2 * r * (dMt.m[2][0] - dMt.m[0][2]) + 2 * z * (dMt.m[1][2] + dMt.m[2][1]) - 4 * y * (dMt.m[2][2] + dMt.m[0][0]);
+        dq[3] = 2 * r * (dMt.m[0][1] - dMt.m[1][0]) + 2 * x * (dMt.m[2][0] + dMt.m[0][2]) + 2 * y * (dMt.m[1][2] + dMt.m[2][1]) - 4 * z * (dMt.m[1][1] + dMt.m[0][0]);
+    }
+    float dop_out = dop;
+    if (HIER) {
+        // backward.cu:458-494: the child's opacity/scale/rotation/SH gradients are dropped and
+        // (1 - t) of its mean gradient moves to the parent (added by k_parent_mean_add).
+        const int parent = a.parent_indices[t_idx];
+        if (parent != -1) {
+            const float tt = a.ts[t_idx];
+            dop_out = 0.f;
+            for (int i = 0; i < 3; i++) dscale[i] = 0.f;
+            for (int i = 0; i < 4; i++) dq[i] = 0.f;
+            rec.parent_dmean[3 * t_idx] = (1.0f - tt) * dmean.x;
+            rec.parent_dmean[3 * t_idx + 1] = (1.0f - tt) * dmean.y;
+            rec.parent_dmean[3 * t_idx + 2] = (1.0f - tt) * dmean.z;
+            dmean = mk(0.f, 0.f, 0.f);
+        }
+    }
+    o.dopacity[idx] = dop_out;
+    for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = dc[i];
+    o.dmean3D[3 * idx] = dmean.x;
+    o.dmean3D[3 * idx + 1] = dmean.y;
+    o.dmean3D[3 * idx + 2] = dmean.z;
+    o.dscale[3 * idx] = dscale[0];
+    o.dscale[3 * idx + 1] = dscale[1];
+    o.dscale[3 * idx + 2] = dscale[2];
+    reinterpret_cast<float4*>(o.drot)[idx] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+}
+
+// Basis function c of the reference's SH colour (forward.cu:20-67) and its gradient with respect to the
+// normalised view direction (the dRGBdx/dy/dz terms of backward.cu:55-139, per coefficient).
+__device__ __forceinline__ float sh_basis(int c, float x, float y, float z, float& gx, float& gy, float& gz)
+{
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    gx = gy = gz = 0.f;
+    switch (c) {
+    case 0: return kSH_C0;
+    case 1: gy = -kSH_C1; return -kSH_C1 * y;
+    case 2: gz = kSH_C1; return kSH_C1 * z;
+    case 3: gx = -kSH_C1; return -kSH_C1 * x;
+    case 4: gx = kSH_C2[0] * y; gy = kSH_C2[0] * x; return kSH_C2[0] * xy;
+    case 5: gy = kSH_C2[1] * z; gz = kSH_C2[1] * y; return kSH_C2[1] * yz;
+    case 6: gx = kSH_C2[2] * 2.f * -x; gy = kSH_C2[2] * 2.f * -y; gz = kSH_C2[2] * 2.f * 2.f * z;
+            return kSH_C2[2] * (2.f * zz - xx - yy);
+    case 7: gx = kSH_C2[3] * z; gz = kSH_C2[3] * x; return kSH_C2[3] * xz;
+    case 8: gx = kSH_C2[4] * 2.f * x; gy = kSH_C2[4] * 2.f * -y; return kSH_C2[4] * (xx - yy);
+    case 9: gx = kSH_C3[0] * 3.f * 2.f * xy; gy = kSH_C3[0] * 3.f * (xx - yy); return kSH_C3[0] * y * (3.f * xx - yy);
+    case 10: gx = kSH_C3[1] * yz; gy = kSH_C3[1] * xz; gz = kSH_C3[1] * xy; return kSH_C3[1] * xy * z;
+    case 11: gx = kSH_C3[2] * -2.f * xy; gy = kSH_C3[2] * (-3.f * yy + 4.f * zz - xx); gz = kSH_C3[2] * 4.f * 2.f * yz;
+             return kSH_C3[2] * y * (4.f * zz - xx - yy);
+    case 12: gx = kSH_C3[3] * -3.f * 2.f * xz; gy = kSH_C3[3] * -3.f * 2.f * yz;
+             gz = kSH_C3[3] * 3.f * (2.f * zz - xx - yy); return kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+    case 13: gx = kSH_C3[4] * (-3.f * xx + 4.f * zz - yy); gy = kSH_C3[4] * -2.f * xy; gz = kSH_C3[4] * 4.f * 2.f * xz;
+             return kSH_C3[4] * x * (4.f * zz - xx - yy);
+    case 14: gx = kSH_C3[5] * 2.f * xz; gy = kSH_C3[5] * -2.f * yz; gz = kSH_C3[5] * (xx - yy);
+             return kSH_C3[5] * z * (xx - yy);
+    default: gx = kSH_C3[6] * 3.f * (xx - yy); gy = kSH_C3[6] * -3.f * 2.f * xy; return kSH_C3[6] * x * (xx - 3.f * yy);
+    }
+}
+
+// SH backward (backward.cu:23-142), one thread per Gaussian.  The wave's 64 coefficient rows are staged
+// through LDS so global reads of shs and writes of dsh are contiguous float4 runs; each thread then
+// walks its own LDS row (coefficient loop unrolled at compile time), writes its dsh row in place and
+// the wave stores the rows back.  Runs after k_gauss_bwd, whose dcolor output is dL/dRGB, and adds
+// dnormvdv(dir, dL/ddir) to dmean3D -- or, for a hierarchy child with a parent, (1 - t) of it to the
+// parent-deferred share (backward.cu:458-494).
+// ALT (alt-rasterizer backward.cu:23-146): coefficient 0 is the separate dc row (gradient to ddc), and the
+// staged rows hold the M higher-order coefficients 1..M.
+template <bool HIER, int MT, bool ALT>  // MT = 0: staged row count a.M known only at run time (up to 16)
+__global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
+                                               BwdScratch rec, hlgs_grads o)
+{
+    constexpr int OFF = ALT ? 1 : 0;  // full coefficient index of staged row 0
+    constexpr int MC = MT ? MT : (16 - OFF);
+    const int M = MT ? MT : a.M;
+    const int M3 = 3 * M;
+    __shared__ float s_rows[64 * kShStride];
+    __shared__ int s_idx[64];
+    __shared__ int s_vis[64];
+    const int lane = threadIdx.x;
+    const int t0 = blockIdx.x * 64;
+    const int n = min(64, a.P - t0);
+    const int t_idx = t0 + lane;
+    const bool active = lane < n;
+    const int idx = active ? (HIER ? a.indices[t_idx] : t_idx) : 0;
+    const bool vis = active && radii[t_idx] > 0;
+    s_idx[lane] = idx;
+    s_vis[lane] = vis;
+    // the visible Gaussian's own inputs, issued before the row copy so both latencies overlap
+    f3 m = mk(0.f, 0.f, 0.f), dcol = mk(0.f, 0.f, 0.f);
+    uint32_t cl = 0;
+    if (vis) {
+        m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+        dcol = mk(o.dcolor[3 * idx], o.dcolor[3 * idx + 1], o.dcolor[3 * idx + 2]);
+        cl = g.clamped[t_idx];
+    }
+    __syncthreads();
+    // rows of invisible Gaussians are not read: they arrive as zeros, which is their dsh row
+    sh_rows_load<3 * MT>(a.shs, s_rows, s_idx, n, lane, M3, s_vis);
+    __syncthreads();
+    float* row = s_rows + lane * kShStride;
+    if (active) {
+        const bool dropped = HIER && a.parent_indices && a.parent_indices[t_idx] != -1;
+        if (!vis) {
+            if (ALT) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
+        } else {
+            const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+            const f3 dir_orig = sub(m, campos);
+            const float len = sqrtf(dot(dir_orig, dir_orig));
+            const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+            const float dR = (cl & 1u) ? 0.f : dcol.x;
+            const float dG = (cl & 2u) ? 0.f : dcol.y;
+            const float dB = (cl & 4u) ? 0.f : dcol.z;
+            const int ncoef = (a.D + 1) * (a.D + 1);
+            float vx = 0.f, vy = 0.f, vz = 0.f;
+            float basis[MC + OFF];
+#pragma unroll
+            for (int c = 0; c < MC + OFF; c++) {
+                float gx, gy, gz;
+                basis[c] = c < ncoef ? sh_basis(c, x, y, z, gx, gy, gz) : 0.f;
+                if (c > 0 && c < ncoef) {
+                    const float* sc = row + 3 * (c - OFF);
+                    const float proj = sc[0] * dR + sc[1] * dG + sc[2] * dB;
+                    vx += proj * gx;
+                    vy += proj * gy;
+                    vz += proj * gz;
+                }
+            }
+            if (ALT) {
+                o.ddc[3 * idx] = basis[0] * dR;
+                o.ddc[3 * idx + 1] = basis[0] * dG;
+                o.ddc[3 * idx + 2] = basis[0] * dB;
+            }
+#pragma unroll
+            for (int c = OFF; c < MC + OFF; c++) {
+                if (c - OFF >= M) break;
+                const float bs = dropped ? 0.f : basis[c];
+                row[3 * (c - OFF)] = bs * dR;
+                row[3 * (c - OFF) + 1] = bs * dG;
+                row[3 * (c - OFF) + 2] = bs * dB;
+            }
+            const f3 d = dnormvdv(dir_orig, mk(vx, vy, vz));
+            if (dropped) {
+                const float w = 1.0f - a.ts[t_idx];
+                rec.parent_dmean[3 * t_idx] += w * d.x;
+                rec.parent_dmean[3 * t_idx + 1] += w * d.y;
+                rec.parent_dmean[3 * t_idx + 2] += w * d.z;
+            } else {
+                o.dmean3D[3 * idx] += d.x;
+                o.dmean3D[3 * idx + 1] += d.y;
+                o.dmean3D[3 * idx + 2] += d.z;
+            }
+        }
+    }
+    __syncthreads();
+    sh_rows_copy<3 * MT, false>(o.dsh, s_rows, s_idx, n, lane, M3);
+}
+
+__global__ void __launch_bounds__(256) k_parent_mean_add(int P, const int* __restrict__ radii,
+                                                         const int* __restrict__ parent_indices,
+                                                         const float* __restrict__ pd, float* __restrict__ dmean3D)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= P || !(radii[t] > 0)) return;
+    const int p = parent_indices[t];
+    if (p == -1) return;
+    for (int i = 0; i < 3; i++) atomicAdd(&dmean3D[3 * p + i], pd[3 * t + i]);
+}
+
+void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
+                      const hlgs_grads& o, bool has_depth, hipStream_t s)
+{
+    const float fy = a.H / (2.0f * a.tanfovy);
+    const float fx = a.W / (2.0f * a.tanfovx);
+    const dim3 grid((a.P + 255) / 256), grid_sh((a.P + 63) / 64);
+#define HLGS_SHK(H, MT, AL) hipLaunchKernelGGL((k_sh_bwd<H, MT, AL>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o)
+#define HLGS_SHB(H)                                                                                        \
+    switch (a.M) {                                                                                         \
+    case 1: HLGS_SHK(H, 1, false); break;                                                                  \
+    case 4: HLGS_SHK(H, 4, false); break;                                                                  \
+    case 9: HLGS_SHK(H, 9, false); break;                                                                  \
+    case 16: HLGS_SHK(H, 16, false); break;                                                                \
+    default: HLGS_SHK(H, 0, false); break;                                                                 \
+    }
+    if (a.indices) {
+        hipLaunchKernelGGL((k_gauss_bwd<true, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
+        if (a.shs) HLGS_SHB(true)
+        if (a.parent_indices)
+            hipLaunchKernelGGL(k_parent_mean_add, grid, dim3(256), 0, s, a.P, radii, a.parent_indices,
+                               rs.parent_dmean, o.dmean3D);
+    } else {
+        if (a.variant == HLGS_VARIANT_ALT)
+            hipLaunchKernelGGL((k_gauss_bwd<false, true>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy,
+                               (int)has_depth);
+        else
+            hipLaunchKernelGGL((k_gauss_bwd<false, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy,
+                               (int)has_depth);
+        if (a.shs && a.variant == HLGS_VARIANT_ALT) {
+            switch (a.M) {  // rest coefficients of degree 1, 2, 3
+            case 3: HLGS_SHK(false, 3, true); break;
+            case 8: HLGS_SHK(false, 8, true); break;
+            case 15: HLGS_SHK(false, 15, true); break;
+            default: HLGS_SHK(false, 0, true); break;
+            }
+        } else if (a.shs) {
+            HLGS_SHB(false)
+        }
+    }
+#undef HLGS_SHB
+#undef HLGS_SHK
+}
+
+}  // namespace hlgs

@@ -267,6 +267,79 @@ def make_dynamic_hierarchy(leaves, skybox_points=0, seed=0):
     return out
 
 
+def chunk_weight(pos, chunk_id, centers, falloff=0.05):
+    """Per-Gaussian weight of chunk `chunk_id` (hierarchy_explicit_loader.cpp:22-52): 1 well inside the chunk's
+    Voronoi cell, 0 beyond (1 + falloff) x the distance to the nearest other chunk centre, linear in between.
+    pos (n,3), centers (C,3); float32 arithmetic as the loader's."""
+    pos = np.asarray(pos, np.float32)
+    c = np.asarray(centers, np.float32)
+    d_cur = np.linalg.norm(pos - c[chunk_id], axis=1).astype(np.float32)
+    others = [np.linalg.norm(pos - c[k], axis=1).astype(np.float32) for k in range(len(c)) if k != chunk_id]
+    d_oth = np.min(np.stack(others), 0) if others else np.full(len(pos), 1e12, np.float32)
+    f = np.float32(falloff)
+    a = np.float32(-1.0) / (np.float32(2.0) * f * d_oth)
+    b = (np.float32(1.0) + f) / (np.float32(2.0) * f)
+    w = np.where(d_cur <= (1 - f) * d_oth, np.float32(1.0),
+                 np.where(d_cur > (1 + f) * d_oth, np.float32(0.0), a * d_cur + b))
+    return w.astype(np.float32)
+
+
+def make_merged_hierarchy(chunks, centers, seed=0, root_scale=1e4):
+    """A multi-chunk hierarchy merged under one root, as mainHierarchyMerger.cpp:94-140 builds it, in the dynamic
+    (.dhier) node layout of make_dynamic_hierarchy.  chunks: one make_gaussians dict per chunk (its leaves);
+    centers (C,3): the chunk centres (center.txt).
+
+    Per chunk (HierarchyExplicitLoader::loadExplicit, hierarchy_explicit_loader.cpp:54-150): every Gaussian is
+    weighted by chunk_weight, dropped at weight 0, and its opacity scaled by the weight; the chunk's tree is built
+    over what is left (make_dynamic_hierarchy) and its root moved to the chunk centre (pos[0] = chunk_center).
+    The merge (mainHierarchyMerger.cpp:111-134) hangs the chunk roots under a new root whose size is set so that
+    no cut ever selects it (bounds[3] = 1e9 there; here its scales are `root_scale`, so max(scale)/distance exceeds
+    any threshold and the chunk roots get interpolation weight 1).  Node ids are pre-order: the root, then chunk
+    0's subtree, then chunk 1's, ..."""
+    subs = []
+    for k, leaves in enumerate(chunks):
+        w = chunk_weight(leaves["means3D"], k, centers)
+        keep = w > 0
+        kept = {key: (v[keep] if isinstance(v, np.ndarray) and v.shape[:1] == w.shape else v)
+                for key, v in leaves.items()}
+        kept["opacities"] = (kept["opacities"].reshape(-1) * w[keep]).astype(np.float32)[:, None]
+        h = make_dynamic_hierarchy(kept, seed=seed + k)
+        h["means3D"] = h["means3D"].copy()
+        h["means3D"][0] = np.asarray(centers[k], np.float32)
+        subs.append(h)
+    sizes = [h["nodes"].shape[0] for h in subs]
+    G = 1 + sum(sizes)
+    nodes = np.zeros((G, 6), np.int32)
+    nodes[0] = (0, -1, len(subs), 1, 0, -1)
+    out = {k: [] for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+    roots = []
+    off = 1
+    for k, h in enumerate(subs):
+        n = h["nodes"].copy()
+        n[:, 0] += 1
+        n[:, 1] = np.where(n[:, 1] >= 0, n[:, 1] + off, 0)
+        n[:, 3] = np.where(n[:, 2] > 0, n[:, 3] + off, 0)
+        n[:, 4] = np.where(n[:, 4] > 0, n[:, 4] + off, 0)
+        n[0, 4] = off + sizes[k] if k + 1 < len(subs) else 0
+        nodes[off:off + sizes[k]] = n
+        roots.append(off)
+        for key in out:
+            out[key].append(h[key])
+        off += sizes[k]
+    cat = {key: np.concatenate(v) for key, v in out.items()}
+    w = np.array([float(cat["opacities"][r - 1, 0]) for r in roots])
+    cm = (w[:, None] * np.stack([cat["means3D"][r - 1] for r in roots])).sum(0) / max(w.sum(), 1e-12)
+    root = dict(means3D=cm.astype(np.float32)[None], scales=np.full((1, 3), root_scale, np.float32),
+                rotations=np.array([[1, 0, 0, 0]], np.float32), opacities=np.array([[w.max()]], np.float32),
+                shs=np.mean(np.stack([cat["shs"][r - 1] for r in roots]), 0, keepdims=True).astype(np.float32))
+    res = {key: np.concatenate([root[key], cat[key]]) for key in out}
+    res["nodes"] = nodes
+    res["sh_degree"] = chunks[0].get("sh_degree", 0)
+    res["skybox_points"] = 0
+    res["chunk_roots"] = np.array(roots, np.int32)
+    return res
+
+
 def _mat_to_quat_fast(Rm):
     """Vectorised branch-free variant for large trees (same convention as _mat_to_quat)."""
     m = Rm

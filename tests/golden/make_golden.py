@@ -10,6 +10,15 @@ where /root/reference exists; the fixtures are committed so tests never need the
   golden_loss.npz    utils/loss_utils.l1_loss / ssim values and their autograd gradients w.r.t. the rendered image,
                      and the full training loss of train_single.py:106-118 (L1, D-SSIM and the masked inverse-depth
                      L1) with its gradients w.r.t. image and inverse depth, in float32 on the CPU.
+  golden_cov3d.npz   the Python covariance of get_covariance (build_scaling_rotation + strip_symmetric,
+                     scene/gaussian_model.py:678-682, utils/general_utils.py:79-110): K1's cov3D (forward.cu:181-215).
+  golden_lerp.npz    render_post's child/parent lerp (gaussian_renderer/__init__.py:304-339) executed from the
+                     reference module itself, and its autograd leaf gradients (lerp_fixture explains the two
+                     stand-in modules that let gaussian_renderer import without its CUDA extensions).
+
+Device shim: the reference's Python hard-codes device='cuda' in a few tensor factories; _CudaToCpu (a torch
+function mode) allocates those on the CPU here.  The intended SPT cut (scene/gaussian_model.py:158-181) is
+unreachable code after a `return`, so it cannot be executed: it stays pinned by its restatement only.
 
 Only data (inputs and expected outputs) is written; no reference source is copied.
 """
@@ -103,6 +112,135 @@ def main():
             loss[f"{k}_{i}"] = v
     np.savez_compressed(os.path.join(OUT, "golden_loss.npz"), **loss)
     print("wrote golden_sh.npz, golden_camera.npz, golden_loss.npz")
+    cov3d_fixture(rng)
+    lerp_fixture(rng)
+
+
+class _CudaToCpu(torch.overrides.TorchFunctionMode):
+    """The reference's Python hard-codes device='cuda' in tensor factories (utils/general_utils.py:87,111;
+    gaussian_renderer/__init__.py:259,326,333-334); this container has no GPU, so inside this mode such a
+    factory call allocates on the CPU instead.  Nothing else about the call changes."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = dict(kwargs or {})
+        if str(kwargs.get("device", "")).startswith("cuda"):
+            kwargs["device"] = "cpu"
+        return func(*args, **kwargs)
+
+
+def cov3d_fixture(rng):
+    """golden_cov3d.npz: the covariance GaussianModel.get_covariance hands the rasterizer when
+    pipe.compute_cov3D_python is set: covariance_activation = build_covariance_from_scaling_rotation
+    (scene/gaussian_model.py:678-682), i.e. utils/general_utils.build_scaling_rotation(modifier * scaling,
+    rotation), L @ L^T, strip_symmetric -- run from the reference's own general_utils on unnormalised quaternions
+    (get_covariance passes _rotation, build_rotation normalises)."""
+    from utils.general_utils import build_scaling_rotation, strip_symmetric
+    out = {}
+    for i, (P, mod) in enumerate([(500, 1.0), (300, 0.7), (200, 1.9)]):
+        scales = np.exp(rng.normal(-3.0, 1.0, (P, 3))).astype(np.float32)
+        rots = rng.normal(0, 1, (P, 4)).astype(np.float32) * rng.uniform(0.2, 3.0, (P, 1)).astype(np.float32)
+        with _CudaToCpu():
+            L = build_scaling_rotation(mod * torch.tensor(scales), torch.tensor(rots))
+            cov = strip_symmetric(L @ L.transpose(1, 2))
+        out[f"scales_{i}"], out[f"rotations_{i}"] = scales, rots
+        out[f"modifier_{i}"], out[f"cov3D_{i}"] = np.float32(mod), cov.numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(OUT, "golden_cov3d.npz"), **out)
+    print("wrote golden_cov3d.npz")
+
+
+def lerp_fixture(rng):
+    """golden_lerp.npz: render_post's child/parent interpolation (gaussian_renderer/__init__.py:304-339) executed
+    from the reference's own module, and its autograd backward.  gaussian_renderer imports the CUDA rasterizer
+    packages at module level; they are not importable here, so two stand-in modules are registered before the
+    import: `diff_gaussian_rasterization`, whose GaussianRasterizer records the tensors render_post hands it (the
+    lerped means3D / scales / rotations / opacities / shs: exactly what the fixture needs) and returns a zero
+    image, and an empty `alt_gaussian_rasterization`.  The lerp itself is the reference's code, run unmodified.
+    Per case: inputs (activated parameters, render/parent indices, weights, skybox rows), the lerped tensors, and
+    the leaf gradients for a seeded upstream gradient on each lerped tensor."""
+    import types
+    captured = {}
+
+    class _Settings:
+        def __init__(self, **kw):
+            self.__dict__.update(kw)
+
+    class _Rasterizer:
+        def __init__(self, raster_settings):
+            self.rs = raster_settings
+
+        def __call__(self, **kw):
+            captured.update(kw)
+            H, W = int(self.rs.image_height), int(self.rs.image_width)
+            n = kw["means3D"].shape[0]
+            return torch.zeros(3, H, W), torch.ones(n, dtype=torch.int32), None
+
+    dgr = types.ModuleType("diff_gaussian_rasterization")
+    dgr.GaussianRasterizationSettings, dgr.GaussianRasterizer, dgr._C = _Settings, _Rasterizer, None
+    saved = {k: sys.modules.get(k) for k in ("diff_gaussian_rasterization", "alt_gaussian_rasterization",
+                                             "gaussian_renderer")}
+    sys.modules["diff_gaussian_rasterization"] = dgr
+    sys.modules["alt_gaussian_rasterization"] = types.ModuleType("alt_gaussian_rasterization")
+    sys.modules.pop("gaussian_renderer", None)
+    real_range = torch.range  # a Python-level wrapper the function mode does not see (skybox rows, :326)
+
+    def cpu_range(*a, **kw):
+        if str(kw.get("device", "")).startswith("cuda"):
+            kw["device"] = "cpu"
+        return real_range(*a, **kw)
+    torch.range = cpu_range
+    try:
+        from gaussian_renderer import render_post
+        out = {}
+        for i, (G, n, sky, deg) in enumerate([(300, 120, 0, 3), (500, 260, 7, 3), (200, 90, 3, 1)]):
+            M = (deg + 1) ** 2
+            leaves = dict(xyz=rng.normal(0, 2, (G, 3)), scaling=np.exp(rng.normal(-3, 0.5, (G, 3))),
+                          rotation=rng.normal(0, 1, (G, 4)), opacity=rng.uniform(0.02, 0.98, (G, 1)),
+                          features=rng.normal(0, 0.3, (G, M, 3)))
+            leaves["rotation"] /= np.linalg.norm(leaves["rotation"], axis=1, keepdims=True)
+            leaves = {k: v.astype(np.float32) for k, v in leaves.items()}
+            ridx = rng.choice(np.arange(sky, G), n, replace=False).astype(np.int32)
+            pidx = rng.integers(sky, G, n).astype(np.int32)
+            pidx[:3] = 0  # roots: parent index left at 0, weight 1 (A-11)
+            w = rng.uniform(0, 1, n).astype(np.float32)
+            w[:3] = 1.0
+            w[3:6] = 0.0
+            t = {k: torch.tensor(v, requires_grad=True) for k, v in leaves.items()}
+            pc = types.SimpleNamespace(get_xyz=t["xyz"], get_opacity=t["opacity"], get_scaling=t["scaling"],
+                                       get_rotation=t["rotation"], get_features=t["features"], skybox_points=sky,
+                                       active_sh_degree=deg, max_sh_degree=deg)
+            cam = types.SimpleNamespace(FoVx=1.0, FoVy=0.8, image_height=4, image_width=6,
+                                        world_view_transform=torch.eye(4), full_proj_transform=torch.eye(4),
+                                        camera_center=torch.zeros(3))
+            pipe = types.SimpleNamespace(compute_cov3D_python=False, convert_SHs_python=False, debug=False)
+            # render_post pads the weight / kids tensors it is handed to full size and reads [:num_entries]
+            wfull = torch.tensor(np.concatenate([w, np.zeros(G - n, np.float32)]))
+            kids = torch.full((G,), 2, dtype=torch.int32)
+            captured.clear()
+            with _CudaToCpu():
+                render_post(cam, pc, pipe, torch.zeros(3), render_indices=torch.tensor(ridx),
+                            parent_indices=torch.tensor(np.concatenate([pidx, np.zeros(G - n, np.int32)])),
+                            interpolation_weights=wfull, num_node_siblings=kids)
+            outs = [captured[k] for k in ("means3D", "scales", "rotations", "opacities", "shs")]
+            ups = [rng.normal(0, 1, tuple(o.shape)).astype(np.float32) for o in outs]
+            grads = torch.autograd.grad(sum((o * torch.tensor(u)).sum() for o, u in zip(outs, ups)),
+                                        [t[k] for k in ("xyz", "scaling", "rotation", "opacity", "features")])
+            for k, v in leaves.items():
+                out[f"{k}_{i}"] = v
+            out[f"render_indices_{i}"], out[f"parent_indices_{i}"], out[f"weights_{i}"] = ridx, pidx, w
+            out[f"skybox_points_{i}"] = np.int32(sky)
+            for k, o, u, g in zip(("means", "scales", "rots", "opac", "shs"), outs, ups, grads):
+                out[f"out_{k}_{i}"] = o.detach().numpy().astype(np.float32)
+                out[f"up_{k}_{i}"] = u
+                out[f"grad_{k}_{i}"] = g.numpy().astype(np.float32)
+        np.savez_compressed(os.path.join(OUT, "golden_lerp.npz"), **out)
+        print("wrote golden_lerp.npz")
+    finally:
+        torch.range = real_range
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
 
 
 if __name__ == "__main__":

@@ -96,7 +96,7 @@ def rel_err(a, b):
     return float(np.abs(a - b).max() / den)
 
 
-def grad_check(a, b, rtol=1e-3, atol_rel=1e-5):
+def grad_check(a, b, rtol=1e-3, atol_rel=1e-5, row_rtol=0.0):
     """Element-wise gradient criterion: |a - b| <= rtol * |b| + atol_rel * max|b| for every entry, so small entries
     (distant Gaussians' SH rows, cancelling sums) are checked too, not only the tensor's largest.  Returns
     (worst ratio |a - b| / bound, ok).  The floor atol_rel * max|b| covers entries whose float sum cancels: the GPU
@@ -105,15 +105,21 @@ def grad_check(a, b, rtol=1e-3, atol_rel=1e-5):
     if b.size == 0:
         return (0.0, a.size == 0)
     bound = rtol * np.abs(b) + atol_rel * max(np.abs(b).max(), 1e-30)
+    if row_rtol > 0 and b.ndim > 1:
+        # per-Gaussian floor: row_rtol x the largest entry of the same Gaussian's gradient (its own scale)
+        rows = b.reshape(b.shape[0], -1)
+        rmax = np.abs(rows).max(1).reshape((b.shape[0],) + (1,) * (b.ndim - 1))
+        bound = np.maximum(bound, rtol * np.abs(b) + row_rtol * rmax)
     ratio = float((np.abs(a - b) / bound).max())
     return ratio, ratio <= 1.0
 
 
-def assert_grad(name, a, b, tol=1e-3):
-    """Both gradient criteria: north_star's max|a-b| / max|b| <= tol, and grad_check element-wise."""
+def assert_grad(name, a, b, tol=1e-3, row_rtol=0.0):
+    """Both gradient criteria: north_star's max|a-b| / max|b| <= tol, and grad_check element-wise (row_rtol > 0 adds
+    grad_check's per-Gaussian floor)."""
     e = rel_err(a, b)
     assert e <= tol, f"{name}: rel err {e}"
-    ratio, ok = grad_check(a, b)
+    ratio, ok = grad_check(a, b, row_rtol=row_rtol)
     assert ok, f"{name}: element-wise |a-b| / (1e-3|b| + 1e-5 max|b|) = {ratio}"
 
 

@@ -266,3 +266,30 @@ def test_lod_interpolation_backward_wide_buckets(deg):
                               dict(means=gs[0], scales=gs[1], rots=gs[2], opac=gs[3], shs=gs[4]))
     for leaf_t, key in zip((m, s, r, o, sh), ("means", "scales", "rots", "opac", "shs")):
         np.testing.assert_allclose(leaf_t.grad.cpu().numpy().reshape(d[key].shape), d[key], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_lod_interpolation_matches_reference_render_post(i):
+    """interpolate_lod (forward and its gather backward) against render_post's lerp block executed from the
+    reference itself, and autograd through it (tests/golden/golden_lerp.npz, make_golden.py lerp_fixture)."""
+    import os
+    import gaussian_hierarchy as GH
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_lerp.npz"))
+    sky = int(z[f"skybox_points_{i}"])
+    leaves = [torch.tensor(z[f"{k}_{i}"], device=DEV, requires_grad=True)
+              for k in ("xyz", "scaling", "rotation", "opacity", "features")]
+    G = leaves[0].shape[0]
+    n = z[f"render_indices_{i}"].shape[0]
+    pad = lambda a, dt: torch.tensor(np.concatenate([a, np.zeros(G - n, a.dtype)]), device=DEV, dtype=dt)  # noqa
+    outs = GH.interpolate_lod(*leaves, torch.tensor(z[f"render_indices_{i}"], device=DEV),
+                              pad(z[f"parent_indices_{i}"], torch.int32), pad(z[f"weights_{i}"], torch.float32), sky)
+    keys = ("means", "scales", "rots", "opac", "shs")
+    for o, k in zip(outs, keys):
+        want = z[f"out_{k}_{i}"]
+        np.testing.assert_allclose(o.detach().cpu().numpy().reshape(want.shape), want, rtol=1e-6, atol=1e-7,
+                                   err_msg=k)
+    sum((o * torch.tensor(z[f"up_{k}_{i}"], device=DEV).reshape(o.shape)).sum() for o, k in zip(outs, keys)).backward()
+    for leaf, k in zip(leaves, keys):
+        want = z[f"grad_{k}_{i}"]
+        np.testing.assert_allclose(leaf.grad.cpu().numpy().reshape(want.shape), want, rtol=1e-5, atol=1e-6,
+                                   err_msg=k)

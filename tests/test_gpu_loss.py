@@ -34,9 +34,9 @@ def test_losses_match_reference_golden(i):
     tot, Ll1, Ls, Ld = loss.photometric_loss(img, g("gt"), float(z[f"lam_{i}"]), inv, g("mono"), g("mask"),
                                              float(z[f"dw_{i}"]))
     tot.backward()
-    assert abs(float(tot) - float(z[f"loss_{i}"])) <= 1e-5 * abs(float(z[f"loss_{i}"]))
-    assert abs(float(Ll1) - float(z[f"l1_{i}"])) <= 1e-5 * abs(float(z[f"l1_{i}"]))
-    assert abs(float(Ld) - float(z[f"depth_l1_{i}"])) <= 1e-5 * abs(float(z[f"depth_l1_{i}"]))
+    assert abs(float(tot.detach()) - float(z[f"loss_{i}"])) <= 1e-5 * abs(float(z[f"loss_{i}"]))
+    assert abs(float(Ll1.detach()) - float(z[f"l1_{i}"])) <= 1e-5 * abs(float(z[f"l1_{i}"]))
+    assert abs(float(Ld.detach()) - float(z[f"depth_l1_{i}"])) <= 1e-5 * abs(float(z[f"depth_l1_{i}"]))
     assert _rel(img.grad.cpu().numpy(), z[f"g_img_{i}"]) <= 1e-4
     assert _rel(inv.grad.cpu().numpy(), z[f"g_inv_{i}"]) <= 1e-6
 

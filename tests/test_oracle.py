@@ -302,3 +302,44 @@ def test_alt_oracle_culls_tiles_and_renders_bg_when_empty():
     fr = O.forward(sc, S.cam_numpy(cam))
     assert fr.R == 0
     np.testing.assert_array_equal(fr.color, np.broadcast_to(np.float32([0.5, 0.25, 0.75])[:, None, None], (3, 64, 64)))
+
+
+# ------------------------------------------------------------------------------------------------------
+# Reference-run fixtures for the Python pieces of the path (tests/golden/make_golden.py)
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_cov3d_matches_reference_build_covariance(i):
+    """K1's computeCov3D (forward.cu:181-215) in the oracle against the reference's own Python covariance
+    (build_scaling_rotation + strip_symmetric, scene/gaussian_model.py:678-682) on the normalised quaternions
+    get_rotation hands the rasterizer (the kernel does not normalise, gaussian_model.py:691)."""
+    z = np.load(os.path.join(GOLD, "golden_cov3d.npz"))
+    s, r, mod = z[f"scales_{i}"], z[f"rotations_{i}"], float(z[f"modifier_{i}"])
+    P = s.shape[0]
+    rn = (r / np.linalg.norm(r.astype(np.float64), axis=1, keepdims=True)).astype(np.float32)
+    cam = S.cam_numpy(S.make_camera(64, 64))
+    sc = dict(means3D=np.tile(np.array([[0.0, 0.0, 5.0]], np.float32), (P, 1)), scales=s, rotations=rn,
+              opacities=np.full((P, 1), 0.5, np.float32), colors_precomp=np.zeros((P, 3), np.float32),
+              scale_modifier=mod)
+    fr = O.forward(sc, cam)
+    want = z[f"cov3D_{i}"].astype(np.float64)
+    scale = np.abs(want).max(1, keepdims=True)  # per-Gaussian: the entries are products of scales
+    np.testing.assert_allclose(fr.cov3D / scale, want / scale, rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_lod_lerp_matches_reference_render_post(i):
+    """The oracle's lerp and its backward against render_post's interpolation block run from the reference
+    (gaussian_renderer/__init__.py:304-339) and torch autograd through it."""
+    z = np.load(os.path.join(GOLD, "golden_lerp.npz"))
+    sky = int(z[f"skybox_points_{i}"])
+    ri, pi, w = z[f"render_indices_{i}"], z[f"parent_indices_{i}"], z[f"weights_{i}"]
+    leaves = [z[f"{k}_{i}"] for k in ("xyz", "scaling", "rotation", "opacity", "features")]
+    keys = ("means", "scales", "rots", "opac", "shs")
+    out = O.lod_interp_forward(sky, ri, pi, w, *leaves)
+    for k in keys:
+        want = z[f"out_{k}_{i}"]
+        np.testing.assert_allclose(out[k].reshape(want.shape), want, rtol=1e-6, atol=1e-7, err_msg=k)
+    d = O.lod_interp_backward(sky, ri, pi, w, leaves[2], leaves[0].shape[0], {k: z[f"up_{k}_{i}"] for k in keys})
+    for k in keys:
+        want = z[f"grad_{k}_{i}"]
+        np.testing.assert_allclose(d[k].reshape(want.shape), want, rtol=1e-5, atol=1e-6, err_msg=k)
