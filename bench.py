@@ -17,6 +17,8 @@ N = 1 measures configs[1] (1M Gaussians); the line also carries, each timed on t
                      offline), stages separately and inclusive (SURVEY 8(d));
   config4_one_gpu    configs[3]'s per-GPU work (4M Gaussians, one view) on one GPU, the N = 1 point of the
                      multi-GPU curve;
+  config5            configs[4]: train_post.py's step (SPT cache, alt rasterizer, L1 + D-SSIM + depth L1, Adam) on a
+                     synthetic 2-chunk merged hierarchy over 1M leaves, camera moving every step;
   cpu_baseline       the oracle on one full frame on all host threads (OpenMP) and on one thread;
   parity             the GPU step against the oracle on the same inputs, in the shared arithmetic contract and in
                      the reference's own float operation order.
@@ -355,6 +357,99 @@ def bench_config4_one_gpu(P, deg, W, H, dev, steps, warmup):
     return out
 
 
+def merged_two_chunk_scene(P, seed=0):
+    """configs[4]'s scene: two chunks of P/2 leaves each (the second shifted 4 units right and 6 deeper), merged
+    under one root (hlgs_core.synthetic.make_merged_hierarchy, after mainHierarchyMerger.cpp:94-140), the SPT
+    structures of build_hierarchical_spt (train_post.py's setup) and the host parameter storage of a cached run."""
+    from hlgs_core import spt
+    from hlgs_core import synthetic as S
+    cam = S.make_camera(1920, 1080)
+    c0 = S.make_gaussians(P // 2, 3, cam, seed=seed + 1)
+    c1 = S.make_gaussians(P - P // 2, 3, cam, seed=seed + 2)
+    c1["means3D"] = c1["means3D"] + np.array([4.0, 0.0, 6.0], np.float32)
+    h = S.make_merged_hierarchy([c0, c1], np.array([[0, 0, 12], [4, 0, 18]], np.float32), seed=seed)
+    nodes = torch.tensor(h["nodes"])
+    xyz = torch.tensor(h["means3D"])
+    log_s = torch.log(torch.tensor(h["scales"]))
+    t0 = time.perf_counter()
+    b = spt.build_hierarchical_spt(nodes, xyz, log_s, 0, 0.5, 0.00228, 256)
+    build_s = time.perf_counter() - t0
+    shs = torch.tensor(h["shs"])
+    op = torch.tensor(h["opacities"]).reshape(-1, 1).clamp(1e-4, 1 - 1e-4)
+    storage = dict(xyz=xyz, f_dc=shs[:, :1].contiguous(), f_rest=shs[:, 1:].contiguous(),
+                   opacity=torch.log(op / (1 - op)), scaling=log_s, rotation=torch.tensor(h["rotations"]))
+    return b, storage, build_s, int(nodes.shape[0])
+
+
+def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080):
+    """configs[4]: train_post.py's training step on a 2-chunk merged hierarchy (synthetic: the example dataset is
+    not available offline), per iteration as train_post.py:323-812 orders it: SPTCache.step (coarse cut, cache
+    bookkeeping, SPT cut, write-back / load through pinned host storage) -> activations -> alt rasterizer
+    (antialiasing, active SH degree 1) -> L1 + D-SSIM (+ masked inverse-depth L1, train_single.py:111-118) ->
+    backward -> dense Adam.  The camera moves every step.  Median host-clock step and per-stage event medians."""
+    from alt_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from hlgs_core import synthetic as S
+    from hlgs_core.loss import photometric_loss
+    from hlgs_core.spt_cache import SPTCache
+    b, storage, build_s, G = merged_two_chunk_scene(P)
+    _mem("config5 scene")
+    cache = SPTCache(storage, b, 0, reuse_tolerance=0.9, device=dev)
+    rng = np.random.default_rng(1)
+    gt = torch.tensor(rng.uniform(0, 1, (3, H, W)).astype(np.float32), device=dev)
+    mono = torch.tensor(rng.uniform(0.05, 0.5, (1, H, W)).astype(np.float32), device=dev)
+    mask = torch.ones((1, H, W), device=dev)
+    bg = torch.zeros(3, device=dev)
+    lrs = dict(xyz=1.6e-4, f_dc=2.5e-3, f_rest=2.5e-3 / 20, opacity=5e-2, scaling=5e-3, rotation=1e-3)
+    path = [S.make_camera(W, H, T=np.array([0.03 * k, 0.01 * k, 0.2 * math.sin(0.3 * k)])) for k in range(steps + 3)]
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    stages = {k: [] for k in ("cache", "forward", "loss", "backward", "adam")}
+    step_ms, resident = [], []
+    for it, cam in enumerate(path):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e = [ev() for _ in range(6)]
+        e[0].record()
+        cache.step(cam["projmatrix"], cam["campos"])
+        e[1].record()
+        p = cache.params
+        s = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=cam["tanfovx"],
+                                          tanfovy=cam["tanfovy"], bg=bg, scale_modifier=1.0,
+                                          viewmatrix=cam["viewmatrix"].to(dev), projmatrix=cam["projmatrix"].to(dev),
+                                          sh_degree=sh_degree, campos=cam["campos"].to(dev), prefiltered=False,
+                                          debug=False, antialiasing=True)
+        means2D = torch.zeros_like(p["xyz"], requires_grad=True)
+        img, radii, invd = GaussianRasterizer(s)(
+            means3D=p["xyz"], means2D=means2D, dc=p["f_dc"], shs=p["f_rest"], opacities=torch.sigmoid(p["opacity"]),
+            scales=torch.exp(p["scaling"]), rotations=torch.nn.functional.normalize(p["rotation"]))
+        img = img.clamp(0, 1)
+        e[2].record()
+        loss = (photometric_loss(img, gt, 0.2, invd, mono, mask, 0.5) if depth else photometric_loss(img, gt, 0.2))[0]
+        e[3].record()
+        loss.backward()
+        e[4].record()
+        cache.optimizer_step(it, lrs)
+        e[5].record()
+        torch.cuda.synchronize()
+        if it >= 3:
+            step_ms.append((time.perf_counter() - t0) * 1e3)
+            for k, (a, bb) in zip(stages, zip(e[:-1], e[1:])):
+                stages[k].append(a.elapsed_time(bb))
+            resident.append(cache.render_indices.numel())
+        for q in p.values():
+            q.grad = None
+    ms = float(np.median(step_ms))
+    out = dict(workload=f"configs[4]: train_post.py step with the SPT cache on a 2-chunk merged hierarchy ({G} "
+                        f"nodes over {P} leaves), {W}x{H}, alt rasterizer (antialiasing, SH degree {sh_degree}), "
+                        f"L1 + D-SSIM{' + depth L1' if depth else ''}, dense Adam, camera moving every step",
+               spt_build_s=round(build_s, 3), resident_median=int(np.median(resident)), ms_per_step=round(ms, 3),
+               value=round(W * H / ms / 1e3, 1), unit="Mpix/s", steps=len(step_ms),
+               stages_ms={k: round(float(np.median(v)), 3) for k, v in stages.items()},
+               timing="median host clock around a synchronised step; stages: median event spans on torch's stream")
+    del cache
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -366,7 +461,7 @@ def main():
     ap.add_argument("--sh-degree", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-timing", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the config3 and config4_one_gpu legs")
+    ap.add_argument("--no-extras", action="store_true", help="skip the config3, config4_one_gpu and config5 legs")
     args = ap.parse_args()
     if os.environ.get("HLGS_BENCH_MEM"):
         _mem_watchdog()
@@ -462,7 +557,7 @@ def main():
             rate = valu / (ms * 1e-3) / 1e9
             roofline["valu_issue"] = dict(wave_instr_per_launch=valu, achieved_Ginstr_s=round(rate, 1),
                                           peak_Ginstr_s=VALU_PEAK_GINSTR, frac=round(rate / VALU_PEAK_GINSTR, 4))
-    cpu = parity = config3 = config4 = None
+    cpu = parity = config3 = config4 = config5 = None
     _mem("main step")
     if rank == 0 and world == 1 and not args.no_extras:
         config3 = bench_config3(1_000_000 if args.P is None else P, deg, W, H, dev)
@@ -470,6 +565,8 @@ def main():
         _mem("config3")
         config4 = bench_config4_one_gpu(4_000_000, deg, W, H, dev, max(5, args.steps // 2), 2)
         _mem("config4")
+        config5 = bench_config5(1_000_000, dev)
+        _mem("config5")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, ref, ref_order = cpu_baseline(P, deg, W, H)
         step()  # one more step on the same inputs, outputs kept for the parity check
@@ -496,7 +593,7 @@ def main():
             "config": {"workload": wl, "num_rendered": nr, "visible": V, "tiles": T,
                        "parallelism": f"view-dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "exchange": exchange_report,
-            "config3": config3, "config4_one_gpu": config4,
+            "config3": config3, "config4_one_gpu": config4, "config5": config5,
             "stages": stage_report, "stages_note": "untimed pass with events around every stage",
         }
         print(json.dumps(line))
