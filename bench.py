@@ -22,8 +22,10 @@ N = 1 measures configs[1] (1M Gaussians); the line also carries, each timed on t
   cpu_baseline       the oracle on one full frame on all host threads (OpenMP) and on one thread;
   parity             the GPU step against the oracle on the same inputs, in the shared arithmetic contract and in
                      the reference's own float operation order.
-N > 1 measures configs[3]: view-data parallel, weak scaling, each rank renders its own view of its own
-4M-Gaussian replica (--P overrides) and the gradients are all-reduced (RCCL over xGMI).
+N > 1: view-data parallel, weak scaling -- each rank renders its own view of its own replica of the same 1M-Gaussian
+scene (--P overrides) and the gradients are all-reduced (RCCL over xGMI), so the per-GPU work equals the N = 1 line's
+and the driver's per-N values form one weak-scaling curve.  The line then also carries config4: configs[3] (4M
+Gaussians per replica, one view per GPU, the same exchange) timed on the same N ranks.
 Inputs are synthetic (seeded), resident in HBM before timing starts.  Rank 0 prints one JSON line.
 """
 import argparse
@@ -450,12 +452,44 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080):
     return out
 
 
+def bench_config4_dp(P, deg, W, H, dev, rank, world, steps, warmup, backend):
+    """configs[3] on the launched ranks: P Gaussians per replica, one 1080p view per GPU, fwd+bwd, RCCL all-reduce of
+    every gradient; barrier + synchronise around the timed steps, the max over ranks."""
+    step, st = make_step(P, deg, W, H, dev, rank, world)
+    for _ in range(warmup):
+        step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(time_exchange=True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    ar_ms = float(np.mean([a.elapsed_time(b) for a, b in st["ar_events"]]))
+    t = torch.tensor([el, ar_ms], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el, ar_ms = float(t[0].item()), float(t[1].item())
+    nbytes = st["exchange"].flat.numel() * 4
+    out = dict(workload=f"configs[3]: {P} Gaussians per replica, SH deg {deg}, {W}x{H}, fwd+bwd with depth, one view "
+                        f"per GPU, {'RCCL' if backend == 'nccl' else backend} grad all-reduce",
+               value=round(world * W * H * steps / el / 1e6, 3), unit="Mpix/s", n_gpus=world,
+               ms_per_step=round(el / steps * 1e3, 4), steps=steps, allreduce_ms=round(ar_ms, 4),
+               bytes_per_step=nbytes, busbw_GBs=round(2 * (world - 1) / world * nbytes / (ar_ms * 1e-3) / 1e9, 1),
+               timing="barrier + synchronise around the timed steps, max over ranks; all-reduce: events around "
+                      "FlatGradExchange.allreduce() (mean, max over ranks)")
+    st["exchange"].close()
+    del step, st
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--P", type=int, default=None, help="Gaussians per replica (default: 1M at N = 1, 4M at N > 1)")
+    ap.add_argument("--P", type=int, default=None, help="Gaussians per replica (default 1M, configs[1])")
     ap.add_argument("--W", type=int, default=1920)
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--sh-degree", type=int, default=3)
@@ -484,7 +518,7 @@ def main():
     from hlgs_core import _lib as L
 
     W, H, deg = args.W, args.H, args.sh_degree
-    P = args.P if args.P is not None else (1_000_000 if world == 1 else 4_000_000)
+    P = args.P if args.P is not None else 1_000_000
     step, st = make_step(P, deg, W, H, dev, rank, world)
     params, exchange = st["params"], st["exchange"]
 
@@ -528,7 +562,7 @@ def main():
         elapsed, ar_ms = float(t[0].item()), float(t[1].item())
         nbytes = exchange.flat.numel() * 4
         exchange_report = dict(
-            collective=f"all_reduce AVG, {backend}", bytes_per_step=nbytes, collectives_per_step=getattr(
+            collective=f"all_reduce {'AVG' if backend == 'nccl' else 'SUM + 1/N scale'}, {backend}", bytes_per_step=nbytes, collectives_per_step=getattr(
                 exchange, "last_collectives", None), allreduce_ms=round(ar_ms, 4),
             busbw_GBs=round(2 * (world - 1) / world * nbytes / (ar_ms * 1e-3) / 1e9, 1) if ar_ms > 0 else None,
             note="events around FlatGradExchange.allreduce() on torch's stream in each timed step (mean; max over "
@@ -567,6 +601,8 @@ def main():
         _mem("config4")
         config5 = bench_config5(1_000_000, dev)
         _mem("config5")
+    if world > 1 and not args.no_extras:
+        config4 = bench_config4_dp(4_000_000, deg, W, H, dev, rank, world, max(5, args.steps // 2), 2, backend)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, ref, ref_order = cpu_baseline(P, deg, W, H)
         step()  # one more step on the same inputs, outputs kept for the parity check
@@ -582,8 +618,8 @@ def main():
                             "alpha < 1/255; forward.cu:538-560, backward.cu:614-643), same frame")
     if rank == 0:
         wl = (f"configs[1]: {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd with depth, one view" if world == 1 else
-              f"configs[3]: {P} Gaussians per replica, SH deg {deg}, {W}x{H}, fwd+bwd with depth, one view per GPU, "
-              + ("RCCL" if backend == "nccl" else backend) + " grad all-reduce")
+              f"configs[1] per GPU, view-data parallel: {P} Gaussians per replica, SH deg {deg}, {W}x{H}, fwd+bwd "
+              f"with depth, one view per GPU, " + ("RCCL" if backend == "nccl" else backend) + " grad all-reduce")
         line = {
             "metric": "forward+backward Mpix/s at 1080p (1M Gaussians); grad max-abs-err vs ref",
             "value": round(value, 3), "unit": "Mpix/s",
@@ -593,7 +629,7 @@ def main():
             "config": {"workload": wl, "num_rendered": nr, "visible": V, "tiles": T,
                        "parallelism": f"view-dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "exchange": exchange_report,
-            "config3": config3, "config4_one_gpu": config4, "config5": config5,
+            "config3": config3, ("config4_one_gpu" if world == 1 else "config4"): config4, "config5": config5,
             "stages": stage_report, "stages_note": "untimed pass with events around every stage",
         }
         print(json.dumps(line))
