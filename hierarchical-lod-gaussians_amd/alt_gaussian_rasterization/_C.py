@@ -14,7 +14,10 @@ import ctypes as C
 
 import torch
 
+_vp = C.c_void_p
+
 from hlgs_core import _lib as L
+from hlgs_core import dp
 from hlgs_core.dp import direct_grad
 
 
@@ -22,10 +25,11 @@ def _dev_f32(t, device):
     return t.to(device=device, dtype=torch.float32).contiguous()
 
 
-def _dest(src, shape, f32):
+def _dest(src, shape, f32, late=False):
     """Gradient output for input `src`: the view hlgs_core.dp.direct_grad offers (a view-DP exchange's flat buffer)
-    when its shape matches, else a fresh tensor.  Every kernel output row is written, so no zero-fill either way."""
-    d = direct_grad(src) if src is not None else None
+    when its shape matches, else a fresh tensor.  Every kernel output row is written, so no zero-fill either way.
+    late: the output is completed by the SH backward (dmean3D, dsh, ddc)."""
+    d = direct_grad(src, late) if src is not None else None
     return d if d is not None and tuple(d.shape) == tuple(shape) else torch.empty(shape, **f32)
 
 
@@ -115,9 +119,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     P = means3D.size(0)
     M = sh.size(1) if (sh is not None and sh.size(0) != 0 and sh.dim() > 1) else 0
     out = dict(dmean2D=torch.empty((P, 3), **f32), dcolor=torch.empty((P, 3), **f32),
-               dopacity=_dest(opacities, (P, 1), f32), dmean3D=_dest(means3D, (P, 3), f32),
-               dcov3D=torch.empty((P, 6), **f32), ddc=_dest(dc, (P, 1, 3), f32),
-               dsh=_dest(sh, (P, M, 3), f32), dscale=_dest(scales, (P, 3), f32),
+               dopacity=_dest(opacities, (P, 1), f32), dmean3D=_dest(means3D, (P, 3), f32, True),
+               dcov3D=torch.empty((P, 6), **f32), ddc=_dest(dc, (P, 1, 3), f32, True),
+               dsh=_dest(sh, (P, M, 3), f32, True), dscale=_dest(scales, (P, 3), f32),
                drot=_dest(rotations, (P, 4), f32))
     order = ("dmean2D", "dcolor", "dopacity", "dmean3D", "dcov3D", "ddc", "dsh", "dscale", "drot")
     if P == 0:
@@ -129,9 +133,15 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     dpix = dL_dout_color.contiguous().float()
     dinv = dL_dout_invdepth.contiguous().float() if dL_dout_invdepth is not None and dL_dout_invdepth.numel() else None
     scratch = torch.empty((lib.hlgs_backward_scratch_size(P, int(R)),), dtype=torch.uint8, device=dev)
-    L.check(lib.hlgs_rasterize_backward(C.byref(a), L.ptr(radii.contiguous()), L.ptr(geomBuffer), L.ptr(imageBuffer),
-                                        L.ptr(binningBuffer), int(R), L.ptr(scratch), L.ptr(dpix), L.ptr(dinv),
-                                        C.byref(g), L.stream()))
+    # the SH backward on an overlapping exchange's late stream (hlgs_core.dp.late_stream_for), else in order
+    late = dp.late_stream_for(out["dmean3D"], out["ddc"], out["dsh"])
+    L.check(lib.hlgs_rasterize_backward_split(C.byref(a), L.ptr(radii.contiguous()), L.ptr(geomBuffer),
+                                              L.ptr(imageBuffer), L.ptr(binningBuffer), int(R), L.ptr(scratch),
+                                              L.ptr(dpix), L.ptr(dinv), C.byref(g), L.stream(),
+                                              _vp(late.cuda_stream) if late is not None else None))
+    if late is not None:
+        dp.note_late_work(late, list(keep.values()) + list(out.values()) +
+                          [radii, geomBuffer, imageBuffer, binningBuffer, scratch, dpix, dinv])
     del keep
     return tuple(out[k] for k in order)
 

@@ -31,7 +31,7 @@ void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
 void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, const BwdScratch& rs,
                       int gx, int gy, const float* dL_dpix, const float* dL_dinv, hipStream_t s);
 void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
-                      const hlgs_grads& o, bool has_depth, hipStream_t s);
+                      const hlgs_grads& o, bool has_depth, hipStream_t s, hipStream_t late, hipEvent_t ev);
 void launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t s);
 void launch_relocation(int P, const float* oo, const float* so, const int* N, const float* binoms, int n_max,
                        float* on, float* sn, hipStream_t s);
@@ -464,9 +464,26 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     return HLGS_OK;
 }
 
+// one hand-over event per thread (a stream wait captures the event's state when it is enqueued, so the event is
+// free for the next call at once)
+static hipEvent_t handover_event()
+{
+    thread_local hipEvent_t ev = nullptr;
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+    return ev;
+}
+
 int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,
                             const void* binning, int R, void* scratch, const float* dL_dcolor,
                             const float* dL_dinvdepth, const hlgs_grads* out, void* stream)
+{
+    return hlgs_rasterize_backward_split(a, radii, geom, img, binning, R, scratch, dL_dcolor, dL_dinvdepth, out, stream,
+                                         nullptr);
+}
+
+int hlgs_rasterize_backward_split(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,
+                                  const void* binning, int R, void* scratch, const float* dL_dcolor,
+                                  const float* dL_dinvdepth, const hlgs_grads* out, void* stream, void* late_stream)
 {
     int rc = validate(a);
     if (rc) return rc;
@@ -500,9 +517,13 @@ int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const v
         stage_mark(s, ST_BLEND_BWD, false);
         if ((rc = check_stage(s, a->debug, "blend_bwd"))) return rc;
     }
+    hipStream_t late = (hipStream_t)late_stream;
+    hipEvent_t ev = nullptr;
+    if (late && !(ev = handover_event())) return fail(HLGS_ERR_DEVICE, "hipEventCreateWithFlags failed");
     stage_mark(s, ST_GAUSS_BWD, true);
-    launch_gauss_bwd(*a, radii, g, rs, *out, dL_dinvdepth != nullptr, s);
+    launch_gauss_bwd(*a, radii, g, rs, *out, dL_dinvdepth != nullptr, s, late, ev);
     stage_mark(s, ST_GAUSS_BWD, false);
+    if (late && (rc = check_stage(late, a->debug, "sh_bwd"))) return rc;
     return check_stage(s, a->debug, "gauss_bwd");
 }
 

@@ -469,13 +469,23 @@ __global__ void __launch_bounds__(256) k_parent_mean_add(int P, const int* __res
     for (int i = 0; i < 3; i++) atomicAdd(&dmean3D[3 * p + i], pd[3 * t + i]);
 }
 
+// late != nullptr: the kernels after k_gauss_bwd (SH backward, which completes dmean3D / dsh / ddc, and the
+// hierarchy parent add) run on `late` behind an event on `s`, and are not joined back into `s`: the opacity, scale and
+// rotation gradients are final on `s` while the SH backward still runs (hlgs_rasterize_backward_split).
 void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
-                      const hlgs_grads& o, bool has_depth, hipStream_t s)
+                      const hlgs_grads& o, bool has_depth, hipStream_t s, hipStream_t late, hipEvent_t ev)
 {
     const float fy = a.H / (2.0f * a.tanfovy);
     const float fx = a.W / (2.0f * a.tanfovx);
     const dim3 grid((a.P + 255) / 256), grid_sh((a.P + 63) / 64);
-#define HLGS_SHK(H, MT, AL) hipLaunchKernelGGL((k_sh_bwd<H, MT, AL>), grid_sh, dim3(64), 0, s, a, radii, g, rs, o)
+    const hipStream_t sl = late ? late : s;
+    auto hand_over = [&]() {
+        if (late) {
+            hipEventRecord(ev, s);
+            hipStreamWaitEvent(late, ev, 0);
+        }
+    };
+#define HLGS_SHK(H, MT, AL) hipLaunchKernelGGL((k_sh_bwd<H, MT, AL>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o)
 #define HLGS_SHB(H)                                                                                        \
     switch (a.M) {                                                                                         \
     case 1: HLGS_SHK(H, 1, false); break;                                                                  \
@@ -486,9 +496,10 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
     }
     if (a.indices) {
         hipLaunchKernelGGL((k_gauss_bwd<true, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
+        hand_over();
         if (a.shs) HLGS_SHB(true)
         if (a.parent_indices)
-            hipLaunchKernelGGL(k_parent_mean_add, grid, dim3(256), 0, s, a.P, radii, a.parent_indices,
+            hipLaunchKernelGGL(k_parent_mean_add, grid, dim3(256), 0, sl, a.P, radii, a.parent_indices,
                                rs.parent_dmean, o.dmean3D);
     } else {
         if (a.variant == HLGS_VARIANT_ALT)
@@ -497,6 +508,7 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
         else
             hipLaunchKernelGGL((k_gauss_bwd<false, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy,
                                (int)has_depth);
+        hand_over();
         if (a.shs && a.variant == HLGS_VARIANT_ALT) {
             switch (a.M) {  // rest coefficients of degree 1, 2, 3
             case 3: HLGS_SHK(false, 3, true); break;

@@ -10,7 +10,10 @@ import ctypes as C
 
 import torch
 
+_vp = C.c_void_p
+
 from hlgs_core import _lib as L
+from hlgs_core import dp
 from hlgs_core.dp import direct_grad
 
 
@@ -20,10 +23,11 @@ def _dev_f32(t, device):
     return t.to(device=device, dtype=torch.float32).contiguous()
 
 
-def _dest(src, shape, f32):
+def _dest(src, shape, f32, late=False):
     """Gradient output for input `src`: the view hlgs_core.dp.direct_grad offers (a view-DP exchange's flat buffer)
-    when its shape matches, else a fresh tensor.  Every kernel output row is written, so no zero-fill either way."""
-    d = direct_grad(src) if src is not None else None
+    when its shape matches, else a fresh tensor.  Every kernel output row is written, so no zero-fill either way.
+    late: the output is completed by the SH backward (dmean3D, dsh, ddc)."""
+    d = direct_grad(src, late) if src is not None else None
     return d if d is not None and tuple(d.shape) == tuple(shape) else torch.empty(shape, **f32)
 
 
@@ -123,8 +127,8 @@ def rasterize_gaussians_backward(bg, render_indices, parent_indices, ts, kids, m
     dev = means3D.device
     f32 = dict(dtype=torch.float32, device=dev)
     out = dict(dmean2D=torch.empty((P_full, 3), **f32), dcolor=torch.empty((P_full, 3), **f32),
-               dopacity=_dest(opacities, (P_full, 1), f32), dmean3D=_dest(means3D, (P_full, 3), f32),
-               dcov3D=torch.empty((P_full, 6), **f32), dsh=_dest(sh, (P_full, M, 3), f32),
+               dopacity=_dest(opacities, (P_full, 1), f32), dmean3D=_dest(means3D, (P_full, 3), f32, True),
+               dcov3D=torch.empty((P_full, 6), **f32), dsh=_dest(sh, (P_full, M, 3), f32, True),
                dscale=_dest(scales, (P_full, 3), f32), drot=_dest(rotations, (P_full, 4), f32))
     g = L.Grads(**{k: L.ptr(v) for k, v in out.items()})
     dpix = dL_dout_color.contiguous().float()
@@ -132,9 +136,15 @@ def rasterize_gaussians_backward(bg, render_indices, parent_indices, ts, kids, m
     if dL_dout_invdepth is not None and dL_dout_invdepth.numel() and dL_dout_invdepth.size(0) != 0:
         dinv = dL_dout_invdepth.contiguous().float()
     scratch = torch.empty((lib.hlgs_backward_scratch_size(P, int(R)),), dtype=torch.uint8, device=dev)
-    L.check(lib.hlgs_rasterize_backward(C.byref(a), L.ptr(radii.contiguous()), L.ptr(geomBuffer), L.ptr(imageBuffer),
-                                        L.ptr(binningBuffer), int(R), L.ptr(scratch), L.ptr(dpix), L.ptr(dinv),
-                                        C.byref(g), L.stream()))
+    # the SH backward on an overlapping exchange's late stream (hlgs_core.dp.late_stream_for), else in order
+    late = dp.late_stream_for(out["dmean3D"], out["dsh"])
+    L.check(lib.hlgs_rasterize_backward_split(C.byref(a), L.ptr(radii.contiguous()), L.ptr(geomBuffer),
+                                              L.ptr(imageBuffer), L.ptr(binningBuffer), int(R), L.ptr(scratch),
+                                              L.ptr(dpix), L.ptr(dinv), C.byref(g), L.stream(),
+                                              _vp(late.cuda_stream) if late is not None else None))
+    if late is not None:
+        dp.note_late_work(late, list(keep.values()) + list(out.values()) +
+                          [radii, geomBuffer, imageBuffer, binningBuffer, scratch, dpix, dinv])
     del keep
     return (out["dmean2D"], out["dcolor"], out["dopacity"], out["dmean3D"], out["dcov3D"], out["dsh"], out["dscale"],
             out["drot"])

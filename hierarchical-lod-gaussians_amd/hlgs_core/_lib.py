@@ -82,6 +82,8 @@ _SIGS = {
                                     _vp, _vp]),
     "hlgs_rasterize_backward": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
                                      C.POINTER(Grads), _vp]),
+    "hlgs_rasterize_backward_split": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
+                                           C.POINTER(Grads), _vp, _vp]),
     "hlgs_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "hlgs_compute_relocation": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "hlgs_adam_update": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, C.c_uint32, C.c_uint32, _vp]),

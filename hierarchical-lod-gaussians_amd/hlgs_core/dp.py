@@ -29,7 +29,7 @@ def _drop_entries(keys, token):
             del _DIRECT[k]
 
 
-def direct_grad(t):
+def direct_grad(t, late=False):
     """Destination for the gradient of input tensor `t`, or None.
 
     Used by the rasterizer backward (diff_gaussian_rasterization._C, alt_gaussian_rasterization._C): when `t` is a
@@ -40,7 +40,9 @@ def direct_grad(t):
 
     The view is handed out at most once per exchange round (until allreduce() / unpack() / release()): two
     rasterizer backwards of one autograd pass both see .grad unset, because AccumulateGrad runs only after both
-    finish; the second one gets None, so autograd sums two distinct tensors instead of the buffer with itself."""
+    finish; the second one gets None, so autograd sums two distinct tensors instead of the buffer with itself.
+
+    late: the backward completes this output on its late stream (the SH backward, see late_stream_for)."""
     e = _DIRECT.get(t.data_ptr()) if t is not None and t.numel() else None
     if e is None:
         return None
@@ -52,7 +54,48 @@ def direct_grad(t):
     if ex.claimed[i] or p.grad is not None or p.shape != t.shape or p.dtype != t.dtype or ex.flat.device != t.device:
         return None
     ex.claimed[i] = True
-    return ex.flat[ex.offsets[i]:ex.offsets[i] + ex.numels[i]].view_as(p)
+    ex.late[i] = bool(late)
+    v = ex.flat[ex.offsets[i]:ex.offsets[i] + ex.numels[i]].view_as(p)
+    _VIEWS[v.data_ptr()] = weakref.ref(ex)
+    return v
+
+
+# data_ptr of a view direct_grad handed out -> weak reference to its exchange (late_stream_for's lookup)
+_VIEWS = {}
+
+
+def late_stream_for(*views):
+    """The stream on which the rasterizer backward may run its late kernels (hlgs_rasterize_backward_split), or None.
+
+    Only when every late output (non-empty views: dmean3D, dsh, ddc) is a direct_grad view of one exchange built with
+    overlap=True: then autograd's only consumer of those tensors is AccumulateGrad adopting them (no kernel), and the
+    exchange joins the late stream before its collective over them (FlatGradExchange.allreduce / join)."""
+    exs = set()
+    for v in views:
+        if v is None or v.numel() == 0:
+            continue
+        r = _VIEWS.get(v.data_ptr())
+        ex = r() if r is not None else None
+        if ex is None or ex.late_stream is None or not ex.flat.data_ptr() <= v.data_ptr() < ex.flat.data_ptr() + \
+                4 * ex.flat.numel():
+            return None
+        exs.add(id(ex))
+        one = ex
+    return one.late_stream if len(exs) == 1 else None
+
+
+def note_late_work(stream, tensors):
+    """After a split backward: the exchange whose late stream this is joins it before reading the late gradients;
+    every tensor the late kernels touch is kept from reuse by the caching allocator until they finish."""
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda and t.numel():
+            t.record_stream(stream)
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    for r in list(_VIEWS.values()):
+        ex = r()
+        if ex is not None and ex.late_stream is stream:
+            ex.pending = ev
 
 
 class FlatGradExchange:
@@ -67,7 +110,7 @@ class FlatGradExchange:
     leaving several buckets to pipeline for a 1M-Gaussian model (236 MB of fp32 gradients).
     """
 
-    def __init__(self, params, bucket_bytes=64 << 20, average=True, group=None, direct=True):
+    def __init__(self, params, bucket_bytes=64 << 20, average=True, group=None, direct=True, overlap=True):
         self.params = list(params)
         self.numels = [p.numel() for p in self.params]
         self.offsets = []
@@ -84,6 +127,11 @@ class FlatGradExchange:
         self.buckets = [(s, min(s + per, total)) for s in range(0, total, per)]
         self.direct = []
         self.claimed = [False] * len(self.params)
+        self.late = [False] * len(self.params)
+        # overlap: the rasterizer backward runs its SH backward on late_stream (hlgs_rasterize_backward_split), so the
+        # collective over the gradients that are final before it (opacity, scale, rotation) starts while it runs
+        self.late_stream = torch.cuda.Stream(device=dev) if (overlap and direct and dev.type == "cuda") else None
+        self.pending = None  # event on late_stream after the last split backward
         self._token = object()
         if direct:
             me = weakref.ref(self)
@@ -99,9 +147,18 @@ class FlatGradExchange:
         self._finalizer()
         self.direct = []
 
+    def join(self):
+        """Order the current stream after the late kernels of the last split backward (the gradients they complete
+        -- dmean3D, dsh, ddc -- are readable on the current stream afterwards).  allreduce() joins by itself."""
+        if self.pending is not None:
+            torch.cuda.current_stream(self.flat.device).wait_event(self.pending)
+            self.pending = None
+
     def release(self):
         """End the exchange round without a collective: the flat buffer may be handed out again."""
+        self.join()
         self.claimed = [False] * len(self.params)
+        self.late = [False] * len(self.params)
 
     def _pack_range(self, a, b):
         for p, off, n in zip(self.params, self.offsets, self.numels):
@@ -137,9 +194,26 @@ class FlatGradExchange:
         base = self.flat.data_ptr()
         in_place = all(p.grad is not None and p.grad.data_ptr() == base + 4 * off
                        for p, off in zip(self.params, self.offsets))
-        spans = [(0, self.flat.numel())] if in_place else self.buckets
-        self.last_collectives = len(spans)
-        for a, b in spans:
+        split = in_place and any(self.late) and not all(self.late)
+        if split:
+            # the early gradients' runs first (their backward is done on this stream), then the join, then the late
+            # runs: elementwise the same reduction as one collective over the whole buffer
+            runs = []
+            for i, (off, n) in enumerate(zip(self.offsets, self.numels)):
+                if runs and runs[-1][2] == self.late[i] and runs[-1][1] == off:
+                    runs[-1][1] = off + n
+                else:
+                    runs.append([off, off + n, self.late[i]])
+            spans = [(a, b) for a, b, lt in runs if not lt] + [None] + [(a, b) for a, b, lt in runs if lt]
+        else:
+            self.join()
+            spans = [(0, self.flat.numel())] if in_place else self.buckets
+        self.last_collectives = sum(1 for sp in spans if sp is not None)
+        for sp in spans:
+            if sp is None:
+                self.join()
+                continue
+            a, b = sp
             self._pack_range(a, b)
             if native_avg:
                 try:
@@ -147,7 +221,7 @@ class FlatGradExchange:
                                                  async_op=True))
                     continue
                 except (RuntimeError, ValueError):  # a collective library without averaging: sum, scale below
-                    if a > 0:  # the op is rejected at its first use, before any bucket went out
+                    if works:  # the op is rejected at its first use, before any collective went out
                         raise
                     _AVG_OK[0] = native_avg = False
             works.append(dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=True))

@@ -10,7 +10,7 @@
  *        ext.cpp:16); split in two phases at the reference's own host sync (rasterizer_impl.cu:330-333)
  *        so that the caller allocates the binning buffer, as the reference's resize lambda did
  *        (rasterize_points.cu:28-34).
- *   hlgs_rasterize_backward                 <- RasterizeGaussiansBackwardCUDA, rasterize_points.cu:141-245
+ *   hlgs_rasterize_backward[_split]         <- RasterizeGaussiansBackwardCUDA, rasterize_points.cu:141-245
  *   hlgs_mark_visible                       <- CudaRasterizer::Rasterizer::markVisible,
  *        rasterizer_impl.cu:145-157 (called as _C.mark_visible at diff_gaussian_rasterization/__init__.py:174)
  *   hlgs_compute_relocation                 <- ComputeRelocationCUDA, rasterize_points.cu:248-271
@@ -149,6 +149,15 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
 int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,
                             const void* binning, int R, void* scratch, const float* dL_dcolor,
                             const float* dL_dinvdepth, const hlgs_grads* out, void* stream);
+/* hlgs_rasterize_backward with the kernels after the covariance backward (the SH backward, which completes dmean3D,
+ * dsh and ddc, and the hierarchy-mode parent mean add) launched on late_stream behind an event on stream, and NOT
+ * joined back: dopacity, dscale, drot, dcov3D, dmean2D and dcolor are final in stream order, dmean3D / dsh / ddc in
+ * late_stream order.  The caller joins (waits on late_stream) before reading those three.  A view-data-parallel
+ * exchange uses it to start the collective over the early gradients while the SH backward runs.
+ * late_stream = NULL is hlgs_rasterize_backward. */
+int hlgs_rasterize_backward_split(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,
+                                  const void* binning, int R, void* scratch, const float* dL_dcolor,
+                                  const float* dL_dinvdepth, const hlgs_grads* out, void* stream, void* late_stream);
 
 /* z > 0.2 visibility (auxiliary.h:164-189); present is P bytes (bool) */
 int hlgs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

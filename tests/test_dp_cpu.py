@@ -124,3 +124,58 @@ def test_view_dp_direct_gradients_gloo(tmp_path):
     for k, e in zip([f for f in r0.files if f != "flags"], expect):
         np.testing.assert_array_equal(r0[k], r1[k])
         np.testing.assert_allclose(r0[k], e, rtol=1e-6, atol=1e-7)
+
+
+def _split_worker(rank, world, port, out_dir):
+    """Early/late split of the exchange (the SH backward's outputs -- dmean3D, dsh -- arrive late): the collectives
+    over the early runs go first, then the late ones; the result must be bitwise the single collective's."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hierarchical-lod-gaussians_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hlgs_core.dp import FlatGradExchange, direct_grad
+    grads = [torch.tensor(g) for g in _rank_grads(rank, world)]  # means3D, scales, rotations, opacities, shs
+    params = [torch.zeros(g.shape, requires_grad=True) for g in grads]
+    late_set = {0, 4}
+
+    class Render(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, split, *ps):
+            ctx.ps, ctx.split = ps, split
+            return sum((p * 0).sum() for p in ps)
+
+        @staticmethod
+        def backward(ctx, _):
+            outs = []
+            for i, (p, g) in enumerate(zip(ctx.ps, grads)):
+                d = direct_grad(p, late=ctx.split and i in late_set)
+                d.copy_(g)
+                outs.append(d)
+            return (None,) + tuple(outs)
+
+    ex = FlatGradExchange(params)
+    res, ncoll = [], []
+    for split in (True, False):
+        for p in params:
+            p.grad = None
+        Render.apply(split, *params).backward()
+        ex.allreduce()
+        ncoll.append(ex.last_collectives)
+        res.append([p.grad.clone() for p in params])
+    ex.close()
+    same = all(torch.equal(a, b) for a, b in zip(*res))
+    np.savez(os.path.join(out_dir, f"s{rank}.npz"), *[t.numpy() for t in res[0]],
+             flags=np.array([same, ncoll == [3, 1]]))
+    dist.destroy_process_group()
+
+
+def test_view_dp_early_late_split_gloo(tmp_path):
+    world = 2
+    port = _free_port()
+    mp.spawn(_split_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    r0, r1 = np.load(tmp_path / "s0.npz"), np.load(tmp_path / "s1.npz")
+    assert r0["flags"].all() and r1["flags"].all()
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hierarchical-lod-gaussians_amd")]
+    expect = [(a + b) / 2 for a, b in zip(_rank_grads(0, world), _rank_grads(1, world))]
+    for k, e in zip([f for f in r0.files if f != "flags"], expect):
+        np.testing.assert_array_equal(r0[k], r1[k])
+        np.testing.assert_allclose(r0[k], e, rtol=1e-6, atol=1e-7)

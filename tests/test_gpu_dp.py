@@ -49,3 +49,58 @@ def test_backward_writes_into_exchange_buffer():
             torch.testing.assert_close(p.grad, 2 * a, rtol=1e-6, atol=1e-6)
     finally:
         ex.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alt", [False, True])
+def test_split_backward_on_late_stream_matches(alt):
+    """With an overlapping exchange the SH backward runs on the exchange's late stream
+    (hlgs_rasterize_backward_split); after join() -- or allreduce() -- every gradient is bitwise the in-order
+    backward's, read on the current stream with no device-wide synchronisation."""
+    from hlgs_core.dp import FlatGradExchange
+    cam = S.make_camera(160, 96)
+    sc = S.make_gaussians(6000, 3, cam, seed=5)
+    g, gd = S.upstream_grads(160, 96, seed=6)
+    t = lambda a: torch.tensor(np.ascontiguousarray(a), device="cuda", requires_grad=True)  # noqa: E731
+    gc, gi = torch.tensor(g, device="cuda"), torch.tensor(gd, device="cuda")
+    if alt:
+        from alt_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+        params = [t(sc["means3D"]), t(sc["scales"]), t(sc["rotations"]), t(sc["opacities"]), t(sc["shs"][:, :1]),
+                  t(sc["shs"][:, 1:])]
+        rast = GaussianRasterizer(GaussianRasterizationSettings(
+            image_height=96, image_width=160, tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
+            bg=torch.zeros(3, device="cuda"), scale_modifier=1.0, viewmatrix=cam["viewmatrix"].cuda(),
+            projmatrix=cam["projmatrix"].cuda(), sh_degree=3, campos=cam["campos"].cuda(), prefiltered=False,
+            debug=False, antialiasing=True))
+    else:
+        from diff_gaussian_rasterization import GaussianRasterizer
+        params = [t(sc["means3D"]), t(sc["scales"]), t(sc["rotations"]), t(sc["opacities"]), t(sc["shs"])]
+        rast = GaussianRasterizer(settings_for(cam, 3, "cuda", do_depth=True))
+
+    def backward():
+        for p in params:
+            p.grad = None
+        if alt:
+            m, s, r, o, dc, sh = params
+            color, _, inv = rast(means3D=m, means2D=torch.zeros_like(m, requires_grad=True), opacities=o, dc=dc,
+                                 shs=sh, scales=s, rotations=r)
+        else:
+            m, s, r, o, sh = params
+            color, _, inv = rast(means3D=m, means2D=torch.zeros_like(m, requires_grad=True), opacities=o, shs=sh,
+                                 scales=s, rotations=r)
+        torch.autograd.backward([color, inv], [gc, gi])
+
+    backward()
+    ref = [p.grad.clone() for p in params]
+    ex = FlatGradExchange(params)
+    try:
+        for _ in range(3):
+            backward()
+            assert ex.pending is not None, "the SH backward did not run on the late stream"
+            ex.join()  # no torch.cuda.synchronize(): ordering comes from the event alone
+            got = [p.grad.clone() for p in params]
+            ex.release()
+            for a, b in zip(ref, got):
+                assert torch.equal(a, b)
+    finally:
+        ex.close()
