@@ -27,6 +27,24 @@ struct PixB {
     uint32_t last;           // n_contrib
 };
 
+// 1/(1 - alpha) for alpha in [0, 0.99].  HLGS_BWD_RCP_NR > 0: that many Newton steps from the bit-pattern seed
+// instead of v_rcp_f32 (A/B of the transcendental's issue cost, tools/valu_probe.hip).
+#ifndef HLGS_BWD_RCP_NR
+#define HLGS_BWD_RCP_NR 0
+#endif
+__device__ __forceinline__ float rcp_one_minus(float alpha)
+{
+    const float d = 1.f - alpha;
+#if HLGS_BWD_RCP_NR > 0
+    float r = __int_as_float(0x7EF311C3 - __float_as_int(d));
+#pragma unroll
+    for (int i = 0; i < HLGS_BWD_RCP_NR; i++) r = r * fmaf(-d, r, 2.f);
+    return r;
+#else
+    return __builtin_amdgcn_rcpf(d);
+#endif
+}
+
 // One (pixel, splat) step of renderCUDA backward (backward.cu:601-718).  The splat's gradient terms
 // are linear in w = G * dL/dalpha and its moments over the pixels,
 //   dL/dmean2D = -o * (conic * [Sum w dx, Sum w dy]) * (W/2, H/2),
@@ -50,7 +68,7 @@ __device__ __forceinline__ uint64_t bwd_pair(PixB& p, uint32_t li, float dx, flo
     const uint64_t valid = __builtin_amdgcn_ballot_w64(li < p.last) & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) &
                            ~__builtin_amdgcn_ballot_w64(e2 < thr);
     if (__builtin_amdgcn_inverse_ballot_w64(valid)) {
-        const float r1m = __builtin_amdgcn_rcpf(1.f - alpha);  // 1/(1-alpha), alpha <= 0.99
+        const float r1m = rcp_one_minus(alpha);
         p.T = p.T * r1m;
         const float weight = alpha * p.T;
         float cd = col.x * p.dr + col.y * p.dg + col.z * p.db;
@@ -95,7 +113,7 @@ __device__ __forceinline__ uint64_t bwd_pair_pred(PixB& p, uint32_t li, float dx
     float alpha = my_alpha;
     if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
     alpha = vb ? alpha : 0.f;
-    const float r1m = __builtin_amdgcn_rcpf(1.f - alpha);
+    const float r1m = rcp_one_minus(alpha);
     p.T = p.T * r1m;
     const float weight = alpha * p.T;
     float cd = col.x * p.dr + col.y * p.dg + col.z * p.db;
