@@ -741,6 +741,32 @@ int hlgs_copy_rows(int T, const hlgs_row_copy* tables, int64_t n, const int* src
     return check_stage(s, false, "copy_rows");
 }
 
+int hlgs_copy_rows_packed(int T, const hlgs_row_copy* tables, int64_t n, const int* dev_rows, const int* host_rows,
+                          void* host, int64_t host_row_bytes, int to_host, void* stream)
+{
+    if (T < 0 || T > kMaxRowTables) return fail(HLGS_ERR_ARG, "at most 32 tables");
+    if (n < 0) return fail(HLGS_ERR_ARG, "n < 0");
+    if (host_row_bytes <= 0 || host_row_bytes % 64 || host_row_bytes > 64 * 4 * kPackSlots)
+        return fail(HLGS_ERR_ARG, "host row size must be a multiple of 64 bytes, at most 1024");
+    if (T == 0 || n == 0) return HLGS_OK;
+    if (!tables || !host) return fail(HLGS_ERR_ARG, "missing tables or host storage");
+    float* tabs[kMaxRowTables];
+    int words[kMaxRowTables];
+    int64_t used = 0;
+    for (int t = 0; t < T; t++) {
+        if (tables[t].row_bytes < 0 || tables[t].row_bytes % 4) return fail(HLGS_ERR_ARG, "row size must be a multiple of 4 bytes");
+        if (tables[t].row_bytes && !tables[t].src) return fail(HLGS_ERR_ARG, "missing tensor");
+        tabs[t] = (float*)tables[t].src;
+        words[t] = (int)(tables[t].row_bytes / 4);
+        used += tables[t].row_bytes;
+    }
+    if (used > host_row_bytes) return fail(HLGS_ERR_ARG, "the tables' rows exceed the host row");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_rows_packed(T, tabs, words, n, dev_rows, host_rows, (float*)host, (int)(host_row_bytes / 4), to_host != 0, s);
+    return check_stage(s, false, "copy_rows_packed");
+}
+
 int hlgs_adam_step(int T, const hlgs_adam_tensor* tensors, int64_t step, int skybox_rows, double beta1, double beta2,
                    double eps, void* stream)
 {

@@ -9,6 +9,9 @@
 //                      may be pinned host memory: the GPU reads and writes it directly over the host link
 //                      instead of a CPU gather/scatter plus a copy.
 //   k_rows_multi    <- the same traffic for all of a step's tensors (parameters and Adam moments) in one launch
+//   k_rows_packed   <- the host legs of that traffic when the host storage is one packed row per Gaussian (all
+//                      six parameters and twelve Adam moments back to back, padded to whole 64-byte lines): every
+//                      wave moves whole host lines instead of one 12-180-byte fragment per tensor
 //   k_cache_lists / k_cache_keep / k_cache_split
 //                   <- the SPT cache's bookkeeping (train_post.py:346-430): which of the previous view's SPTs
 //                      are reused, which are loaded, the new SPT_counts prefix, and which cached Gaussians stay
@@ -206,7 +209,10 @@ __global__ void __launch_bounds__(256) k_rows_multi(RowTabs tabs, int64_t n, con
     uint32_t* __restrict__ dst = static_cast<uint32_t*>(tb.dst);
     // lanes own U consecutive words (U = 4 for device-only tables, whose interior row chunks move as one 16-byte
     // access; 1 otherwise, since a 16-byte access to host memory may straddle a page)
-    const int U = tb.device_only ? 4 : 1;
+#ifndef HLGS_ROWS_WIDE
+#define HLGS_ROWS_WIDE 1  // 0: 4-byte lanes everywhere; 1: 16-byte lanes for device-only tables; 2: only if rows are whole 16-byte chunks
+#endif
+    const int U = (HLGS_ROWS_WIDE == 1 && tb.device_only) || (HLGS_ROWS_WIDE == 2 && tb.device_only && (words & 3) == 0) ? 4 : 1;
     const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * U, S = (int64_t)gridDim.x * 256 * U;
     int64_t r = w0 / words, k = w0 - r * words;
     const int64_t dr = S / words, dk = S - dr * words;
@@ -234,6 +240,74 @@ __global__ void __launch_bounds__(256) k_rows_multi(RowTabs tabs, int64_t n, con
             r++;
         }
     }
+}
+
+// ---------------------------------------------------------------- packed host rows
+// Host row h = words [h * hw, (h + 1) * hw) of `host`: table 0's row, table 1's row, ..., then zero padding to hw
+// (a multiple of 16 words, so a row is whole 64-byte lines).  One wave per row at a time; lane l owns host words
+// l, l + 64, l + 128, l + 192 of every row, so each store (to host) or load (from host) instruction of the wave
+// covers 256 contiguous bytes of the host row, and the device side of the same instruction is one contiguous run
+// per table row.  A lane's (table, word) for each of its slots is found once, before the row loop.
+struct PackTabs {
+    float* t[kMaxRowTables];
+    int words[kMaxRowTables];
+};
+
+template <bool TO_HOST>
+__global__ void __launch_bounds__(256) k_rows_packed(PackTabs tabs, int T, int64_t n, const int* __restrict__ dev_rows,
+                                                     const int* __restrict__ host_rows, float* __restrict__ host,
+                                                     int hw)
+{
+    const int lane = threadIdx.x & 63;
+    float* base[kPackSlots];
+    int width[kPackSlots], off[kPackSlots];
+    bool live[kPackSlots];
+#pragma unroll
+    for (int m = 0; m < kPackSlots; m++) {
+        const int w = lane + 64 * m;
+        int start = 0, t = 0;
+        while (t < T && w >= start + tabs.words[t]) start += tabs.words[t++];
+        live[m] = t < T;  // a data word (else padding, or beyond the row when m * 64 >= hw)
+        base[m] = live[m] ? tabs.t[t] : nullptr;
+        width[m] = live[m] ? tabs.words[t] : 0;
+        off[m] = w - start;
+    }
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t r = wave; r < n; r += nwaves) {
+        const int64_t dr = dev_rows ? dev_rows[r] : r;
+        const int64_t hr = host_rows ? host_rows[r] : r;
+        float* hrow = host + hr * hw;
+        if (TO_HOST) {
+            float v[kPackSlots];
+#pragma unroll
+            for (int m = 0; m < kPackSlots; m++) v[m] = live[m] ? base[m][dr * width[m] + off[m]] : 0.f;
+#pragma unroll
+            for (int m = 0; m < kPackSlots; m++)
+                if (lane + 64 * m < hw) hrow[lane + 64 * m] = v[m];  // padding words too: whole lines
+        } else {
+            float v[kPackSlots];
+#pragma unroll
+            for (int m = 0; m < kPackSlots; m++) v[m] = live[m] ? hrow[lane + 64 * m] : 0.f;
+#pragma unroll
+            for (int m = 0; m < kPackSlots; m++)
+                if (live[m]) base[m][dr * width[m] + off[m]] = v[m];
+        }
+    }
+}
+
+void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, const int* dev_rows,
+                        const int* host_rows, float* host, int hw, bool to_host, hipStream_t s)
+{
+    PackTabs pt{};
+    for (int t = 0; t < T; t++) {
+        pt.t[t] = tabs[t];
+        pt.words[t] = words[t];
+    }
+    const int64_t blocks = std::min<int64_t>((n + 3) / 4, 2048);  // 4 waves (rows) per block, grid-stride above
+    if (blocks <= 0) return;
+    if (to_host) hipLaunchKernelGGL(k_rows_packed<true>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw);
+    else hipLaunchKernelGGL(k_rows_packed<false>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw);
 }
 
 void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_rows, const int* dst_rows, hipStream_t s)

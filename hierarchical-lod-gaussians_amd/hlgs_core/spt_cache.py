@@ -7,9 +7,11 @@ The reference keeps every Gaussian in host storage (GaussianModel.move_storage_t
   coarse cut             :326-343  -> spt.upper_tree_cut (one workgroup, k_upper_cut)
   bookkeeping            :346-430  -> hlgs_spt_cache_plan (k_cache_lists + two scans + k_cache_split), with
                                       get_spt_cut_cuda on the SPTs to load
-  write-back and load    :439-479  -> hlgs_copy_rows: three launches move all six parameters and their twelve
-                                      Adam moments (write-back, resident compaction, load); the host side is
-                                      pinned memory the GPU reads and writes directly
+  write-back and load    :439-479  -> three launches move all six parameters and their twelve Adam moments:
+                                      write-back and load with hlgs_copy_rows_packed, resident compaction with
+                                      hlgs_copy_rows.  The host side is pinned memory the GPU reads and writes
+                                      directly, one packed row per Gaussian (all eighteen rows back to back,
+                                      padded to whole 64-byte lines), so the host link carries whole lines
   optimizer step         :786-812  -> hlgs_adam_step (one launch over the six tensors, skybox gradients zeroed)
 
 Differences from the reference: when the Gaussian budget forces a second pass, each pass
@@ -55,6 +57,25 @@ def copy_rows(pairs, n, src_rows=None, dst_rows=None):
     L.check(lib.hlgs_copy_rows(len(pairs), tabs, int(n), _p(src_rows), _p(dst_rows), L.stream()))
 
 
+def copy_rows_packed(dev_tables, n, dev_rows, host_rows, host, to_host):
+    """Host legs with packed host storage (hlgs_copy_rows_packed): host[host_rows[i]] holds the rows of every
+    device table back to back; to_host writes whole host rows from dev_t[dev_rows[i]], else the tables' parts are
+    read back into dev_t[dev_rows[i]].  None row lists are the identity."""
+    lib = L.load()
+    if n == 0 or not dev_tables:
+        return
+    if host.device.type != "cpu" or not host.is_pinned() or not host.is_contiguous():
+        raise RuntimeError("packed host storage must be a contiguous pinned tensor")
+    tabs = (L.RowCopy * len(dev_tables))()
+    for k, d in enumerate(dev_tables):
+        if not d.is_contiguous() or d.dtype != torch.float32:
+            raise RuntimeError("device tables must be contiguous float32")
+        L.require_gpu(d)
+        tabs[k] = L.RowCopy(d.data_ptr(), None, _row_bytes(d))
+    L.check(lib.hlgs_copy_rows_packed(len(dev_tables), tabs, int(n), _p(dev_rows), _p(host_rows), host.data_ptr(),
+                                      host.stride(0) * host.element_size(), 1 if to_host else 0, L.stream()))
+
+
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, lrs, step, skybox_points=0, beta1=0.9, beta2=0.999, eps=1e-8):
     """The dense Adam of train_post.py:786-812 over a list of float32 tensors (in place, one launch): grads of
     the first skybox_points rows are zeroed, then OurAdam._single_tensor_adam2 with state step `step` (the
@@ -83,13 +104,23 @@ class SPTCache:
     def __init__(self, storage, spt, skybox_points, opt_storage=None, reuse_tolerance=0.9,
                  max_gaussian_budget=100_000_000, distance_multiplier_until_budget=1.5, use_frustum_culling=True,
                  use_bounding_spheres=True, device="cuda"):
-        pin = lambda t: t if t.device.type != "cpu" or t.is_pinned() else t.contiguous().pin_memory()  # noqa: E731
-        self.storage = {k: pin(storage[k].contiguous()) for k in NAMES}
-        if opt_storage is None:
-            opt_storage = {k: {"exp_avgs": torch.zeros_like(self.storage[k]),
-                               "exp_avgs_sqs": torch.zeros_like(self.storage[k])} for k in NAMES}
-        self.opt_storage = {k: {s: pin(opt_storage[k][s].contiguous()) for s in ("exp_avgs", "exp_avgs_sqs")}
-                            for k in NAMES}
+        # packed pinned host storage: one row per Gaussian holding its six parameter rows, then the six exp_avgs and
+        # the six exp_avg_sqs rows, padded to whole 64-byte lines; self.storage / self.opt_storage are views of it
+        G = int(storage[NAMES[0]].shape[0])
+        shapes = {k: tuple(storage[k].shape[1:]) for k in NAMES}
+        widths = [math.prod(shapes[k]) for k in NAMES] * 3
+        hw = -(-sum(widths) // 16) * 16
+        self.host = torch.zeros((G, hw), dtype=torch.float32).pin_memory()
+        offs = [sum(widths[:i]) for i in range(len(widths))]
+        view = lambda i, k: self.host[:, offs[i]:offs[i] + widths[i]].view((G,) + shapes[k])  # noqa: E731
+        self.storage = {k: view(i, k) for i, k in enumerate(NAMES)}
+        self.opt_storage = {k: {"exp_avgs": view(len(NAMES) + i, k), "exp_avgs_sqs": view(2 * len(NAMES) + i, k)}
+                            for i, k in enumerate(NAMES)}
+        for k in NAMES:
+            self.storage[k].copy_(storage[k].reshape((G,) + shapes[k]))
+            if opt_storage is not None:
+                self.opt_storage[k]["exp_avgs"].copy_(opt_storage[k]["exp_avgs"].reshape((G,) + shapes[k]))
+                self.opt_storage[k]["exp_avgs_sqs"].copy_(opt_storage[k]["exp_avgs_sqs"].reshape((G,) + shapes[k]))
         self.device = torch.device(device)
         dev = self.device
         self.nodes = spt["upper_tree_nodes"].to(dev, torch.int32).contiguous()
@@ -113,7 +144,7 @@ class SPTCache:
         self.render_indices = torch.arange(0, self.sky, device=dev, dtype=torch.int32)
         head = torch.arange(0, self.sky, device=dev, dtype=torch.int32)
         self.params = {k: self._alloc(k, self.sky) for k in NAMES}
-        copy_rows([(self.storage[k], self.params[k]) for k in NAMES], self.sky, head, None)
+        copy_rows_packed([self.params[k] for k in NAMES], self.sky, None, head, self.host, to_host=False)
         self.exp_avgs = {k: torch.zeros_like(self.params[k]) for k in NAMES}
         self.exp_avg_sqs = {k: torch.zeros_like(self.params[k]) for k in NAMES}
         self.prev_SPT_indices = torch.empty(0, dtype=torch.int32, device=dev)
@@ -188,18 +219,16 @@ class SPTCache:
     def _move(self, pl):
         dev_t = [self.params[k] for k in NAMES] + [self.exp_avgs[k] for k in NAMES] + \
                 [self.exp_avg_sqs[k] for k in NAMES]
-        host_t = [self.storage[k] for k in NAMES] + [self.opt_storage[k]["exp_avgs"] for k in NAMES] + \
-                 [self.opt_storage[k]["exp_avgs_sqs"] for k in NAMES]
         wb = pl["write_back_rows"]
         # write the evicted rows back to storage (:439-444, :473-474)
-        copy_rows([(d.detach(), h) for d, h in zip(dev_t, host_t)], wb.numel(), wb, pl["write_back_indices"])
+        copy_rows_packed([d.detach() for d in dev_t], wb.numel(), wb, pl["write_back_indices"], self.host, to_host=True)
         nk = pl["keep_rows"].numel()
         load = pl["load_from_disk_indices"]
         rows = nk + load.numel()
         new_t = [torch.empty((rows,) + tuple(d.shape[1:]), dtype=d.dtype, device=self.device) for d in dev_t]
         # resident rows that stay, then the loaded rows (:446-479)
         copy_rows([(d.detach(), n) for d, n in zip(dev_t, new_t)], nk, pl["keep_rows"], None)
-        copy_rows([(h, n[nk:]) for h, n in zip(host_t, new_t)], load.numel(), load, None)
+        copy_rows_packed([n[nk:] for n in new_t], load.numel(), None, load, self.host, to_host=False)
         k6 = len(NAMES)
         self.params = {k: new_t[i].requires_grad_(True) for i, k in enumerate(NAMES)}
         self.exp_avgs = {k: new_t[k6 + i] for i, k in enumerate(NAMES)}

@@ -311,6 +311,15 @@ typedef struct hlgs_row_copy {
 } hlgs_row_copy;
 int hlgs_copy_rows(int T, const hlgs_row_copy* tables, int64_t n, const int* src_rows, const int* dst_rows,
                    void* stream);
+/* The host legs of the same traffic with packed host storage: host row h (host_row_bytes bytes, a multiple of 64,
+ * at most 1024; pinned host memory) holds the T device tables' rows back to back -- table t's row at the sum of the
+ * earlier tables' row_bytes -- then zero padding.  tables[t].src is the device table (dst is ignored), float32
+ * rows.  to_host != 0: host[host_rows[i]] = (dev_0[dev_rows[i]], dev_1[dev_rows[i]], ..., 0...) -- whole host
+ * rows, padding included;  to_host == 0: dev_t[dev_rows[i]] = the table's part of host[host_rows[i]].  NULL row
+ * lists are the identity.  Every store or load the GPU issues to host memory covers whole 64-byte lines, where
+ * per-tensor host storage takes one 12-180-byte fragment per tensor and row (train_post.py:439-479). */
+int hlgs_copy_rows_packed(int T, const hlgs_row_copy* tables, int64_t n, const int* dev_rows, const int* host_rows,
+                          void* host, int64_t host_row_bytes, int to_host, void* stream);
 /* Dense Adam step of the cached training loop (train_post.py:786-812: skybox gradient rows zeroed, then
  * OurAdam._single_tensor_adam2, scene/OurAdam.py:357-448, with state step = step) over T (at most 32) tensors in
  * one launch.  The scalars follow torch: lr, betas and eps are the caller's doubles; step_size =

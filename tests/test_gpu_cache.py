@@ -142,6 +142,32 @@ def test_copy_rows_tables_and_identity():
         copy_rows([(torch.zeros(4, 3), dev[0])], 4, None, None)  # unpinned host memory is refused
 
 
+@pytest.mark.parametrize("tables", [NAMES * 3, NAMES, ("opacity", "f_dc", "xyz")])
+def test_copy_rows_packed_both_directions(tables):
+    """hlgs_copy_rows_packed against torch indexing: whole host rows written (padding zeroed), tables read back,
+    identity and explicit row lists, the full 18-table row of the cache (708 -> 768 bytes) and partial prefixes."""
+    from hlgs_core.spt_cache import copy_rows_packed
+    rng = np.random.default_rng(5)
+    widths = [int(np.prod(SHAPES[k])) for k in tables]
+    hw = -(-sum(widths) // 16) * 16
+    host = torch.tensor(rng.normal(size=(700, hw)).astype(np.float32)).pin_memory()
+    dev = [torch.tensor(rng.normal(size=(90,) + SHAPES[k]).astype(np.float32), device=DEV) for k in tables]
+    src = torch.tensor(rng.permutation(90)[:77].astype(np.int32), device=DEV)
+    dst = torch.tensor(rng.permutation(700)[:77].astype(np.int32), device=DEV)
+    want = host.clone()
+    packed = torch.cat([d.cpu().reshape(90, -1) for d in dev], 1)
+    want[dst.cpu().long()] = torch.nn.functional.pad(packed, (0, hw - packed.shape[1]))[src.cpu().long()]
+    copy_rows_packed(dev, 77, src, dst, host, to_host=True)
+    torch.cuda.synchronize()
+    assert torch.equal(host, want)
+    out = [torch.full((77,) + SHAPES[k], float("nan"), device=DEV) for k in tables]
+    copy_rows_packed(out, 77, None, dst, host, to_host=False)
+    got = torch.cat([o.cpu().reshape(77, -1) for o in out], 1)
+    assert torch.equal(got, host[dst.cpu().long(), :packed.shape[1]])
+    with pytest.raises(RuntimeError):
+        copy_rows_packed(dev, 4, None, None, torch.zeros(8, hw), to_host=True)  # unpinned host memory is refused
+
+
 def test_adam_step_matches_restatement():
     from hlgs_core.spt_cache import adam_step
     g = torch.Generator().manual_seed(5)

@@ -1,5 +1,6 @@
 # A/B of libhlgs.so variants (tools/build_variant.py; C = the in-tree build) on the SPT cache's row moves: the config5
-# camera path under rocprofv3, per-call durations of k_rows_multi in step order (write-back, compaction, load).
+# camera path under rocprofv3, mean per-call durations of the three legs (write-back k_rows_packed<true>, compaction
+# k_rows_multi, load k_rows_packed<false>) over the steps after the first.
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 V=hierarchical-lod-gaussians_amd/lib/variants
@@ -9,9 +10,14 @@ for v in ${VARIANTS:-C}; do
   python3 - "$v" gpurun_out/abr_$v/run_kernel_trace.csv <<'PY'
 import csv, sys
 v, path = sys.argv[1:]
-d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(open(path))
-     if "k_rows_multi" in r["Kernel_Name"]]
-legs = list(zip(*[d[i:i + 3] for i in range(3, len(d) - 2, 3)]))
-print(v, " ".join(f"{name} {sum(x) / len(x):.1f}" for name, x in zip(("writeback", "compact", "load"), legs)))
+rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+legs = {"writeback": [], "compact": [], "load": []}
+for r in rows:
+    n, d = r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    if "k_rows_packed<true>" in n: legs["writeback"].append(d)
+    elif "k_rows_multi" in n: legs["compact"].append(d)
+    elif "k_rows_packed<false>" in n: legs["load"].append(d)
+skip = {"writeback": 0, "compact": 0, "load": 2}  # setup head load and the first step's full load
+print(v, " ".join(f"{k} {sum(x[skip[k]:]) / max(1, len(x[skip[k]:])):.1f} (n={len(x)})" for k, x in legs.items()))
 PY
 done
