@@ -577,7 +577,7 @@ int hlgs_morton_codes(int P, const float* xyz, const float* mn, const float* mx,
 size_t hlgs_upper_cut_scratch_size(int N)
 {
     const size_t cap = 2 * (size_t)(N > 0 ? N : 0) + 2;
-    return 2 * align_up(sizeof(int) * cap) + align_up(2 * sizeof(int)) + kAlign;
+    return 2 * align_up(sizeof(int) * cap) + align_up(2 * sizeof(int)) + align_up(upper_cut_state_bytes()) + kAlign;
 }
 
 int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
@@ -595,8 +595,12 @@ int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* 
     const int cap = 2 * N + 2;
     char* p = static_cast<char*>(aligned(scratch));
     CutArgs a{N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum, use_lod,
-              take<int>(p, cap), take<int>(p, cap), N, cut, nullptr};
+              take<int>(p, cap), take<int>(p, cap), N, cut, nullptr, nullptr, nullptr, nullptr};
     a.count = take<int>(p, 2);
+    char* q = take<char>(p, upper_cut_state_bytes());
+    a.state = reinterpret_cast<CutState*>(q);
+    a.arrive = reinterpret_cast<unsigned*>(q + sizeof(CutState));
+    a.level_counts = reinterpret_cast<int*>(a.arrive + kCutLevelLaunches);
     launch_upper_cut(a, s);
     int rc = check_stage(s, false, "upper_tree_cut");
     if (rc) return rc;

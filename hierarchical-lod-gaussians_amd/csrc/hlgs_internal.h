@@ -125,6 +125,11 @@ __device__ __forceinline__ bool guard_fail(const Guard& gd)
 // leaves go to the cut, then the non-leaves whose LOD condition is false, each group in frontier order; the
 // next frontier is the first children of the expanded nodes in order, then their first children's next
 // siblings in order (scene/gaussian_model.py:364-404).
+constexpr int kCutLevelLaunches = 8;  // wide-level launches queued after the narrow walk (stream.hip)
+constexpr int kCutMaxBlocks = 64;      // workgroups of one wide level (all resident at once)
+struct CutState {          // the walk's state between k_upper_cut and the k_cut_level launches
+    int size, total, parity, overflow;
+};
 struct CutArgs {
     int N;
     const int* nodes;      // N x 6 HierarchyNode rows: 2 child_count, 3 first_child, 4 next_sibling
@@ -140,7 +145,11 @@ struct CutArgs {
     int capacity;          // entries of cut
     int* cut;
     int* count;            // [0] = cut size, [1] = overflow flag
+    CutState* state;
+    unsigned* arrive;      // kCutLevelLaunches arrival counters
+    int* level_counts;     // 3 x kCutMaxBlocks
 };
+size_t upper_cut_state_bytes();
 
 // SPT cache bookkeeping of one streaming step (stream.hip, train_post.py:346-430)
 struct CacheArgs {

@@ -29,26 +29,39 @@ namespace hlgs {
 // Per level the frontier (the reference's `stack`) is filtered by the cull; leaves go to the cut, then the
 // non-leaves whose condition is false, each group in frontier order; the next frontier is the first children
 // of the expanded nodes in order, followed by their first children's next siblings in order.
-__device__ __forceinline__ int cut_state(const CutArgs& a, int v)
+// A node's cut state (0 culled, 1 leaf -> cut, 2 condition false -> cut, 3 expand), with its first child and that
+// child's next sibling when it expands.  Every load that depends only on v is issued before any test, so a level
+// costs two dependent global round trips (v's row, then the first child's sibling).
+struct CutNode {
+    int st, fc, ns;
+};
+template <bool SIB = true>
+__device__ __forceinline__ CutNode cut_node(const CutArgs& a, int v)
 {
 #pragma clang fp contract(off)
-    // 0 culled, 1 leaf -> cut, 2 condition false -> cut, 3 expand
     const float px = a.xyz[3 * v], py = a.xyz[3 * v + 1], pz = a.xyz[3 * v + 2];
+    const float r = a.use_frustum ? a.bounds[v] : 0.f;
+    const int kids = a.nodes[6 * v + 2], fc = a.nodes[6 * v + 3];
+    const float md = a.use_lod ? a.min_dist2[v] : 0.f;
+    CutNode c{3, 0, 0};
     if (a.use_frustum) {
-        const float r = a.bounds[v];
         for (int k = 0; k < 4; k++) {
             const float* pl = a.planes + 4 * k;
             const float sd = px * pl[0] + py * pl[1] + pz * pl[2] + pl[3];  // torch.sum over 3, then + distance
-            if (sd + r < 0.f) return 0;
+            if (sd + r < 0.f) c.st = 0;
         }
     }
-    if (a.nodes[6 * v + 2] == 0) return 1;
-    if (a.use_lod) {
+    if (c.st == 3 && kids == 0) c.st = 1;
+    if (c.st == 3 && a.use_lod) {
         const float dx = a.campos[0] - px, dy = a.campos[1] - py, dz = a.campos[2] - pz;
         const float d2 = dx * dx + dy * dy + dz * dz;
-        if (!(a.min_dist2[v] > d2 * a.dmul)) return 2;
+        if (!(md > d2 * a.dmul)) c.st = 2;
     }
-    return 3;
+    if (SIB && c.st == 3) {
+        c.fc = fc;
+        c.ns = a.nodes[6 * fc + 4];
+    }
+    return c;
 }
 
 // exclusive prefix of `flag` over the 1024-thread block; returns the block total in *total
@@ -70,76 +83,210 @@ __device__ __forceinline__ int block_excl(int flag, int* s_w, int* total)
     return before + in_wave;
 }
 
-// Pass 1 classifies the level once (the states go to LDS when the level fits, so pass 2 does not reload the nodes)
-// and counts with wave ballots and LDS atomics, without block barriers, so the waves' node loads overlap.
-constexpr int kCutLds = 48 * 1024;
+// Narrow levels (the top of the tree) are walked by one workgroup, k_upper_cut: thread t owns a contiguous run of
+// ceil(size / 1024) frontier entries, visited in batches of eight whose loads are all issued together.  Pass 1
+// counts the three outcomes per thread, one three-way block scan turns the counts into output offsets, and pass 2
+// re-classifies the same entries and writes the cut (leaves, then condition-false nodes) and the next frontier
+// (first children, then their siblings) in frontier order.  A level costs ~3 us that way, but one CU streams only
+// ~160 nodes per us, and the last levels of a 1M-leaf upper tree hold 4k-22k nodes.  So once a level exceeds
+// kCutNarrow entries the workgroup hands off (CutState), and each following level runs as one launch of
+// k_cut_level over many workgroups: the same two passes, with the per-workgroup outcome counts combined through
+// an arrival counter (every workgroup of a level is resident: a level uses at most kCutMaxBlocks = 64).  A fixed number
+// of such launches is queued; a final k_upper_cut in resume mode finishes any deeper levels and writes the count.
+constexpr int kCutBatch = 8;
+constexpr int kCutNarrow = 1024;
 
-__global__ void __launch_bounds__(1024) k_upper_cut(CutArgs a)
+// exclusive prefix of (x, y, z) over the 1024-thread block, and the block totals
+__device__ __forceinline__ int3 block_excl3(int3 v, int* s_w, int3* tot)
 {
-    __shared__ int s_w[16];
-    __shared__ int s_n[3];
-    __shared__ uint8_t s_st[kCutLds];
-    int* front = a.front_a;
-    int* next = a.front_b;
-    int size = a.N > 0 ? 1 : 0;
-    if (threadIdx.x == 0) front[0] = 0;  // root_node = 0
-    int total = 0;
-    bool overflow = false;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int3 inc = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int x = __shfl_up(inc.x, d, 64), y = __shfl_up(inc.y, d, 64), z = __shfl_up(inc.z, d, 64);
+        if (lane >= d) { inc.x += x; inc.y += y; inc.z += z; }
+    }
+    __syncthreads();  // s_w is free
+    if (lane == 63) { s_w[3 * w] = inc.x; s_w[3 * w + 1] = inc.y; s_w[3 * w + 2] = inc.z; }
+    __syncthreads();
+    int3 before = make_int3(0, 0, 0), t = make_int3(0, 0, 0);
+    for (int k = 0; k < 16; k++) {
+        const int cx = s_w[3 * k], cy = s_w[3 * k + 1], cz = s_w[3 * k + 2];
+        if (k < w) { before.x += cx; before.y += cy; before.z += cz; }
+        t.x += cx; t.y += cy; t.z += cz;
+    }
+    *tot = t;
+    return make_int3(before.x + inc.x - v.x, before.y + inc.y - v.y, before.z + inc.z - v.z);
+}
+
+// Outcome counts of frontier entries [i0, i1)
+__device__ __forceinline__ int3 cut_count(const CutArgs& a, const int* front, int i0, int i1)
+{
+    int3 n = make_int3(0, 0, 0);
+    for (int b = i0; b < i1; b += kCutBatch) {
+        int v[kCutBatch];
+#pragma unroll
+        for (int j = 0; j < kCutBatch; j++) v[j] = b + j < i1 ? front[b + j] : -1;
+#pragma unroll
+        for (int j = 0; j < kCutBatch; j++) {
+            if (v[j] < 0) continue;
+            const int st = cut_node<false>(a, v[j]).st;
+            n.x += st == 1;
+            n.y += st == 2;
+            n.z += st == 3;
+        }
+    }
+    return n;
+}
+
+// Writes of frontier entries [i0, i1): leaves at cut[o1...], condition-false nodes at cut[o2...], first children at
+// next[o3...] and their siblings at next[n3 + o3...]
+__device__ __forceinline__ void cut_write(const CutArgs& a, const int* front, int* next, int i0, int i1, int o1,
+                                          int o2, int o3, int n3)
+{
+    for (int b = i0; b < i1; b += kCutBatch) {
+        int v[kCutBatch];
+#pragma unroll
+        for (int j = 0; j < kCutBatch; j++) v[j] = b + j < i1 ? front[b + j] : -1;
+#pragma unroll
+        for (int j = 0; j < kCutBatch; j++) {
+            if (v[j] < 0) continue;
+            const CutNode c = cut_node(a, v[j]);
+            if (c.st == 1) a.cut[o1++] = v[j];
+            else if (c.st == 2) a.cut[o2++] = v[j];
+            else if (c.st == 3) {
+                next[o3] = c.fc;
+                next[n3 + o3] = c.ns;
+                o3++;
+            }
+        }
+    }
+}
+
+// resume = 0: start at the root and hand off at the first level wider than kCutNarrow;  resume = 1: continue from
+// the state the level launches left, to the end, and write the count.
+__global__ void __launch_bounds__(1024) k_upper_cut(CutArgs a, int resume)
+{
+    __shared__ int s_w[16 * 3];
+    CutState* cs = a.state;
+    int size, total, parity, overflow;
+    if (!resume) {
+        size = a.N > 0 ? 1 : 0;
+        total = 0;
+        parity = 0;
+        overflow = 0;
+        if (threadIdx.x == 0) a.front_a[0] = 0;  // root_node = 0
+        if (threadIdx.x < kCutLevelLaunches) a.arrive[threadIdx.x] = 0;
+    } else {
+        size = cs->size;
+        total = cs->total;
+        parity = cs->parity;
+        overflow = cs->overflow;
+    }
+#ifdef HLGS_CUT_CLOCKS  // diagnostic build: per-level (realtime, core clock, size) at the unused tail of cut
+    int level = 0;
+#endif
     __syncthreads();
     while (size > 0 && !overflow) {
-        // pass 1: classify, level totals of the three outcomes
-        if (threadIdx.x < 3) s_n[threadIdx.x] = 0;
-        __syncthreads();
-        const bool cached = size <= kCutLds;
-        for (int c0 = 0; c0 < size; c0 += 1024) {
-            const int i = c0 + threadIdx.x;
-            const int st = i < size ? cut_state(a, front[i]) : 0;
-            if (cached && i < size) s_st[i] = (uint8_t)st;
-            const uint64_t b1 = __ballot(st == 1), b2 = __ballot(st == 2), b3 = __ballot(st == 3);
-            if (lane == 0) {
-                if (b1) atomicAdd(&s_n[0], __popcll(b1));
-                if (b2) atomicAdd(&s_n[1], __popcll(b2));
-                if (b3) atomicAdd(&s_n[2], __popcll(b3));
-            }
+        if (!resume && size > kCutNarrow) break;  // hand off to k_cut_level
+#ifdef HLGS_CUT_CLOCKS
+        if (threadIdx.x == 0 && level < 40) {
+            long long* d = reinterpret_cast<long long*>(a.cut + a.capacity - 256) + 3 * level;
+            d[0] = (long long)__builtin_amdgcn_s_memrealtime();
+            d[1] = (long long)__builtin_amdgcn_s_memtime();
+            d[2] = size;
         }
-        __syncthreads();
-        const int n1 = s_n[0], n2 = s_n[1], n3 = s_n[2];
-        if (total + n1 + n2 > a.capacity || 2 * n3 > a.capacity) { overflow = true; break; }
-        // pass 2: write the cut and the next frontier in the reference's order
-        int o1 = 0, o2 = 0, o3 = 0;
-        for (int c0 = 0; c0 < size; c0 += 1024) {
-            const int i = c0 + threadIdx.x;
-            const int v = i < size ? front[i] : 0;
-            const int st = i < size ? (cached ? (int)s_st[i] : cut_state(a, v)) : 0;
-            int t1, t2, t3;
-            const int p1 = block_excl(st == 1, s_w, &t1);
-            const int p2 = block_excl(st == 2, s_w, &t2);
-            const int p3 = block_excl(st == 3, s_w, &t3);
-            if (st == 1) a.cut[total + o1 + p1] = v;
-            if (st == 2) a.cut[total + n1 + o2 + p2] = v;
-            if (st == 3) {
-                const int fc = a.nodes[6 * v + 3];
-                next[o3 + p3] = fc;
-                next[n3 + o3 + p3] = a.nodes[6 * fc + 4];
-            }
-            o1 += t1; o2 += t2; o3 += t3;
-        }
-        total += n1 + n2;
-        size = 2 * n3;
-        int* t = front; front = next; next = t;
-        __syncthreads();
+        level++;
+#endif
+        const int* front = parity ? a.front_b : a.front_a;
+        int* next = parity ? a.front_a : a.front_b;
+        const int K = (size + 1023) / 1024;
+        const int i0 = min(size, (int)threadIdx.x * K), i1 = min(size, i0 + K);
+        int3 tot;
+        const int3 o = block_excl3(cut_count(a, front, i0, i1), s_w, &tot);
+        if (total + tot.x + tot.y > a.capacity || 2 * tot.z > a.capacity) { overflow = 1; break; }
+        cut_write(a, front, next, i0, i1, total + o.x, total + tot.x + o.y, o.z, tot.z);
+        total += tot.x + tot.y;
+        size = 2 * tot.z;
+        parity ^= 1;
+        __syncthreads();  // the next frontier is visible to the whole workgroup
     }
     if (threadIdx.x == 0) {
-        a.count[0] = total;
-        a.count[1] = overflow ? 1 : 0;
+        cs->size = overflow ? 0 : size;
+        cs->total = total;
+        cs->parity = parity;
+        cs->overflow = overflow;
+        if (resume || size == 0 || overflow) {
+            a.count[0] = total;
+            a.count[1] = overflow;
+        }
+    }
+}
+
+// One wide level over many workgroups (launch number `launch` of kCutLevelLaunches).  Workgroup b owns the contiguous
+// entries [b E, (b + 1) E) with E = 1024 * ceil(size / (1024 * kCutMaxBlocks)); the workgroups of the level publish
+// their outcome counts, then wait until all of them have (they are all resident), so each can form its offsets.
+__global__ void __launch_bounds__(1024) k_cut_level(CutArgs a, int launch)
+{
+    __shared__ int s_w[16 * 3];
+    __shared__ int3 s_pre, s_tot;
+    CutState* cs = a.state;
+    const int size = cs->size;
+    if (size == 0 || cs->overflow) return;
+    const int per = 1024 * ((size + 1024 * kCutMaxBlocks - 1) / (1024 * kCutMaxBlocks));
+    const int nb = (size + per - 1) / per;
+    const int b = blockIdx.x;
+    if (b >= nb) return;
+    const int total = cs->total, parity = cs->parity;
+    const int* front = parity ? a.front_b : a.front_a;
+    int* next = parity ? a.front_a : a.front_b;
+    const int K = per / 1024;
+    const int e0 = b * per, e1 = min(size, e0 + per);
+    const int i0 = min(e1, e0 + (int)threadIdx.x * K), i1 = min(e1, i0 + K);
+    int3 bt;
+    const int3 o = block_excl3(cut_count(a, front, i0, i1), s_w, &bt);
+    if (threadIdx.x == 0) {
+        int* pb = a.level_counts + 3 * b;
+        __hip_atomic_store(pb, bt.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pb + 1, bt.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pb + 2, bt.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(a.arrive + launch, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(a.arrive + launch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nb)
+            __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+    // workgroup prefix and level totals over the published counts (thread t < nb holds workgroup t's)
+    int3 mine = make_int3(0, 0, 0);
+    if ((int)threadIdx.x < nb) {
+        const int* pt = a.level_counts + 3 * threadIdx.x;
+        mine = make_int3(__hip_atomic_load(pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __hip_atomic_load(pt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __hip_atomic_load(pt + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    int3 tot;
+    const int3 pre = block_excl3(mine, s_w, &tot);
+    if ((int)threadIdx.x == b) s_pre = pre;
+    __syncthreads();
+    const int3 bp = s_pre;
+    if (total + tot.x + tot.y > a.capacity || 2 * tot.z > a.capacity) {
+        if (b == 0 && threadIdx.x == 0) cs->overflow = 1;
+        return;
+    }
+    cut_write(a, front, next, i0, i1, total + bp.x + o.x, total + tot.x + bp.y + o.y, bp.z + o.z, tot.z);
+    if (b == 0 && threadIdx.x == 0) {  // every workgroup read the state before it arrived
+        cs->size = 2 * tot.z;
+        cs->total = total + tot.x + tot.y;
+        cs->parity = parity ^ 1;
     }
 }
 
 void launch_upper_cut(const CutArgs& a, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_upper_cut, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_upper_cut, dim3(1), dim3(1024), 0, s, a, 0);
+    const int blocks = std::min(kCutMaxBlocks, (2 * a.N + 2 + 1023) / 1024);
+    for (int l = 0; l < kCutLevelLaunches; l++) hipLaunchKernelGGL(k_cut_level, dim3(blocks), dim3(1024), 0, s, a, l);
+    hipLaunchKernelGGL(k_upper_cut, dim3(1), dim3(1024), 0, s, a, 1);
 }
+size_t upper_cut_state_bytes() { return sizeof(CutState) + sizeof(unsigned) * kCutLevelLaunches + sizeof(int) * 3 * kCutMaxBlocks; }
 
 // ---------------------------------------------------------------- row gather / scatter
 // 16 lanes per row (four rows per wave); each lane moves 16-byte words when the row size and both bases allow,

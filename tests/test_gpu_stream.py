@@ -41,6 +41,21 @@ def test_upper_tree_cut_matches_reference_walk(seed, dmul, frustum, lod):
     np.testing.assert_array_equal(got.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("n,frustum,lod", [(40000, False, False), (40000, True, True), (300000, False, False)])
+def test_upper_tree_cut_wide_levels(n, frustum, lod):
+    """Levels wider than the single-workgroup walk's 1,024 entries run as multi-workgroup launches (k_cut_level);
+    300k leaves give nine such levels, one more than are queued, so the resume walk finishes the last one."""
+    from hlgs_core import spt
+    nodes, xyz, bounds, md2 = _upper_tree(n, 7)
+    cam = S.make_camera(320, 240, T=np.array([0.05, 0.0, 0.3]))
+    planes = spt.extract_frustum_planes(cam["projmatrix"])
+    t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
+    got = spt.upper_tree_cut(t(nodes), t(xyz), t(bounds), t(md2), planes, cam["campos"], 1.0, frustum, lod)
+    want = SR.upper_tree_cut(nodes, xyz, bounds, md2, planes.numpy(), cam["campos"].numpy(), 1.0, frustum, lod)
+    assert len(want) > 2048
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("width,dtype", [(3, torch.float32), (45, torch.float32), (4, torch.float32),
                                          (6, torch.int32), (1, torch.float32)])
 def test_gather_scatter_rows_with_pinned_host_storage(width, dtype):

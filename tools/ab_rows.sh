@@ -11,13 +11,14 @@ for v in ${VARIANTS:-C}; do
 import csv, sys
 v, path = sys.argv[1:]
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-legs = {"writeback": [], "compact": [], "load": []}
+legs = {"upper_cut": [], "writeback": [], "compact": [], "load": []}
 for r in rows:
     n, d = r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    if "k_rows_packed<true>" in n: legs["writeback"].append(d)
+    if "k_upper_cut" in n: legs["upper_cut"].append(d)
+    elif "k_rows_packed<true>" in n: legs["writeback"].append(d)
     elif "k_rows_multi" in n: legs["compact"].append(d)
     elif "k_rows_packed<false>" in n: legs["load"].append(d)
-skip = {"writeback": 0, "compact": 0, "load": 2}  # setup head load and the first step's full load
+skip = {"upper_cut": 1, "writeback": 0, "compact": 0, "load": 2}  # setup head load and the first step's full load
 print(v, " ".join(f"{k} {sum(x[skip[k]:]) / max(1, len(x[skip[k]:])):.1f} (n={len(x)})" for k, x in legs.items()))
 PY
 done
