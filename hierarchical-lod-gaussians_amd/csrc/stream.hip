@@ -457,8 +457,58 @@ void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, 
     else hipLaunchKernelGGL(k_rows_packed<false>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw);
 }
 
+// Compaction inside device memory (dst_rows = identity, every table device-only): dst_t[i] = src_t[src_rows[i]].
+// Lane = one 16-byte chunk of the destination (aligned store).  Its four source words lie in rows r .. r_end; when
+// those rows are consecutive in the source too (src_rows[r_end] - src_rows[r] = r_end - r, which holds inside the
+// long runs of kept rows) they are one contiguous 16-byte load at 4-byte alignment, otherwise four word loads.
+__global__ void __launch_bounds__(256) k_rows_compact(RowTabs tabs, int64_t n, const int* __restrict__ src_rows)
+{
+    const RowCopy& tb = tabs.t[blockIdx.y];
+    const int64_t words = tb.row_bytes >> 2;
+    if (words == 0) return;
+    const uint32_t* __restrict__ src = static_cast<const uint32_t*>(tb.src);
+    uint32_t* __restrict__ dst = static_cast<uint32_t*>(tb.dst);
+    const int64_t total = n * words;
+    const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4, S = (int64_t)gridDim.x * 256 * 4;
+    int64_t r = w0 / words, k = w0 - r * words;
+    const int64_t dr = S / words, dk = S - dr * words;
+    for (int64_t w = w0; w < total; w += S) {
+        const int64_t r_end = r + (k + 3) / words;
+        const int64_t s0 = src_rows[r];
+        if (w + 4 <= total && src_rows[r_end] - s0 == r_end - r) {
+            *reinterpret_cast<uint4*>(dst + w) = *reinterpret_cast<const uint4_a4*>(src + s0 * words + k);
+        } else {
+            int64_t rr = r, kk = k;
+            for (int u = 0; u < 4 && w + u < total; u++) {
+                dst[w + u] = src[(int64_t)src_rows[rr] * words + kk];
+                if (++kk == words) { kk = 0; rr++; }
+            }
+        }
+        r += dr;
+        k += dk;
+        while (k >= words) { k -= words; r++; }
+    }
+}
+
 void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_rows, const int* dst_rows, hipStream_t s)
 {
+#ifndef HLGS_ROWS_COMPACT
+#define HLGS_ROWS_COMPACT 1
+#endif
+    bool compact = HLGS_ROWS_COMPACT && src_rows && !dst_rows;
+    for (int t = 0; t < T && compact; t++)
+        compact = tabs[t].device_only && (reinterpret_cast<uintptr_t>(tabs[t].dst) & 15u) == 0;
+    if (compact) {
+        RowTabs rt{};
+        int64_t most = 0;
+        for (int t = 0; t < T; t++) {
+            rt.t[t] = tabs[t];
+            most = std::max<int64_t>(most, (n * (tabs[t].row_bytes >> 2) + 3) / 4);
+        }
+        const int64_t blocks = std::min<int64_t>((most + 255) / 256, 2048);
+        if (blocks > 0) hipLaunchKernelGGL(k_rows_compact, dim3((unsigned)blocks, T), dim3(256), 0, s, rt, n, src_rows);
+        return;
+    }
     RowTabs rt{};
     int64_t most = 0;
     for (int t = 0; t < T; t++) {
