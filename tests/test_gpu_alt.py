@@ -113,14 +113,19 @@ def test_alt_colors_precomp_path():
     _compare(sc, cam, use_colors=True)
 
 
-@pytest.mark.parametrize("P,W,H", [(2500, 160, 128), (40000, 128, 128)])
-def test_alt_tile_culling_lists_bit_exact(P, W, H):
+@pytest.mark.parametrize("P,W,H,stretch", [(2500, 160, 128, 1.0), (40000, 128, 128, 1.0), (3000, 320, 256, 30.0)])
+def test_alt_tile_culling_lists_bit_exact(P, W, H, stretch):
     """Binned instances after the exact per-tile culling, their depth order, num_rendered (culled instances
-    included) and per-pixel contributor counts equal the oracle's."""
+    included) and per-pixel contributor counts equal the oracle's.  stretch: every third splat made a long thin
+    rotated ellipse spanning many tiles, where the binning walk's per-row candidate columns (alt_row_cols) cut
+    most of the rect and must never drop a tile the per-tile test keeps."""
     from alt_gaussian_rasterization import _C
     from diff_gaussian_rasterization import _C as HC
     sc, cam = _alt_scene(P, 1, W, H, seed=21)
     sc["means3D"][::9, 2] = 6.0  # depth ties
+    if stretch > 1.0:
+        sc["scales"][::3, 0] *= stretch
+        sc["opacities"][::3] = 0.9
     fr = O.forward(dict(sc), S.cam_numpy(cam))
     t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
     e = torch.empty(0, device=DEV)
