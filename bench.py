@@ -403,6 +403,8 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080):
     bg = torch.zeros(3, device=dev)
     lrs = dict(xyz=1.6e-4, f_dc=2.5e-3, f_rest=2.5e-3 / 20, opacity=5e-2, scaling=5e-3, rotation=1e-3)
     path = [S.make_camera(W, H, T=np.array([0.03 * k, 0.01 * k, 0.2 * math.sin(0.3 * k)])) for k in range(steps + 3)]
+    # camera tensors live on the GPU, as the reference's Camera objects do (scene/cameras.py:102-107 .cuda())
+    path = [{k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in c.items()} for c in path]
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     stages = {k: [] for k in ("cache", "forward", "loss", "backward", "adam")}
     step_ms, resident = [], []

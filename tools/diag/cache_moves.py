@@ -10,7 +10,7 @@ b, storage, _, G = bench.merged_two_chunk_scene(1_000_000)
 cache = SPTCache(storage, b, 0, reuse_tolerance=0.9)
 W, H = 1920, 1080
 for k in range(12):
-    cam = S.make_camera(W, H, T=np.array([0.03 * k, 0.01 * k, 0.2 * math.sin(0.3 * k)]))
+    cam = {k_: (v.cuda() if torch.is_tensor(v) else v) for k_, v in S.make_camera(W, H, T=np.array([0.03 * k, 0.01 * k, 0.2 * math.sin(0.3 * k)])).items()}
     torch.cuda.synchronize(); t0 = time.perf_counter()
     cache.step(cam["projmatrix"], cam["campos"])
     torch.cuda.synchronize(); dt = (time.perf_counter() - t0) * 1e3
