@@ -771,6 +771,35 @@ int hlgs_copy_rows_packed(int T, const hlgs_row_copy* tables, int64_t n, const i
     return check_stage(s, false, "copy_rows_packed");
 }
 
+int hlgs_load_rows_packed(int T, const hlgs_row_copy* tables, int64_t n, const int* host_rows, const int* resident_of,
+                          const void* host, int64_t host_row_bytes, void* stream)
+{
+    if (T < 0 || T > kMaxRowTables) return fail(HLGS_ERR_ARG, "at most 32 tables");
+    if (n < 0) return fail(HLGS_ERR_ARG, "n < 0");
+    if (host_row_bytes <= 0 || host_row_bytes % 64 || host_row_bytes > 64 * 4 * kPackSlots)
+        return fail(HLGS_ERR_ARG, "host row size must be a multiple of 64 bytes, at most 1024");
+    if (T == 0 || n == 0) return HLGS_OK;
+    if (!tables || !host || !host_rows) return fail(HLGS_ERR_ARG, "missing tables, rows or host storage");
+    float* dst[kMaxRowTables];
+    const float* res[kMaxRowTables];
+    int words[kMaxRowTables];
+    int64_t used = 0;
+    for (int t = 0; t < T; t++) {
+        if (tables[t].row_bytes < 0 || tables[t].row_bytes % 4) return fail(HLGS_ERR_ARG, "row size must be a multiple of 4 bytes");
+        if (tables[t].row_bytes && (!tables[t].dst || (resident_of && !tables[t].src))) return fail(HLGS_ERR_ARG, "missing tensor");
+        dst[t] = (float*)tables[t].dst;
+        res[t] = (const float*)tables[t].src;
+        words[t] = (int)(tables[t].row_bytes / 4);
+        used += tables[t].row_bytes;
+    }
+    if (used > host_row_bytes) return fail(HLGS_ERR_ARG, "the tables' rows exceed the host row");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_rows_packed(T, dst, words, n, nullptr, host_rows, (float*)host, (int)(host_row_bytes / 4), false, s, res,
+                       resident_of);
+    return check_stage(s, false, "load_rows_packed");
+}
+
 int hlgs_adam_step(int T, const hlgs_adam_tensor* tensors, int64_t step, int skybox_rows, double beta1, double beta2,
                    double eps, void* stream)
 {

@@ -196,7 +196,8 @@ void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_row
                        hipStream_t s);
 constexpr int kPackSlots = 4;  // packed host rows of up to 4 x 64 words (1 KiB)
 void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, const int* dev_rows,
-                        const int* host_rows, float* host, int hw, bool to_host, hipStream_t s);
+                        const int* host_rows, float* host, int hw, bool to_host, hipStream_t s,
+                        const float* const* resident = nullptr, const int* resident_of = nullptr);
 // optim.hip: one dense Adam step over up to kMaxRowTables tensors (OurAdam._single_tensor_adam2)
 struct AdamTensor {
     float* param;

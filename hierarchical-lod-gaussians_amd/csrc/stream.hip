@@ -397,16 +397,21 @@ __global__ void __launch_bounds__(256) k_rows_multi(RowTabs tabs, int64_t n, con
 // per table row.  A lane's (table, word) for each of its slots is found once, before the row loop.
 struct PackTabs {
     float* t[kMaxRowTables];
+    const float* res[kMaxRowTables];  // load only: the resident tables rows may be taken from (see resident_of)
     int words[kMaxRowTables];
 };
 
+// Load with resident_of (per host row: the resident row that holds the same Gaussian, or -1): a row still resident
+// -- written back by this very step and loaded again, as the upper-tree Gaussians are every step -- is copied from
+// the resident tables instead of over the host link.  The write-back has already put the same bits in host storage.
 template <bool TO_HOST>
 __global__ void __launch_bounds__(256) k_rows_packed(PackTabs tabs, int T, int64_t n, const int* __restrict__ dev_rows,
                                                      const int* __restrict__ host_rows, float* __restrict__ host,
-                                                     int hw)
+                                                     int hw, const int* __restrict__ resident_of)
 {
     const int lane = threadIdx.x & 63;
     float* base[kPackSlots];
+    const float* res[kPackSlots];
     int width[kPackSlots], off[kPackSlots];
     bool live[kPackSlots];
 #pragma unroll
@@ -416,6 +421,7 @@ __global__ void __launch_bounds__(256) k_rows_packed(PackTabs tabs, int T, int64
         while (t < T && w >= start + tabs.words[t]) start += tabs.words[t++];
         live[m] = t < T;  // a data word (else padding, or beyond the row when m * 64 >= hw)
         base[m] = live[m] ? tabs.t[t] : nullptr;
+        res[m] = live[m] ? tabs.res[t] : nullptr;
         width[m] = live[m] ? tabs.words[t] : 0;
         off[m] = w - start;
     }
@@ -434,8 +440,14 @@ __global__ void __launch_bounds__(256) k_rows_packed(PackTabs tabs, int T, int64
                 if (lane + 64 * m < hw) hrow[lane + 64 * m] = v[m];  // padding words too: whole lines
         } else {
             float v[kPackSlots];
+            const int64_t rr = resident_of ? resident_of[hr] : -1;  // wave-uniform
+            if (rr >= 0) {
 #pragma unroll
-            for (int m = 0; m < kPackSlots; m++) v[m] = live[m] ? hrow[lane + 64 * m] : 0.f;
+                for (int m = 0; m < kPackSlots; m++) v[m] = live[m] ? res[m][rr * width[m] + off[m]] : 0.f;
+            } else {
+#pragma unroll
+                for (int m = 0; m < kPackSlots; m++) v[m] = live[m] ? hrow[lane + 64 * m] : 0.f;
+            }
 #pragma unroll
             for (int m = 0; m < kPackSlots; m++)
                 if (live[m]) base[m][dr * width[m] + off[m]] = v[m];
@@ -444,17 +456,19 @@ __global__ void __launch_bounds__(256) k_rows_packed(PackTabs tabs, int T, int64
 }
 
 void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, const int* dev_rows,
-                        const int* host_rows, float* host, int hw, bool to_host, hipStream_t s)
+                        const int* host_rows, float* host, int hw, bool to_host, hipStream_t s,
+                        const float* const* resident, const int* resident_of)
 {
     PackTabs pt{};
     for (int t = 0; t < T; t++) {
         pt.t[t] = tabs[t];
+        pt.res[t] = resident ? resident[t] : nullptr;
         pt.words[t] = words[t];
     }
     const int64_t blocks = std::min<int64_t>((n + 3) / 4, 2048);  // 4 waves (rows) per block, grid-stride above
     if (blocks <= 0) return;
-    if (to_host) hipLaunchKernelGGL(k_rows_packed<true>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw);
-    else hipLaunchKernelGGL(k_rows_packed<false>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw);
+    if (to_host) hipLaunchKernelGGL(k_rows_packed<true>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw, (const int*)nullptr);
+    else hipLaunchKernelGGL(k_rows_packed<false>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw, resident_of);
 }
 
 // Compaction inside device memory (dst_rows = identity, every table device-only): dst_t[i] = src_t[src_rows[i]].

@@ -8,8 +8,9 @@ The reference keeps every Gaussian in host storage (GaussianModel.move_storage_t
   bookkeeping            :346-430  -> hlgs_spt_cache_plan (k_cache_lists + two scans + k_cache_split), with
                                       get_spt_cut_cuda on the SPTs to load
   write-back and load    :439-479  -> three launches move all six parameters and their twelve Adam moments:
-                                      write-back and load with hlgs_copy_rows_packed, resident compaction with
-                                      hlgs_copy_rows.  The host side is pinned memory the GPU reads and writes
+                                      write-back with hlgs_copy_rows_packed, resident compaction with
+                                      hlgs_copy_rows, load with hlgs_load_rows_packed (rows the write-back has
+                                      just stored and the step loads again come from their resident rows).  The host side is pinned memory the GPU reads and writes
                                       directly, one packed row per Gaussian (all eighteen rows back to back,
                                       padded to whole 64-byte lines), so the host link carries whole lines
   optimizer step         :786-812  -> hlgs_adam_step (one launch over the six tensors, skybox gradients zeroed)
@@ -74,6 +75,26 @@ def copy_rows_packed(dev_tables, n, dev_rows, host_rows, host, to_host):
         tabs[k] = L.RowCopy(d.data_ptr(), None, _row_bytes(d))
     L.check(lib.hlgs_copy_rows_packed(len(dev_tables), tabs, int(n), _p(dev_rows), _p(host_rows), host.data_ptr(),
                                       host.stride(0) * host.element_size(), 1 if to_host else 0, L.stream()))
+
+
+def load_rows_packed(dst_tables, n, host_rows, host, resident_tables=None, resident_of=None):
+    """Load leg (hlgs_load_rows_packed): dst_t[i] = the table's part of host[host_rows[i]], except rows with
+    resident_of[host_rows[i]] = r >= 0, which are copied from resident_tables[t][r] on the device."""
+    lib = L.load()
+    if n == 0 or not dst_tables:
+        return
+    if host.device.type != "cpu" or not host.is_pinned() or not host.is_contiguous():
+        raise RuntimeError("packed host storage must be a contiguous pinned tensor")
+    tabs = (L.RowCopy * len(dst_tables))()
+    res = resident_tables if resident_of is not None else [None] * len(dst_tables)
+    for k, (d, r) in enumerate(zip(dst_tables, res)):
+        for t in (d,) if r is None else (d, r):
+            if not t.is_contiguous() or t.dtype != torch.float32:
+                raise RuntimeError("device tables must be contiguous float32")
+            L.require_gpu(t)
+        tabs[k] = L.RowCopy(_p(r) if r is not None else None, d.data_ptr(), _row_bytes(d))
+    L.check(lib.hlgs_load_rows_packed(len(dst_tables), tabs, int(n), _p(host_rows), _p(resident_of), host.data_ptr(),
+                                      host.stride(0) * host.element_size(), L.stream()))
 
 
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, lrs, step, skybox_points=0, beta1=0.9, beta2=0.999, eps=1e-8):
@@ -147,6 +168,8 @@ class SPTCache:
         copy_rows_packed([self.params[k] for k in NAMES], self.sky, None, head, self.host, to_host=False)
         self.exp_avgs = {k: torch.zeros_like(self.params[k]) for k in NAMES}
         self.exp_avg_sqs = {k: torch.zeros_like(self.params[k]) for k in NAMES}
+        # per storage row: the resident row holding it while a step's write-back and load run, else -1
+        self.resident_of = torch.full((G,), -1, dtype=torch.int32, device=dev)
         self.prev_SPT_indices = torch.empty(0, dtype=torch.int32, device=dev)
         self.prev_SPT_distances = torch.empty(0, dtype=torch.float32, device=dev)
         self.prev_SPT_counts = torch.empty(0, dtype=torch.int32, device=dev)
@@ -228,7 +251,16 @@ class SPTCache:
         new_t = [torch.empty((rows,) + tuple(d.shape[1:]), dtype=d.dtype, device=self.device) for d in dev_t]
         # resident rows that stay, then the loaded rows (:446-479)
         copy_rows([(d.detach(), n) for d, n in zip(dev_t, new_t)], nk, pl["keep_rows"], None)
-        copy_rows_packed([n[nk:] for n in new_t], load.numel(), None, load, self.host, to_host=False)
+        # rows written back above and loaded again (the upper-tree Gaussians, every step) come from their resident
+        # rows, the rest over the host link
+        if wb.numel():
+            wbi = pl["write_back_indices"].long()
+            self.resident_of[wbi] = wb
+            load_rows_packed([n[nk:] for n in new_t], load.numel(), load, self.host, [d.detach() for d in dev_t],
+                             self.resident_of)
+            self.resident_of[wbi] = -1
+        else:
+            load_rows_packed([n[nk:] for n in new_t], load.numel(), load, self.host)
         k6 = len(NAMES)
         self.params = {k: new_t[i].requires_grad_(True) for i, k in enumerate(NAMES)}
         self.exp_avgs = {k: new_t[k6 + i] for i, k in enumerate(NAMES)}

@@ -320,6 +320,13 @@ int hlgs_copy_rows(int T, const hlgs_row_copy* tables, int64_t n, const int* src
  * per-tensor host storage takes one 12-180-byte fragment per tensor and row (train_post.py:439-479). */
 int hlgs_copy_rows_packed(int T, const hlgs_row_copy* tables, int64_t n, const int* dev_rows, const int* host_rows,
                           void* host, int64_t host_row_bytes, int to_host, void* stream);
+/* The load leg of a cache step with rows that are still resident (train_post.py:446-479 after the write-back of
+ * :439-444): dst_t[i] = the table's part of host[host_rows[i]] for i < n, except that a host row h with
+ * resident_of[h] = r >= 0 is taken from src_t[r] (tables[t].src, the resident table) instead of over the host
+ * link -- the step's write-back has just stored the same bits at h.  tables[t].dst is the destination table;
+ * resident_of is indexed by host row (NULL: every row from the host). */
+int hlgs_load_rows_packed(int T, const hlgs_row_copy* tables, int64_t n, const int* host_rows, const int* resident_of,
+                          const void* host, int64_t host_row_bytes, void* stream);
 /* Dense Adam step of the cached training loop (train_post.py:786-812: skybox gradient rows zeroed, then
  * OurAdam._single_tensor_adam2, scene/OurAdam.py:357-448, with state step = step) over T (at most 32) tensors in
  * one launch.  The scalars follow torch: lr, betas and eps are the caller's doubles; step_size =

@@ -168,6 +168,32 @@ def test_copy_rows_packed_both_directions(tables):
         copy_rows_packed(dev, 4, None, None, torch.zeros(8, hw), to_host=True)  # unpinned host memory is refused
 
 
+def test_load_rows_packed_takes_resident_rows_from_the_device():
+    """hlgs_load_rows_packed: host rows marked in resident_of come from the resident tables, the others from the
+    packed host rows; a row marked resident whose host copy differs proves the source."""
+    from hlgs_core.spt_cache import load_rows_packed
+    rng = np.random.default_rng(9)
+    tables = NAMES * 3
+    widths = [int(np.prod(SHAPES[k])) for k in tables]
+    hw = -(-sum(widths) // 16) * 16
+    host = torch.tensor(rng.normal(size=(500, hw)).astype(np.float32)).pin_memory()
+    res = [torch.tensor(rng.normal(size=(80,) + SHAPES[k]).astype(np.float32), device=DEV) for k in tables]
+    rows = torch.tensor(rng.permutation(500)[:120].astype(np.int32), device=DEV)
+    resident_of = torch.full((500,), -1, dtype=torch.int32, device=DEV)
+    marked = rows[::2].long()
+    resident_of[marked] = torch.tensor(rng.permutation(80)[:marked.numel()].astype(np.int32), device=DEV)
+    out = [torch.full((120,) + SHAPES[k], float("nan"), device=DEV) for k in tables]
+    load_rows_packed(out, 120, rows, host, res, resident_of)
+    got = torch.cat([o.cpu().reshape(120, -1) for o in out], 1)
+    packed_res = torch.cat([r.cpu().reshape(80, -1) for r in res], 1)
+    ro = resident_of.cpu().long()[rows.cpu().long()]
+    want = torch.where((ro >= 0)[:, None], packed_res[ro.clamp(min=0)], host[rows.cpu().long(), :packed_res.shape[1]])
+    assert torch.equal(got, want)
+    out2 = [torch.empty((120,) + SHAPES[k], device=DEV) for k in tables]
+    load_rows_packed(out2, 120, rows, host)  # no resident_of: everything over the host link
+    assert torch.equal(torch.cat([o.cpu().reshape(120, -1) for o in out2], 1), host[rows.cpu().long(), :packed_res.shape[1]])
+
+
 def test_adam_step_matches_restatement():
     from hlgs_core.spt_cache import adam_step
     g = torch.Generator().manual_seed(5)
