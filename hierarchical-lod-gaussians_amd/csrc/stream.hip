@@ -465,7 +465,12 @@ void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, 
         pt.res[t] = resident ? resident[t] : nullptr;
         pt.words[t] = words[t];
     }
-    const int64_t blocks = std::min<int64_t>((n + 3) / 4, 2048);  // 4 waves (rows) per block, grid-stride above
+#ifndef HLGS_WB_BLOCKS
+#define HLGS_WB_BLOCKS 128
+#endif
+    // 4 waves (rows) per block, grid-stride above.  The write-back is bound by the host link, not by waves: a
+    // small grid moves it as fast and leaves the CUs to the compaction and load running beside it (SPTCache)
+    const int64_t blocks = std::min<int64_t>((n + 3) / 4, to_host ? HLGS_WB_BLOCKS : 2048);
     if (blocks <= 0) return;
     if (to_host) hipLaunchKernelGGL(k_rows_packed<true>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw, (const int*)nullptr);
     else hipLaunchKernelGGL(k_rows_packed<false>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw, resident_of);

@@ -162,8 +162,13 @@ def check(rc):
         raise RuntimeError(f"libhlgs error {rc}: {msg}")
 
 
+_GPU = []  # torch.cuda.is_available(), asked once per process (it costs a few us per call on every launch path)
+
+
 def require_gpu(*tensors):
-    if not torch.cuda.is_available():
+    if not _GPU:
+        _GPU.append(torch.cuda.is_available())
+    if not _GPU[0]:
         raise RuntimeError("libhlgs needs a HIP device (MI355X); torch.cuda.is_available() is False")
     for t in tensors:
         if t is not None and t.numel() and not t.is_cuda:

@@ -170,6 +170,11 @@ class SPTCache:
         self.exp_avg_sqs = {k: torch.zeros_like(self.params[k]) for k in NAMES}
         # per storage row: the resident row holding it while a step's write-back and load run, else -1
         self.resident_of = torch.full((G,), -1, dtype=torch.int32, device=dev)
+        # the write-back crosses the host link on its own stream, beside the compaction, the load and the rest of
+        # the training step; the next step's load waits for it (wb_done)
+        self.wb_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        self.wb_done = None
+        self._wb_hold = None
         self.prev_SPT_indices = torch.empty(0, dtype=torch.int32, device=dev)
         self.prev_SPT_distances = torch.empty(0, dtype=torch.float32, device=dev)
         self.prev_SPT_counts = torch.empty(0, dtype=torch.int32, device=dev)
@@ -189,11 +194,15 @@ class SPTCache:
         coarse = _spt.upper_tree_cut(self.nodes, self.xyz, self.bounds, self.min_distance_squared, planes, cam,
                                      distance_multiplier, self.use_frustum, True)
         n_cut, m, R = coarse.numel(), self.prev_SPT_indices.numel(), self.render_indices.numel()
-        i32 = lambda n: torch.empty(max(n, 1), dtype=torch.int32, device=dev)  # noqa: E731
-        f32 = lambda n: torch.empty(max(n, 1), dtype=torch.float32, device=dev)  # noqa: E731
-        out = dict(keep_spt_indices=i32(m), keep_spt_distances=f32(m), keep_spt_counts=i32(m),
-                   load_spt_indices=i32(n_cut), load_spt_distances=f32(n_cut), upper_render=i32(n_cut),
-                   keep_rows=i32(R), render_kept=i32(R), write_back_rows=i32(R), write_back_indices=i32(R))
+        # the ten output lists carved from one int32 allocation (the distances as float32 views of it)
+        sizes = dict(keep_spt_indices=m, keep_spt_distances=m, keep_spt_counts=m, load_spt_indices=n_cut,
+                     load_spt_distances=n_cut, upper_render=n_cut, keep_rows=R, render_kept=R, write_back_rows=R,
+                     write_back_indices=R)
+        lens = [(max(n, 1) + 63) // 64 * 64 for n in sizes.values()]
+        flat = torch.empty(sum(lens), dtype=torch.int32, device=dev)
+        out = {}
+        for (k, n), part in zip(sizes.items(), flat.split(lens)):
+            out[k] = part[:max(n, 1)].view(torch.float32) if k.endswith("distances") else part[:max(n, 1)]
         a = L.CacheArgs(n_cut, _p(coarse), _p(self.nodes), _p(self.xyz), _p(cam), float(distance_multiplier),
                         self.num_spts, m, _p(self.prev_SPT_indices), _p(self.prev_SPT_distances),
                         _p(self.prev_SPT_counts), R, _p(self.render_indices), int(self.n_loaded), self.sky,
@@ -243,16 +252,36 @@ class SPTCache:
         dev_t = [self.params[k] for k in NAMES] + [self.exp_avgs[k] for k in NAMES] + \
                 [self.exp_avg_sqs[k] for k in NAMES]
         wb = pl["write_back_rows"]
-        # write the evicted rows back to storage (:439-444, :473-474)
-        copy_rows_packed([d.detach() for d in dev_t], wb.numel(), wb, pl["write_back_indices"], self.host, to_host=True)
+        cur = torch.cuda.current_stream(self.device)
+        prev_wb, prev_hold = self.wb_done, self._wb_hold
+        # write the evicted rows back to storage (:439-444, :473-474), on the write-back stream: nothing in this step
+        # reads those host rows (the rows it loads again come from their resident rows, below)
+        if wb.numel():
+            self.wb_stream.wait_stream(cur)
+            with torch.cuda.stream(self.wb_stream):
+                copy_rows_packed([d.detach() for d in dev_t], wb.numel(), wb, pl["write_back_indices"], self.host,
+                                 to_host=True)
+                self.wb_done = torch.cuda.Event()
+                self.wb_done.record(self.wb_stream)
+            # the write-back's inputs stay referenced until the next step has waited for it (then their memory
+            # may go back to this stream's allocations)
+            self._wb_hold = (dev_t, wb, pl["write_back_indices"])
         nk = pl["keep_rows"].numel()
         load = pl["load_from_disk_indices"]
         rows = nk + load.numel()
-        new_t = [torch.empty((rows,) + tuple(d.shape[1:]), dtype=d.dtype, device=self.device) for d in dev_t]
+        # the eighteen new resident tensors carved from one allocation (each 256-byte aligned)
+        widths = [math.prod(d.shape[1:]) for d in dev_t]
+        lens = [(rows * w + 63) // 64 * 64 for w in widths]
+        flat = torch.empty(sum(lens), dtype=torch.float32, device=self.device)
+        new_t = [part[:rows * w].view((rows,) + tuple(d.shape[1:]))
+                 for part, w, d in zip(flat.split(lens), widths, dev_t)]
         # resident rows that stay, then the loaded rows (:446-479)
         copy_rows([(d.detach(), n) for d, n in zip(dev_t, new_t)], nk, pl["keep_rows"], None)
         # rows written back above and loaded again (the upper-tree Gaussians, every step) come from their resident
-        # rows, the rest over the host link
+        # rows, the rest over the host link once the previous step's write-back has landed
+        if prev_wb is not None:
+            cur.wait_event(prev_wb)
+            del prev_hold
         if wb.numel():
             wbi = pl["write_back_indices"].long()
             self.resident_of[wbi] = wb
@@ -265,6 +294,12 @@ class SPTCache:
         self.params = {k: new_t[i].requires_grad_(True) for i, k in enumerate(NAMES)}
         self.exp_avgs = {k: new_t[k6 + i] for i, k in enumerate(NAMES)}
         self.exp_avg_sqs = {k: new_t[2 * k6 + i] for i, k in enumerate(NAMES)}
+
+    def sync_storage(self):
+        """Wait until the last write-back has landed in host storage.  Call before reading self.storage /
+        self.opt_storage on the host (the reference's write-back is a synchronous .cpu() copy)."""
+        if self.wb_done is not None:
+            self.wb_done.synchronize()
 
     # ------------------------------------------------------------ optimizer step (:786-812)
     def optimizer_step(self, iteration, lrs):

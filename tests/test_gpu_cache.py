@@ -114,6 +114,7 @@ def test_spt_cache_views_match_restatement(rtol, budget):
         for t in range(len(orc.dev)):
             orc.dev[t] = (orc.dev[t] + np.float32(0.001 * (step + 1) * (t + 1))).astype(np.float32)
     assert reused > 0 or rtol < 0.1
+    cache.sync_storage()
     host = [cache.storage[k] for k in NAMES] + [cache.opt_storage[k]["exp_avgs"] for k in NAMES] + \
            [cache.opt_storage[k]["exp_avgs_sqs"] for k in NAMES]
     for t, (h, w) in enumerate(zip(host, orc.host)):
