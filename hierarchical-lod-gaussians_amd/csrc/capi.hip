@@ -580,6 +580,29 @@ size_t hlgs_upper_cut_scratch_size(int N)
     return 2 * align_up(sizeof(int) * cap) + align_up(2 * sizeof(int)) + align_up(upper_cut_state_bytes()) + kAlign;
 }
 
+static int upper_cut_launch(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
+                            const float* planes, const float* campos, float distance_multiplier, int use_frustum,
+                            int use_lod, void* scratch, int* cut, int* count_out, hipStream_t s, int** count_dev)
+{
+    if (!nodes || !xyz || !cut || !scratch || (use_frustum && (!bounds || !planes)) ||
+        (use_lod && (!min_dist2 || !campos)))
+        return fail(HLGS_ERR_ARG, "missing tensor");
+    hipGetLastError();
+    const int cap = 2 * N + 2;
+    char* p = static_cast<char*>(aligned(scratch));
+    CutArgs a{N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum, use_lod,
+              take<int>(p, cap), take<int>(p, cap), N, cut, nullptr, nullptr, nullptr, nullptr};
+    a.count = take<int>(p, 2);
+    if (count_out) a.count = count_out;
+    char* q = take<char>(p, upper_cut_state_bytes());
+    a.state = reinterpret_cast<CutState*>(q);
+    a.arrive = reinterpret_cast<unsigned*>(q + sizeof(CutState));
+    a.level_counts = reinterpret_cast<int*>(a.arrive + kCutLevelLaunches);
+    launch_upper_cut(a, s);
+    *count_dev = a.count;
+    return check_stage(s, false, "upper_tree_cut");
+}
+
 int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
                         const float* planes, const float* campos, float distance_multiplier, int use_frustum,
                         int use_lod, void* scratch, int* cut, int* count, void* stream)
@@ -587,29 +610,33 @@ int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* 
     *count = 0;
     if (N < 0) return fail(HLGS_ERR_ARG, "N < 0");
     if (N == 0) return HLGS_OK;
-    if (!nodes || !xyz || !cut || !scratch || (use_frustum && (!bounds || !planes)) ||
-        (use_lod && (!min_dist2 || !campos)))
-        return fail(HLGS_ERR_ARG, "missing tensor");
     hipStream_t s = (hipStream_t)stream;
-    hipGetLastError();
-    const int cap = 2 * N + 2;
-    char* p = static_cast<char*>(aligned(scratch));
-    CutArgs a{N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum, use_lod,
-              take<int>(p, cap), take<int>(p, cap), N, cut, nullptr, nullptr, nullptr, nullptr};
-    a.count = take<int>(p, 2);
-    char* q = take<char>(p, upper_cut_state_bytes());
-    a.state = reinterpret_cast<CutState*>(q);
-    a.arrive = reinterpret_cast<unsigned*>(q + sizeof(CutState));
-    a.level_counts = reinterpret_cast<int*>(a.arrive + kCutLevelLaunches);
-    launch_upper_cut(a, s);
-    int rc = check_stage(s, false, "upper_tree_cut");
+    int* dev = nullptr;
+    int rc = upper_cut_launch(N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum,
+                              use_lod, scratch, cut, nullptr, s, &dev);
     if (rc) return rc;
     int host[2];
-    HLGS_TRY_HIP(hipMemcpyAsync(host, a.count, sizeof(host), hipMemcpyDeviceToHost, s));
+    HLGS_TRY_HIP(hipMemcpyAsync(host, dev, sizeof(host), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipStreamSynchronize(s));
     if (host[1]) return fail(HLGS_ERR_ARG, "upper-tree cut outgrew the node count (not a tree?)");
     *count = host[0];
     return HLGS_OK;
+}
+
+int hlgs_upper_tree_cut_device(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
+                               const float* planes, const float* campos, float distance_multiplier, int use_frustum,
+                               int use_lod, void* scratch, int* cut, int* count_device, void* stream)
+{
+    if (N < 0) return fail(HLGS_ERR_ARG, "N < 0");
+    if (!count_device) return fail(HLGS_ERR_ARG, "missing count");
+    hipStream_t s = (hipStream_t)stream;
+    if (N == 0) {
+        HLGS_TRY_HIP(hipMemsetAsync(count_device, 0, 2 * sizeof(int), s));
+        return HLGS_OK;
+    }
+    int* dev = nullptr;
+    return upper_cut_launch(N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum,
+                            use_lod, scratch, cut, count_device, s, &dev);
 }
 
 int hlgs_gather_rows(int64_t n, int row_bytes, const int64_t* idx, const void* src, void* dst, void* stream)
@@ -661,6 +688,7 @@ int hlgs_spt_cache_plan(const hlgs_cache_args* a, hlgs_cache_plan* pl, void* scr
     char* p = static_cast<char*>(aligned(scratch));
     CacheArgs c{};
     c.n_cut = a->n_cut;
+    c.n_cut_dev = a->n_cut_device;
     c.cut = a->cut;
     c.nodes = a->upper_nodes;
     c.xyz = a->upper_xyz;
@@ -704,9 +732,10 @@ int hlgs_spt_cache_plan(const hlgs_cache_args* a, hlgs_cache_plan* pl, void* scr
     }
     int rc = check_stage(s, false, "spt_cache_plan");
     if (rc) return rc;
-    int host[5];
+    int host[6];
     HLGS_TRY_HIP(hipMemcpyAsync(host, c.sizes, sizeof(host), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipStreamSynchronize(s));
+    if (host[5]) return fail(HLGS_ERR_ARG, "upper-tree cut outgrew the node count (not a tree?)");
     pl->n_kept = host[0];
     pl->n_load = host[1];
     pl->n_upper = host[2];

@@ -153,7 +153,8 @@ size_t upper_cut_state_bytes();
 
 // SPT cache bookkeeping of one streaming step (stream.hip, train_post.py:346-430)
 struct CacheArgs {
-    int n_cut;
+    int n_cut;                // the cut's length, or its capacity when n_cut_dev is set
+    const int* n_cut_dev;     // [count, overflow] of the device-side upper cut, or NULL
     const int* cut;           // coarse cut of the upper tree
     const int* nodes;         // upper-tree HierarchyNode rows
     const float* xyz;

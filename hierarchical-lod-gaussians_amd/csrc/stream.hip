@@ -590,11 +590,12 @@ __global__ void __launch_bounds__(1024) k_cache_lists(CacheArgs a)
     //    upper-tree Gaussians to render (first_child <= 0; a leaf holding SPT 0 is in both lists, as in the
     //    reference's two masks)
     int ns = 0, nu = 0;
-    for (int c0 = 0; c0 < a.n_cut; c0 += 1024) {
+    const int n_cut = a.n_cut_dev ? (a.n_cut_dev[1] ? 0 : min(a.n_cut_dev[0], a.n_cut)) : a.n_cut;
+    for (int c0 = 0; c0 < n_cut; c0 += 1024) {
         const int i = c0 + threadIdx.x;
         int v = 0, fc = -1;
         bool leaf = false;
-        if (i < a.n_cut) {
+        if (i < n_cut) {
             v = a.cut[i];
             leaf = a.nodes[6 * v + 2] == 0;
             fc = a.nodes[6 * v + 3];
@@ -677,6 +678,7 @@ __global__ void __launch_bounds__(1024) k_cache_lists(CacheArgs a)
         a.sizes[1] = nl;
         a.sizes[2] = nu;
         a.sizes[3] = prefix;
+        a.sizes[5] = a.n_cut_dev ? (a.n_cut_dev[1] || a.n_cut_dev[0] > a.n_cut) : 0;  // the cut overflowed
     }
 }
 

@@ -4,7 +4,8 @@ The reference keeps every Gaussian in host storage (GaussianModel.move_storage_t
 :430-460) and, per training view, keeps on the GPU only the Gaussians of the SPTs the view cuts:
 
   setup                  train_post.py:208-231  (skybox resident, empty SPT state)
-  coarse cut             :326-343  -> spt.upper_tree_cut (one workgroup, k_upper_cut)
+  coarse cut             :326-343  -> hlgs_upper_tree_cut_device (k_upper_cut + k_cut_level), its length read
+                                      on the device by the plan
   bookkeeping            :346-430  -> hlgs_spt_cache_plan (k_cache_lists + two scans + k_cache_split), with
                                       get_spt_cut_cuda on the SPTs to load
   write-back and load    :439-479  -> three launches move all six parameters and their twelve Adam moments:
@@ -175,6 +176,7 @@ class SPTCache:
         self.wb_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
         self.wb_done = None
         self._wb_hold = None
+        self._cut = self._cut_scratch = self._cut_count = None
         self.prev_SPT_indices = torch.empty(0, dtype=torch.int32, device=dev)
         self.prev_SPT_distances = torch.empty(0, dtype=torch.float32, device=dev)
         self.prev_SPT_counts = torch.empty(0, dtype=torch.int32, device=dev)
@@ -191,9 +193,19 @@ class SPTCache:
         dev = self.device
         cam = camera_center.detach().reshape(-1)[:3].to(dev, torch.float32).contiguous()
         planes = _spt.extract_frustum_planes(full_proj_transform.to(dev, torch.float32)) if self.use_frustum else None
-        coarse = _spt.upper_tree_cut(self.nodes, self.xyz, self.bounds, self.min_distance_squared, planes, cam,
-                                     distance_multiplier, self.use_frustum, True)
-        n_cut, m, R = coarse.numel(), self.prev_SPT_indices.numel(), self.render_indices.numel()
+        # coarse cut with its length left on the device (hlgs_upper_tree_cut_device): the plan reads it, so the step
+        # has one host synchronisation, the plan's
+        N = self.nodes.size(0)
+        if self._cut is None:
+            self._cut = torch.empty((max(N, 1),), dtype=torch.int32, device=dev)
+            self._cut_scratch = torch.empty(lib.hlgs_upper_cut_scratch_size(N), dtype=torch.uint8, device=dev)
+            self._cut_count = torch.zeros((2,), dtype=torch.int32, device=dev)
+        L.check(lib.hlgs_upper_tree_cut_device(N, _p(self.nodes), _p(self.xyz), _p(self.bounds),
+                                               _p(self.min_distance_squared), _p(planes), _p(cam),
+                                               float(distance_multiplier), int(bool(self.use_frustum)), 1,
+                                               _p(self._cut_scratch), _p(self._cut), _p(self._cut_count), L.stream()))
+        coarse = self._cut
+        n_cut, m, R = N, self.prev_SPT_indices.numel(), self.render_indices.numel()
         # the ten output lists carved from one int32 allocation (the distances as float32 views of it)
         sizes = dict(keep_spt_indices=m, keep_spt_distances=m, keep_spt_counts=m, load_spt_indices=n_cut,
                      load_spt_distances=n_cut, upper_render=n_cut, keep_rows=R, render_kept=R, write_back_rows=R,
@@ -206,7 +218,7 @@ class SPTCache:
         a = L.CacheArgs(n_cut, _p(coarse), _p(self.nodes), _p(self.xyz), _p(cam), float(distance_multiplier),
                         self.num_spts, m, _p(self.prev_SPT_indices), _p(self.prev_SPT_distances),
                         _p(self.prev_SPT_counts), R, _p(self.render_indices), int(self.n_loaded), self.sky,
-                        self.rtol, self.atol)
+                        self.rtol, self.atol, _p(self._cut_count))
         pl = L.CachePlan(*[out[f].data_ptr() for f, _ in L.CachePlan._fields_[:10]])
         scratch = torch.empty(lib.hlgs_spt_cache_scratch_size(n_cut, m, R, self.num_spts), dtype=torch.uint8,
                               device=dev)

@@ -239,6 +239,11 @@ int hlgs_morton_codes(int P, const float* xyz, const float* mn, const float* mx,
  * visited.  cut (device, N entries) receives the nodes in the reference's order; *count (host) their number.
  * scratch: hlgs_upper_cut_scratch_size(N) bytes.  One host synchronisation (the reference's len()). */
 size_t hlgs_upper_cut_scratch_size(int N);
+/* The same cut without the host read: the count and an overflow flag land in count_device[0..1] (device memory),
+ * for hlgs_spt_cache_plan's n_cut_device, which reads them in its own single host synchronisation. */
+int hlgs_upper_tree_cut_device(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
+                               const float* planes, const float* campos, float distance_multiplier, int use_frustum,
+                               int use_lod, void* scratch, int* cut, int* count_device, void* stream);
 int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
                         const float* planes, const float* campos, float distance_multiplier, int use_frustum,
                         int use_lod, void* scratch, int* cut, int* count, void* stream);
@@ -282,6 +287,8 @@ typedef struct hlgs_cache_args {
     int n_loaded_prev;                 /* len(load_from_disk_indices) of the previous pass */
     int skybox_points;
     float rtol, atol;                  /* isclose of the reused distances (Reuse_SPT_Tolerarance, 0.05) */
+    const int* n_cut_device;           /* NULL, or the [count, overflow] words of hlgs_upper_tree_cut_device: the
+                                          cut's length is then read on the device and n_cut is its capacity */
 } hlgs_cache_args;
 typedef struct hlgs_cache_plan {
     int* keep_spt_indices;             /* m: keep_SPT_indices */
