@@ -12,8 +12,12 @@ constexpr int kScanItems = 2048;    // elements per scan block (256 threads x 8)
 constexpr int kSortCap = 4096;      // largest per-tile list sorted in one LDS pass
 constexpr int kWaveSortCap = 1024;  // longest per-tile list sorted in registers by one wave
 constexpr size_t kAlign = 256;
-constexpr int kBinThreads = 1024;   // LDS-histogram binning: threads per block
-constexpr int kBinGauss = 4096;     // Gaussians per binning block
+
+#ifndef HLGS_BIN_GAUSS
+#define HLGS_BIN_GAUSS 4096
+#endif
+constexpr int kBinGauss = HLGS_BIN_GAUSS;  // Gaussians per binning block
+constexpr int kBinThreads = kBinGauss / 4; // LDS-histogram binning: threads per block (four Gaussians each)
 constexpr int kBinMaxTiles = 16384; // tile grids up to this use LDS histograms (2 x 64 KiB)
 
 // The blend backward splits each tile's list into up to kBwdSplits + 1 chunks of bwd_chunk_len(count) entries (a
