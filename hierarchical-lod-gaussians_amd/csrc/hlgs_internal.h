@@ -13,11 +13,7 @@ constexpr int kSortCap = 4096;      // largest per-tile list sorted in one LDS p
 constexpr int kWaveSortCap = 1024;  // longest per-tile list sorted in registers by one wave
 constexpr size_t kAlign = 256;
 
-#ifndef HLGS_BIN_GAUSS
-#define HLGS_BIN_GAUSS 4096
-#endif
-constexpr int kBinGauss = HLGS_BIN_GAUSS;  // Gaussians per binning block
-constexpr int kBinThreads = kBinGauss / 4; // LDS-histogram binning: threads per block (four Gaussians each)
+// Gaussians per binning block: 4,096 or 2,048 chosen per launch (raster_fwd.hip bin_gauss); threads = Gaussians / 4
 constexpr int kBinMaxTiles = 16384; // tile grids up to this use LDS histograms (2 x 64 KiB)
 
 // The blend backward splits each tile's list into up to kBwdSplits + 1 chunks of bwd_chunk_len(count) entries (a

@@ -302,16 +302,17 @@ __global__ void __launch_bounds__(64) k_preprocess_sh(hlgs_raster_args a, Geom g
 }
 
 // ------------------------------------------------------------------------------------------------
-// Tile binning with block-level LDS histograms.  A block owns kBinGauss consecutive Gaussians; its
+// Tile binning with block-level LDS histograms.  A block owns BG consecutive Gaussians (bin_gauss); its
 // instances are counted per tile in LDS and each non-empty bin costs one coalesced device atomic,
 // instead of one lane-scattered atomic per (Gaussian, tile) instance.
 // ------------------------------------------------------------------------------------------------
-// s_pre[k] = exclusive prefix of tiles_touched over the block's kBinGauss Gaussians (0 past P), s_pre[kBinGauss] =
+// s_pre[k] = exclusive prefix of tiles_touched over the block's BG Gaussians (0 past P), s_pre[BG] =
 // the block's total: thread t scans its four consecutive entries, then the 1024 thread totals are scanned.
+template <int BG>
 __device__ __forceinline__ void block_rect_prefix(int P, const Geom& g, uint32_t* s_pre, uint32_t* s_w)
 {
-    static_assert(kBinGauss == 4 * kBinThreads, "four Gaussians per thread");
-    const int g0 = blockIdx.x * kBinGauss, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    constexpr int BT = BG / 4;  // threads: four Gaussians each
+    const int g0 = blockIdx.x * BG, t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t a[4], sum = 0, mx = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -321,7 +322,7 @@ __device__ __forceinline__ void block_rect_prefix(int P, const Geom& g, uint32_t
         mx = max(mx, a[k]);
     }
     for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
-    if (lane == 0) atomicMax(&s_w[kBinThreads / 64], mx);
+    if (lane == 0) atomicMax(&s_w[(BG / 4) / 64], mx);
     uint32_t x = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -331,7 +332,7 @@ __device__ __forceinline__ void block_rect_prefix(int P, const Geom& g, uint32_t
     if (lane == 63) s_w[w] = x;
     __syncthreads();
     uint32_t base = 0, total = 0;
-    for (int i = 0; i < kBinThreads / 64; i++) {
+    for (int i = 0; i < (BG / 4) / 64; i++) {
         const uint32_t c = s_w[i];
         if (i < w) base += c;
         total += c;
@@ -342,24 +343,24 @@ __device__ __forceinline__ void block_rect_prefix(int P, const Geom& g, uint32_t
         s_pre[4 * t + k] = run;
         run += a[k];
     }
-    if (t == 0) s_pre[kBinGauss] = total;
+    if (t == 0) s_pre[BG] = total;
     __syncthreads();
 }
 
-// the block's longest rect (s_w[kBinThreads / 64], zeroed before block_rect_prefix)
+// the block's longest rect (s_w[(BG / 4) / 64], zeroed before block_rect_prefix)
 constexpr uint32_t kNarrowRect = 64;
 
 // Calls f(idx, tile) for every binned instance of the block's Gaussians: every tile of the rect, or for the
 // alt rasterizer the tiles alt_tile_keep leaves (rasterizer_impl.cu:147-179 of alt-rasterizer).  The block's
 // instances are numbered Gaussian by Gaussian (s_pre) and each thread takes one contiguous run of them, so a
 // Gaussian whose rect spans thousands of tiles is spread over the whole block instead of serialising one thread.
-template <typename F>
+template <int BG, typename F>
 __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy, bool alt, const uint32_t* s_pre,
                                                   const uint32_t* s_w, F&& f)
 {
-    const int g0 = blockIdx.x * kBinGauss;
-    if (s_w[kBinThreads / 64] <= kNarrowRect) {  // no wide rect in this block: one thread per Gaussian
-        for (int k = threadIdx.x; k < kBinGauss; k += kBinThreads) {
+    const int g0 = blockIdx.x * BG;
+    if (s_w[(BG / 4) / 64] <= kNarrowRect) {  // no wide rect in this block: one thread per Gaussian
+        for (int k = threadIdx.x; k < BG; k += (BG / 4)) {
             if (s_pre[k + 1] == s_pre[k]) continue;
             const int idx = g0 + k;
             const float2 xy = g.means2D[idx];
@@ -380,12 +381,12 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
         }
         return;
     }
-    const uint32_t total = s_pre[kBinGauss];
-    const uint32_t chunk = (total + kBinThreads - 1) / kBinThreads;
+    const uint32_t total = s_pre[BG];
+    const uint32_t chunk = (total + (BG / 4) - 1) / (BG / 4);
     uint32_t i = threadIdx.x * chunk;
     const uint32_t iend = min(total, i + chunk);
     if (i >= iend) return;
-    int lo = 0, hi = kBinGauss - 1;  // last k with s_pre[k] <= i: the Gaussian holding instance i
+    int lo = 0, hi = BG - 1;  // last k with s_pre[k] <= i: the Gaussian holding instance i
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (s_pre[mid] <= i) lo = mid;
@@ -420,22 +421,23 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
     }
 }
 
-__global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
+template <int BG>
+__global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
                                                              uint32_t* __restrict__ tile_count, int gx, int gy, int alt,
                                                              uint32_t* __restrict__ block_tot)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
-    __shared__ uint32_t s_pre[kBinGauss + 1];
-    __shared__ uint32_t s_w[kBinThreads / 64 + 1];
+    __shared__ uint32_t s_pre[BG + 1];
+    __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
     const int T = gx * gy;
-    for (int t = threadIdx.x; t < T; t += kBinThreads) s_hist[t] = 0;
-    if (threadIdx.x == 0) s_w[kBinThreads / 64] = 0;
+    for (int t = threadIdx.x; t < T; t += (BG / 4)) s_hist[t] = 0;
+    if (threadIdx.x == 0) s_w[(BG / 4) / 64] = 0;
     __syncthreads();
-    block_rect_prefix(P, g, s_pre, s_w);
-    if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[kBinGauss];
-    for_each_instance(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
+    block_rect_prefix<BG>(P, g, s_pre, s_w);
+    if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[BG];
+    for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
     __syncthreads();
-    for (int t = threadIdx.x; t < T; t += kBinThreads) {
+    for (int t = threadIdx.x; t < T; t += (BG / 4)) {
         const uint32_t c = s_hist[t];
         if (c) atomicAdd(&tile_count[t], c);
     }
@@ -444,39 +446,40 @@ __global__ void __launch_bounds__(kBinThreads) k_count_tiles(int P, const int* _
 // Same block -> Gaussian mapping as k_count_tiles: reserve the block's run inside every tile segment
 // with one returning atomic per bin, then hand out slots from LDS.  Slot order inside a tile is
 // irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
-__global__ void __launch_bounds__(kBinThreads) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
+template <int BG>
+__global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
                                                                   uint64_t* __restrict__ keys, int gx, int gy, int alt,
                                                                   Guard gd, const uint32_t* __restrict__ block_base)
 {
     if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
-    __shared__ uint32_t s_pre[kBinGauss + 1];
-    __shared__ uint32_t s_w[kBinThreads / 64 + 1];
+    __shared__ uint32_t s_pre[BG + 1];
+    __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
     const int T = gx * gy;
     uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
     uint32_t* s_rank = s_hist + T; // per-tile running rank
-    for (int t = threadIdx.x; t < T; t += kBinThreads) { s_cnt[t] = 0; s_rank[t] = 0; }
-    if (threadIdx.x == 0) s_w[kBinThreads / 64] = 0;
+    for (int t = threadIdx.x; t < T; t += (BG / 4)) { s_cnt[t] = 0; s_rank[t] = 0; }
+    if (threadIdx.x == 0) s_w[(BG / 4) / 64] = 0;
     __syncthreads();
-    block_rect_prefix(P, g, s_pre, s_w);
+    block_rect_prefix<BG>(P, g, s_pre, s_w);
     {  // point_offsets (the inclusive scan of tiles_touched) = the block's base (k_plan) + the block-local prefix
-        const int g0 = blockIdx.x * kBinGauss, g1 = min(P, g0 + kBinGauss);
+        const int g0 = blockIdx.x * BG, g1 = min(P, g0 + BG);
         const uint32_t base = block_base[blockIdx.x];
-        for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += kBinThreads) {
+        for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += (BG / 4)) {
             const int k = idx - g0;
             g.point_offsets[idx] = base + s_pre[k + 1];
             if (radii[idx] > 0) g.splat[4 * (size_t)idx + 3].x = __uint_as_float(base + s_pre[k]);
         }
     }
-    for_each_instance(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
+    for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
     __syncthreads();
-    for (int t = threadIdx.x; t < T; t += kBinThreads) {
+    for (int t = threadIdx.x; t < T; t += (BG / 4)) {
         const uint32_t c = s_cnt[t];
         s_cnt[t] = c ? ranges[t].x + atomicAdd(&cursor[t], c) : 0u;
     }
     __syncthreads();
-    for_each_instance(g, gx, gy, alt, s_pre, s_w, [&](int idx, int tile) {
+    for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int tile) {
         const uint32_t r = atomicAdd(&s_rank[tile], 1u);
         keys[s_cnt[tile] + r] = ((uint64_t)__float_as_uint(g.depths[idx]) << 32) | (uint32_t)idx;
     });
@@ -909,10 +912,13 @@ __global__ void __launch_bounds__(256) k_relocation(int P, const float* __restri
 // host launchers
 // ------------------------------------------------------------------------------------------------
 // LDS-histogram binning with the one-block plan: tile grids up to kBinMaxTiles and up to kPlanRun * 1024 blocks of
-// kBinGauss Gaussians (67M); anything larger takes the generic per-Gaussian path.
+// bin_gauss(P) Gaussians (67M); anything larger takes the generic per-Gaussian path.
+// Gaussians per binning block: 4,096, or 2,048 when that would leave fewer than ~200 blocks for the 256 CUs
+int bin_gauss(int P) { return P >= 200 * 4096 ? 4096 : 2048; }
+
 bool lds_binning(int P, int gx, int gy)
 {
-    return gx * gy <= kBinMaxTiles && (long)(P + kBinGauss - 1) / kBinGauss <= (long)kPlanRun * 1024;
+    return gx * gy <= kBinMaxTiles && (long)(P + bin_gauss(P) - 1) / bin_gauss(P) <= (long)kPlanRun * 1024;
 }
 
 // Dynamic LDS above 64 KiB must be opted into per kernel (idempotent; done once per process).
@@ -922,8 +928,10 @@ static void allow_big_lds()
     if (done) return;
     // the kernels' static LDS (the block's rect prefix, ~16 KiB) comes out of the same 160 KiB
     const int dyn = 2 * (int)sizeof(uint32_t) * kBinMaxTiles;
-    hipFuncSetAttribute((const void*)k_count_tiles, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_scatter_keys_lds, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_count_tiles<4096>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_count_tiles<2048>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_scatter_keys_lds<4096>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_scatter_keys_lds<2048>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
     hipGetLastError();
     done = true;
 }
@@ -933,15 +941,20 @@ void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_c
 {
     const size_t lds = sizeof(uint32_t) * (size_t)gx * gy;
     allow_big_lds();
-    hipLaunchKernelGGL(k_count_tiles, dim3((P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads), lds, s, P, radii, g,
-                       tile_count, gx, gy, (int)alt, g.scan_tmp);
+    const int bg = bin_gauss(P);
+    if (bg == 4096)
+        hipLaunchKernelGGL(k_count_tiles<4096>, dim3((P + 4095) / 4096), dim3(1024), lds, s, P, radii, g, tile_count, gx,
+                           gy, (int)alt, g.scan_tmp);
+    else
+        hipLaunchKernelGGL(k_count_tiles<2048>, dim3((P + 2047) / 2048), dim3(512), lds, s, P, radii, g, tile_count, gx,
+                           gy, (int)alt, g.scan_tmp);
 }
 
 void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, hipStream_t s)
 {
     static_assert(kPlanRun * 1024 >= kBinMaxTiles, "one k_plan block covers every LDS-binned tile grid");
 
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, (P + kBinGauss - 1) / kBinGauss, im.tile_count,
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, (P + bin_gauss(P) - 1) / bin_gauss(P), im.tile_count,
                        im.tile_cursor, im.ranges, T, im.misc, host);
 }
 
@@ -996,9 +1009,14 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
     if (timing) stage_mark(s, 3, true);
     if (lds_binning(a.P, gx, gy)) {
         allow_big_lds();
-        hipLaunchKernelGGL(k_scatter_keys_lds, dim3((a.P + kBinGauss - 1) / kBinGauss), dim3(kBinThreads),
-                           2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy,
-                           alt, gd, g.scan_tmp);
+        if (bin_gauss(a.P) == 4096)
+            hipLaunchKernelGGL(k_scatter_keys_lds<4096>, dim3((a.P + 4095) / 4096), dim3(1024),
+                               2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys,
+                               gx, gy, alt, gd, g.scan_tmp);
+        else
+            hipLaunchKernelGGL(k_scatter_keys_lds<2048>, dim3((a.P + 2047) / 2048), dim3(512),
+                               2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys,
+                               gx, gy, alt, gd, g.scan_tmp);
     } else
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
                            im.tile_cursor, b.keys, gx, gy, alt, gd);
