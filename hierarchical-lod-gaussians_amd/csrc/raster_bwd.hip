@@ -19,16 +19,31 @@ namespace hlgs {
 // (accum_rec, last_alpha, last_color) only to form dL/dalpha = <c - accum, dL/dpixel>, which is linear
 // in the accumulators; so one scalar ARD = <accum, dL/dpixel> (+ depth term), updated by the current
 // splat once its own step is done, carries the same information.
+//
+// The background term of dL/dalpha, -T_final <bg, dL/dpixel> / (1 - alpha) (backward.cu:688-691), rides along in ARD:
+// with ARD' = ARD + T_final <bg, dL/dpixel> / T_behind (T_behind = transmittance behind the current splat), the
+// recursion is unchanged (T_final bgd / T_i = (1 - alpha_i) T_final bgd / T_behind) and dL/dalpha = T (cd - ARD'),
+// so the step needs no product with 1/(1 - alpha) beyond the transmittance update.
 struct PixB {
     float T;                 // transmittance in front of the current splat
-    float TB;                // T_final * <bg, dL/dpixel>
-    float ARD;               // <accum_rec, dL/dpixel> + accum_invdepth * dL/dinvdepth
+    float ARD;               // <accum_rec, dL/dpixel> + accum_invdepth * dL/dinvdepth + T_final <bg, dL/dpixel> / T_behind
     float dr, dg, db, dinv;  // dL/dpixel, dL/dinvdepth
     uint32_t last;           // n_contrib
 };
 
+// 1 if o G <= 0.99, else 0: the reference's dL/dalpha = 0 above the alpha clamp (backward.cu:619, 693) as a factor.
+// fma(-2^40, ta, 2^40 next(0.99f)) is exactly 2^40 (next(0.99f) - ta) for ta near 0.99f (both operands scaled by a
+// power of two), so it is >= 2^16 for ta <= 0.99f and <= 0 for ta > 0.99f; the clamp makes it 1 or 0 (NaN -> 0).
+__device__ __forceinline__ float below_clamp(float test_alpha)
+{
+    return __builtin_amdgcn_fmed3f(fmaf(-1099511627776.0f, test_alpha, 1088516562944.0f + 65536.0f), 0.f, 1.f);
+}
+
 // 1/(1 - alpha) for alpha in [0, 0.99].  HLGS_BWD_RCP_NR > 0: that many Newton steps from the bit-pattern seed
 // instead of v_rcp_f32 (A/B of the transcendental's issue cost, tools/valu_probe.hip).
+#ifndef HLGS_BWD_HOIST
+#define HLGS_BWD_HOIST 1
+#endif
 #ifndef HLGS_BWD_RCP_NR
 #define HLGS_BWD_RCP_NR 0
 #endif
@@ -53,22 +68,29 @@ __device__ __forceinline__ float rcp_one_minus(float alpha)
 //   acc = [Sum w dx, Sum w dy, Sum w dx^2, Sum w dx dy, Sum w dy^2, Sum w*mult, dcolor r g b, dinvdepth]
 // q = (-a/2, -b, -c/2) * log2(e) so that G = exp2(q0 dx^2 + q1 dx dy + q2 dy^2) = exp(power).
 // ALT: the alt rasterizer's backward (alt-rasterizer/cuda_rasterizer/backward.cu:596-624) has no
-// o * G > 0.99 => dL/dalpha = 0 rule; its doubled background term is folded into p.TB by the caller.
+// o * G > 0.99 => dL/dalpha = 0 rule; its doubled background term is folded into ARD by the caller.
 template <bool INTERP, bool DEPTH, bool ALT>
 __device__ __forceinline__ uint64_t bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& q, const float4& col,
                                              float invz, float tt, float fr, float thr, float (&acc)[10])
 {
     const float e2 = splat_e2(q, dx, dy);  // power * log2(e)
-    const float G = __builtin_amdgcn_exp2f(e2);
+    // The falloff, alpha and 1/(1 - alpha) are computed for every lane ahead of the validity branch (HLGS_BWD_HOIST):
+    // they depend on the pair alone, so their transcendental latency overlaps the compare -> SALU -> exec chain that
+    // decides the branch instead of following it.
+    float G = __builtin_amdgcn_exp2f(e2);
     const float test_alpha = q.w * G;
     const float my_alpha = fminf(0.99f, test_alpha);
     float alpha = my_alpha;
     if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
+    float r1m = rcp_one_minus(alpha);
+    if (!ALT) G *= below_clamp(test_alpha);
+#if HLGS_BWD_HOIST
+    asm volatile("" : "+v"(G), "+v"(r1m), "+v"(alpha));  // keep them above the branch
+#endif
     // alpha >= 1/255 (alpha_e2_threshold), as a wave mask: one v_cmp per test, combined in SALU (the wave is full)
     const uint64_t valid = __builtin_amdgcn_ballot_w64(li < p.last) & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) &
                            ~__builtin_amdgcn_ballot_w64(e2 < thr);
     if (__builtin_amdgcn_inverse_ballot_w64(valid)) {
-        const float r1m = rcp_one_minus(alpha);
         p.T = p.T * r1m;
         const float weight = alpha * p.T;
         float cd = col.x * p.dr + col.y * p.dg + col.z * p.db;
@@ -79,8 +101,7 @@ __device__ __forceinline__ uint64_t bwd_pair(PixB& p, uint32_t li, float dx, flo
         acc[7] += weight * p.dg;
         acc[8] += weight * p.db;
         if (DEPTH) acc[9] += weight * p.dinv;
-        float dL_dalpha = raw * p.T - p.TB * r1m;
-        if (!ALT) dL_dalpha = test_alpha > 0.99f ? 0.f : dL_dalpha;
+        const float dL_dalpha = raw * p.T;
         const float w = G * dL_dalpha;
         const float wdx = w * dx, wdy = w * dy;
         acc[0] += wdx;
@@ -91,50 +112,6 @@ __device__ __forceinline__ uint64_t bwd_pair(PixB& p, uint32_t li, float dx, flo
         if (INTERP) acc[5] += (tt - powf(1.0f - my_alpha, fr - 1.0f) * (tt - 1.0f) * fr) * w;
         else acc[5] += w;
     }
-    return valid;
-}
-
-// bwd_pair without the exec-masked branch: every lane runs the step and an invalid pair is neutralised by two
-// selects (alpha -> 0 makes 1/(1 - alpha) = 1, so T, ARD and the colour moments are unchanged; w -> 0 clears the
-// geometric moments).  Valid pairs run the very same operations as bwd_pair.  Two such steps on different
-// quadrants share one basic block, so their dependency chains (exp2 -> alpha -> rcp -> T -> moments) interleave.
-template <bool INTERP, bool DEPTH, bool ALT>
-__device__ __forceinline__ uint64_t bwd_pair_pred(PixB& p, uint32_t li, float dx, float dy, const float4& q,
-                                                  const float4& col, float invz, float tt, float fr, float thr,
-                                                  float (&acc)[10])
-{
-    const float e2 = splat_e2(q, dx, dy);
-    const uint64_t valid = __builtin_amdgcn_ballot_w64(li < p.last) & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) &
-                           ~__builtin_amdgcn_ballot_w64(e2 < thr);
-    const bool vb = __builtin_amdgcn_inverse_ballot_w64(valid);
-    const float G = __builtin_amdgcn_exp2f(e2);
-    const float test_alpha = q.w * G;
-    const float my_alpha = fminf(0.99f, test_alpha);
-    float alpha = my_alpha;
-    if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
-    alpha = vb ? alpha : 0.f;
-    const float r1m = rcp_one_minus(alpha);
-    p.T = p.T * r1m;
-    const float weight = alpha * p.T;
-    float cd = col.x * p.dr + col.y * p.dg + col.z * p.db;
-    if (DEPTH) cd += invz * p.dinv;
-    const float raw = cd - p.ARD;
-    p.ARD = fmaf(alpha, raw, p.ARD);
-    acc[6] += weight * p.dr;
-    acc[7] += weight * p.dg;
-    acc[8] += weight * p.db;
-    if (DEPTH) acc[9] += weight * p.dinv;
-    float dL_dalpha = raw * p.T - p.TB * r1m;
-    if (!ALT) dL_dalpha = test_alpha > 0.99f ? 0.f : dL_dalpha;
-    const float w = vb ? G * dL_dalpha : 0.f;
-    const float wdx = w * dx, wdy = w * dy;
-    acc[0] += wdx;
-    acc[1] += wdy;
-    acc[2] = fmaf(wdx, dx, acc[2]);
-    acc[3] = fmaf(wdx, dy, acc[3]);
-    acc[4] = fmaf(wdy, dy, acc[4]);
-    if (INTERP) acc[5] += (tt - powf(1.0f - my_alpha, fr - 1.0f) * (tt - 1.0f) * fr) * w;
-    else acc[5] += w;
     return valid;
 }
 
@@ -177,11 +154,11 @@ struct BwdArgs {
 // 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
 // whose n_contrib lies behind it) run bwd_pair, the ten moments are folded over the wave, and one record per
 // (tile, splat) is stored after the batch.
-#ifndef HLGS_BWD_PAIRS
-#define HLGS_BWD_PAIRS 0  // 1: interleave two quadrants' steps (bwd_pair_pred); measured slower (496 vs 423 us)
+#ifndef HLGS_BWD_RS
+#define HLGS_BWD_RS 1  // reduce-scatter of the ten moments (wave_reduce10_rs); 0: full-wave reductions (wave_reduce10)
 #endif
 #ifndef HLGS_BWD_PREFETCH
-#define HLGS_BWD_PREFETCH (!HLGS_BWD_PAIRS)  // next splat's LDS reads ahead of this one's reduction
+#define HLGS_BWD_PREFETCH 1  // next splat's LDS reads ahead of this one's reduction
 #endif
 #ifndef HLGS_BWD_WAVES
 #define HLGS_BWD_WAVES 5  // waves per SIMD: 96 VGPRs
@@ -220,6 +197,11 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     const size_t HW = (size_t)H * W;
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
     const float lx = (float)(tx0 + (lane & 7)), ly = (float)(ty0 + (lane >> 3));
+#if HLGS_BWD_RS
+    // the reduced moment this lane stores (wave_reduce10_rs layout), as an offset into s_m; -1: none
+    const int wm_i = (lane & 3) ? -1 : reduce10_index(lane >> 4, (lane >> 2) & 3);
+    const int wm = wm_i < 0 ? -1 : 64 * wm_i;
+#endif
 
     // lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant k
     PixB ps[4];
@@ -233,25 +215,25 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         const float tf = inside ? final_Ts[pid] : 0.f;
         p.T = tf;
         p.last = inside ? n_contrib[pid] : 0u;
-        p.ARD = 0.f;
         p.dr = inside ? dL_dpixels[pid] : 0.f;
         p.dg = inside ? dL_dpixels[HW + pid] : 0.f;
         p.db = inside ? dL_dpixels[2 * HW + pid] : 0.f;
         p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
-        if (p.last > cnt) {  // still blending at the chunk's end (so the forward sampled it there, with T >= 1e-4)
-            const float* sk = st + k * 5 * 64;
-            p.T = sk[0];
-            float behind = sk[64] * p.dr + sk[128] * p.dg + sk[192] * p.db;
-            if (DEPTH) behind += sk[256] * p.dinv;
-            p.ARD = behind / p.T;  // <accum_rec, dL/dpixel> (+ depth) at the chunk's end
-        }
         float bgd = 0.f;
         bgd += bg[0] * p.dr;
         bgd += bg[1] * p.dg;
         bgd += bg[2] * p.db;
         // the alt rasterizer's ar includes the final colour's T_final * bg and adds the bg term once more
         // (alt-rasterizer backward.cu:608, 619): the background enters dL/dalpha twice
-        p.TB = ALT ? 2.f * (tf * bgd) : tf * bgd;
+        if (ALT) bgd *= 2.f;
+        p.ARD = bgd;  // T_final <bg, dL/dpixel> / T_final
+        if (p.last > cnt) {  // still blending at the chunk's end (so the forward sampled it there, with T >= 1e-4)
+            const float* sk = st + k * 5 * 64;
+            p.T = sk[0];
+            float behind = sk[64] * p.dr + sk[128] * p.dg + sk[192] * p.db;
+            if (DEPTH) behind += sk[256] * p.dinv;
+            p.ARD = fmaf(tf, bgd, behind) / p.T;  // <accum_rec, dL/dpixel> (+ depth, + bg term) at the chunk's end
+        }
         uint32_t m = min(p.last, cnt);
         for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
         qlast[k] = __builtin_amdgcn_readfirstlane(m);
@@ -327,46 +309,11 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                     acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
                 }
                 uint64_t any = 0;  // lanes with a valid pair (wave mask)
-#if HLGS_BWD_PAIRS
-                // quadrants taken two at a time (predicated steps in one block: interleaved chains), a lone one
-                // with the exec-masked step; qm is wave-uniform
-#define HLGS_P1(k)                                                                                                \
-    any |= bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * ((k) & 1)), xy.y - (ly + 8.f * ((k) >> 1)), co, \
-                                        col, xy.z, tf.x, tf.y, col.w, acc)
-#define HLGS_PP(k)                                                                                                \
-    any |= bwd_pair_pred<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * ((k) & 1)),                           \
-                                             xy.y - (ly + 8.f * ((k) >> 1)), co, col, xy.z, tf.x, tf.y, col.w, acc)
-                switch (qm) {
-                case 1: HLGS_P1(0); break;
-                case 2: HLGS_P1(1); break;
-                case 4: HLGS_P1(2); break;
-                case 8: HLGS_P1(3); break;
-                case 3: HLGS_PP(0); HLGS_PP(1); break;
-                case 5: HLGS_PP(0); HLGS_PP(2); break;
-                case 6: HLGS_PP(1); HLGS_PP(2); break;
-                case 9: HLGS_PP(0); HLGS_PP(3); break;
-                case 10: HLGS_PP(1); HLGS_PP(3); break;
-                case 12: HLGS_PP(2); HLGS_PP(3); break;
-                case 7: HLGS_PP(0); HLGS_PP(1); HLGS_P1(2); break;
-                case 11: HLGS_PP(0); HLGS_PP(1); HLGS_P1(3); break;
-                case 13: HLGS_PP(0); HLGS_PP(2); HLGS_P1(3); break;
-                case 14: HLGS_PP(1); HLGS_PP(2); HLGS_P1(3); break;
-                case 15:  // two pairs; the barrier keeps the scheduler from overlapping all four chains (registers)
-                    HLGS_PP(0); HLGS_PP(1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    HLGS_PP(2); HLGS_PP(3);
-                    break;
-                default: break;
-                }
-#undef HLGS_P1
-#undef HLGS_PP
-#else
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     if ((qm >> k) & 1u)  // uniform branch
                         any |= bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), co, col,
                                                        xy.z, tf.x, tf.y, col.w, acc);
-#endif
                 const int jc = j;
 #if HLGS_BWD_PREFETCH
                 if (todo) {
@@ -378,6 +325,10 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                 }
 #endif
                 if (any) {
+#if HLGS_BWD_RS
+                    const float r = wave_reduce10_rs(acc);
+                    if (wm >= 0) s_m[wm + jc] = r;
+#else
                     float r0, r1, r2;
                     wave_reduce10(acc, r0, r1, r2);
                     if ((lane & 15) == 0) {
@@ -386,6 +337,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                         s_m[64 * (4 + c) + jc] = r1;
                         if (!(row & 1)) s_m[64 * (8 + (row >> 1)) + jc] = r2;
                     }
+#endif
                 }
             }
         }

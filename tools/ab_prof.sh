@@ -5,6 +5,7 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 V=hierarchical-lod-gaussians_amd/lib/variants
 VARS="${VARIANTS:-A B C}"
 for v in $VARS; do
+  [ "${SKIP_TESTS:-0}" = 1 ] && break  # timing-only diagnostic variants (parity deliberately broken)
   if [ $v = C ]; then L=""; else L=$V/$v.so; fi
   HLGS_LIBRARY=$L timeout -k 10 600 python -m pytest tests/test_gpu_parity.py tests/test_gpu_alt.py -q -x -p no:cacheprovider > gpurun_out/abt_$v.log 2>&1
   rc=$?; echo "$v tests rc=$rc $(tail -1 gpurun_out/abt_$v.log)"; [ $rc -eq 0 ] || exit $rc
