@@ -33,6 +33,7 @@ import json
 import math
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -153,8 +154,18 @@ def cpu_baseline(P, deg, W, H, reference_order=True):
                                       sample=f"same frame, {dt1:.2f} s on 1 thread"))
     ref_order = None
     if reference_order:
-        with O.reference_order():
-            ref_order = _oracle_frame(O, sc, cn, g, gd)[1]
+        # the reference order twice: uncontracted, and with a*b+c contracted (the reference is built by nvcc with
+        # --fmad=true); each serial, on its own thread (ctypes releases the GIL)
+        ref_order = {}
+
+        def run(key):
+            with O.reference_order(omp=key):
+                ref_order[key] = _oracle_frame(O, sc, cn, g, gd, omp=key)[1]
+        th = [threading.Thread(target=run, args=(k,)) for k in (False, "fma")]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
     return summary, ref, ref_order
 
 
@@ -616,8 +627,14 @@ def main():
         parity = parity_report(gpu, ref, "oracle (C restatement of the reference; alpha decided in the shared "
                                          "arithmetic contract, A-17), identical inputs, full configs[1] frame")
         parity["reference_order"] = parity_report(
-            gpu, ref_order, "oracle with alpha decided in the reference's own float op order (power, expf, "
-                            "alpha < 1/255; forward.cu:538-560, backward.cu:614-643), same frame")
+            gpu, ref_order[False], "oracle with alpha decided in the reference's own float op order (power, expf, "
+                                   "alpha < 1/255; forward.cu:538-560, backward.cu:614-643), no contraction, same frame")
+        parity["reference_order_fma"] = parity_report(
+            gpu, ref_order["fma"], "the same reference-order oracle built with a*b+c contracted (nvcc's default "
+                                   "--fmad=true; hierarchy-rasterizer/setup.py:31), same frame")
+        parity["reference_variance"] = parity_report(
+            ref_order["fma"], ref_order[False], "the reference order's own build-to-build variance: contracted vs "
+                                                "uncontracted oracle, same frame (no GPU involved)")
     if rank == 0:
         wl = (f"configs[1]: {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd with depth, one view" if world == 1 else
               f"configs[1] per GPU, view-data parallel: {P} Gaussians per replica, SH deg {deg}, {W}x{H}, fwd+bwd "

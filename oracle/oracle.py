@@ -15,6 +15,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _SRC = os.path.join(_HERE, "hlgs_oracle.c")
 _LIB = os.path.join(_HERE, "build", "libhlgs_oracle.so")
 _LIB_OMP = os.path.join(_HERE, "build", "libhlgs_oracle_omp.so")  # all-cores timing leg of bench.py only
+# The same source with a*b+c contracted into FMAs (gcc -ffp-contract=fast -mfma): the reference is built by nvcc with
+# its default --fmad=true (submodules/hierarchy-rasterizer/setup.py:31 passes no --fmad=false), so its float results
+# are those of a contracted build.  Used only to measure how far two faithful builds of the reference's own operation
+# order differ from each other (tests/test_gpu_refparity.py, bench.py parity.reference_order).
+_LIB_FMA = os.path.join(_HERE, "build", "libhlgs_oracle_fma.so")
 
 _f = C.POINTER(C.c_float)
 _i = C.POINTER(C.c_int)
@@ -27,8 +32,9 @@ def build(force=False):
     for the all-cores CPU baseline (libhlgs_oracle_omp.so; its gradient sums use atomics, so it is never a
     parity reference)."""
     os.makedirs(os.path.dirname(_LIB), exist_ok=True)
-    base = ["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-ffp-contract=off", "-fno-fast-math"]
-    for lib_, extra in ((_LIB, []), (_LIB_OMP, ["-fopenmp"])):
+    base = ["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-fno-fast-math"]
+    for lib_, extra in ((_LIB, ["-ffp-contract=off"]), (_LIB_OMP, ["-ffp-contract=off", "-fopenmp"]),
+                        (_LIB_FMA, ["-ffp-contract=fast", "-mfma"])):
         if force or not os.path.exists(lib_) or os.path.getmtime(lib_) < os.path.getmtime(_SRC):
             subprocess.check_call(base + extra + ["-o", lib_, _SRC, "-lm"])
     return _LIB
@@ -62,11 +68,12 @@ _libs = {}
 
 
 def lib(omp=False):
-    """The serial oracle (omp=False, every parity check) or its OpenMP build (timing only)."""
+    """The serial oracle (omp=False, every parity check), its OpenMP build (omp=True, timing only) or its contracted
+    build (omp="fma", the reference-variance measurement)."""
     L = _libs.get(omp)
     if L is None:
         build()
-        L = C.CDLL(_LIB_OMP if omp else _LIB)
+        L = C.CDLL(_LIB_FMA if omp == "fma" else _LIB_OMP if omp else _LIB)
         L.orc_set_alpha_mode.argtypes = [C.c_int]
         L.orc_get_alpha_mode.restype = C.c_int
         L.orc_num_threads.restype = C.c_int
