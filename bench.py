@@ -313,7 +313,8 @@ def make_step(P, deg, W, H, dev, rank, world, exchange_on=True):
     g_col, g_inv = torch.tensor(g_np, device=dev), torch.tensor(gd_np, device=dev)
     rs = settings_for(cam, deg, dev)
     rast = GaussianRasterizer(rs)
-    exchange = FlatGradExchange(params) if (world > 1 and exchange_on) else None
+    # overlap: the rasterizer is the only consumer of means3D / shs in this step (hlgs_core.dp.FlatGradExchange)
+    exchange = FlatGradExchange(params, overlap=True) if (world > 1 and exchange_on) else None
     st = dict(params=params, rs=rs, rast=rast, exchange=exchange, g_col=g_col, g_inv=g_inv, ar_events=[])
 
     def step(time_exchange=False):

@@ -51,13 +51,33 @@ def direct_grad(t, late=False):
         _DIRECT.pop(t.data_ptr(), None)
         return None
     i = e[2]
-    if ex.claimed[i] or p.grad is not None or p.shape != t.shape or p.dtype != t.dtype or ex.flat.device != t.device:
+    if ex.adopted[i] and p.grad is None:
+        # the view handed out in an earlier backward was adopted as .grad and then dropped (set to None) without
+        # allreduce() / unpack() / release(): that round was abandoned, so this backward starts a new one
+        ex._stale_round()
+    if ex.claimed[i]:
+        # a second gradient for this parameter in one autograd pass (e.g. two renders of the same leaves): autograd
+        # sums it with the view on the current stream, so the late kernels writing the view must be done first
+        ex.join()
+        return None
+    if p.grad is not None or p.shape != t.shape or p.dtype != t.dtype or ex.flat.device != t.device:
         return None
     ex.claimed[i] = True
     ex.late[i] = bool(late)
     v = ex.flat[ex.offsets[i]:ex.offsets[i] + ex.numels[i]].view_as(p)
     _VIEWS[v.data_ptr()] = weakref.ref(ex)
     return v
+
+
+def _adopt_hook(exref, i):
+    """Post-accumulate-grad hook: records that parameter i's .grad is the exchange's view (so a later backward that
+    finds .grad reset to None knows the round was abandoned, see direct_grad)."""
+    def hook(p):
+        ex = exref()
+        if ex is not None and ex.claimed[i] and p.grad is not None and \
+                p.grad.data_ptr() == ex.flat.data_ptr() + 4 * ex.offsets[i]:
+            ex.adopted[i] = True
+    return hook
 
 
 # data_ptr of a view direct_grad handed out -> weak reference to its exchange (late_stream_for's lookup)
@@ -110,7 +130,7 @@ class FlatGradExchange:
     leaving several buckets to pipeline for a 1M-Gaussian model (236 MB of fp32 gradients).
     """
 
-    def __init__(self, params, bucket_bytes=64 << 20, average=True, group=None, direct=True, overlap=True):
+    def __init__(self, params, bucket_bytes=64 << 20, average=True, group=None, direct=True, overlap=False):
         self.params = list(params)
         self.numels = [p.numel() for p in self.params]
         self.offsets = []
@@ -128,17 +148,27 @@ class FlatGradExchange:
         self.direct = []
         self.claimed = [False] * len(self.params)
         self.late = [False] * len(self.params)
-        # overlap: the rasterizer backward runs its SH backward on late_stream (hlgs_rasterize_backward_split), so the
-        # collective over the gradients that are final before it (opacity, scale, rotation) starts while it runs
+        self.adopted = [False] * len(self.params)  # a handed-out view became .grad (post-accumulate hook)
+        # overlap (opt-in): the rasterizer backward runs its SH backward on late_stream (hlgs_rasterize_backward_split),
+        # so the collective over the gradients that are final before it (opacity, scale, rotation) starts while it
+        # runs.  Then means3D / shs / dc .grad are complete on the current stream only after allreduce(), join() or
+        # release(); code that reads them in between (clipping, NaN checks, densification statistics) calls join()
+        # first.  A second gradient into those leaves from another rasterizer call in the same backward is ordered
+        # by direct_grad (it joins); one from any other loss term is not, so overlap=True requires that the
+        # rasterizer be the only consumer of means3D / shs / dc in the loss.
         self.late_stream = torch.cuda.Stream(device=dev) if (overlap and direct and dev.type == "cuda") else None
         self.pending = None  # event on late_stream after the last split backward
         self._token = object()
+        self._hooks = []
+        self._warned = False
         if direct:
             me = weakref.ref(self)
             for i, p in enumerate(self.params):
                 if p.is_contiguous() and p.dtype == torch.float32:
                     _DIRECT[p.data_ptr()] = (weakref.ref(p), me, i, self._token)
                     self.direct.append(p.data_ptr())
+                    if p.requires_grad and hasattr(p, "register_post_accumulate_grad_hook"):
+                        self._hooks.append(p.register_post_accumulate_grad_hook(_adopt_hook(me, i)))
         self._finalizer = weakref.finalize(self, _drop_entries, list(self.direct), self._token)
 
     def close(self):
@@ -146,6 +176,18 @@ class FlatGradExchange:
         whenever the parameter tensors are replaced: entries are keyed by storage address."""
         self._finalizer()
         self.direct = []
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    def _stale_round(self):
+        if not self._warned:
+            import warnings
+            warnings.warn("FlatGradExchange: gradients were reset without allreduce()/unpack()/release(); starting a "
+                          "new exchange round (call release() after a backward whose gradients are not exchanged)",
+                          RuntimeWarning, stacklevel=3)
+            self._warned = True
+        self.release()
 
     def join(self):
         """Order the current stream after the late kernels of the last split backward (the gradients they complete
@@ -159,6 +201,7 @@ class FlatGradExchange:
         self.join()
         self.claimed = [False] * len(self.params)
         self.late = [False] * len(self.params)
+        self.adopted = [False] * len(self.params)
 
     def _pack_range(self, a, b):
         for p, off, n in zip(self.params, self.offsets, self.numels):

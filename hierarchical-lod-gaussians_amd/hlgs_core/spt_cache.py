@@ -132,7 +132,7 @@ class SPTCache:
         shapes = {k: tuple(storage[k].shape[1:]) for k in NAMES}
         widths = [math.prod(shapes[k]) for k in NAMES] * 3
         hw = -(-sum(widths) // 16) * 16
-        self.host = torch.zeros((G, hw), dtype=torch.float32).pin_memory()
+        self.host = torch.zeros((G, hw), dtype=torch.float32, pin_memory=True)  # pinned at allocation: no pageable copy
         offs = [sum(widths[:i]) for i in range(len(widths))]
         view = lambda i, k: self.host[:, offs[i]:offs[i] + widths[i]].view((G,) + shapes[k])  # noqa: E731
         self.storage = {k: view(i, k) for i, k in enumerate(NAMES)}

@@ -92,12 +92,54 @@ def test_split_backward_on_late_stream_matches(alt):
 
     backward()
     ref = [p.grad.clone() for p in params]
-    ex = FlatGradExchange(params)
+    ex = FlatGradExchange(params, overlap=True)
     try:
         for _ in range(3):
             backward()
             assert ex.pending is not None, "the SH backward did not run on the late stream"
             ex.join()  # no torch.cuda.synchronize(): ordering comes from the event alone
+            got = [p.grad.clone() for p in params]
+            ex.release()
+            for a, b in zip(ref, got):
+                assert torch.equal(a, b)
+    finally:
+        ex.close()
+
+
+@pytest.mark.gpu
+def test_overlap_two_renders_of_the_same_leaves_in_one_backward():
+    """overlap=True with two rasterizer calls on the same leaves in one autograd pass: the second backward finds the
+    parameter's view claimed, joins the late stream before autograd sums its gradient with the view, and the summed
+    gradients are bitwise those of the in-order backward."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from hlgs_core.dp import FlatGradExchange
+    cam = S.make_camera(160, 96)
+    sc = S.make_gaussians(6000, 3, cam, seed=7)
+    g, gd = S.upstream_grads(160, 96, seed=8)
+    t = lambda a: torch.tensor(np.ascontiguousarray(a), device="cuda", requires_grad=True)  # noqa: E731
+    gc, gi = torch.tensor(g, device="cuda"), torch.tensor(gd, device="cuda")
+    params = [t(sc["means3D"]), t(sc["scales"]), t(sc["rotations"]), t(sc["opacities"]), t(sc["shs"])]
+    rast = GaussianRasterizer(settings_for(cam, 3, "cuda", do_depth=True))
+
+    def backward():
+        for p in params:
+            p.grad = None
+        m, s_, r, o, sh = params
+        outs, grads = [], []
+        for k in range(2):
+            color, _, inv = rast(means3D=m, means2D=torch.zeros_like(m, requires_grad=True), opacities=o, shs=sh,
+                                 scales=s_, rotations=r)
+            outs += [color, inv]
+            grads += [gc * (k + 1), gi]
+        torch.autograd.backward(outs, grads)
+
+    backward()
+    ref = [p.grad.clone() for p in params]
+    ex = FlatGradExchange(params, overlap=True)
+    try:
+        for _ in range(3):
+            backward()
+            ex.join()
             got = [p.grad.clone() for p in params]
             ex.release()
             for a, b in zip(ref, got):
