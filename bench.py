@@ -96,7 +96,9 @@ def cpu_model():
 
 
 def _mem(tag):
-    """HLGS_BENCH_MEM=1: peak and current host RSS after each leg, on stderr (diagnostics only)."""
+    """A progress line per leg on stderr (so a long run is visibly alive); with HLGS_BENCH_MEM=1 also the peak and
+    current host RSS (diagnostics only)."""
+    print(f"[bench] {tag} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
     if os.environ.get("HLGS_BENCH_MEM"):
         import resource
         cur = int(open("/proc/self/statm").read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
@@ -395,39 +397,63 @@ def merged_two_chunk_scene(P, seed=0):
     return b, storage, build_s, int(nodes.shape[0])
 
 
-def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080):
+def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, rank=0, world=1, backend=None):
     """configs[4]: train_post.py's training step on a 2-chunk merged hierarchy (synthetic: the example dataset is
     not available offline), per iteration as train_post.py:323-812 orders it: SPTCache.step (coarse cut, cache
     bookkeeping, SPT cut, write-back / load through pinned host storage) -> activations -> alt rasterizer
     (antialiasing, active SH degree 1) -> L1 + D-SSIM (+ masked inverse-depth L1, train_single.py:111-118) ->
-    backward -> dense Adam.  The camera moves every step.  Median host-clock step and per-stage event medians."""
+    backward -> dense Adam.  The camera moves every step.  Median host-clock step and per-stage event medians.
+
+    world > 1: view-data parallel, one view per rank.  Each step the ranks gather every rank's view
+    (gather_views), every rank's SPTCache.step computes the union cut of the batch, so all replicas hold the same
+    resident set; each rank renders its own view, the gradients of SPTCache.params are all-reduced (RCCL, averaged;
+    the rasterizer backward writes them straight into the exchange's flat buffer) and the dense Adam runs replicated.
+    Barrier + synchronise around the timed steps, max over ranks; all-reduce time and bus bandwidth reported."""
     from alt_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from hlgs_core import synthetic as S
+    from hlgs_core.dp import FlatGradExchange
     from hlgs_core.loss import photometric_loss
-    from hlgs_core.spt_cache import SPTCache
+    from hlgs_core.spt_cache import NAMES, SPTCache, gather_views
     b, storage, build_s, G = merged_two_chunk_scene(P)
     _mem("config5 scene")
     cache = SPTCache(storage, b, 0, reuse_tolerance=0.9, device=dev)
-    rng = np.random.default_rng(1)
+    rng = np.random.default_rng(1 + rank)
     gt = torch.tensor(rng.uniform(0, 1, (3, H, W)).astype(np.float32), device=dev)
     mono = torch.tensor(rng.uniform(0.05, 0.5, (1, H, W)).astype(np.float32), device=dev)
     mask = torch.ones((1, H, W), device=dev)
     bg = torch.zeros(3, device=dev)
     lrs = dict(xyz=1.6e-4, f_dc=2.5e-3, f_rest=2.5e-3 / 20, opacity=5e-2, scaling=5e-3, rotation=1e-3)
-    path = [S.make_camera(W, H, T=np.array([0.03 * k, 0.01 * k, 0.2 * math.sin(0.3 * k)])) for k in range(steps + 3)]
+    # rank r's camera path is offset sideways: the views of one step differ
+    path = [S.make_camera(W, H, T=np.array([0.03 * k + 0.4 * rank, 0.01 * k, 0.2 * math.sin(0.3 * k)]))
+            for k in range(steps + 3)]
     # camera tensors live on the GPU, as the reference's Camera objects do (scene/cameras.py:102-107 .cuda())
     path = [{k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in c.items()} for c in path]
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    stages = {k: [] for k in ("cache", "forward", "loss", "backward", "adam")}
-    step_ms, resident = [], []
+    stages = {k: [] for k in ("cache", "forward", "loss", "backward", "allreduce", "adam")}
+    step_ms, resident, nbytes = [], [], []
+    t_loop = None
     for it, cam in enumerate(path):
+        if world > 1 and it == 3:
+            dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        e = [ev() for _ in range(6)]
+        if it == 3:
+            t_loop = t0
+        e = [ev() for _ in range(7)]
         e[0].record()
-        cache.step(cam["projmatrix"], cam["campos"])
+        trace = os.environ.get("HLGS_BENCH_TRACE")
+        if trace:
+            print(f"[config5 r{rank}] step {it}", file=sys.stderr, flush=True)
+        if world > 1:
+            fpts, cams = gather_views(cam["projmatrix"], cam["campos"])
+            cache.step(fpts, cams)
+        else:
+            cache.step(cam["projmatrix"], cam["campos"])
         e[1].record()
         p = cache.params
+        if trace:
+            print(f"[config5 r{rank}] resident {cache.render_indices.numel()}", file=sys.stderr, flush=True)
+        ex = FlatGradExchange([p[k] for k in NAMES]) if world > 1 else None
         s = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=cam["tanfovx"],
                                           tanfovy=cam["tanfovy"], bg=bg, scale_modifier=1.0,
                                           viewmatrix=cam["viewmatrix"].to(dev), projmatrix=cam["projmatrix"].to(dev),
@@ -443,8 +469,15 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080):
         e[3].record()
         loss.backward()
         e[4].record()
-        cache.optimizer_step(it, lrs)
+        if ex is not None:
+            if trace:
+                print(f"[config5 r{rank}] allreduce {ex.flat.numel()}", file=sys.stderr, flush=True)
+            ex.allreduce()
+            nbytes.append(ex.flat.numel() * 4)
+            ex.close()
         e[5].record()
+        cache.optimizer_step(it, lrs)
+        e[6].record()
         torch.cuda.synchronize()
         if it >= 3:
             step_ms.append((time.perf_counter() - t0) * 1e3)
@@ -453,14 +486,32 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080):
             resident.append(cache.render_indices.numel())
         for q in p.values():
             q.grad = None
-    ms = float(np.median(step_ms))
+    el = time.perf_counter() - t_loop
+    if world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = time.perf_counter() - t_loop
+        ar = float(np.mean(stages["allreduce"]))
+        t = torch.tensor([el, ar], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, ar = float(t[0].item()), float(t[1].item())
+    ms = float(np.median(step_ms)) if world == 1 else el / len(step_ms) * 1e3
     out = dict(workload=f"configs[4]: train_post.py step with the SPT cache on a 2-chunk merged hierarchy ({G} "
                         f"nodes over {P} leaves), {W}x{H}, alt rasterizer (antialiasing, SH degree {sh_degree}), "
-                        f"L1 + D-SSIM{' + depth L1' if depth else ''}, dense Adam, camera moving every step",
+                        f"L1 + D-SSIM{' + depth L1' if depth else ''}, dense Adam, camera moving every step" +
+                        ("" if world == 1 else f"; view-data parallel over {world} ranks: union cut of the gathered "
+                                               f"views, {'RCCL' if backend == 'nccl' else backend} all-reduce of the "
+                                               f"resident gradients, replicated Adam"),
                spt_build_s=round(build_s, 3), resident_median=int(np.median(resident)), ms_per_step=round(ms, 3),
-               value=round(W * H / ms / 1e3, 1), unit="Mpix/s", steps=len(step_ms),
-               stages_ms={k: round(float(np.median(v)), 3) for k, v in stages.items()},
-               timing="median host clock around a synchronised step; stages: median event spans on torch's stream")
+               value=round(world * W * H / ms / 1e3, 1), unit="Mpix/s", steps=len(step_ms), n_gpus=world,
+               stages_ms={k: round(float(np.median(v)), 3) for k, v in stages.items() if world > 1 or k != "allreduce"},
+               timing=("median host clock around a synchronised step; stages: median event spans on torch's stream"
+                       if world == 1 else "barrier + synchronise around the timed steps, max over ranks; stages: "
+                                          "median event spans on torch's stream"))
+    if world > 1:
+        nb = float(np.median(nbytes))
+        out.update(allreduce_ms=round(ar, 4), bytes_per_step=int(nb),
+                   busbw_GBs=round(2 * (world - 1) / world * nb / (ar * 1e-3) / 1e9, 1))
     del cache
     torch.cuda.empty_cache()
     return out
@@ -616,7 +667,13 @@ def main():
         config5 = bench_config5(1_000_000, dev)
         _mem("config5")
     if world > 1 and not args.no_extras:
-        config4 = bench_config4_dp(4_000_000, deg, W, H, dev, rank, world, max(5, args.steps // 2), 2, backend)
+        if not os.environ.get("HLGS_BENCH_SKIP_CONFIG4"):  # rehearsals over gloo skip the 944 MB exchange
+            config4 = bench_config4_dp(4_000_000, deg, W, H, dev, rank, world, max(5, args.steps // 2), 2, backend)
+            _mem("config4 view-dp")
+        config5 = bench_config5(int(os.environ.get("HLGS_BENCH_CONFIG5_P", "1000000")), dev, rank=rank, world=world,
+                                backend=backend,
+                                steps=int(os.environ.get("HLGS_BENCH_CONFIG5_STEPS", "20")))
+        _mem("config5 view-dp")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, ref, ref_order = cpu_baseline(P, deg, W, H)
         step()  # one more step on the same inputs, outputs kept for the parity check

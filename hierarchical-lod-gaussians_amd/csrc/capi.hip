@@ -581,16 +581,18 @@ size_t hlgs_upper_cut_scratch_size(int N)
 }
 
 static int upper_cut_launch(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
-                            const float* planes, const float* campos, float distance_multiplier, int use_frustum,
-                            int use_lod, void* scratch, int* cut, int* count_out, hipStream_t s, int** count_dev)
+                            int nviews, const float* planes, const float* campos, float distance_multiplier,
+                            int use_frustum, int use_lod, void* scratch, int* cut, int* count_out, hipStream_t s,
+                            int** count_dev)
 {
+    if (nviews < 1) return fail(HLGS_ERR_ARG, "n_views < 1");
     if (!nodes || !xyz || !cut || !scratch || (use_frustum && (!bounds || !planes)) ||
         (use_lod && (!min_dist2 || !campos)))
         return fail(HLGS_ERR_ARG, "missing tensor");
     hipGetLastError();
     const int cap = 2 * N + 2;
     char* p = static_cast<char*>(aligned(scratch));
-    CutArgs a{N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum, use_lod,
+    CutArgs a{N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum, use_lod, nviews,
               take<int>(p, cap), take<int>(p, cap), N, cut, nullptr, nullptr, nullptr, nullptr};
     a.count = take<int>(p, 2);
     if (count_out) a.count = count_out;
@@ -612,7 +614,7 @@ int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* 
     if (N == 0) return HLGS_OK;
     hipStream_t s = (hipStream_t)stream;
     int* dev = nullptr;
-    int rc = upper_cut_launch(N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum,
+    int rc = upper_cut_launch(N, nodes, xyz, bounds, min_dist2, 1, planes, campos, distance_multiplier, use_frustum,
                               use_lod, scratch, cut, nullptr, s, &dev);
     if (rc) return rc;
     int host[2];
@@ -623,9 +625,10 @@ int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* 
     return HLGS_OK;
 }
 
-int hlgs_upper_tree_cut_device(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
-                               const float* planes, const float* campos, float distance_multiplier, int use_frustum,
-                               int use_lod, void* scratch, int* cut, int* count_device, void* stream)
+int hlgs_upper_tree_cut_views_device(int N, const int* nodes, const float* xyz, const float* bounds,
+                                     const float* min_dist2, int n_views, const float* planes, const float* campos,
+                                     float distance_multiplier, int use_frustum, int use_lod, void* scratch, int* cut,
+                                     int* count_device, void* stream)
 {
     if (N < 0) return fail(HLGS_ERR_ARG, "N < 0");
     if (!count_device) return fail(HLGS_ERR_ARG, "missing count");
@@ -635,8 +638,16 @@ int hlgs_upper_tree_cut_device(int N, const int* nodes, const float* xyz, const 
         return HLGS_OK;
     }
     int* dev = nullptr;
-    return upper_cut_launch(N, nodes, xyz, bounds, min_dist2, planes, campos, distance_multiplier, use_frustum,
-                            use_lod, scratch, cut, count_device, s, &dev);
+    return upper_cut_launch(N, nodes, xyz, bounds, min_dist2, n_views, planes, campos, distance_multiplier,
+                            use_frustum, use_lod, scratch, cut, count_device, s, &dev);
+}
+
+int hlgs_upper_tree_cut_device(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
+                               const float* planes, const float* campos, float distance_multiplier, int use_frustum,
+                               int use_lod, void* scratch, int* cut, int* count_device, void* stream)
+{
+    return hlgs_upper_tree_cut_views_device(N, nodes, xyz, bounds, min_dist2, 1, planes, campos, distance_multiplier,
+                                            use_frustum, use_lod, scratch, cut, count_device, stream);
 }
 
 int hlgs_gather_rows(int64_t n, int row_bytes, const int64_t* idx, const void* src, void* dst, void* stream)
@@ -693,6 +704,7 @@ int hlgs_spt_cache_plan(const hlgs_cache_args* a, hlgs_cache_plan* pl, void* scr
     c.nodes = a->upper_nodes;
     c.xyz = a->upper_xyz;
     c.campos = a->campos;
+    c.nviews = a->n_views > 1 ? a->n_views : 1;
     c.dmul = a->distance_multiplier;
     c.num_spts = a->num_spts;
     c.m = a->m;

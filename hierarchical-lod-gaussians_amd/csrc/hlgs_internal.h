@@ -136,10 +136,11 @@ struct CutArgs {
     const float* xyz;
     const float* bounds;
     const float* min_dist2;
-    const float* planes;   // 4 x (nx, ny, nz, d), normalised as extract_frustum_planes does
-    const float* campos;
+    const float* planes;   // nviews x 4 x (nx, ny, nz, d), normalised as extract_frustum_planes does
+    const float* campos;   // nviews x 3
     float dmul;
     int use_frustum, use_lod;
+    int nviews;            // >= 1: the cut serves the union of the views (visible in any frustum, LOD of the nearest)
     int* front_a;
     int* front_b;
     int capacity;          // entries of cut
@@ -158,7 +159,8 @@ struct CacheArgs {
     const int* cut;           // coarse cut of the upper tree
     const int* nodes;         // upper-tree HierarchyNode rows
     const float* xyz;
-    const float* campos;
+    const float* campos;      // nviews x 3: an SPT's distance is that of the nearest camera
+    int nviews;
     float dmul;
     int num_spts;
     int m;                    // previous step's SPTs

@@ -44,17 +44,26 @@ __device__ __forceinline__ CutNode cut_node(const CutArgs& a, int v)
     const int kids = a.nodes[6 * v + 2], fc = a.nodes[6 * v + 3];
     const float md = a.use_lod ? a.min_dist2[v] : 0.f;
     CutNode c{3, 0, 0};
-    if (a.use_frustum) {
-        for (int k = 0; k < 4; k++) {
-            const float* pl = a.planes + 4 * k;
-            const float sd = px * pl[0] + py * pl[1] + pz * pl[2] + pl[3];  // torch.sum over 3, then + distance
-            if (sd + r < 0.f) c.st = 0;
+    if (a.use_frustum) {  // culled unless the sphere reaches into some view's frustum
+        bool any = false;
+        for (int g = 0; g < a.nviews; g++) {
+            bool in = true;
+            for (int k = 0; k < 4; k++) {
+                const float* pl = a.planes + 16 * g + 4 * k;
+                const float sd = px * pl[0] + py * pl[1] + pz * pl[2] + pl[3];  // torch.sum over 3, then + distance
+                if (sd + r < 0.f) in = false;
+            }
+            any = any || in;
         }
+        if (!any) c.st = 0;
     }
     if (c.st == 3 && kids == 0) c.st = 1;
-    if (c.st == 3 && a.use_lod) {
-        const float dx = a.campos[0] - px, dy = a.campos[1] - py, dz = a.campos[2] - pz;
-        const float d2 = dx * dx + dy * dy + dz * dz;
+    if (c.st == 3 && a.use_lod) {  // the nearest camera decides (min over views of the squared distance)
+        float d2 = INFINITY;
+        for (int g = 0; g < a.nviews; g++) {
+            const float dx = a.campos[3 * g] - px, dy = a.campos[3 * g + 1] - py, dz = a.campos[3 * g + 2] - pz;
+            d2 = fminf(d2, dx * dx + dy * dy + dz * dz);
+        }
         if (!(md > d2 * a.dmul)) c.st = 2;
     }
     if (SIB && c.st == 3) {
@@ -605,10 +614,14 @@ __global__ void __launch_bounds__(1024) k_cache_lists(CacheArgs a)
         const int ps = block_excl(is_s, s_w, &ts);
         const int pu = block_excl(is_u, s_w, &tu);
         if (is_s) {
-            const float dx = a.xyz[3 * v] - a.campos[0], dy = a.xyz[3 * v + 1] - a.campos[1],
-                        dz = a.xyz[3 * v + 2] - a.campos[2];
+            float d2 = INFINITY;  // nearest camera
+            for (int g = 0; g < a.nviews; g++) {
+                const float dx = a.xyz[3 * v] - a.campos[3 * g], dy = a.xyz[3 * v + 1] - a.campos[3 * g + 1],
+                            dz = a.xyz[3 * v + 2] - a.campos[3 * g + 2];
+                d2 = fminf(d2, dx * dx + dy * dy + dz * dz);
+            }
             a.spt_idx[ns + ps] = fc;
-            a.spt_dist[ns + ps] = sqrtf(dx * dx + dy * dy + dz * dz) * a.dmul;
+            a.spt_dist[ns + ps] = sqrtf(d2) * a.dmul;
         }
         if (is_u) a.upper[nu + pu] = a.nodes[6 * v + 5];
         ns += ts;

@@ -49,7 +49,8 @@ class CacheArgs(C.Structure):
     _fields_ = [("n_cut", _i), ("cut", _vp), ("upper_nodes", _vp), ("upper_xyz", _vp), ("campos", _vp),
                 ("distance_multiplier", _f), ("num_spts", _i), ("m", _i), ("prev_spt_indices", _vp),
                 ("prev_spt_distances", _vp), ("prev_spt_counts", _vp), ("R", _i), ("render_indices", _vp),
-                ("n_loaded_prev", _i), ("skybox_points", _i), ("rtol", _f), ("atol", _f), ("n_cut_device", _vp)]
+                ("n_loaded_prev", _i), ("skybox_points", _i), ("rtol", _f), ("atol", _f), ("n_cut_device", _vp),
+                ("n_views", _i)]
 
 
 class CachePlan(C.Structure):
@@ -91,6 +92,8 @@ _SIGS = {
     "hlgs_upper_cut_scratch_size": (_sz, [_i]),
     "hlgs_upper_tree_cut": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, C.POINTER(_i), _vp]),
     "hlgs_upper_tree_cut_device": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, _vp, _vp]),
+    "hlgs_upper_tree_cut_views_device": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _i, _i, _vp, _vp, _vp,
+                                              _vp]),
     "hlgs_gather_rows": (_i, [C.c_int64, _i, _vp, _vp, _vp, _vp]),
     "hlgs_spt_cache_scratch_size": (_sz, [_i, _i, _i, _i]),
     "hlgs_spt_cache_plan": (_i, [C.POINTER(CacheArgs), C.POINTER(CachePlan), _vp, _vp]),

@@ -115,6 +115,27 @@ def adam_step(params, grads, exp_avgs, exp_avg_sqs, lrs, step, skybox_points=0, 
                                L.stream()))
 
 
+def gather_views(full_proj_transform, camera_center, group=None):
+    """Every rank's training view, in rank order: (G, 4, 4) projection matrices and (G, 3) camera centres.
+
+    The view-data-parallel config #5 step: each rank trains its own view, and every rank passes the
+    gathered batch to SPTCache.step, so all ranks compute the same union cut from the same inputs and hold the same
+    resident set in the same order -- the gradient all-reduce over SPTCache.params is then elementwise, and the
+    replicated Adam step keeps the replicas identical.  One small all_gather (19 floats per rank)."""
+    import torch.distributed as dist
+    fpt = full_proj_transform.detach().reshape(-1)[:16].float()
+    cam = camera_center.detach().reshape(-1)[:3].float()
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return fpt.reshape(1, 4, 4), cam.reshape(1, 3)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else \
+        torch.device("cpu")
+    v = torch.cat([fpt, cam]).to(dev)
+    out = [torch.empty_like(v) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, v, group=group)
+    st = torch.stack(out)
+    return st[:, :16].reshape(-1, 4, 4).contiguous(), st[:, 16:19].contiguous()
+
+
 class SPTCache:
     """Resident set of a cached training run.  storage: dict name -> host tensor of all Gaussians (rows), for
     the names in NAMES; opt_storage: dict name -> {"exp_avgs", "exp_avgs_sqs"} of the same shapes (zero-filled
@@ -188,11 +209,19 @@ class SPTCache:
 
     # ------------------------------------------------------------ bookkeeping (:326-430)
     def plan(self, full_proj_transform, camera_center, distance_multiplier=1.0):
-        """One bookkeeping pass for a view; no parameter moves.  Returns the reference's per-pass variables."""
+        """One bookkeeping pass for a view; no parameter moves.  Returns the reference's per-pass variables.
+
+        A batch of G views (full_proj_transform G x 4 x 4, camera_center G x 3; one view per rank of a
+        view-data-parallel step) gives the union cut: visible in any frustum, each LOD decision and SPT
+        distance taken from the nearest camera.  With one view it is the reference's cut, bit for bit."""
         lib = L.load()
         dev = self.device
-        cam = camera_center.detach().reshape(-1)[:3].to(dev, torch.float32).contiguous()
-        planes = _spt.extract_frustum_planes(full_proj_transform.to(dev, torch.float32)) if self.use_frustum else None
+        fpt = full_proj_transform.detach().to(dev, torch.float32)
+        G = fpt.shape[0] if fpt.dim() == 3 else 1
+        fpt = fpt.reshape(G, 4, 4)
+        cam = camera_center.detach().to(dev, torch.float32).reshape(G, -1)[:, :3].contiguous()
+        planes = (torch.stack([_spt.extract_frustum_planes(fpt[g]) for g in range(G)]).contiguous()
+                  if self.use_frustum else None)
         # coarse cut with its length left on the device (hlgs_upper_tree_cut_device): the plan reads it, so the step
         # has one host synchronisation, the plan's
         N = self.nodes.size(0)
@@ -200,10 +229,11 @@ class SPTCache:
             self._cut = torch.empty((max(N, 1),), dtype=torch.int32, device=dev)
             self._cut_scratch = torch.empty(lib.hlgs_upper_cut_scratch_size(N), dtype=torch.uint8, device=dev)
             self._cut_count = torch.zeros((2,), dtype=torch.int32, device=dev)
-        L.check(lib.hlgs_upper_tree_cut_device(N, _p(self.nodes), _p(self.xyz), _p(self.bounds),
-                                               _p(self.min_distance_squared), _p(planes), _p(cam),
-                                               float(distance_multiplier), int(bool(self.use_frustum)), 1,
-                                               _p(self._cut_scratch), _p(self._cut), _p(self._cut_count), L.stream()))
+        L.check(lib.hlgs_upper_tree_cut_views_device(N, _p(self.nodes), _p(self.xyz), _p(self.bounds),
+                                                     _p(self.min_distance_squared), G, _p(planes), _p(cam),
+                                                     float(distance_multiplier), int(bool(self.use_frustum)), 1,
+                                                     _p(self._cut_scratch), _p(self._cut), _p(self._cut_count),
+                                                     L.stream()))
         coarse = self._cut
         n_cut, m, R = N, self.prev_SPT_indices.numel(), self.render_indices.numel()
         # the ten output lists carved from one int32 allocation (the distances as float32 views of it)
@@ -218,7 +248,7 @@ class SPTCache:
         a = L.CacheArgs(n_cut, _p(coarse), _p(self.nodes), _p(self.xyz), _p(cam), float(distance_multiplier),
                         self.num_spts, m, _p(self.prev_SPT_indices), _p(self.prev_SPT_distances),
                         _p(self.prev_SPT_counts), R, _p(self.render_indices), int(self.n_loaded), self.sky,
-                        self.rtol, self.atol, _p(self._cut_count))
+                        self.rtol, self.atol, _p(self._cut_count), G)
         pl = L.CachePlan(*[out[f].data_ptr() for f, _ in L.CachePlan._fields_[:10]])
         scratch = torch.empty(lib.hlgs_spt_cache_scratch_size(n_cut, m, R, self.num_spts), dtype=torch.uint8,
                               device=dev)
@@ -243,7 +273,7 @@ class SPTCache:
             load_SPT_indices=load_idx, upper_tree_nodes_to_render=out["upper_render"][:nu], prefix=prefix,
             distance_multiplier=distance_multiplier)
 
-    # ------------------------------------------------------------ one view (:326-483)
+    # ------------------------------------------------------------ one view (:326-483), or a batch of views
     def step(self, full_proj_transform, camera_center):
         dm = 1.0
         while True:

@@ -247,6 +247,15 @@ int hlgs_upper_tree_cut_device(int N, const int* nodes, const float* xyz, const 
 int hlgs_upper_tree_cut(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
                         const float* planes, const float* campos, float distance_multiplier, int use_frustum,
                         int use_lod, void* scratch, int* cut, int* count, void* stream);
+/* The cut for a batch of n_views training views (one per rank of a view-data-parallel step): planes
+ * n_views x 4 x 4, campos n_views x 3.  A node survives the cull if its sphere reaches into ANY view's frustum, and
+ * expands if min_dist2 > min over views |campos_g - p|^2 * distance_multiplier (the nearest camera decides).  With
+ * n_views = 1 this is hlgs_upper_tree_cut_device, bit for bit.  Every rank computing it from the same gathered views
+ * obtains the same cut (no train_post.py counterpart: the reference trains one view per step). */
+int hlgs_upper_tree_cut_views_device(int N, const int* nodes, const float* xyz, const float* bounds,
+                                     const float* min_dist2, int n_views, const float* planes, const float* campos,
+                                     float distance_multiplier, int use_frustum, int use_lod, void* scratch, int* cut,
+                                     int* count_device, void* stream);
 /* SPT construction (GaussianModel.build_hierarchical_SPT + get_min_distance, scene/gaussian_model.py:184-352), host
  * code over host arrays: nodes G x 6 (HierarchyNode), xyz G x 3, log_scales G x 3 (unactivated, as _scaling);
  * root = the hierarchy root (the reference's default root_node 100000 is its skybox size).  The result is an
@@ -289,6 +298,8 @@ typedef struct hlgs_cache_args {
     float rtol, atol;                  /* isclose of the reused distances (Reuse_SPT_Tolerarance, 0.05) */
     const int* n_cut_device;           /* NULL, or the [count, overflow] words of hlgs_upper_tree_cut_device: the
                                           cut's length is then read on the device and n_cut is its capacity */
+    int n_views;                       /* 0 or 1: campos is one camera; > 1: campos is n_views x 3 and each SPT's
+                                          distance is that of the nearest camera (hlgs_upper_tree_cut_views_device) */
 } hlgs_cache_args;
 typedef struct hlgs_cache_plan {
     int* keep_spt_indices;             /* m: keep_SPT_indices */

@@ -26,21 +26,31 @@ def frustum_visible(p, r, planes):
     return True
 
 
-def lod_expand(p, md2, cam, dmul):
+def _d2(p, c):
     f = np.float32
-    dx, dy, dz = f(cam[0] - p[0]), f(cam[1] - p[1]), f(cam[2] - p[2])
-    d2 = f(f(f(dx * dx) + f(dy * dy)) + f(dz * dz))
+    dx, dy, dz = f(c[0] - p[0]), f(c[1] - p[1]), f(c[2] - p[2])
+    return f(f(f(dx * dx) + f(dy * dy)) + f(dz * dz))
+
+
+def lod_expand(p, md2, cam, dmul):
+    """cam: one camera (3,) or a batch of views (G, 3): the nearest camera's squared distance decides."""
+    f = np.float32
+    d2 = min(_d2(p, c) for c in np.asarray(cam, np.float32).reshape(-1, 3))
     return md2 > f(d2 * f(dmul))
 
 
 def upper_tree_cut(nodes, xyz, bounds, md2, planes, cam, dmul=1.0, use_frustum=True, use_lod=True):
+    """planes (4, 4) and cam (3,) for one view, or (G, 4, 4) and (G, 3) for the union cut of a batch of views
+    (visible in any frustum, nearest camera for the LOD condition; DESIGN §7 -- the reference trains one view per
+    step, so the batch form has no counterpart there and reduces to it for G = 1)."""
     nodes = np.asarray(nodes)
     xyz = np.asarray(xyz, np.float32)
+    pls = None if planes is None else np.asarray(planes, np.float32).reshape(-1, 4, 4)
     stack = [0]
     cut = []
     while stack:
         if use_frustum:
-            stack = [v for v in stack if frustum_visible(xyz[v], np.float32(bounds[v]), planes)]
+            stack = [v for v in stack if any(frustum_visible(xyz[v], np.float32(bounds[v]), pl) for pl in pls)]
         cut += [v for v in stack if nodes[v, 2] == 0]
         stack = [v for v in stack if nodes[v, 2] > 0]
         if use_lod:
@@ -205,11 +215,15 @@ def isclose32(a, b, rtol, atol):
 
 
 def spt_distances(xyz, cam, dmul):
-    """(upper_tree_xyz[i] - camera_position).pow(2).sum(1).sqrt() * distance_multiplier, float32."""
-    d = (np.asarray(xyz, np.float32) - np.asarray(cam, np.float32)).astype(np.float32)
-    q = (d * d).astype(np.float32)
-    s = ((q[:, 0] + q[:, 1]).astype(np.float32) + q[:, 2]).astype(np.float32)
-    return (np.sqrt(s).astype(np.float32) * np.float32(dmul)).astype(np.float32)
+    """(upper_tree_xyz[i] - camera_position).pow(2).sum(1).sqrt() * distance_multiplier, float32; for a batch of
+    views (cam G x 3) the nearest camera's distance."""
+    best = None
+    for c in np.asarray(cam, np.float32).reshape(-1, 3):
+        d = (np.asarray(xyz, np.float32) - c).astype(np.float32)
+        q = (d * d).astype(np.float32)
+        s = ((q[:, 0] + q[:, 1]).astype(np.float32) + q[:, 2]).astype(np.float32)
+        best = s if best is None else np.minimum(best, s)
+    return (np.sqrt(best).astype(np.float32) * np.float32(dmul)).astype(np.float32)
 
 
 def cache_pass(nodes, xyz, coarse, cam, dmul, prev_idx, prev_dist, prev_counts, render, n_loaded_prev, sky, rtol,

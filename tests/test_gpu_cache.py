@@ -52,10 +52,12 @@ class _Oracle:
         self.prev = (np.zeros(0, np.int32), np.zeros(0, np.float32), np.zeros(0, np.int32))
 
     def step(self, cam):
+        """cam: one camera dict, or a list of them (a batch of views: the union cut)."""
         from hlgs_core import spt
         b = self.b
-        planes = spt.extract_frustum_planes(cam["projmatrix"]).numpy()
-        campos = cam["campos"].numpy()
+        cams = cam if isinstance(cam, (list, tuple)) else [cam]
+        planes = np.stack([spt.extract_frustum_planes(c["projmatrix"]).numpy() for c in cams])
+        campos = np.stack([c["campos"].numpy().reshape(-1)[:3] for c in cams])
         cut_fn = lambda i, d: O.spt_cut(b["SPT_gaussian_indices"], b["SPT_starts"], b["SPT_max"],  # noqa: E731
                                         b["SPT_min"], i, d, compat=True)
         dm = 1.0
@@ -216,3 +218,31 @@ def test_adam_step_matches_restatement():
             assert torch.equal(x.cpu(), y)  # skybox rows zeroed, the rest untouched
     for a, b in zip(dp + dm + dv, ps + ms + vs):
         torch.testing.assert_close(a.cpu(), b, rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("views", [2, 3])
+def test_spt_cache_view_batches_match_restatement(views):
+    """A batch of views per step (one per rank of the view-data-parallel config #5 step): the union cut --
+    visible in any frustum, the nearest camera's LOD and SPT distance -- over several steps, against the
+    restatement, bit-exact, including the moved rows."""
+    from hlgs_core.spt_cache import SPTCache
+    sky = 4
+    b, storage = _scene(sky)
+    cams = _cameras()
+    batches = [[cams[(i + k) % len(cams)] for k in range(views)] for i in range(4)]
+    cache = SPTCache(storage, b, sky, reuse_tolerance=0.9)
+    orc = _Oracle(b, storage, sky, 0.9, 10 ** 9)
+    sizes = []
+    for step, batch in enumerate(batches):
+        got = cache.step(torch.stack([c["projmatrix"] for c in batch]), torch.stack([c["campos"] for c in batch]))
+        want = orc.step(batch)
+        pl = cache.last_plan
+        for k in ("SPT_indices", "SPT_distances", "SPT_counts", "load_from_disk_indices"):
+            np.testing.assert_array_equal(pl[k].cpu().numpy(), want[k], err_msg=f"{k} batch {step}")
+        np.testing.assert_array_equal(got.cpu().numpy(), want["render_indices"])
+        for t, (g, w) in enumerate(zip(_dev_list(cache), orc.dev)):
+            np.testing.assert_array_equal(g.detach().cpu().numpy(), w, err_msg=f"tensor {t} batch {step}")
+        sizes.append(len(want["render_indices"]))
+    # the union cut of a batch holds at least as many Gaussians as the cut of its first view alone
+    single = _Oracle(b, storage, sky, 0.9, 10 ** 9)
+    assert sizes[0] >= len(single.step(batches[0][0])["render_indices"])
