@@ -15,6 +15,11 @@ where /root/reference exists; the fixtures are committed so tests never need the
   golden_lerp.npz    render_post's child/parent lerp (gaussian_renderer/__init__.py:304-339) executed from the
                      reference module itself, and its autograd leaf gradients (lerp_fixture explains the two
                      stand-in modules that let gaussian_renderer import without its CUDA extensions).
+  golden_spt.npz     train_post.py's SPT machinery executed from scene/gaussian_model.py and scene/OurAdam.py
+                     themselves (spt_fixture): GaussianModel.build_hierarchical_SPT with get_min_distance and
+                     cut_hierarchy_on_condition (:184-404), extract_frustum_planes / frustum_cull_spheres (:55-103),
+                     the coarse cut of train_post.py:330-343 for several cameras and distance multipliers, and
+                     OurAdam._single_tensor_adam2 (:357-457) as train_post.py:802-818 calls it.
 
 Device shim: the reference's Python hard-codes device='cuda' in a few tensor factories; _CudaToCpu (a torch
 function mode) allocates those on the CPU here.  The intended SPT cut (scene/gaussian_model.py:158-181) is
@@ -114,6 +119,7 @@ def main():
     print("wrote golden_sh.npz, golden_camera.npz, golden_loss.npz")
     cov3d_fixture(rng)
     lerp_fixture(rng)
+    spt_fixture(rng)
 
 
 class _CudaToCpu(torch.overrides.TorchFunctionMode):
@@ -126,6 +132,129 @@ class _CudaToCpu(torch.overrides.TorchFunctionMode):
         if str(kwargs.get("device", "")).startswith("cuda"):
             kwargs["device"] = "cpu"
         return func(*args, **kwargs)
+
+
+class _CudaToCpuAll(_CudaToCpu):
+    """_CudaToCpu, and Tensor.cuda() / .to("cuda") keep the tensor where it is (scene/gaussian_model.py moves its SPT
+    arrays with .cuda(); utils/reloc_utils.py builds its binomial table with .cuda() at import)."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        if func is torch.Tensor.cuda:
+            return args[0]
+        if func is torch.Tensor.to:
+            args = tuple("cpu" if (isinstance(a, str) and a.startswith("cuda")) or
+                         (isinstance(a, torch.device) and a.type == "cuda") else a for a in args)
+        return super().__torch_function__(func, types, args, kwargs)
+
+
+def spt_fixture(rng):
+    """golden_spt.npz: the SPT streaming machinery of train_post.py run from the reference's own modules.
+
+    scene/gaussian_model.py imports plyfile, simple_knn._C, gaussian_hierarchy._C, gaussian_renderer and
+    utils.reloc_utils (which imports diff_gaussian_rasterization) at module level; none is importable here, so empty
+    stand-in modules carrying the imported names are registered first (none of those names is called by the code run
+    here).  A GaussianModel is made without __init__ and given the attributes build_hierarchical_SPT reads (nodes,
+    _xyz, _scaling, scaling_activation = exp).  build_hierarchical_SPT's coarse cut starts at cut_hierarchy_on_condition's
+    default root_node = 100000, the skybox size of the reference's scenes; the synthetic scenes here have a small
+    skybox, so that default is bound to their root (root_node = skybox_points) -- the only argument changed.
+    Per case: the hierarchy (create_from_hier layout, hlgs_core.synthetic), the SPT arrays and the upper tree; per
+    camera and distance multiplier: the frustum planes, the sphere visibility and the coarse cut of
+    train_post.py:330-343.  Adam: _single_tensor_adam2 on seeded tensors, as train_post.py:802-818 calls it."""
+    import functools
+    import importlib.util
+    import types
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(OUT)), "hierarchical-lod-gaussians_amd"))
+    from hlgs_core import synthetic as S
+    stubs = {"plyfile": dict(PlyData=None, PlyElement=None), "simple_knn": {}, "simple_knn._C": dict(distCUDA2=None),
+             "gaussian_hierarchy": {},
+             "gaussian_hierarchy._C": dict(load_hierarchy=None, write_hierarchy=None, load_dynamic_hierarchy=None,
+                                           write_dynamic_hierarchy=None, get_morton_indices=None,
+                                           get_spt_cut_cuda=None),
+             "gaussian_renderer": dict(occlusion_cull=None),
+             "diff_gaussian_rasterization": dict(compute_relocation=None)}
+    saved = {k: sys.modules.get(k) for k in list(stubs) + ["scene", "scene.gaussian_model", "utils.reloc_utils"]}
+    for k, attrs in stubs.items():
+        m = types.ModuleType(k)
+        m.__dict__.update(attrs)
+        sys.modules[k] = m
+    # the `scene` package without scene/__init__.py (which imports the dataset readers, cv2, PIL): a package module
+    # whose path is the reference's scene/ directory, so scene.gaussian_model and scene.OurAdam load from their files
+    pkg = types.ModuleType("scene")
+    pkg.__path__ = [os.path.join(REF, "scene")]
+    sys.modules["scene"] = pkg
+    try:
+        with _CudaToCpuAll():
+            from scene.gaussian_model import GaussianModel
+        out = {}
+        cams = [S.make_camera(320, 240, T=np.array([0.0, 0.0, 0.3])),
+                S.make_camera(320, 240, T=np.array([0.4, -0.1, 1.2])),
+                S.make_camera(320, 240, R=np.array([[np.cos(0.6), 0, np.sin(0.6)], [0, 1, 0],
+                                                    [-np.sin(0.6), 0, np.cos(0.6)]]), T=np.array([-0.6, 0.0, 1.0]))]
+        cases = [(1400, 4, 2.0, 0.02, 20, True), (1000, 0, 5.0, 0.05, 10, True), (1200, 3, 1.0, 0.02, 30, False)]
+        for i, (n, sky, volume, tg, min_size, spheres) in enumerate(cases):
+            h = S.make_dynamic_hierarchy(S.make_gaussians(n, 0, S.make_camera(256, 192), seed=100 + i),
+                                         skybox_points=sky, seed=100 + i)
+            nodes = torch.tensor(h["nodes"])
+            nodes[:, 3] = torch.where(nodes[:, 2] == 2, nodes[:, 3], torch.zeros_like(nodes[:, 3]))  # :1065
+            xyz = torch.tensor(h["means3D"])
+            log_s = torch.log(torch.tensor(h["scales"]))
+            gm = GaussianModel.__new__(GaussianModel)
+            gm.nodes, gm._xyz, gm._scaling, gm.scaling_activation = nodes, xyz, log_s, torch.exp
+            gm.skybox_points = sky
+            gm.cut_hierarchy_on_condition = functools.partial(GaussianModel.cut_hierarchy_on_condition, gm,
+                                                              root_node=sky)
+            with _CudaToCpuAll():
+                roots = gm.build_hierarchical_SPT(volume, tg, min_size, use_bounding_spheres=spheres)
+            for k, v in dict(nodes=nodes, xyz=xyz, log_scales=log_s).items():
+                out[f"in_{k}_{i}"] = v.numpy()
+            out[f"params_{i}"] = np.array([sky, volume, tg, min_size, int(spheres)], np.float64)
+            for k in ("SPT_starts", "SPT_min", "SPT_max", "SPT_gaussian_indices", "upper_tree_nodes",
+                      "upper_tree_xyz", "upper_tree_scaling", "min_distance_squared"):
+                out[f"{k}_{i}"] = getattr(gm, k).numpy()
+            out[f"SPT_root_hierarchy_indices_{i}"] = roots.numpy()
+            bounds = gm.bounding_sphere_radii if spheres else \
+                gm.scaling_activation(torch.max(gm.upper_tree_scaling, dim=-1)[0]) * 3.0  # train_post.py:330-333
+            out[f"bounds_{i}"] = bounds.numpy()
+            for c, cam in enumerate(cams):
+                planes = gm.extract_frustum_planes(cam["projmatrix"])
+                vis = gm.frustum_cull_spheres(gm.upper_tree_xyz, bounds, planes)
+                out[f"planes_{i}_{c}"], out[f"visible_{i}_{c}"] = planes.numpy(), vis.numpy()
+                for d, dm in enumerate((1.0, 2.25)):
+                    cpos = cam["campos"]
+                    cull = lambda idx: gm.frustum_cull_spheres(gm.upper_tree_xyz[idx], bounds[idx], planes)  # noqa
+                    lod = lambda idx: gm.min_distance_squared[idx] > \
+                        (cpos - gm.upper_tree_xyz[idx]).square().sum(dim=-1) * dm  # noqa: E731
+                    with _CudaToCpuAll():
+                        cut = GaussianModel.cut_hierarchy_on_condition(gm, gm.upper_tree_nodes, lod,
+                                                                       return_upper_tree=False, root_node=0,
+                                                                       leave_out_of_cut_condition=cull)
+                    out[f"coarse_cut_{i}_{c}_{d}"] = cut.numpy().astype(np.int32)
+            for c, cam in enumerate(cams):
+                out[f"campos_{c}"], out[f"projmatrix_{c}"] = cam["campos"].numpy(), cam["projmatrix"].numpy()
+        # OurAdam._single_tensor_adam2, loaded from its file (scene/OurAdam.py imports torch only)
+        spec = importlib.util.spec_from_file_location("_ref_ouradam", os.path.join(REF, "scene", "OurAdam.py"))
+        oa = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(oa)
+        for j, (shape, lr, it) in enumerate([((300, 3), 1.6e-4, 0), ((120, 15, 3), 1.25e-4, 7), ((400, 1), 5e-2, 4999)]):
+            p0 = rng.normal(0, 1, shape).astype(np.float32)
+            g = rng.normal(0, 0.1, shape).astype(np.float32)
+            m = rng.normal(0, 0.01, shape).astype(np.float32)
+            v = np.abs(rng.normal(0, 0.001, shape)).astype(np.float32)
+            tp, tm, tv = torch.tensor(p0), torch.tensor(m), torch.tensor(v)
+            oa._single_tensor_adam2([tp], [torch.tensor(g)], [tm], [tv], None, [torch.tensor(it)], amsgrad=False,
+                                    beta1=0.9, beta2=0.999, lr=lr, weight_decay=0, eps=1e-8, maximize=False,
+                                    capturable=False)
+            out[f"adam_in_{j}"] = np.stack([p0, g, m, v])
+            out[f"adam_lr_it_{j}"] = np.array([lr, it], np.float64)
+            out[f"adam_out_{j}"] = np.stack([tp.numpy(), tm.numpy(), tv.numpy()])
+        np.savez_compressed(os.path.join(OUT, "golden_spt.npz"), **out)
+        print("wrote golden_spt.npz")
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
 
 
 def cov3d_fixture(rng):
