@@ -70,19 +70,41 @@ STAGE_KERNEL = {"preprocess": "k_preprocess", "count_tiles": "k_count_tiles", "s
                 "blend_bwd": "k_blend_bwd", "gauss_bwd": "k_gauss_bwd"}
 
 
+def running_lib_sha16():
+    """Hash of the libhlgs.so this process loaded (the build identity PMC profiles are matched against)."""
+    import hashlib
+    from hlgs_core import _lib as L
+    path = getattr(L.load(), "_name", None)
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except (OSError, TypeError):
+        return None
+
+
+def pmc_profile(name="pmc_traffic.json"):
+    """The latest committed PMC summary (tools/profile_round.sh + tools/summarize_profile.py / summarize_stalls.py):
+    (dict, path relative to the repo, matches) where matches says whether it was measured on the library running
+    now (the hashes in its build block agree); (None, None, False) when there is none."""
+    prof = os.path.join(ROOT, "profiles")
+    rounds = sorted(d for d in os.listdir(prof) if os.path.exists(os.path.join(prof, d, name))) \
+        if os.path.isdir(prof) else []
+    if not rounds:
+        return None, None, False
+    path = os.path.join(prof, rounds[-1], name)
+    d = json.load(open(path))
+    sha = (d.get("build") or {}).get("lib_sha16")
+    return d, os.path.relpath(path, ROOT), bool(sha) and sha == running_lib_sha16()
+
+
 def pmc_traffic(stage, field="hbm_bytes"):
     """Per-launch HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) -- or another field, e.g. valu_wave_instr -- of the
-    stage's kernel from the latest committed rocprofv3 PMC profile (tools/profile_round.sh +
-    tools/summarize_profile.py), or None."""
-    prof = os.path.join(ROOT, "profiles")
-    rounds = sorted(d for d in os.listdir(prof) if os.path.exists(os.path.join(prof, d, "pmc_traffic.json"))) \
-        if os.path.isdir(prof) else []
-    if not rounds or stage not in STAGE_KERNEL:
-        return None, None
-    path = os.path.join(prof, rounds[-1], "pmc_traffic.json")
-    ks = json.load(open(path))["kernels"]
-    hits = [v[field] for k, v in ks.items() if STAGE_KERNEL[stage] in k and v.get(field)]
-    return (sum(hits) if hits else None), os.path.relpath(path, ROOT)
+    stage's kernel from the latest committed rocprofv3 PMC profile, with its source and whether that profile is of
+    the running library (None values when there is no profile)."""
+    d, src, match = pmc_profile()
+    if d is None or stage not in STAGE_KERNEL:
+        return None, None, False
+    hits = [v[field] for k, v in d["kernels"].items() if STAGE_KERNEL[stage] in k and v.get(field)]
+    return (sum(hits) if hits else None), src, match
 
 
 def cpu_model():
@@ -647,15 +669,26 @@ def main():
     if dom is not None and stats.get(dom, (0, 0))[1] > 0:
         ms = stats[dom][0]
         ach = round(algorithmic_bytes(dom, P, V, nr, W * H, T, M, 1) / (ms * 1e-3) / 1e9, 1)
-        traffic, src = pmc_traffic(dom) if P == 1_000_000 else (None, None)
+        traffic, src, fresh = pmc_traffic(dom) if P == 1_000_000 else (None, None, False)
+        # counter traffic is attached only when the committed PMC profile was measured on the library running now
         roofline = dict(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                        traffic=traffic, traffic_unit="bytes/launch", traffic_source=src, kernel=dom,
-                        kernel_ms=round(ms, 4), launches=stats[dom][1])
-        valu, _ = pmc_traffic(dom, "valu_wave_instr") if P == 1_000_000 else (None, None)
-        if valu:
+                        traffic=traffic if fresh else None, traffic_unit="bytes/launch", traffic_source=src,
+                        kernel=dom, kernel_ms=round(ms, 4), launches=stats[dom][1], lib_sha16=running_lib_sha16())
+        if traffic and not fresh:
+            roofline["traffic_stale"] = dict(bytes_per_launch=traffic, note=f"{src} was measured on another build "
+                                                                             "of libhlgs.so; not attached")
+        valu, _, vfresh = pmc_traffic(dom, "valu_wave_instr") if P == 1_000_000 else (None, None, False)
+        if valu and vfresh:
             rate = valu / (ms * 1e-3) / 1e9
             roofline["valu_issue"] = dict(wave_instr_per_launch=valu, achieved_Ginstr_s=round(rate, 1),
                                           peak_Ginstr_s=VALU_PEAK_GINSTR, frac=round(rate / VALU_PEAK_GINSTR, 4))
+            st, _, sfresh = pmc_profile("stalls.json")
+            clk = [v.get("clock_GHz") for k, v in (st or {}).get("kernels", {}).items()
+                   if STAGE_KERNEL[dom] in k and v.get("clock_GHz")] if sfresh else []
+            if clk:  # the same rate against the ceiling at the clock the PMC pass measured for this kernel
+                peak_m = 256 * 4 * clk[0] / 2
+                roofline["valu_issue"].update(measured_clock_GHz=clk[0], peak_at_measured_clock_Ginstr_s=round(peak_m, 1),
+                                              frac_at_measured_clock=round(rate / peak_m, 4))
     cpu = parity = config3 = config4 = config5 = None
     _mem("main step")
     if rank == 0 and world == 1 and not args.no_extras:

@@ -47,6 +47,8 @@ def build(force=False, extra=None, verbose=False):
     os.makedirs(OBJDIR, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
+        if not os.path.exists(os.path.join(LIBDIR, "build_info.json")):
+            write_build_info()
         return LIB
     with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), 8)) as ex:
         objs = list(ex.map(lambda s: _compile(s, extra), SOURCES))
@@ -54,9 +56,35 @@ def build(force=False, extra=None, verbose=False):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    write_build_info()
     if verbose:
         print("built", LIB)
     return LIB
+
+
+def lib_sha16(path=LIB):
+    """First 16 hex digits of the library's SHA-256: the build identity profiles are matched against."""
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def write_build_info():
+    """lib/build_info.json: the library's hash and the git HEAD it was built from (the GPU box gets the tree without
+    .git, so the commit is recorded here, at build time)."""
+    import json
+    head, dirty = None, None
+    try:
+        root = os.path.dirname(PKG)
+        head = subprocess.run(["git", "-C", root, "rev-parse", "HEAD"], capture_output=True, text=True,
+                              check=True).stdout.strip()
+        dirty = bool(subprocess.run(["git", "-C", root, "status", "--porcelain", "--untracked-files=no", "--",
+                                     "hierarchical-lod-gaussians_amd/csrc", "include"], capture_output=True,
+                                    text=True).stdout.strip())
+    except (OSError, subprocess.CalledProcessError):
+        pass
+    json.dump(dict(lib_sha16=lib_sha16(), head=head, sources_dirty=dirty),
+              open(os.path.join(LIBDIR, "build_info.json"), "w"))
 
 
 if __name__ == "__main__":

@@ -15,6 +15,21 @@ import shutil
 import sys
 
 
+def build_identity():
+    """The profiled library: its hash (hashed here, on the box, from the very file the passes loaded) and the commit
+    recorded at build time (hierarchical-lod-gaussians_amd/lib/build_info.json)."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "hierarchical-lod-gaussians_amd", "lib", "libhlgs.so")
+    info = {}
+    try:
+        info = json.load(open(os.path.join(os.path.dirname(lib), "build_info.json")))
+    except (OSError, ValueError):
+        pass
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib) else None
+    return dict(lib_sha16=sha, head=info.get("head"), sources_dirty=info.get("sources_dirty"))
+
+
 def per_kernel(path, counter):
     vals = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
@@ -58,7 +73,7 @@ def main(src, dst):
                       lds_wave_instr=round(lds.get(k, 0.0)))
     json.dump(dict(note="per launch; fetch = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE (KiB -> bytes); "
                         "*_wave_instr = SQ_INSTS_* (wave instructions issued, all CUs)",
-                   kernels=out), open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+                   build=build_identity(), kernels=out), open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 

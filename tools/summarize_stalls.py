@@ -80,8 +80,10 @@ def main(src, dst):
             d["write_bytes"] = round(1024 * a.get("WRITE_SIZE", 0.0))
         out[k] = d
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from summarize_profile import build_identity
     json.dump(dict(note=__doc__.strip().splitlines()[0] + " (see tools/summarize_stalls.py for conventions)",
-                   kernels=out), open(dst, "w"), indent=1)
+                   build=build_identity(), kernels=out), open(dst, "w"), indent=1)
     for k, d in out.items():
         if "blend" in k or "preprocess" in k:
             print(k, json.dumps({x: d.get(x) for x in ("pmc_pass_us", "clock_GHz", "valu_issue_frac", "salu_per_cu_cycle",
