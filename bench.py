@@ -682,8 +682,8 @@ def main():
             rate = valu / (ms * 1e-3) / 1e9
             roofline["valu_issue"] = dict(wave_instr_per_launch=valu, achieved_Ginstr_s=round(rate, 1),
                                           peak_Ginstr_s=VALU_PEAK_GINSTR, frac=round(rate / VALU_PEAK_GINSTR, 4))
-            st, _, sfresh = pmc_profile("stalls.json")
-            clk = [v.get("clock_GHz") for k, v in (st or {}).get("kernels", {}).items()
+            stalls, _, sfresh = pmc_profile("stalls.json")
+            clk = [v.get("clock_GHz") for k, v in (stalls or {}).get("kernels", {}).items()
                    if STAGE_KERNEL[dom] in k and v.get("clock_GHz")] if sfresh else []
             if clk:  # the same rate against the ceiling at the clock the PMC pass measured for this kernel
                 peak_m = 256 * 4 * clk[0] / 2

@@ -56,9 +56,11 @@ struct Geom {
 // 64-byte per-Gaussian record read by the blend kernels: one half cache line per (tile, Gaussian)
 // instance instead of one line per attribute array.
 //   [0] x, y, conic.a, conic.b      [1] conic.c, opacity, r, g
-//   [2] b, 1/depth, t, 1/num_kids    [3] record-slot base, first tile x | y << 16, rect width (int bits),
+//   [2] b, 1/depth, t, 1/num_kids    [3] unused, first tile x | y << 16, rect width (int bits),
 //                                        alpha threshold on e2 (alpha_e2_threshold)
-// [3].x = point_offsets - tiles_touched is written by the scatter, after the scan; the rest by the preprocess.
+// All written by the preprocess.  The Gaussian's record-slot base (the exclusive scan of the rect sizes) is read by
+// the blend backward from point_offsets[idx - 1]: writing it into the record after the scan cost the key scatter a
+// partial-line write per visible Gaussian.
 Geom carve_geom(void* base, int P, size_t* total);
 
 // Per-pixel / per-tile state (ImageState, rasterizer_impl.h:47-54) plus binning counters.

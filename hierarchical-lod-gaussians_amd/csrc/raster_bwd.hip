@@ -251,6 +251,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
             const uint32_t pos = range.x + li_top - lane;
             const uint32_t id = point_list[pos];
             const float4* sr = g.splat + 4 * (size_t)id;
+            const uint32_t sbase = id ? g.point_offsets[id - 1] : 0u;
             const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
             qm = quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
@@ -261,7 +262,8 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
             if (INTERP) s_tf[lane] = make_float2(r2.z, r2.w);
             const int x0 = __float_as_int(r3.y) & 0xffff, y0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
             const int w = __float_as_int(r3.z);
-            slot = __float_as_uint(r3.x) + (uint32_t)((ty - y0) * w + (tx - x0));
+            // the Gaussian's record slots start at the exclusive scan of the rect sizes (point_offsets is inclusive)
+            slot = sbase + (uint32_t)((ty - y0) * w + (tx - x0));
         }
 #pragma unroll
         for (int v = 0; v < 10; v++) s_m[64 * v + lane] = 0.f;

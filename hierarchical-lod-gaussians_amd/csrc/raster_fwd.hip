@@ -469,7 +469,6 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += (BG / 4)) {
             const int k = idx - g0;
             g.point_offsets[idx] = base + s_pre[k + 1];
-            if (radii[idx] > 0) g.splat[4 * (size_t)idx + 3].x = __uint_as_float(base + s_pre[k]);
         }
     }
     for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
@@ -594,7 +593,6 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
     if (guard_fail(gd)) return;
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= P || radii[idx] <= 0) return;
-    g.splat[4 * (size_t)idx + 3].x = __uint_as_float(g.point_offsets[idx] - g.tiles_touched[idx]);
     const float2 xy = g.means2D[idx];
     const int2 ext = g.rects[idx];
     int x0, y0, x1, y1;

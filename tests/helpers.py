@@ -54,7 +54,9 @@ def gpu_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_cov=
     return out
 
 
-def oracle_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_cov=False):
+def oracle_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_cov=False, lib=False):
+    """lib: the oracle build (False: the serial reference of every parity check; "fma": the same source with FMA
+    contraction, for build-to-build variance)."""
     from oracle import oracle as O
     sc = dict(means3D=scene["means3D"], opacities=scene["opacities"], sh_degree=scene.get("sh_degree", 0))
     if use_colors:
@@ -67,7 +69,7 @@ def oracle_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_c
         sc["scales"] = scene["scales"]
         sc["rotations"] = scene["rotations"]
     camn = S.cam_numpy(cam)
-    fr = O.forward(sc, camn, do_depth=do_depth)
+    fr = O.forward(sc, camn, do_depth=do_depth, omp=lib)
     out = dict(color=fr.color, radii=fr.radii, invdepth=fr.invdepth, frame=fr)
     if grads is not None:
         g, gd = grads
