@@ -421,83 +421,53 @@ __device__ __forceinline__ float dpp(float v)
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW, 0xF, BC));
 }
 
-// Butterfly reduce-scatter of ten per-lane values over the 64-lane wave.  v_permlane32_swap folds two
-// values at once (rows 0-1 keep the sum of one, rows 2-3 of the other), v_permlane16_swap folds again
-// across row pairs, and four fused row-DPP adds finish inside each 16-lane row: 28 VALU instructions
-// where ten independent full-wave DPP sums take 60.  Totals land in every lane of a row:
-//   r0 rows 0..3 = v0, v2, v1, v3;   r1 rows 0..3 = v4, v6, v5, v7;   r2 rows 0..3 = v8, v8, v9, v9.
-__device__ __forceinline__ float fold32(float x, float y)
-{
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float fold16(float x, float y)
-{
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ void wave_reduce10(const float (&v)[10], float& r0, float& r1, float& r2)
-{
-    const float a0 = fold32(v[0], v[1]), a2 = fold32(v[2], v[3]), a4 = fold32(v[4], v[5]);
-    const float a6 = fold32(v[6], v[7]), a8 = fold32(v[8], v[9]);
-    r0 = fold16(a0, a2);
-    r1 = fold16(a4, a6);
-    r2 = fold16(a8, a8);
-#define HLGS_DPP_ROW(ctrl)                                                                                 \
-    "v_add_f32_dpp %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                        \
-    "v_add_f32_dpp %1, %1, %1 " ctrl " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                        \
-    "v_add_f32_dpp %2, %2, %2 " ctrl " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-    asm volatile("s_nop 1\n\t"
-                 HLGS_DPP_ROW("quad_perm:[1,0,3,2]")
-                 HLGS_DPP_ROW("quad_perm:[2,3,0,1]")
-                 HLGS_DPP_ROW("row_ror:4")
-                 HLGS_DPP_ROW("row_ror:8")
-                 "s_nop 1"
-                 : "+v"(r0), "+v"(r1), "+v"(r2));
-#undef HLGS_DPP_ROW
-}
-
-
 // Reduce-scatter of ten per-lane values over the wave, cheapest stages first (issue costs measured by
 // tools/issue_probe.hip: a DPP add 4.2 cycles per wave instruction, a permlane swap 8.3).  Each fold halves the number
 // of registers: within each 16-lane row, bank-masked DPP adds fold lanes l and l^8 (values 2i into lanes 0-7, 2i+1 into
 // lanes 8-15), then l and l^4 (per 4-lane bank); permlane32 / permlane16 swaps fold the halves and the row pairs; a
-// quad_perm full reduction finishes each bank.  18 DPP + 3 permlane swaps, where the full-wave reduction of ten values
-// (wave_reduce10) takes 12 DPP + 8 permlane swaps.  (row_ror:n: lane l reads lane l - n of its row.)  The result w holds, in every lane of row rho and bank beta
-// (lane = 16 rho + 4 beta + i), the total of value reduce10_index(rho, beta), or nothing for rho = 3.
+// quad_perm full reduction finishes each bank.  18 DPP + 3 permlane swaps, where ten full-wave reductions take
+// 12 DPP + 8 permlane swaps.  (row_ror:n: lane l reads lane l - n of its row.)  The result w holds, in every lane of
+// row rho and bank beta (lane = 16 rho + 4 beta + i), the total of value reduce10_index(rho, beta), or nothing for
+// rho = 3.
 __device__ __forceinline__ int reduce10_index(int rho, int beta)
 {
     const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
     return rho == 0 ? cb : rho == 2 ? 4 + cb : rho == 1 ? ((beta & 1) ? -1 : 8 + (beta >> 1)) : -1;
 }
+// One instruction stream, ordered so that every DPP / permlane-swap source was written at least two instructions
+// earlier where the sequence allows it (the gfx950 VALU-write -> DPP-read and -> permlane-swap-read hazards need two
+// wait states): 4 s_nop where the builtin-and-asm version took 7.
 __device__ __forceinline__ float wave_reduce10_rs(const float (&v)[10])
 {
-    float s0, s1, s2, s3, s4, t0, t1, t2;
+    float s0, s1, s2, s3, s4, t0, t1, t2, z, w;
 #define HLGS_FOLD8(d, a, b)                                                                                        \
     "v_add_f32_dpp " d ", " a ", " a " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
     "v_add_f32_dpp " d ", " b ", " b " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
 #define HLGS_FOLD4(d, a, b)                                                                                        \
     "v_add_f32_dpp " d ", " a ", " a " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
     "v_add_f32_dpp " d ", " b ", " b " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
-    asm volatile("s_nop 1\n\t"
-                 HLGS_FOLD8("%0", "%8", "%9") HLGS_FOLD8("%1", "%10", "%11") HLGS_FOLD8("%2", "%12", "%13")
-                 HLGS_FOLD8("%3", "%14", "%15") HLGS_FOLD8("%4", "%16", "%17")
-                 HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%7", "%4", "%4")
-                 "s_nop 1"
-                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2)
+    asm volatile("s_nop 0\n\t"
+                 "v_mov_b32 %8, 0\n\t"
+                 HLGS_FOLD8("%0", "%10", "%11") HLGS_FOLD8("%1", "%12", "%13") HLGS_FOLD8("%2", "%14", "%15")
+                 HLGS_FOLD8("%3", "%16", "%17") HLGS_FOLD8("%4", "%18", "%19")
+                 HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%7", "%4", "%4")
+                 "v_permlane32_swap_b32 %5, %6\n\t"   // t0 (written two instructions back), t1
+                 "v_add_f32 %5, %5, %6\n\t"           // rows 0-1: t0, rows 2-3: t1
+                 "v_permlane32_swap_b32 %7, %8\n\t"   // t2 (two back), 0
+                 "v_add_f32 %7, %7, %8\n\t"           // rows 0-1: t2, rows 2-3: 0
+                 "s_nop 1\n\t"
+                 "v_permlane16_swap_b32 %5, %7\n\t"
+                 "v_add_f32 %9, %5, %7\n\t"           // row 0: t0, row 1: t2, row 2: t1, row 3: 0
+                 "s_nop 1\n\t"
+                 "v_add_f32_dpp %9, %9, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\t"
+                 "v_add_f32_dpp %9, %9, %9 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(z),
+                   "=&v"(w)
                  : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]),
                    "v"(v[9]));
 #undef HLGS_FOLD8
 #undef HLGS_FOLD4
-    const float u0 = fold32(t0, t1);   // rows 0-1: t0, rows 2-3: t1
-    const float u1 = fold32(t2, 0.f);  // rows 0-1: t2, rows 2-3: 0
-    float w = fold16(u0, u1);          // row 0: t0, row 1: t2, row 2: t1, row 3: 0
-    asm volatile("s_nop 1\n\t"
-                 "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 1\n\t"
-                 "v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 1"
-                 : "+v"(w));
     return w;
 }
 

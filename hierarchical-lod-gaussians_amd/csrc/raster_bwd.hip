@@ -154,12 +154,6 @@ struct BwdArgs {
 // 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
 // whose n_contrib lies behind it) run bwd_pair, the ten moments are folded over the wave, and one record per
 // (tile, splat) is stored after the batch.
-#ifndef HLGS_BWD_RS
-#define HLGS_BWD_RS 1  // reduce-scatter of the ten moments (wave_reduce10_rs); 0: full-wave reductions (wave_reduce10)
-#endif
-#ifndef HLGS_BWD_PREFETCH
-#define HLGS_BWD_PREFETCH 1  // next splat's LDS reads ahead of this one's reduction
-#endif
 #ifndef HLGS_BWD_WAVES
 #define HLGS_BWD_WAVES 5  // waves per SIMD: 96 VGPRs
 #endif
@@ -182,7 +176,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
     __shared__ float4 s_col[64];  // r, g, b, alpha threshold on e2
     __shared__ float2 s_tf[64];   // interpolation t, 1/kids
-    __shared__ float s_m[64 * 10];  // reduced moments per splat
+    __shared__ float s_m[64 * 11];  // reduced moments per splat (+ a spare row the non-storing lanes write)
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
     const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
@@ -197,11 +191,10 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     const size_t HW = (size_t)H * W;
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
     const float lx = (float)(tx0 + (lane & 7)), ly = (float)(ty0 + (lane >> 3));
-#if HLGS_BWD_RS
-    // the reduced moment this lane stores (wave_reduce10_rs layout), as an offset into s_m; -1: none
+    // the reduced moment this lane stores (wave_reduce10_rs layout) as an offset into s_m; lanes holding no total
+    // store into the spare row s_m[640..703]
     const int wm_i = (lane & 3) ? -1 : reduce10_index(lane >> 4, (lane >> 2) & 3);
-    const int wm = wm_i < 0 ? -1 : 64 * wm_i;
-#endif
+    const int wmd = wm_i < 0 ? 640 : 64 * wm_i;
 
     // lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant k
     PixB ps[4];
@@ -285,61 +278,39 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                 qv[k] = m;
             }
             uint64_t todo = qv[0] | qv[1] | qv[2] | qv[3];
-            // the next visited splat's LDS reads are issued after this splat's pixel steps and before its
-            // reduction, which covers their latency (the splat data is dead by then, so no extra registers)
-            int j = todo ? __builtin_ctzll(todo) : 0;
-#if HLGS_BWD_PREFETCH
-            float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
-            float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
-#endif
-            while (todo) {
-#if !HLGS_BWD_PREFETCH
-                j = __builtin_ctzll(todo);
-                const float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
-                const float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
-#endif
-                todo &= todo - 1;
-                const uint32_t li = li_top - (uint32_t)j;
-                const uint32_t qm = (uint32_t)((qv[0] >> j) & 1u) | ((uint32_t)((qv[1] >> j) & 1u) << 1) |
-                                    ((uint32_t)((qv[2] >> j) & 1u) << 2) | ((uint32_t)((qv[3] >> j) & 1u) << 3);
-                float acc[10];
+            // Splat loop with the least scalar bookkeeping: the visited bit is cleared (s_bitset0), the next visited
+            // splat found by s_ff1 (-1 once none is left; its LDS reads use index 0 then), and every visited splat
+            // is reduced (0.15% of them have no valid pair), so no per-pass wave-mask tracking.
+            if (todo) {
+                int j = __builtin_ctzll(todo);
+                float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
+                float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
+                while (true) {
+                    int jn;  // s_ff1: -1 once todo is empty
+                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
+                    const uint32_t li = li_top - (uint32_t)j;
+                    float acc[10];
 #pragma unroll
-                for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
-                    uint64_t z;
-                    asm volatile("v_mov_b64 %0, 0" : "=v"(z));
-                    acc[v] = __uint_as_float((uint32_t)z);
-                    acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
-                }
-                uint64_t any = 0;  // lanes with a valid pair (wave mask)
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    if ((qm >> k) & 1u)  // uniform branch
-                        any |= bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), co, col,
-                                                       xy.z, tf.x, tf.y, col.w, acc);
-                const int jc = j;
-#if HLGS_BWD_PREFETCH
-                if (todo) {
-                    j = __builtin_ctzll(todo);
-                    xy = s_xy[j];
-                    co = s_q[j];
-                    col = s_col[j];
-                    if (INTERP) tf = s_tf[j];
-                }
-#endif
-                if (any) {
-#if HLGS_BWD_RS
-                    const float r = wave_reduce10_rs(acc);
-                    if (wm >= 0) s_m[wm + jc] = r;
-#else
-                    float r0, r1, r2;
-                    wave_reduce10(acc, r0, r1, r2);
-                    if ((lane & 15) == 0) {
-                        const int row = lane >> 4, c = ((row & 1) << 1) | (row >> 1);
-                        s_m[64 * c + jc] = r0;
-                        s_m[64 * (4 + c) + jc] = r1;
-                        if (!(row & 1)) s_m[64 * (8 + (row >> 1)) + jc] = r2;
+                    for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
+                        uint64_t z;
+                        asm volatile("v_mov_b64 %0, 0" : "=v"(z));
+                        acc[v] = __uint_as_float((uint32_t)z);
+                        acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
                     }
-#endif
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if ((qv[k] >> j) & 1u)  // uniform branch
+                            bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)),
+                                                         co, col, xy.z, tf.x, tf.y, col.w, acc);
+                    const int jl = jn < 0 ? 0 : jn;  // the next visited splat's LDS reads ahead of the reduction
+                    xy = s_xy[jl];
+                    co = s_q[jl];
+                    col = s_col[jl];
+                    if (INTERP) tf = s_tf[jl];
+                    // every lane stores (the spare row takes the non-totals), so no exec-mask change
+                    s_m[wmd + j] = wave_reduce10_rs(acc);
+                    if (jn < 0) break;
+                    j = jn;
                 }
             }
         }
