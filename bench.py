@@ -321,6 +321,27 @@ def bench_config3(P, deg, W, H, dev, iters=20, tau_px=6.0):
                 timing=f"median of {iters} event spans per stage on torch's stream")
 
 
+EXCHANGE = os.environ.get("HLGS_EXCHANGE", "factored")  # "plain": every gradient all-reduced (the A/B reference)
+
+
+def make_exchange(params, means, sh, dc=None):
+    """The view-DP gradient exchange of the N > 1 legs: colour-factored SH gradients by default (hlgs_core.dp: the SH
+    leaves are exchanged as 3-float colour gradients, all-gathered, and rebuilt on every rank); HLGS_EXCHANGE=plain
+    all-reduces every gradient, with the SH backward overlapping the early collective (the rasterizer is the only
+    consumer of means3D / shs in these steps)."""
+    from hlgs_core.dp import FlatGradExchange
+    if EXCHANGE == "plain":
+        return FlatGradExchange(params, overlap=True)
+    return FlatGradExchange(params, colour_factor=dict(means=means, sh=sh, dc=dc))
+
+
+def exchange_fields(ex, world, ms):
+    """bytes and achieved per-GPU link rate of one exchange (ms: its measured time)."""
+    ar, ag, link = ex.link_bytes(world)
+    return dict(mode=EXCHANGE, allreduce_bytes=ar, allgather_bytes_per_rank=ag, link_bytes_per_gpu=link,
+                link_GBs=round(link / (ms * 1e-3) / 1e9, 1) if ms > 0 else None)
+
+
 def make_step(P, deg, W, H, dev, rank, world, exchange_on=True):
     """One rank's training view: its scene replica, rasterizer and upstream gradients; returns step() and state."""
     from diff_gaussian_rasterization import GaussianRasterizer
@@ -337,8 +358,7 @@ def make_step(P, deg, W, H, dev, rank, world, exchange_on=True):
     g_col, g_inv = torch.tensor(g_np, device=dev), torch.tensor(gd_np, device=dev)
     rs = settings_for(cam, deg, dev)
     rast = GaussianRasterizer(rs)
-    # overlap: the rasterizer is the only consumer of means3D / shs in this step (hlgs_core.dp.FlatGradExchange)
-    exchange = FlatGradExchange(params, overlap=True) if (world > 1 and exchange_on) else None
+    exchange = make_exchange(params, means3D, shs) if (world > 1 and exchange_on) else None
     st = dict(params=params, rs=rs, rast=rast, exchange=exchange, g_col=g_col, g_inv=g_inv, ar_events=[])
 
     def step(time_exchange=False):
@@ -433,7 +453,6 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
     Barrier + synchronise around the timed steps, max over ranks; all-reduce time and bus bandwidth reported."""
     from alt_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from hlgs_core import synthetic as S
-    from hlgs_core.dp import FlatGradExchange
     from hlgs_core.loss import photometric_loss
     from hlgs_core.spt_cache import NAMES, SPTCache, gather_views
     b, storage, build_s, G = merged_two_chunk_scene(P)
@@ -475,7 +494,7 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
         p = cache.params
         if trace:
             print(f"[config5 r{rank}] resident {cache.render_indices.numel()}", file=sys.stderr, flush=True)
-        ex = FlatGradExchange([p[k] for k in NAMES]) if world > 1 else None
+        ex = make_exchange([p[k] for k in NAMES], p["xyz"], p["f_rest"], p["f_dc"]) if world > 1 else None
         s = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=cam["tanfovx"],
                                           tanfovy=cam["tanfovy"], bg=bg, scale_modifier=1.0,
                                           viewmatrix=cam["viewmatrix"].to(dev), projmatrix=cam["projmatrix"].to(dev),
@@ -495,7 +514,7 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
             if trace:
                 print(f"[config5 r{rank}] allreduce {ex.flat.numel()}", file=sys.stderr, flush=True)
             ex.allreduce()
-            nbytes.append(ex.flat.numel() * 4)
+            nbytes.append(ex.link_bytes(world))
             ex.close()
         e[5].record()
         cache.optimizer_step(it, lrs)
@@ -531,9 +550,10 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
                        if world == 1 else "barrier + synchronise around the timed steps, max over ranks; stages: "
                                           "median event spans on torch's stream"))
     if world > 1:
-        nb = float(np.median(nbytes))
-        out.update(allreduce_ms=round(ar, 4), bytes_per_step=int(nb),
-                   busbw_GBs=round(2 * (world - 1) / world * nb / (ar * 1e-3) / 1e9, 1))
+        ar_b, ag_b, link = (int(np.median([x[i] for x in nbytes])) for i in range(3))
+        out.update(exchange_ms=round(ar, 4), exchange=dict(
+            mode=EXCHANGE, allreduce_bytes=ar_b, allgather_bytes_per_rank=ag_b, link_bytes_per_gpu=link,
+            link_GBs=round(link / (ar * 1e-3) / 1e9, 1) if ar > 0 else None))
     del cache
     torch.cuda.empty_cache()
     return out
@@ -557,13 +577,12 @@ def bench_config4_dp(P, deg, W, H, dev, rank, world, steps, warmup, backend):
     t = torch.tensor([el, ar_ms], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el, ar_ms = float(t[0].item()), float(t[1].item())
-    nbytes = st["exchange"].flat.numel() * 4
     out = dict(workload=f"configs[3]: {P} Gaussians per replica, SH deg {deg}, {W}x{H}, fwd+bwd with depth, one view "
-                        f"per GPU, {'RCCL' if backend == 'nccl' else backend} grad all-reduce",
+                        f"per GPU, {'RCCL' if backend == 'nccl' else backend} gradient exchange ({EXCHANGE})",
                value=round(world * W * H * steps / el / 1e6, 3), unit="Mpix/s", n_gpus=world,
-               ms_per_step=round(el / steps * 1e3, 4), steps=steps, allreduce_ms=round(ar_ms, 4),
-               bytes_per_step=nbytes, busbw_GBs=round(2 * (world - 1) / world * nbytes / (ar_ms * 1e-3) / 1e9, 1),
-               timing="barrier + synchronise around the timed steps, max over ranks; all-reduce: events around "
+               ms_per_step=round(el / steps * 1e3, 4), steps=steps, exchange_ms=round(ar_ms, 4),
+               exchange=exchange_fields(st["exchange"], world, ar_ms),
+               timing="barrier + synchronise around the timed steps, max over ranks; exchange: events around "
                       "FlatGradExchange.allreduce() (mean, max over ranks)")
     st["exchange"].close()
     del step, st
@@ -647,13 +666,14 @@ def main():
         t = torch.tensor([elapsed, ar_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, ar_ms = float(t[0].item()), float(t[1].item())
-        nbytes = exchange.flat.numel() * 4
         exchange_report = dict(
-            collective=f"all_reduce {'AVG' if backend == 'nccl' else 'SUM + 1/N scale'}, {backend}", bytes_per_step=nbytes, collectives_per_step=getattr(
-                exchange, "last_collectives", None), allreduce_ms=round(ar_ms, 4),
-            busbw_GBs=round(2 * (world - 1) / world * nbytes / (ar_ms * 1e-3) / 1e9, 1) if ar_ms > 0 else None,
+            collective=(f"all_reduce {'AVG' if backend == 'nccl' else 'SUM + 1/N scale'}" +
+                        (" + all_gather of the colour-gradient rows" if EXCHANGE != "plain" else "") + f", {backend}"),
+            collectives_per_step=getattr(exchange, "last_collectives", None), exchange_ms=round(ar_ms, 4),
+            **exchange_fields(exchange, world, ar_ms),
             note="events around FlatGradExchange.allreduce() on torch's stream in each timed step (mean; max over "
-                 "ranks); bus bandwidth = 2(N-1)/N x bytes / time")
+                 "ranks), the SH rebuild included; link bytes per GPU = 2(N-1)/N x all-reduced bytes + (N-1) x gathered "
+                 "row bytes")
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * W * H * args.steps / elapsed / 1e6

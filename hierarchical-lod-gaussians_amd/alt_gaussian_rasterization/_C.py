@@ -118,10 +118,14 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     f32 = dict(dtype=torch.float32, device=dev)
     P = means3D.size(0)
     M = sh.size(1) if (sh is not None and sh.size(0) != 0 and sh.dim() > 1) else 0
+    # a colour-factored view-DP exchange takes dL/dRGB instead of the dc / SH gradients (hlgs_core.dp.colour_factor);
+    # not with an empty sh, whose SH backward does not run at all (A-19)
+    fac = dp.colour_factor(sh, dc) if M > 0 and dc is not None and dc.numel() else None
     out = dict(dmean2D=torch.empty((P, 3), **f32), dcolor=torch.empty((P, 3), **f32),
                dopacity=_dest(opacities, (P, 1), f32), dmean3D=_dest(means3D, (P, 3), f32, True),
-               dcov3D=torch.empty((P, 6), **f32), ddc=_dest(dc, (P, 1, 3), f32, True),
-               dsh=_dest(sh, (P, M, 3), f32, True), dscale=_dest(scales, (P, 3), f32),
+               dcov3D=torch.empty((P, 6), **f32),
+               ddc=fac[2] if fac is not None else _dest(dc, (P, 1, 3), f32, True),
+               dsh=fac[1] if fac is not None else _dest(sh, (P, M, 3), f32, True), dscale=_dest(scales, (P, 3), f32),
                drot=_dest(rotations, (P, 4), f32))
     order = ("dmean2D", "dcolor", "dopacity", "dmean3D", "dcov3D", "ddc", "dsh", "dscale", "drot")
     if P == 0:
@@ -129,7 +133,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     a, keep, P, M = _raster_args(background, means3D, colors, opacities, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, dc, sh, degree,
                                  campos, False, antialiasing, debug)
-    g = L.Grads(**{k: L.ptr(v) for k, v in out.items()})
+    g = L.Grads(**{k: L.ptr(v) for k, v in out.items()}, drgb=L.ptr(fac[0]) if fac is not None else None)
     dpix = dL_dout_color.contiguous().float()
     dinv = dL_dout_invdepth.contiguous().float() if dL_dout_invdepth is not None and dL_dout_invdepth.numel() else None
     scratch = torch.empty((lib.hlgs_backward_scratch_size(P, int(R)),), dtype=torch.uint8, device=dev)
@@ -142,6 +146,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     if late is not None:
         dp.note_late_work(late, list(keep.values()) + list(out.values()) +
                           [radii, geomBuffer, imageBuffer, binningBuffer, scratch, dpix, dinv])
+    if fac is not None:
+        fac[3](keep["campos"], degree, L.VARIANT_ALT)
     del keep
     return tuple(out[k] for k in order)
 

@@ -33,6 +33,8 @@ void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
 void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
                       const hlgs_grads& o, bool has_depth, hipStream_t s, hipStream_t late, hipEvent_t ev);
 void launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t s);
+void launch_sh_from_colour(int P, int V, int D, int M, bool alt, const float* means, const float* campos,
+                           const float* drgb, int64_t stride, float scale, float* dsh, float* ddc, hipStream_t s);
 void launch_relocation(int P, const float* oo, const float* so, const int* N, const float* binoms, int n_max,
                        float* on, float* sn, hipStream_t s);
 size_t ssim_partials(int C, int H, int W);
@@ -525,6 +527,21 @@ int hlgs_rasterize_backward_split(const hlgs_raster_args* a, const int* radii, c
     stage_mark(s, ST_GAUSS_BWD, false);
     if (late && (rc = check_stage(late, a->debug, "sh_bwd"))) return rc;
     return check_stage(s, a->debug, "gauss_bwd");
+}
+
+int hlgs_sh_grad_from_colour(int P, int V, int D, int M, int variant, const float* means3D, const float* campos,
+                             const float* drgb, int64_t view_stride, float scale, float* dsh, float* ddc, void* stream)
+{
+    const bool alt = variant == HLGS_VARIANT_ALT;
+    if (P < 0 || V < 1 || D < 0 || D > 3 || M < 0 || M > 16 - (alt ? 1 : 0) || (V > 1 && view_stride < 3 * (int64_t)P))
+        return fail(HLGS_ERR_ARG, "sh_grad_from_colour: bad P, V, D or M");
+    if (P == 0 || M == 0 && !alt) return HLGS_OK;
+    if (!means3D || !campos || !drgb || (M > 0 && !dsh) || (alt && !ddc))
+        return fail(HLGS_ERR_ARG, "sh_grad_from_colour: missing buffer");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_sh_from_colour(P, V, D, M, alt, means3D, campos, drgb, view_stride, scale, dsh, ddc, s);
+    return check_stage(s, false, "sh_grad_from_colour");
 }
 
 int hlgs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -399,12 +399,18 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
     __syncthreads();
     // rows of invisible Gaussians are not read: they arrive as zeros, which is their dsh row
     sh_rows_load<3 * MT>(a.shs, s_rows, s_idx, n, lane, M3, s_vis);
+    // colour-factored mode (o.drgb, view-data-parallel exchange): the masked dL/dRGB row replaces dsh / ddc
+    const bool factored = o.drgb != nullptr;  // uniform
     __syncthreads();
     float* row = s_rows + lane * kShStride;
     if (active) {
         const bool dropped = HIER && a.parent_indices && a.parent_indices[t_idx] != -1;
         if (!vis) {
-            if (ALT) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
+            if (factored) {
+                o.drgb[3 * idx] = 0.f; o.drgb[3 * idx + 1] = 0.f; o.drgb[3 * idx + 2] = 0.f;
+            } else if (ALT) {
+                o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f;
+            }
         } else {
             const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
             const f3 dir_orig = sub(m, campos);
@@ -428,13 +434,18 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
                     vz += proj * gz;
                 }
             }
-            if (ALT) {
+            if (factored) {
+                o.drgb[3 * idx] = dropped ? 0.f : dR;
+                o.drgb[3 * idx + 1] = dropped ? 0.f : dG;
+                o.drgb[3 * idx + 2] = dropped ? 0.f : dB;
+            } else if (ALT) {
                 o.ddc[3 * idx] = basis[0] * dR;
                 o.ddc[3 * idx + 1] = basis[0] * dG;
                 o.ddc[3 * idx + 2] = basis[0] * dB;
             }
 #pragma unroll
             for (int c = OFF; c < MC + OFF; c++) {
+                if (factored) break;
                 if (c - OFF >= M) break;
                 const float bs = dropped ? 0.f : basis[c];
                 row[3 * (c - OFF)] = bs * dR;
@@ -454,8 +465,93 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
             }
         }
     }
+    if (factored) return;  // wave-uniform
     __syncthreads();
     sh_rows_copy<3 * MT, false>(o.dsh, s_rows, s_idx, n, lane, M3);
+}
+
+// hlgs_sh_grad_from_colour: one thread per Gaussian rebuilds its averaged SH gradient row from the V views' colour
+// gradients, with the per-view products basis_c(dir_v) * dL/dRGB_v in k_sh_bwd's operation order, summed in view
+// order and scaled once; rows go out through LDS as contiguous float4 runs (as k_sh_bwd's).
+template <int MT, bool ALT>  // MT = 0: row count M known only at run time (up to 16)
+__global__ void __launch_bounds__(64) k_sh_from_colour(int P, int V, int D, int M_rt, const float* __restrict__ means,
+                                                       const float* __restrict__ campos, const float* __restrict__ drgb,
+                                                       int64_t stride, float scale, float* __restrict__ dsh,
+                                                       float* __restrict__ ddc)
+{
+    constexpr int OFF = ALT ? 1 : 0;
+    constexpr int MC = MT ? MT : (16 - OFF);
+    const int M = MT ? MT : M_rt;
+    __shared__ float s_rows[64 * kShStride];
+    __shared__ int s_idx[64];
+    const int lane = threadIdx.x;
+    const int t0 = blockIdx.x * 64;
+    const int n = min(64, P - t0);
+    const int p = t0 + lane;
+    s_idx[lane] = p;
+    float acc[3 * (MC + OFF)];
+#pragma unroll
+    for (int i = 0; i < 3 * (MC + OFF); i++) acc[i] = 0.f;
+    if (lane < n) {
+        const f3 m = mk(means[3 * p], means[3 * p + 1], means[3 * p + 2]);
+        const int ncoef = (D + 1) * (D + 1);
+        for (int v = 0; v < V; v++) {
+            const float* d = drgb + v * stride + 3 * (int64_t)p;
+            const float* cp = campos + v * stride;
+            const float dR = d[0], dG = d[1], dB = d[2];
+            const f3 dir_orig = sub(m, mk(cp[0], cp[1], cp[2]));
+            const float len = sqrtf(dot(dir_orig, dir_orig));
+            const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+#pragma unroll
+            for (int c = 0; c < MC + OFF; c++) {
+                float gx, gy, gz;
+                const float bs = c < ncoef ? sh_basis(c, x, y, z, gx, gy, gz) : 0.f;
+                acc[3 * c] += bs * dR;
+                acc[3 * c + 1] += bs * dG;
+                acc[3 * c + 2] += bs * dB;
+            }
+        }
+        if (ALT) {
+            ddc[3 * p] = scale * acc[0];
+            ddc[3 * p + 1] = scale * acc[1];
+            ddc[3 * p + 2] = scale * acc[2];
+        }
+        float* row = s_rows + lane * kShStride;
+#pragma unroll
+        for (int c = OFF; c < MC + OFF; c++) {
+            if (c - OFF >= M) break;
+            row[3 * (c - OFF)] = scale * acc[3 * c];
+            row[3 * (c - OFF) + 1] = scale * acc[3 * c + 1];
+            row[3 * (c - OFF) + 2] = scale * acc[3 * c + 2];
+        }
+    }
+    __syncthreads();
+    sh_rows_copy<3 * MT, false>(dsh, s_rows, s_idx, n, lane, 3 * M);
+}
+
+void launch_sh_from_colour(int P, int V, int D, int M, bool alt, const float* means, const float* campos,
+                           const float* drgb, int64_t stride, float scale, float* dsh, float* ddc, hipStream_t s)
+{
+    const dim3 grid((P + 63) / 64);
+#define HLGS_SFC(MT, AL) hipLaunchKernelGGL((k_sh_from_colour<MT, AL>), grid, dim3(64), 0, s, P, V, D, M, means, campos, \
+                                           drgb, stride, scale, dsh, ddc)
+    if (alt) {
+        switch (M) {
+        case 3: HLGS_SFC(3, true); break;
+        case 8: HLGS_SFC(8, true); break;
+        case 15: HLGS_SFC(15, true); break;
+        default: HLGS_SFC(0, true); break;
+        }
+    } else {
+        switch (M) {
+        case 1: HLGS_SFC(1, false); break;
+        case 4: HLGS_SFC(4, false); break;
+        case 9: HLGS_SFC(9, false); break;
+        case 16: HLGS_SFC(16, false); break;
+        default: HLGS_SFC(0, false); break;
+        }
+    }
+#undef HLGS_SFC
 }
 
 __global__ void __launch_bounds__(256) k_parent_mean_add(int P, const int* __restrict__ radii,

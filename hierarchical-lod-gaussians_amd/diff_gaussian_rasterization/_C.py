@@ -126,11 +126,14 @@ def rasterize_gaussians_backward(bg, render_indices, parent_indices, ts, kids, m
                                          tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
     dev = means3D.device
     f32 = dict(dtype=torch.float32, device=dev)
+    # a colour-factored view-DP exchange takes dL/dRGB instead of the SH gradient (hlgs_core.dp.colour_factor)
+    fac = dp.colour_factor(sh) if M > 0 and keep["indices"] is None else None
     out = dict(dmean2D=torch.empty((P_full, 3), **f32), dcolor=torch.empty((P_full, 3), **f32),
                dopacity=_dest(opacities, (P_full, 1), f32), dmean3D=_dest(means3D, (P_full, 3), f32, True),
-               dcov3D=torch.empty((P_full, 6), **f32), dsh=_dest(sh, (P_full, M, 3), f32, True),
+               dcov3D=torch.empty((P_full, 6), **f32),
+               dsh=fac[1] if fac is not None else _dest(sh, (P_full, M, 3), f32, True),
                dscale=_dest(scales, (P_full, 3), f32), drot=_dest(rotations, (P_full, 4), f32))
-    g = L.Grads(**{k: L.ptr(v) for k, v in out.items()})
+    g = L.Grads(**{k: L.ptr(v) for k, v in out.items()}, drgb=L.ptr(fac[0]) if fac is not None else None)
     dpix = dL_dout_color.contiguous().float()
     dinv = None
     if dL_dout_invdepth is not None and dL_dout_invdepth.numel() and dL_dout_invdepth.size(0) != 0:
@@ -145,6 +148,8 @@ def rasterize_gaussians_backward(bg, render_indices, parent_indices, ts, kids, m
     if late is not None:
         dp.note_late_work(late, list(keep.values()) + list(out.values()) +
                           [radii, geomBuffer, imageBuffer, binningBuffer, scratch, dpix, dinv])
+    if fac is not None:
+        fac[3](keep["campos"], degree, L.VARIANT_HIERARCHY)
     del keep
     return (out["dmean2D"], out["dcolor"], out["dopacity"], out["dmean3D"], out["dcov3D"], out["dsh"], out["dscale"],
             out["drot"])

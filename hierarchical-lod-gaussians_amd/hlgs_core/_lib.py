@@ -34,7 +34,7 @@ VARIANT_ALT = 1
 
 class Grads(C.Structure):
     _fields_ = [("dmean2D", _vp), ("dcolor", _vp), ("dopacity", _vp), ("dmean3D", _vp), ("dcov3D", _vp),
-                ("dsh", _vp), ("dscale", _vp), ("drot", _vp), ("ddc", _vp)]
+                ("dsh", _vp), ("dscale", _vp), ("drot", _vp), ("ddc", _vp), ("drgb", _vp)]
 
 
 class HierInfo(C.Structure):
@@ -85,6 +85,7 @@ _SIGS = {
                                      C.POINTER(Grads), _vp]),
     "hlgs_rasterize_backward_split": (_i, [C.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
                                            C.POINTER(Grads), _vp, _vp]),
+    "hlgs_sh_grad_from_colour": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, C.c_int64, _f, _vp, _vp, _vp]),
     "hlgs_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "hlgs_compute_relocation": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "hlgs_adam_update": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, C.c_uint32, C.c_uint32, _vp]),

@@ -5,6 +5,14 @@ collective is one all-reduce of the Gaussian gradients (RCCL over xGMI with back
 CPU).  Gradients are packed into one flat fp32 buffer so RCCL moves a few large messages instead of
 one per parameter tensor, then averaged (the reference trains one view per step; G views per step is
 an effective batch of G).
+
+Colour-factored SH exchange (colour_factor=...).  One view's SH gradient is an outer product per Gaussian,
+dL/dsh[c] = basis_c(view direction) * dL/dRGB (computeColorFromSH backward, backward.cu:23-142), so a rank does not
+need the other ranks' (D+1)^2 x 3 SH rows, only their 3-float colour gradients and camera centres: the SH parameters
+leave the all-reduce, the rasterizer backward writes dL/dRGB into the exchange (hlgs_grads.drgb), one all-gather moves
+those rows, and every rank rebuilds the averaged SH gradient with hlgs_sh_grad_from_colour -- the same products,
+summed in rank order, identical on every rank.  At SH degree 3 a Gaussian's exchange drops from 59 all-reduced floats
+(2 (N-1)/N x 236 bytes over each GPU's links) to 11 all-reduced plus 3 gathered per rank.
 """
 import weakref
 
@@ -118,6 +126,78 @@ def note_late_work(stream, tensors):
             ex.pending = ev
 
 
+class _ColourFactor:
+    """Per-exchange state of the colour-factored SH gradient: this rank's row [campos x, y, z, pad | dL/dRGB P x 3],
+    the gathered rows of all ranks, and the buffers the rebuilt SH (and alt-variant dc) gradients live in."""
+
+    def __init__(self, means, sh, dc, world, dev):
+        self.means, self.sh, self.dc = means, sh, dc
+        P = means.shape[0]
+        self.row = P * 3 + 4
+        self.mine = torch.zeros(self.row, dtype=torch.float32, device=dev)
+        self.gathered = torch.empty((max(1, world), self.row), dtype=torch.float32, device=dev)
+        self.sh_buf = torch.empty(sh.shape, dtype=torch.float32, device=dev)
+        self.dc_buf = torch.empty(dc.shape, dtype=torch.float32, device=dev) if dc is not None else None
+        self.written = False  # a backward wrote this round's row
+        self.D = 0
+        self.variant = 0
+
+
+# SH parameter data_ptr -> (weak ref to the parameter, weak ref to its exchange)
+_FACTOR = {}
+
+
+def colour_factor(sh, dc=None):
+    """For the rasterizer backward: (drgb view P x 3, dsh destination, ddc destination or None, record) when `sh` is the
+    SH parameter of a colour-factored exchange whose round has not produced its row yet, else None.  The backward writes
+    dL/dRGB into drgb (hlgs_grads.drgb) instead of dsh / ddc and calls record(campos, degree, variant); the returned
+    dsh / ddc views become the leaves' .grad and are filled by the exchange's allreduce()."""
+    e = _FACTOR.get(sh.data_ptr()) if sh is not None and sh.numel() else None
+    if e is None:
+        return None
+    p, ex = e[0](), e[1]()
+    if p is None or ex is None or ex.cf is None:
+        _FACTOR.pop(sh.data_ptr(), None)
+        return None
+    cf = ex.cf
+    if cf.written or p.grad is not None or p.shape != sh.shape or (dc is not None) != (cf.dc is not None) or \
+            (dc is not None and cf.dc.grad is not None):
+        return None
+    P = cf.means.shape[0]
+    if sh.shape[0] != P or (dc is not None and dc.shape[0] != P):
+        return None
+
+    def record(campos, degree, variant):
+        cf.mine[:3].copy_(campos.reshape(-1)[:3])
+        cf.D, cf.variant, cf.written = int(degree), int(variant), True
+    # fresh views per call, so autograd adopts them as .grad (it steals a gradient nothing else references)
+    return (cf.mine[4:].view(P, 3), cf.sh_buf.view(cf.sh.shape), cf.dc_buf.view(cf.dc.shape) if dc is not None else None,
+            record)
+
+
+def _check_factored(cf):
+    """The rebuilt gradient reaches the leaves only if their .grad is the exchange's buffer (autograd adopted the views
+    colour_factor handed out): a second gradient into those leaves in the same backward (another rasterizer call, another
+    loss term) makes autograd sum into a new tensor, which the factored exchange cannot complete."""
+    for t, buf in ((cf.sh, cf.sh_buf), (cf.dc, cf.dc_buf)):
+        if t is not None and (t.grad is None or t.grad.data_ptr() != buf.data_ptr()):
+            raise RuntimeError("FlatGradExchange(colour_factor=...): the SH leaves received a gradient besides the "
+                               "factored rasterizer backward in this step; use the plain exchange for such losses")
+
+
+def rebuild_sh(cf, world):
+    """hlgs_sh_grad_from_colour over the gathered rows (rank order), averaged: fills cf.sh_buf / cf.dc_buf."""
+    from hlgs_core import _lib as L
+    lib = L.load()
+    L.require_gpu(cf.gathered, cf.means, cf.sh_buf)
+    P = cf.means.shape[0]
+    M = cf.sh.shape[1] if cf.sh.dim() > 1 else 0
+    base = cf.gathered.data_ptr()
+    L.check(lib.hlgs_sh_grad_from_colour(P, world, cf.D, M, cf.variant, L.ptr(cf.means.detach().contiguous()), base,
+                                         base + 16, cf.row, 1.0 / world, L.ptr(cf.sh_buf),
+                                         L.ptr(cf.dc_buf) if cf.dc_buf is not None else None, L.stream()))
+
+
 class FlatGradExchange:
     """Pack -> all-reduce -> hand back, for a fixed list of parameter tensors.
 
@@ -130,8 +210,20 @@ class FlatGradExchange:
     leaving several buckets to pipeline for a 1M-Gaussian model (236 MB of fp32 gradients).
     """
 
-    def __init__(self, params, bucket_bytes=64 << 20, average=True, group=None, direct=True, overlap=False):
-        self.params = list(params)
+    def __init__(self, params, bucket_bytes=64 << 20, average=True, group=None, direct=True, overlap=False,
+                 colour_factor=None):
+        # colour_factor = dict(means=<means3D leaf>, sh=<SH leaf (P, M, 3)>, dc=<the alt variant's dc leaf> or None):
+        # the SH leaves leave the flat buffer and are exchanged as colour gradients (module docstring); needs averaging
+        self.cf = None
+        params = list(params)
+        if colour_factor is not None:
+            sh, dc = colour_factor["sh"], colour_factor.get("dc")
+            assert average, "the colour-factored SH exchange averages"
+            world = dist.get_world_size(group) if dist.is_initialized() else 1
+            self.cf = _ColourFactor(colour_factor["means"], sh, dc, world, sh.device)
+            params = [p for p in params if p is not sh and p is not dc]
+            _FACTOR[sh.data_ptr()] = (weakref.ref(sh), weakref.ref(self))
+        self.params = params
         self.numels = [p.numel() for p in self.params]
         self.offsets = []
         off = 0
@@ -171,9 +263,20 @@ class FlatGradExchange:
                         self._hooks.append(p.register_post_accumulate_grad_hook(_adopt_hook(me, i)))
         self._finalizer = weakref.finalize(self, _drop_entries, list(self.direct), self._token)
 
+    def link_bytes(self, world):
+        """(all-reduced bytes, bytes all-gathered per rank, bytes each GPU moves over its links per exchange for a ring
+        of `world` ranks: 2 (N-1)/N of the all-reduced buffer plus (N-1) gathered rows)."""
+        ar = 4 * self.flat.numel()
+        ag = 4 * self.cf.row if self.cf is not None else 0
+        return ar, ag, int(2 * (world - 1) / world * ar + (world - 1) * ag)
+
     def close(self):
         """Stop offering the flat buffer to the rasterizer backward.  Rebuild the exchange (and close the old one)
         whenever the parameter tensors are replaced: entries are keyed by storage address."""
+        if self.cf is not None:
+            e = _FACTOR.get(self.cf.sh.data_ptr())
+            if e is not None and e[1]() is self:
+                del _FACTOR[self.cf.sh.data_ptr()]
         self._finalizer()
         self.direct = []
         for h in self._hooks:
@@ -202,6 +305,8 @@ class FlatGradExchange:
         self.claimed = [False] * len(self.params)
         self.late = [False] * len(self.params)
         self.adopted = [False] * len(self.params)
+        if self.cf is not None:
+            self.cf.written = False
 
     def _pack_range(self, a, b):
         for p, off, n in zip(self.params, self.offsets, self.numels):
@@ -227,9 +332,34 @@ class FlatGradExchange:
     def allreduce(self):
         """All-reduce every parameter's .grad across the process group (mean if average, else sum)."""
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            if self.cf is not None and self.cf.written:
+                _check_factored(self.cf)
+                self.cf.gathered[0].copy_(self.cf.mine)
+                rebuild_sh(self.cf, 1)
             self.release()
             return
         world = dist.get_world_size(self.group)
+        cf_work = None
+        if self.cf is not None:
+            cf = self.cf
+            if cf.written:  # the rows of all ranks, gathered while the flat buffer is reduced below
+                _check_factored(cf)
+                if cf.mine.is_cuda and dist.get_backend(self.group) != "nccl":
+                    # gloo has no all_gather of device tensors (one-GPU rehearsals): each rank's row in its own slot
+                    # of a zeroed buffer, summed -- the same rows, twice the bytes
+                    me = dist.get_rank(self.group)
+                    cf.gathered.zero_()
+                    cf.gathered[me].copy_(cf.mine)
+                    cf_work = dist.all_reduce(cf.gathered, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                elif dist.get_backend(self.group) == "nccl":  # RCCL writes the rows straight into the [world, row] buffer
+                    cf_work = dist.all_gather_into_tensor(cf.gathered, cf.mine, group=self.group, async_op=True)
+                else:
+                    cf_work = dist.all_gather(list(cf.gathered.unbind(0)), cf.mine, group=self.group, async_op=True)
+            else:  # the backward did not factor (no rasterizer call saw the exchange): plain averaged all-reduce
+                for t in (cf.sh, cf.dc):
+                    if t is not None and t.grad is not None:
+                        dist.all_reduce(t.grad, op=dist.ReduceOp.SUM, group=self.group)
+                        t.grad.mul_(1.0 / world)
         native_avg = self.average and dist.get_backend(self.group) == "nccl" and _AVG_OK[0]
         works = []
         # gradients the backward already wrote into the flat buffer need no packing, so there is nothing for the
@@ -272,4 +402,7 @@ class FlatGradExchange:
             w.wait()
         if self.average and not native_avg:
             self.flat.mul_(1.0 / world)
+        if cf_work is not None:
+            cf_work.wait()
+            rebuild_sh(self.cf, world)
         self.unpack()

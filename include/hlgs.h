@@ -103,6 +103,9 @@ typedef struct hlgs_grads {
     float* dscale;    /* P_full x 3 */
     float* drot;      /* P_full x 4 */
     float* ddc;       /* HLGS_VARIANT_ALT: P_full x 3, else NULL */
+    float* drgb;      /* NULL, or P_full x 3: the colour-factored SH gradient (hlgs_sh_grad_from_colour) -- the SH
+                         backward then writes dL/dRGB with the clamp mask applied (zero rows for Gaussians it skips)
+                         here instead of dsh / ddc, and still adds its view-direction term to dmean3D */
 } hlgs_grads;
 
 const char* hlgs_last_error(void);
@@ -158,6 +161,18 @@ int hlgs_rasterize_backward(const hlgs_raster_args* a, const int* radii, const v
 int hlgs_rasterize_backward_split(const hlgs_raster_args* a, const int* radii, const void* geom, const void* img,
                                   const void* binning, int R, void* scratch, const float* dL_dcolor,
                                   const float* dL_dinvdepth, const hlgs_grads* out, void* stream, void* late_stream);
+
+/* The averaged SH gradient of a view-data-parallel step, rebuilt from each view's colour gradient.
+ * One view's SH gradient is an outer product per Gaussian, dL/dsh[c] = basis_c(dir) * dL/dRGB with the clamp mask
+ * applied (computeColorFromSH backward, backward.cu:23-142; alt-rasterizer backward.cu:23-146), so ranks exchange the
+ * 3-float dL/dRGB rows (hlgs_grads.drgb) instead of the (D+1)^2 x 3 SH rows, and each rank forms
+ *   dsh[p][c - OFF][ch] = scale * sum_v basis_c(normalize(mean_p - campos_v)) * drgb[v][p][ch]
+ * in view order v = 0..V-1.  View v's campos (3 floats) and drgb (P x 3) start view_stride floats after view v-1's
+ * (an exchange gathers them as one row per rank: [campos, pad | drgb]); means3D: P x 3 (device).  dsh: P x M x 3 holds
+ * coefficients OFF..OFF+M-1 (OFF = 1 for HLGS_VARIANT_ALT, whose coefficient 0 goes to ddc: P x 3; OFF = 0 and ddc
+ * NULL otherwise); coefficients at or above (D+1)^2 are zero. */
+int hlgs_sh_grad_from_colour(int P, int V, int D, int M, int variant, const float* means3D, const float* campos,
+                             const float* drgb, int64_t view_stride, float scale, float* dsh, float* ddc, void* stream);
 
 /* z > 0.2 visibility (auxiliary.h:164-189); present is P bytes (bool) */
 int hlgs_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -179,3 +179,97 @@ def test_view_dp_early_late_split_gloo(tmp_path):
     for k, e in zip([f for f in r0.files if f != "flags"], expect):
         np.testing.assert_array_equal(r0[k], r1[k])
         np.testing.assert_allclose(r0[k], e, rtol=1e-6, atol=1e-7)
+
+
+def _sh_basis_np(dirs, ncoef):
+    """Real SH basis of the reference's colour (utils/sh_utils.py constants, forward.cu:20-67) at unit directions
+    (N, 3), degrees up to 3: (N, ncoef).  Test restatement of what hlgs_sh_grad_from_colour evaluates."""
+    C0, C1 = 0.28209479177387814, 0.4886025119029199
+    C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396]
+    C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+          1.445305721320277, -0.5900435899266435]
+    x, y, z = dirs[:, 0], dirs[:, 1], dirs[:, 2]
+    xx, yy, zz, xy, yz, xz = x * x, y * y, z * z, x * y, y * z, x * z
+    b = [np.full_like(x, C0), -C1 * y, C1 * z, -C1 * x,
+         C2[0] * xy, C2[1] * yz, C2[2] * (2 * zz - xx - yy), C2[3] * xz, C2[4] * (xx - yy),
+         C3[0] * y * (3 * xx - yy), C3[1] * xy * z, C3[2] * y * (4 * zz - xx - yy),
+         C3[3] * z * (2 * zz - 3 * xx - 3 * yy), C3[4] * x * (4 * zz - xx - yy), C3[5] * z * (xx - yy),
+         C3[6] * x * (xx - 3 * yy)]
+    return np.stack(b[:ncoef], 1)
+
+
+def _rank_colour_grads(rank, world):
+    """The rank's dL/dRGB with the SH clamp mask applied (what the factored backward hands the exchange), its camera
+    centre, and the oracle's full gradients of the same view."""
+    from hlgs_core import synthetic as S
+    from oracle import oracle as O
+    cam = S.ring_camera(64, 48, rank, world)
+    sc = S.make_gaussians(300, 1, S.make_camera(64, 48), seed=0)
+    fr = O.forward(sc, S.cam_numpy(cam))
+    g = O.backward(fr, sc, *S.upstream_grads(64, 48, seed=1 + rank))
+    cl = fr.clamped[:, None] >> np.arange(3)[None, :] & 1
+    drgb = np.where((cl == 0) & (fr.radii[:, None] > 0), g["dcolor"], 0.0).astype(np.float32)
+    return drgb, S.cam_numpy(cam)["campos"].astype(np.float32), g
+
+
+def _factor_worker(rank, world, port, out_dir):
+    """Colour-factored exchange plumbing over gloo: the SH leaf leaves the flat buffer, each rank's [campos | dL/dRGB]
+    row is all-gathered and the SH gradient rebuilt from the rows in rank order (the HIP rebuild,
+    hlgs_sh_grad_from_colour, is checked on the GPU by tests/test_gpu_dp.py; here a numpy restatement stands in)."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hierarchical-lod-gaussians_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hlgs_core import dp
+    from hlgs_core.dp import FlatGradExchange, colour_factor
+    drgb, campos, g = _rank_colour_grads(rank, world)
+    grads = [torch.tensor(g[k]) for k in ("dmean3D", "dscale", "drot", "dopacity")]
+    params = [torch.zeros(x.shape, requires_grad=True) for x in grads]
+    means = torch.tensor(_rank_means())
+    shs = torch.zeros(g["dsh"].shape, requires_grad=True)
+
+    def rebuild(cf, V):
+        P = cf.means.shape[0]
+        rows = cf.gathered.numpy()
+        m = cf.means.detach().numpy().astype(np.float64)
+        acc = np.zeros((P, 4, 3))
+        for v in range(V):
+            d = m - rows[v, :3].astype(np.float64)
+            acc += _sh_basis_np(d / np.linalg.norm(d, axis=1, keepdims=True), 4)[:, :, None] * \
+                rows[v, 4:].reshape(P, 1, 3)
+        cf.sh_buf.copy_(torch.tensor(acc / V, dtype=torch.float32))
+    dp.rebuild_sh = rebuild
+
+    ex = FlatGradExchange(params + [shs], colour_factor=dict(means=means, sh=shs))
+    assert all(p is not shs for p in ex.params)  # the SH leaf is not all-reduced
+    fac = colour_factor(shs)
+    fac[0].copy_(torch.tensor(drgb))
+    fac[3](torch.tensor(campos), 1, 0)
+    for p, x in zip(params, grads):
+        p.grad = x.clone()
+    shs.grad = fac[1]  # what autograd does with the view the backward returns
+    ex.allreduce()
+    ok = shs.grad.data_ptr() == ex.cf.sh_buf.data_ptr() and not ex.cf.written
+    ex.close()
+    np.savez(os.path.join(out_dir, f"f{rank}.npz"), *[p.grad.numpy() for p in params], shs.grad.numpy(),
+             flags=np.array([ok]))
+    dist.destroy_process_group()
+
+
+def _rank_means():
+    from hlgs_core import synthetic as S
+    return S.make_gaussians(300, 1, S.make_camera(64, 48), seed=0)["means3D"]
+
+
+def test_view_dp_colour_factored_sh_gloo(tmp_path):
+    world = 2
+    port = _free_port()
+    mp.spawn(_factor_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    r0, r1 = np.load(tmp_path / "f0.npz"), np.load(tmp_path / "f1.npz")
+    assert r0["flags"].all() and r1["flags"].all()
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "hierarchical-lod-gaussians_amd")]
+    g0, g1 = _rank_colour_grads(0, world)[2], _rank_colour_grads(1, world)[2]
+    expect = [(g0[k] + g1[k]) / 2 for k in ("dmean3D", "dscale", "drot", "dopacity", "dsh")]
+    files = [f for f in r0.files if f != "flags"]
+    for k, e in zip(files, expect):
+        np.testing.assert_array_equal(r0[k], r1[k])
+        np.testing.assert_allclose(r0[k], e, rtol=1e-5, atol=1e-7)

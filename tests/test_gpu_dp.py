@@ -146,3 +146,83 @@ def test_overlap_two_renders_of_the_same_leaves_in_one_backward():
                 assert torch.equal(a, b)
     finally:
         ex.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alt", [False, True])
+def test_colour_factored_sh_exchange(alt):
+    """Colour-factored exchange (FlatGradExchange(colour_factor=...)): the backward hands the exchange dL/dRGB instead of
+    the SH gradient and the exchange rebuilds it (hlgs_sh_grad_from_colour).  One view: every gradient bitwise the plain
+    backward's.  Two views' rows rebuilt together: the average of the two views' SH (and dc) gradients."""
+    import ctypes as C
+    from hlgs_core import _lib as L
+    from hlgs_core.dp import FlatGradExchange
+    W, H = 160, 96
+    cams = [S.make_camera(W, H), S.make_camera(W, H, T=np.array([0.3, -0.1, 0.2]))]
+    sc = S.make_gaussians(6000, 3, cams[0], seed=7)
+    g, gd = S.upstream_grads(W, H, seed=8)
+    t = lambda a: torch.tensor(np.ascontiguousarray(a), device="cuda", requires_grad=True)  # noqa: E731
+    gc, gi = torch.tensor(g, device="cuda"), torch.tensor(gd, device="cuda")
+    if alt:
+        from alt_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+        params = [t(sc["means3D"]), t(sc["scales"]), t(sc["rotations"]), t(sc["opacities"]), t(sc["shs"][:, :1]),
+                  t(sc["shs"][:, 1:])]
+
+        def rast(cam):
+            return GaussianRasterizer(GaussianRasterizationSettings(
+                image_height=H, image_width=W, tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
+                bg=torch.zeros(3, device="cuda"), scale_modifier=1.0, viewmatrix=cam["viewmatrix"].cuda(),
+                projmatrix=cam["projmatrix"].cuda(), sh_degree=3, campos=cam["campos"].cuda(), prefiltered=False,
+                debug=False, antialiasing=True))
+        factor = dict(means=params[0], sh=params[5], dc=params[4])
+    else:
+        from diff_gaussian_rasterization import GaussianRasterizer
+        params = [t(sc["means3D"]), t(sc["scales"]), t(sc["rotations"]), t(sc["opacities"]), t(sc["shs"])]
+
+        def rast(cam):
+            return GaussianRasterizer(settings_for(cam, 3, "cuda", do_depth=True))
+        factor = dict(means=params[0], sh=params[4])
+
+    def backward(cam):
+        for p in params:
+            p.grad = None
+        if alt:
+            m, s, r, o, dc, sh = params
+            color, _, inv = rast(cam)(means3D=m, means2D=torch.zeros_like(m, requires_grad=True), opacities=o, dc=dc,
+                                      shs=sh, scales=s, rotations=r)
+        else:
+            m, s, r, o, sh = params
+            color, _, inv = rast(cam)(means3D=m, means2D=torch.zeros_like(m, requires_grad=True), opacities=o, shs=sh,
+                                      scales=s, rotations=r)
+        torch.autograd.backward([color, inv], [gc, gi])
+
+    plain = []
+    for cam in cams:
+        backward(cam)
+        plain.append([p.grad.clone() for p in params])
+    ex = FlatGradExchange(params, colour_factor=factor)
+    rows = []
+    try:
+        for cam, ref in zip(cams, plain):
+            backward(cam)
+            assert ex.cf.written, "the backward did not take the colour-factored path"
+            rows.append(ex.cf.mine.clone())
+            ex.allreduce()  # one rank: the rebuild from this view's row alone
+            for a, p in zip(ref, params):
+                assert torch.equal(a, p.grad)
+    finally:
+        ex.close()
+    # two views rebuilt together, averaged, against the mean of the two views' plain gradients
+    P = params[0].shape[0]
+    rows = torch.stack(rows).contiguous()
+    sh_p = params[5] if alt else params[4]
+    dsh = torch.empty_like(sh_p)
+    ddc = torch.empty_like(params[4]) if alt else None
+    lib = L.load()
+    L.check(lib.hlgs_sh_grad_from_colour(P, 2, 3, sh_p.shape[1], L.VARIANT_ALT if alt else L.VARIANT_HIERARCHY,
+                                         L.ptr(params[0].detach()), rows.data_ptr(), rows.data_ptr() + 16,
+                                         rows.shape[1], 0.5, L.ptr(dsh), L.ptr(ddc) if alt else None, L.stream()))
+    i_sh = 5 if alt else 4
+    torch.testing.assert_close(dsh, 0.5 * (plain[0][i_sh] + plain[1][i_sh]), rtol=1e-6, atol=1e-7)
+    if alt:
+        torch.testing.assert_close(ddc, 0.5 * (plain[0][4] + plain[1][4]), rtol=1e-6, atol=1e-7)
