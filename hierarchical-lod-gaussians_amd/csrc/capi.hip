@@ -97,6 +97,7 @@ Geom carve_geom(void* base, int P, size_t* total)
     g.point_offsets = take<uint32_t>(p, P);
     g.rects = take<int2>(p, P);
     g.splat = take<float4>(p, 4 * (size_t)P);
+    g.sh_jac = take<float>(p, 9 * (size_t)P);
     g.scan_tmp = take<uint32_t>(p, scan_scratch_elems(P));
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return g;

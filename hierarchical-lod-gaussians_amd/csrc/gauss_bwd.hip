@@ -368,10 +368,14 @@ __device__ __forceinline__ float sh_basis(int c, float x, float y, float z, floa
 // parent-deferred share (backward.cu:458-494).
 // ALT (alt-rasterizer backward.cu:23-146): coefficient 0 is the separate dc row (gradient to ddc), and the
 // staged rows hold the M higher-order coefficients 1..M.
-template <bool HIER, int MT, bool ALT>  // MT = 0: staged row count a.M known only at run time (up to 16)
+// JAC: the forward left d colour / d view direction in Geom::sh_jac (sh_jac_written), so no SH row is read: the view
+// direction term is dot(dRGBd{x,y,z}, dL/dRGB) in the reference's order (backward.cu:139-141) and the dsh rows are
+// basis x dL/dRGB, built in LDS and stored as contiguous float4 runs.
+template <bool HIER, int MT, bool ALT, bool JAC>  // MT = 0: staged row count a.M known only at run time (up to 16)
 __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
                                                BwdScratch rec, hlgs_grads o)
 {
+    static_assert(!(JAC && HIER), "the hierarchy-mode preprocess leaves no Jacobian");
     constexpr int OFF = ALT ? 1 : 0;  // full coefficient index of staged row 0
     constexpr int MC = MT ? MT : (16 - OFF);
     const int M = MT ? MT : a.M;
@@ -389,16 +393,27 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
     s_idx[lane] = idx;
     s_vis[lane] = vis;
     // the visible Gaussian's own inputs, issued before the row copy so both latencies overlap
-    f3 m = mk(0.f, 0.f, 0.f), dcol = mk(0.f, 0.f, 0.f);
+    f3 m = mk(0.f, 0.f, 0.f), dcol = mk(0.f, 0.f, 0.f), jx = m, jy = m, jz = m;
     uint32_t cl = 0;
     if (vis) {
         m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
         dcol = mk(o.dcolor[3 * idx], o.dcolor[3 * idx + 1], o.dcolor[3 * idx + 2]);
         cl = g.clamped[t_idx];
+        if (JAC) {
+            const float* J = g.sh_jac + 9 * (size_t)t_idx;
+            jx = mk(J[0], J[1], J[2]);
+            jy = mk(J[3], J[4], J[5]);
+            jz = mk(J[6], J[7], J[8]);
+        }
     }
-    __syncthreads();
-    // rows of invisible Gaussians are not read: they arrive as zeros, which is their dsh row
-    sh_rows_load<3 * MT>(a.shs, s_rows, s_idx, n, lane, M3, s_vis);
+    if (JAC) {  // invisible rows are zero
+        if (!vis)
+            for (int c = 0; c < M3; c++) s_rows[lane * kShStride + c] = 0.f;
+    } else {
+        __syncthreads();
+        // rows of invisible Gaussians are not read: they arrive as zeros, which is their dsh row
+        sh_rows_load<3 * MT>(a.shs, s_rows, s_idx, n, lane, M3, s_vis);
+    }
     // colour-factored mode (o.drgb, view-data-parallel exchange): the masked dL/dRGB row replaces dsh / ddc
     const bool factored = o.drgb != nullptr;  // uniform
     __syncthreads();
@@ -426,13 +441,19 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
             for (int c = 0; c < MC + OFF; c++) {
                 float gx, gy, gz;
                 basis[c] = c < ncoef ? sh_basis(c, x, y, z, gx, gy, gz) : 0.f;
-                if (c > 0 && c < ncoef) {
+                if (!JAC && c > 0 && c < ncoef) {
                     const float* sc = row + 3 * (c - OFF);
                     const float proj = sc[0] * dR + sc[1] * dG + sc[2] * dB;
                     vx += proj * gx;
                     vy += proj * gy;
                     vz += proj * gz;
                 }
+            }
+            if (JAC) {
+                const f3 d = mk(dR, dG, dB);
+                vx = dot(jx, d);
+                vy = dot(jy, d);
+                vz = dot(jz, d);
             }
             if (factored) {
                 o.drgb[3 * idx] = dropped ? 0.f : dR;
@@ -581,7 +602,12 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
             hipStreamWaitEvent(late, ev, 0);
         }
     };
-#define HLGS_SHK(H, MT, AL) hipLaunchKernelGGL((k_sh_bwd<H, MT, AL>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o)
+    const bool jac = sh_jac_written(a);  // the forward's preprocess left d colour / d direction (no SH row reads)
+#define HLGS_SHK(H, MT, AL)                                                                                \
+    do {                                                                                                   \
+        if (!(H) && jac) hipLaunchKernelGGL((k_sh_bwd<false, MT, AL, true>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o); \
+        else hipLaunchKernelGGL((k_sh_bwd<H, MT, AL, false>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o); \
+    } while (0)
 #define HLGS_SHB(H)                                                                                        \
     switch (a.M) {                                                                                         \
     case 1: HLGS_SHK(H, 1, false); break;                                                                  \

@@ -50,6 +50,8 @@ struct Geom {
     uint32_t* point_offsets;  // P, inclusive scan of tiles_touched
     int2* rects;              // P, per-axis 3-sigma extent in pixels
     float4* splat;            // P x 4: the blend kernels' per-Gaussian record (see SplatRec)
+    float* sh_jac;            // P x 9: d colour / d view direction (dRGBdx, dRGBdy, dRGBdz), written by k_preprocess_sh
+                              // for the visible Gaussians when sh_jac_written(); the SH backward then reads no SH rows
     uint32_t* scan_tmp;
 };
 
@@ -61,6 +63,18 @@ struct Geom {
 // All written by the preprocess.  The Gaussian's record-slot base (the exclusive scan of the rect sizes) is read by
 // the blend backward from point_offsets[idx - 1]: writing it into the record after the scan cost the key scatter a
 // partial-line write per visible Gaussian.
+// lds_binning(P, gx, gy): the LDS-histogram binning plan applies (raster_fwd.hip)
+bool lds_binning(int P, int gx, int gy);
+// Does the forward's preprocess (k_preprocess_sh) leave Geom::sh_jac for the SH backward?  Same condition as its launch.
+#ifndef HLGS_SH_JAC
+#define HLGS_SH_JAC 1  // 0: no Jacobian; the SH backward reads the SH rows again (A/B)
+#endif
+inline bool sh_jac_written(const hlgs_raster_args& a)
+{
+    if (!HLGS_SH_JAC) return false;
+    const int gx = (a.W + 15) / 16, gy = (a.H + 15) / 16;
+    return !a.indices && !a.colors_precomp && a.shs && a.M > 0 && a.M <= 16 && lds_binning(a.P, gx, gy);
+}
 Geom carve_geom(void* base, int P, size_t* total);
 
 // Per-pixel / per-tile state (ImageState, rasterizer_impl.h:47-54) plus binning counters.

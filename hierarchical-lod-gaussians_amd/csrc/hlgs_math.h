@@ -116,6 +116,49 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, SHLoad shv, f3 pos, f3 campos, 
     return mk(fmaxf(res.x, 0.0f), fmaxf(res.y, 0.0f), fmaxf(res.z, 0.0f));
 }
 
+// d colour / d (normalised) view direction of the SH colour: the reference's dRGBdx, dRGBdy, dRGBdz
+// (backward.cu:55-139), in its operation order (glm scalar * vec3 products left to right), from the coefficients the
+// forward already holds; the SH backward dots them with dL/dRGB.  `shv(c)` returns coefficient c as (r, g, b).
+template <typename SHLoad>
+__device__ __forceinline__ void sh_dir_jacobian(int deg, SHLoad shv, float x, float y, float z, f3& ddx, f3& ddy, f3& ddz)
+{
+    ddx = ddy = ddz = mk(0.f, 0.f, 0.f);
+    if (deg < 1) return;
+    ddx = scl(-kSH_C1, shv(3));
+    ddy = scl(-kSH_C1, shv(1));
+    ddz = scl(kSH_C1, shv(2));
+    if (deg < 2) return;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    ddx = add(ddx, add(add(add(scl(kSH_C2[0] * y, shv(4)), scl(kSH_C2[2] * 2.f * -x, shv(6))), scl(kSH_C2[3] * z, shv(7))),
+                       scl(kSH_C2[4] * 2.f * x, shv(8))));
+    ddy = add(ddy, add(add(add(scl(kSH_C2[0] * x, shv(4)), scl(kSH_C2[1] * z, shv(5))), scl(kSH_C2[2] * 2.f * -y, shv(6))),
+                       scl(kSH_C2[4] * 2.f * -y, shv(8))));
+    ddz = add(ddz, add(add(scl(kSH_C2[1] * y, shv(5)), scl(kSH_C2[2] * 2.f * 2.f * z, shv(6))), scl(kSH_C2[3] * x, shv(7))));
+    if (deg < 3) return;
+    f3 sx = scl(2.f * xy, scl(3.f, scl(kSH_C3[0], shv(9))));
+    sx = add(sx, scl(yz, scl(kSH_C3[1], shv(10))));
+    sx = add(sx, scl(xy, scl(-2.f, scl(kSH_C3[2], shv(11)))));
+    sx = add(sx, scl(2.f * xz, scl(-3.f, scl(kSH_C3[3], shv(12)))));
+    sx = add(sx, scl(-3.f * xx + 4.f * zz - yy, scl(kSH_C3[4], shv(13))));
+    sx = add(sx, scl(xz, scl(2.f, scl(kSH_C3[5], shv(14)))));
+    sx = add(sx, scl(xx - yy, scl(3.f, scl(kSH_C3[6], shv(15)))));
+    ddx = add(ddx, sx);
+    f3 sy = scl(xx - yy, scl(3.f, scl(kSH_C3[0], shv(9))));
+    sy = add(sy, scl(xz, scl(kSH_C3[1], shv(10))));
+    sy = add(sy, scl(-3.f * yy + 4.f * zz - xx, scl(kSH_C3[2], shv(11))));
+    sy = add(sy, scl(2.f * yz, scl(-3.f, scl(kSH_C3[3], shv(12)))));
+    sy = add(sy, scl(xy, scl(-2.f, scl(kSH_C3[4], shv(13)))));
+    sy = add(sy, scl(yz, scl(-2.f, scl(kSH_C3[5], shv(14)))));
+    sy = add(sy, scl(2.f * xy, scl(-3.f, scl(kSH_C3[6], shv(15)))));
+    ddy = add(ddy, sy);
+    f3 sz = scl(xy, scl(kSH_C3[1], shv(10)));
+    sz = add(sz, scl(2.f * yz, scl(4.f, scl(kSH_C3[2], shv(11)))));
+    sz = add(sz, scl(2.f * zz - xx - yy, scl(3.f, scl(kSH_C3[3], shv(12)))));
+    sz = add(sz, scl(2.f * xz, scl(4.f, scl(kSH_C3[4], shv(13)))));
+    sz = add(sz, scl(xx - yy, scl(kSH_C3[5], shv(14))));
+    ddz = add(ddz, sz);
+}
+
 __device__ __forceinline__ m3 quat_rot(const float q[4])
 {
     float r = q[0], x = q[1], y = q[2], z = q[3];

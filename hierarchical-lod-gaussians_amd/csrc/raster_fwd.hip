@@ -275,15 +275,21 @@ __global__ void __launch_bounds__(64) k_preprocess_sh(hlgs_raster_args a, Geom g
     const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
     const f3 mean_r = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
     uint32_t cb = 0;
-    f3 col;
-    if (ALT) {
-        const float* d0 = a.dc + 3 * (size_t)t_idx;
-        col = sh_to_rgb(a.D, [&](int c) {
-            return c == 0 ? mk(d0[0], d0[1], d0[2]) : mk(row[3 * c - 3], row[3 * c - 2], row[3 * c - 1]);
-        }, mean_r, campos, cb);
-    } else {
-        col = sh_to_rgb(a.D, [&](int c) { return mk(row[3 * c], row[3 * c + 1], row[3 * c + 2]); }, mean_r, campos,
-                        cb);
+    const float* d0 = ALT ? a.dc + 3 * (size_t)t_idx : nullptr;
+    auto shv = [&](int c) {
+        if (ALT) return c == 0 ? mk(d0[0], d0[1], d0[2]) : mk(row[3 * c - 3], row[3 * c - 2], row[3 * c - 1]);
+        return mk(row[3 * c], row[3 * c + 1], row[3 * c + 2]);
+    };
+    const f3 col = sh_to_rgb(a.D, shv, mean_r, campos, cb);
+    if (HLGS_SH_JAC) {  // d colour / d view direction for the SH backward (Geom::sh_jac), from the coefficients in LDS
+        const f3 d = sub(mean_r, campos);
+        const float len = sqrtf(dot(d, d));
+        f3 jx, jy, jz;
+        sh_dir_jacobian(a.D, shv, d.x / len, d.y / len, d.z / len, jx, jy, jz);
+        float* J = g.sh_jac + 9 * (size_t)t_idx;
+        J[0] = jx.x; J[1] = jx.y; J[2] = jx.z;
+        J[3] = jy.x; J[4] = jy.y; J[5] = jy.z;
+        J[6] = jz.x; J[7] = jz.y; J[8] = jz.z;
     }
     g.clamped[t_idx] = cb;
     g.depths[t_idx] = o.depth;
