@@ -22,8 +22,9 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
 void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s);
 void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, hipStream_t s);
 bool lds_binning(int P, int gx, int gy);
+uint32_t* bin_histogram(const Img& im, int P, int gx, int gy);
 void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
-                        hipStream_t s);
+                        hipStream_t s, uint32_t* hist);
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
                     int gy, uint32_t max_count, hipStream_t s, bool timing, Guard gd);
 void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, int gx, int gy,
@@ -302,7 +303,7 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
         launch_preprocess(*a, g, radii, nullptr, gx, gy, ZeroJob{im.tile_count, T, seen, a->P}, s);
         stage_mark(s, ST_PRE, false);
         stage_mark(s, ST_COUNT_TILES, true);
-        launch_count_tiles(a->P, radii, g, im.tile_count, gx, gy, alt, s);
+        launch_count_tiles(a->P, radii, g, im.tile_count, gx, gy, alt, s, bin_histogram(im, a->P, gx, gy));
         stage_mark(s, ST_COUNT_TILES, false);
         if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
         stage_mark(s, ST_SCAN, true);

@@ -427,10 +427,13 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
     }
 }
 
+// hist != nullptr (bin_histogram): the block's per-tile counts are stored as row blockIdx.x of hist (coalesced), and
+// k_tile_offsets turns the rows into per-(block, tile) offsets and tile totals; otherwise they are added to
+// tile_count with one device atomic per non-empty tile.
 template <int BG>
 __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
                                                              uint32_t* __restrict__ tile_count, int gx, int gy, int alt,
-                                                             uint32_t* __restrict__ block_tot)
+                                                             uint32_t* __restrict__ block_tot, uint32_t* __restrict__ hist)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_pre[BG + 1];
@@ -443,20 +446,82 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[BG];
     for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
     __syncthreads();
+    if (hist) {
+        uint32_t* row = hist + (size_t)blockIdx.x * T;
+        for (int t = threadIdx.x; t < T; t += (BG / 4)) row[t] = s_hist[t];
+        return;
+    }
     for (int t = threadIdx.x; t < T; t += (BG / 4)) {
         const uint32_t c = s_hist[t];
         if (c) atomicAdd(&tile_count[t], c);
     }
 }
 
+// The count blocks' histogram rows (nb x T) -> in place, each block's exclusive offset inside every tile's segment (the
+// blocks in order), and tile_count[t] = the tile's total.  32 tiles per workgroup (128-byte row segments), 32 row
+// groups of 32 threads; each thread takes a contiguous run of blocks down its tile's column, issues all of a run's
+// loads before adding (up to 8 held in registers, so the offsets are written without a second read), and the 32 run
+// totals of a tile are scanned in LDS.  With it the binning has no device atomics and a tile's segment holds the
+// blocks' runs in block order.
+__global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hist, int nb, int T,
+                                                       uint32_t* __restrict__ tile_count)
+{
+    __shared__ uint32_t s_part[32][33];
+    const int c = threadIdx.x & 31, r = threadIdx.x >> 5;
+    const int t = blockIdx.x * 32 + c;
+    const int run = (nb + 31) / 32, b0 = r * run, b1 = min(nb, b0 + run);
+    constexpr int K = 8;
+    uint32_t v[K];
+    uint32_t sum = 0;
+    if (t < T) {
+        if (run <= K) {
+#pragma unroll
+            for (int k = 0; k < K; k++) v[k] = b0 + k < b1 ? hist[(size_t)(b0 + k) * T + t] : 0u;
+#pragma unroll
+            for (int k = 0; k < K; k++) sum += v[k];
+        } else {
+            for (int b = b0; b < b1; b++) sum += hist[(size_t)b * T + t];
+        }
+    }
+    s_part[r][c] = sum;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        const uint32_t x = s_part[i][c];
+        if (i < r) off += x;
+        tot += x;
+    }
+    if (t >= T) return;
+    if (run <= K) {
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            if (b0 + k < b1) {
+                hist[(size_t)(b0 + k) * T + t] = off;
+                off += v[k];
+            }
+    } else {
+        for (int b = b0; b < b1; b++) {
+            uint32_t* h = hist + (size_t)b * T + t;
+            const uint32_t x = *h;
+            *h = off;
+            off += x;
+        }
+    }
+    if (r == 0) tile_count[t] = tot;
+}
+
 // Same block -> Gaussian mapping as k_count_tiles: reserve the block's run inside every tile segment
 // with one returning atomic per bin, then hand out slots from LDS.  Slot order inside a tile is
 // irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
+// hist != nullptr: the block's base inside each tile segment is ranges[t].x + its k_tile_offsets offset, so the block
+// walks its instances once (no count walk, no returning device atomics).
 template <int BG>
 __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
                                                                   uint64_t* __restrict__ keys, int gx, int gy, int alt,
-                                                                  Guard gd, const uint32_t* __restrict__ block_base)
+                                                                  Guard gd, const uint32_t* __restrict__ block_base,
+                                                                  const uint32_t* __restrict__ hist)
 {
     if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
@@ -477,11 +542,16 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
             g.point_offsets[idx] = base + s_pre[k + 1];
         }
     }
-    for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
-    __syncthreads();
-    for (int t = threadIdx.x; t < T; t += (BG / 4)) {
-        const uint32_t c = s_cnt[t];
-        s_cnt[t] = c ? ranges[t].x + atomicAdd(&cursor[t], c) : 0u;
+    if (hist) {
+        const uint32_t* row = hist + (size_t)blockIdx.x * T;
+        for (int t = threadIdx.x; t < T; t += (BG / 4)) s_cnt[t] = ranges[t].x + row[t];
+    } else {
+        for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
+        __syncthreads();
+        for (int t = threadIdx.x; t < T; t += (BG / 4)) {
+            const uint32_t c = s_cnt[t];
+            s_cnt[t] = c ? ranges[t].x + atomicAdd(&cursor[t], c) : 0u;
+        }
     }
     __syncthreads();
     for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int tile) {
@@ -771,6 +841,15 @@ struct FwdArgs {
 // set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
 // visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
 // ------------------------------------------------------------------------------------------------
+#ifndef HLGS_BIN_HIST
+#define HLGS_BIN_HIST 1  // atomic-free binning through stored per-block histograms (0: device atomics)
+#endif
+#ifndef HLGS_FWD_PREFETCH_ID
+#define HLGS_FWD_PREFETCH_ID 1
+#endif
+#ifndef HLGS_FWD_BITSET
+#define HLGS_FWD_BITSET 1
+#endif
 template <bool INTERP, bool DEPTH, bool SEEN>  // SEEN: A.seen is set (the per-splat mask is only kept then)
 __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 {
@@ -799,6 +878,11 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
     // per-lane predicates are kept as wave masks (the wave is always full): compares are ballots of one v_cmp
     // each, their combinations scalar mask operations, and selects read them back with inverse_ballot
     uint64_t done = __builtin_amdgcn_ballot_w64(!(px < A.W && py < A.H));
+#if HLGS_FWD_PREFETCH_ID
+    // each batch's list entries are loaded one batch ahead, so a batch waits for one dependent load (its records),
+    // not two
+    uint32_t next_id = range.x + lane < range.y ? A.point_list[range.x + lane] : 0u;
+#endif
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if (done == ~0ull) break;
         if (base == next_split && st) {  // wave-uniform; never past kBwdSplits boundaries (bwd_chunk_len)
@@ -812,8 +896,14 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
         const uint32_t pos = base + lane;
         uint32_t my_id = 0;
         bool hit = false;
+#if HLGS_FWD_PREFETCH_ID
+        my_id = next_id;
+        next_id = pos + 64 < range.y ? A.point_list[pos + 64] : 0u;
+#endif
         if (pos < range.y) {
+#if !HLGS_FWD_PREFETCH_ID
             my_id = A.point_list[pos];
+#endif
             const float4* rec = A.splat + 4 * (size_t)my_id;
             const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
@@ -828,8 +918,13 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
         __syncthreads();
         uint64_t seen_mask = 0;
         while (todo) {
+#if HLGS_FWD_BITSET
+            int j;  // find-first-set and clear it: two SALU instead of four
+            asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(j), "+s"(todo));
+#else
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
+#endif
             const float4 xy = s_xy[j];
             const float4 co = s_co[j];
             const float4 c = s_col[j];
@@ -940,18 +1035,34 @@ static void allow_big_lds()
     done = true;
 }
 
+// Scratch for the count blocks' histogram rows: the image buffer's split state (written only later, by the forward
+// blend), when nb x T words fit in it; nullptr -> the device-atomic binning.
+uint32_t* bin_histogram(const Img& im, int P, int gx, int gy)
+{
+#if HLGS_BIN_HIST
+    const size_t T = (size_t)gx * gy, nb = (size_t)(P + bin_gauss(P) - 1) / bin_gauss(P);
+    if (lds_binning(P, gx, gy) && nb * T <= T * kBwdSplits * (size_t)kSplitFloats)
+        return reinterpret_cast<uint32_t*>(im.split_state);
+#endif
+    return nullptr;
+}
+
 void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
-                        hipStream_t s)
+                        hipStream_t s, uint32_t* hist)
 {
     const size_t lds = sizeof(uint32_t) * (size_t)gx * gy;
     allow_big_lds();
     const int bg = bin_gauss(P);
     if (bg == 4096)
         hipLaunchKernelGGL(k_count_tiles<4096>, dim3((P + 4095) / 4096), dim3(1024), lds, s, P, radii, g, tile_count, gx,
-                           gy, (int)alt, g.scan_tmp);
+                           gy, (int)alt, g.scan_tmp, hist);
     else
         hipLaunchKernelGGL(k_count_tiles<2048>, dim3((P + 2047) / 2048), dim3(512), lds, s, P, radii, g, tile_count, gx,
-                           gy, (int)alt, g.scan_tmp);
+                           gy, (int)alt, g.scan_tmp, hist);
+    if (hist) {
+        const int T = gx * gy, nb = (P + bin_gauss(P) - 1) / bin_gauss(P);
+        hipLaunchKernelGGL(k_tile_offsets, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, tile_count);
+    }
 }
 
 void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, hipStream_t s)
@@ -1016,11 +1127,11 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
         if (bin_gauss(a.P) == 4096)
             hipLaunchKernelGGL(k_scatter_keys_lds<4096>, dim3((a.P + 4095) / 4096), dim3(1024),
                                2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys,
-                               gx, gy, alt, gd, g.scan_tmp);
+                               gx, gy, alt, gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy));
         else
             hipLaunchKernelGGL(k_scatter_keys_lds<2048>, dim3((a.P + 2047) / 2048), dim3(512),
                                2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys,
-                               gx, gy, alt, gd, g.scan_tmp);
+                               gx, gy, alt, gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy));
     } else
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
                            im.tile_cursor, b.keys, gx, gy, alt, gd);
