@@ -69,53 +69,82 @@ __device__ __forceinline__ float rcp_one_minus(float alpha)
 // q = (-a/2, -b, -c/2) * log2(e) so that G = exp2(q0 dx^2 + q1 dx dy + q2 dy^2) = exp(power).
 // ALT: the alt rasterizer's backward (alt-rasterizer/cuda_rasterizer/backward.cu:596-624) has no
 // o * G > 0.99 => dL/dalpha = 0 rule; its doubled background term is folded into ARD by the caller.
-template <bool INTERP, bool DEPTH, bool ALT>
-__device__ __forceinline__ uint64_t bwd_pair(PixB& p, uint32_t li, float dx, float dy, const float4& q, const float4& col,
-                                             float invz, float tt, float fr, float thr, float (&acc)[10])
+//
+// The pair step in two halves.  The front (falloff, alpha, 1/(1 - alpha), the threshold tests) depends on the pair
+// alone; the back (transmittance, ARD and the moments) on the pixel's replay state.
+struct BwdFront {
+    float G, alpha, r1m, my_alpha, dx, dy;
+    uint64_t ok;  // wave mask: alpha >= 1/255 (alpha_e2_threshold)
+};
+
+template <bool INTERP, bool ALT>
+__device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& q, float tt, float fr, float thr)
 {
+    BwdFront f;
+    f.dx = dx;
+    f.dy = dy;
     const float e2 = splat_e2(q, dx, dy);  // power * log2(e)
-    // The falloff, alpha and 1/(1 - alpha) are computed for every lane ahead of the validity branch (HLGS_BWD_HOIST):
-    // they depend on the pair alone, so their transcendental latency overlaps the compare -> SALU -> exec chain that
-    // decides the branch instead of following it.
     float G = __builtin_amdgcn_exp2f(e2);
     const float test_alpha = q.w * G;
-    const float my_alpha = fminf(0.99f, test_alpha);
-    float alpha = my_alpha;
-    if (INTERP) alpha = tt * my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - my_alpha, fr));
-    float r1m = rcp_one_minus(alpha);
+    f.my_alpha = fminf(0.99f, test_alpha);
+    f.alpha = f.my_alpha;
+    if (INTERP) f.alpha = tt * f.my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - f.my_alpha, fr));
+    f.r1m = rcp_one_minus(f.alpha);
     if (!ALT) G *= below_clamp(test_alpha);
-#if HLGS_BWD_HOIST
-    asm volatile("" : "+v"(G), "+v"(r1m), "+v"(alpha));  // keep them above the branch
-#endif
-    // alpha >= 1/255 (alpha_e2_threshold), as a wave mask: one v_cmp per test, combined in SALU (the wave is full)
-    const uint64_t valid = __builtin_amdgcn_ballot_w64(li < p.last) & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) &
-                           ~__builtin_amdgcn_ballot_w64(e2 < thr);
+    f.G = G;
+    // as wave masks: one v_cmp per test, combined in SALU (the wave is full)
+    f.ok = ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < thr);
+    return f;
+}
+
+template <bool INTERP, bool DEPTH>
+__device__ __forceinline__ void bwd_back(PixB& p, uint32_t li, const BwdFront& f, const float4& col, float invz, float tt,
+                                         float fr, float (&acc)[10])
+{
+    const uint64_t valid = __builtin_amdgcn_ballot_w64(li < p.last) & f.ok;
     if (__builtin_amdgcn_inverse_ballot_w64(valid)) {
-        p.T = p.T * r1m;
+        const float alpha = f.alpha, dx = f.dx, dy = f.dy;
+        p.T = p.T * f.r1m;
         const float weight = alpha * p.T;
+        // <colour, dL/dpixel> stays uncontracted: it feeds dL/dalpha and through it the ill-conditioned conic ->
+        // scale / rotation chain, where contracting it moved the GPU further from the oracle than the oracle's own
+        // contracted build is (tests/test_gpu_configs.py).  The colour / depth moments feed only dL/dcolour and
+        // dL/ddepth and are contracted (four VALU fewer per pass).
         float cd = col.x * p.dr + col.y * p.dg + col.z * p.db;
         if (DEPTH) cd += invz * p.dinv;
         const float raw = cd - p.ARD;
         p.ARD = fmaf(alpha, raw, p.ARD);
-        acc[6] += weight * p.dr;
-        acc[7] += weight * p.dg;
-        acc[8] += weight * p.db;
-        if (DEPTH) acc[9] += weight * p.dinv;
+        acc[6] = fmaf(weight, p.dr, acc[6]);
+        acc[7] = fmaf(weight, p.dg, acc[7]);
+        acc[8] = fmaf(weight, p.db, acc[8]);
+        if (DEPTH) acc[9] = fmaf(weight, p.dinv, acc[9]);
         const float dL_dalpha = raw * p.T;
-        const float w = G * dL_dalpha;
+        const float w = f.G * dL_dalpha;
         const float wdx = w * dx, wdy = w * dy;
         acc[0] += wdx;
         acc[1] += wdy;
         acc[2] = fmaf(wdx, dx, acc[2]);
         acc[3] = fmaf(wdx, dy, acc[3]);
         acc[4] = fmaf(wdy, dy, acc[4]);
-        if (INTERP) acc[5] += (tt - powf(1.0f - my_alpha, fr - 1.0f) * (tt - 1.0f) * fr) * w;
+        if (INTERP) acc[5] += (tt - powf(1.0f - f.my_alpha, fr - 1.0f) * (tt - 1.0f) * fr) * w;
         else acc[5] += w;
     }
-    return valid;
 }
 
-// Per-splat record from the reduced moments (see bwd_pair); co = conic and opacity of the splat.
+// One quadrant pass: the front is computed for every lane ahead of the validity branch (HLGS_BWD_HOIST), so its
+// transcendental latency overlaps the compare -> SALU -> exec chain that decides the branch instead of following it.
+template <bool INTERP, bool DEPTH, bool ALT, int K>
+__device__ __forceinline__ void bwd_pass(PixB (&ps)[4], uint32_t li, float lx, float ly, const float4& xy, const float4& q,
+                                         const float4& col, float2 tf, float (&acc)[10])
+{
+    BwdFront f = bwd_front<INTERP, ALT>(xy.x - (lx + 8.f * (K & 1)), xy.y - (ly + 8.f * (K >> 1)), q, tf.x, tf.y, col.w);
+#if HLGS_BWD_HOIST
+    asm volatile("" : "+v"(f.G), "+v"(f.r1m), "+v"(f.alpha));  // keep them above the branch
+#endif
+    bwd_back<INTERP, DEPTH>(ps[K], li, f, col, xy.z, tf.x, tf.y, acc);
+}
+
+// Per-splat record from the reduced moments (see bwd_back); co = conic and opacity of the splat.
 __device__ __forceinline__ void finish_record(const float* m, float4 co, float ddelx_dx, float ddely_dy, float4& ra,
                                               float4& rb, float2& rc)
 {
@@ -152,7 +181,7 @@ struct BwdArgs {
 // lies behind the chunk's end starts from the forward's sample there (transmittance, and what was blended behind
 // it), otherwise from its final state, as the reference's single back-to-front pass has it at that point.  Each
 // 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
-// whose n_contrib lies behind it) run bwd_pair, the ten moments are folded over the wave, and one record per
+// whose n_contrib lies behind it) run bwd_pass, the ten moments are folded over the wave, and one record per
 // (tile, splat) is stored after the batch.
 #ifndef HLGS_BWD_WAVES
 #define HLGS_BWD_WAVES 5  // waves per SIMD: 96 VGPRs
@@ -297,11 +326,11 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                         acc[v] = __uint_as_float((uint32_t)z);
                         acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
                     }
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        if ((qv[k] >> j) & 1u)  // uniform branch
-                            bwd_pair<INTERP, DEPTH, ALT>(ps[k], li, xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)),
-                                                         co, col, xy.z, tf.x, tf.y, col.w, acc);
+                    // uniform branches: the quadrants this splat visits, in quadrant order
+                    if ((qv[0] >> j) & 1u) bwd_pass<INTERP, DEPTH, ALT, 0>(ps, li, lx, ly, xy, co, col, tf, acc);
+                    if ((qv[1] >> j) & 1u) bwd_pass<INTERP, DEPTH, ALT, 1>(ps, li, lx, ly, xy, co, col, tf, acc);
+                    if ((qv[2] >> j) & 1u) bwd_pass<INTERP, DEPTH, ALT, 2>(ps, li, lx, ly, xy, co, col, tf, acc);
+                    if ((qv[3] >> j) & 1u) bwd_pass<INTERP, DEPTH, ALT, 3>(ps, li, lx, ly, xy, co, col, tf, acc);
                     const int jl = jn < 0 ? 0 : jn;  // the next visited splat's LDS reads ahead of the reduction
                     xy = s_xy[jl];
                     co = s_q[jl];
