@@ -99,6 +99,7 @@ Geom carve_geom(void* base, int P, size_t* total)
     g.rects = take<int2>(p, P);
     g.splat = take<float4>(p, 4 * (size_t)P);
     g.sh_jac = take<float>(p, 9 * (size_t)P);
+    g.qmask = take<uint32_t>(p, (size_t)P);
     g.scan_tmp = take<uint32_t>(p, scan_scratch_elems(P));
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return g;
@@ -267,6 +268,8 @@ size_t hlgs_backward_scratch_size(int P, int R)
 }
 
 static void* aligned(const void* p) { return (void*)align_up((size_t)p); }
+
+int hlgs_point_list_entry_shift(int P) { return pack_entries(P) ? kEntryShift : 0; }
 
 size_t hlgs_binning_point_list_offset(int R)
 {

@@ -264,14 +264,108 @@ __device__ __forceinline__ bool foot_touches(const SplatFoot& f, float qx, float
                           fminf(q_edge_v(f, v0, u0, u1), q_edge_v(f, v1, u0, u1)));
     return m <= f.t;
 }
-__device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, float thr, int x0, int y0)
+__device__ __forceinline__ uint32_t quad_mask_foot(const SplatFoot& f, int x0, int y0)
 {
-    const SplatFoot f = splat_foot(x, y, co, thr);
     uint32_t m = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++)
         if (foot_touches(f, (float)(x0 + 8 * (q & 1)), (float)(y0 + 8 * (q >> 1)))) m |= 1u << q;
     return m;
+}
+__device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, float thr, int x0, int y0)
+{
+    return quad_mask_foot(splat_foot(x, y, co, thr), x0, y0);
+}
+// The same footprint test in band form, for the key scatter, which classifies every (Gaussian, tile) instance: per
+// 8-row band of the tile, the exact x-extent of the footprint ellipse Q <= t inside the band (the ellipse's
+// rightmost / leftmost point clamped into the band, where the concave chord ends peak), widened by a tolerance far
+// above the rounding of the hardware square roots and reciprocals used here; an 8x8 block is reached iff that extent
+// overlaps its columns.  det = ac - b^2 is formed with Kahan's compensated product so it does not cancel for
+// elongated splats.  The extents are set up once per tile row of the rect (row_bands), so a tile costs four interval
+// tests instead of sixteen edge minimisations.  tools/cull_check.py checks it against brute force like foot_touches.
+struct SplatBands {
+    float x, y, nb, det, at, ia, vmax, vr, tol;
+    int mode;  // as SplatFoot
+};
+__device__ __forceinline__ SplatBands splat_bands(float x, float y, float4 co, float thr)
+{
+    const SplatFoot f = splat_foot(x, y, co, thr);
+    SplatBands s;
+    s.x = x; s.y = y;
+    s.nb = s.det = s.at = s.ia = s.vmax = s.vr = s.tol = 0.f;
+    s.mode = f.mode;
+    if (f.mode) return s;
+    const float a = co.x, b = co.y, c = co.z, t = f.t;
+    const float bb = b * b, e = fmaf(-b, b, bb);  // e = bb - b^2 exactly
+    const float det = fmaf(a, c, -bb) + e;
+    if (!(det > 0.f)) { s.mode = 1; return s; }
+    const float idet = __builtin_amdgcn_rcpf(det);
+    s.ia = __builtin_amdgcn_rcpf(a);
+    const float vmax = __builtin_amdgcn_sqrtf(a * t * idet);
+    s.nb = -b;
+    s.det = det;
+    s.at = a * t;
+    s.vmax = fmaf(vmax, 1e-4f, vmax) + 1e-3f;
+    s.vr = -b * __builtin_amdgcn_sqrtf(t * idet * __builtin_amdgcn_rcpf(c));
+    s.tol = 2e-3f * (__builtin_amdgcn_sqrtf(s.at) + fabsf(b) * vmax) * s.ia + 2e-3f;
+    return s;
+}
+// The footprint's x-extent [umin, umax] (offsets from the centre) inside the band v in [v0, v0 + 7]; empty: +-3e38.
+__device__ __forceinline__ void band_extent(const SplatBands& s, float v0, float& umin, float& umax)
+{
+    const float lo = fmaxf(v0, -s.vmax), hi = fminf(v0 + 7.f, s.vmax);
+    if (!(lo <= hi)) { umin = 3e38f; umax = -3e38f; return; }  // empty: overlaps no column
+    const float vR = __builtin_amdgcn_fmed3f(s.vr, lo, hi), vL = __builtin_amdgcn_fmed3f(-s.vr, lo, hi);
+    umax = fmaf(s.nb, vR, __builtin_amdgcn_sqrtf(fmaxf(fmaf(-s.det * vR, vR, s.at), 0.f))) * s.ia + s.tol;
+    umin = fmaf(s.nb, vL, -__builtin_amdgcn_sqrtf(fmaxf(fmaf(-s.det * vL, vL, s.at), 0.f))) * s.ia - s.tol;
+}
+// One tile row of a Gaussian's rect: the extents in its two 8-row bands, set up once for every tile of the row.
+struct RowBands {
+    float cx, lo0, hi0, lo1, hi1;
+    int mode;
+};
+__device__ __forceinline__ RowBands row_bands(const SplatBands& s, int ty)
+{
+    RowBands r;
+    r.cx = s.x;
+    r.mode = s.mode;
+    r.lo0 = r.lo1 = 3e38f;
+    r.hi0 = r.hi1 = -3e38f;
+    if (s.mode) return r;
+    const float v0 = (float)(ty * HLGS_TILE) - s.y;
+    band_extent(s, v0, r.lo0, r.hi0);
+    band_extent(s, v0 + 8.f, r.lo1, r.hi1);
+    return r;
+}
+// Quadrant mask of tile column tx in that row: bit q set iff band q >> 1 reaches columns of half q & 1.
+__device__ __forceinline__ uint32_t row_quad_mask(const RowBands& r, int tx)
+{
+    if (r.mode) return r.mode == 1 ? 0xFu : 0u;
+    const float u0 = (float)(tx * HLGS_TILE) - r.cx, u7 = u0 + 7.f, u8 = u0 + 8.f, u15 = u0 + 15.f;
+    return (r.hi0 >= u0 && r.lo0 <= u7 ? 1u : 0u) | (r.hi0 >= u8 && r.lo0 <= u15 ? 2u : 0u) |
+           (r.hi1 >= u0 && r.lo1 <= u7 ? 4u : 0u) | (r.hi1 >= u8 && r.lo1 <= u15 ? 8u : 0u);
+}
+
+// Quadrant masks of the first kRectMasks tiles of a splat's rect (row-major from (x0, y0), width x1 - x0), nibble r for
+// rect tile r: set up by the preprocess, which holds the splat's footprint anyway, and kept in Geom::qmask.
+constexpr int kRectMasks = 8;
+__device__ __forceinline__ uint32_t rect_quad_masks(float x, float y, float4 co, float thr, int x0, int y0, int x1, int y1)
+{
+    const SplatBands s = splat_bands(x, y, co, thr);
+    const int w = x1 - x0, n = min((x1 - x0) * (y1 - y0), kRectMasks);
+    uint32_t m = 0;
+    RowBands row;
+    for (int r = 0; r < n; r++) {
+        const int ty = y0 + r / w, tx = x0 + r % w;
+        if (r == 0 || tx == x0) row = row_bands(s, ty);
+        m |= row_quad_mask(row, tx) << (4 * r);
+    }
+    return m;
+}
+// The quadrant mask of rect tile r from the record's masks; tiles past kRectMasks take every quadrant (conservative).
+__device__ __forceinline__ uint32_t rect_tile_mask(uint32_t masks, uint32_t r)
+{
+    return r < (uint32_t)kRectMasks ? (masks >> (4 * r)) & 0xFu : 0xFu;
 }
 
 // Splat falloff in base 2.  conic_q pre-scales the conic by -log2(e) * (1/2, 1, 1/2); splat_e2 returns

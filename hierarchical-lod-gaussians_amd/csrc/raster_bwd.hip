@@ -173,6 +173,7 @@ struct BwdArgs {
     const float* dL_dpixels;
     const float* dL_dinvdepths;
     BwdScratch rec;
+    int pack;  // point_list entries are packed (pack_entries)
 };
 
 // One wave per (tile, chunk of the tile's list), back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8
@@ -271,12 +272,16 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         float4 my_co = make_float4(0.f, 0.f, 0.f, 0.f);
         if (lane_valid) {
             const uint32_t pos = range.x + li_top - lane;
-            const uint32_t id = point_list[pos];
+            uint32_t id = point_list[pos], pm = 0;
+            if (A.pack) {  // packed entry (pack_entries): the quadrant mask comes with it
+                pm = id & ((1u << kEntryShift) - 1u);
+                id >>= kEntryShift;
+            }
             const float4* sr = g.splat + 4 * (size_t)id;
             const uint32_t sbase = id ? g.point_offsets[id - 1] : 0u;
             const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            qm = quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
+            qm = A.pack ? pm : quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
             s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
             s_q[lane] = conic_q(co);
             my_co = co;
@@ -368,7 +373,7 @@ void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
     const int T = gx * gy;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     BwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, im.final_T, im.n_contrib, im.split_state, a.bg, dL_dpix,
-              dL_dinv, rs};
+              dL_dinv, rs, (int)pack_entries(a.P)};
 #define HLGS_BB(I, Dp, Al) hipLaunchKernelGGL((k_blend_bwd<I, Dp, Al>), dim3((kBwdSplits + 1) * T), dim3(64), 0, s, A)
     if (a.variant == HLGS_VARIANT_ALT) { if (dL_dinv) HLGS_BB(false, true, true); else HLGS_BB(false, false, true); }
     else if (interp) { if (dL_dinv) HLGS_BB(true, true, false); else HLGS_BB(true, false, false); }

@@ -161,8 +161,11 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
         rec[1] = make_float4(conic_z, opacity * h_scale, cr, cg);
         const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
         rec[2] = make_float4(cbl, 1.f / p_view.z, tt, fr);
-        rec[3] = make_float4(0.f, __int_as_float(x0 | (y0 << 16)), __int_as_float(x1 - x0),
-                             alpha_e2_threshold(opacity * h_scale, interp, tt, fr));
+        const float thr = alpha_e2_threshold(opacity * h_scale, interp, tt, fr);
+        if (pack_entries(a.P))
+            g.qmask[t_idx] = rect_quad_masks(pix_x, pix_y, make_float4(conic_x, conic_y, conic_z, opacity * h_scale), thr,
+                                             x0, y0, x1, y1);
+        rec[3] = make_float4(0.f, __int_as_float(x0 | (y0 << 16)), __int_as_float(x1 - x0), thr);
     }
     if (tile_count) {  // only when the tile grid is too large for the LDS-histogram binning
         const float4 co = make_float4(conic_x, conic_y, conic_z, opacity * h_scale);
@@ -303,8 +306,11 @@ __global__ void __launch_bounds__(64) k_preprocess_sh(hlgs_raster_args a, Geom g
     rec[1] = make_float4(o.conic_z, opacity * o.h_scale, col.x, col.y);
     const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
     rec[2] = make_float4(col.z, 1.f / o.depth, tt, fr);
-    rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0),
-                         alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr));
+    const float thr = alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr);
+    if (pack_entries(a.P))
+        g.qmask[t_idx] = rect_quad_masks(o.pix_x, o.pix_y, make_float4(o.conic_x, o.conic_y, o.conic_z, opacity * o.h_scale),
+                                         thr, o.x0, o.y0, o.x1, o.y1);
+    rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -356,33 +362,64 @@ __device__ __forceinline__ void block_rect_prefix(int P, const Geom& g, uint32_t
 // the block's longest rect (s_w[(BG / 4) / 64], zeroed before block_rect_prefix)
 constexpr uint32_t kNarrowRect = 64;
 
-// Calls f(idx, tile) for every binned instance of the block's Gaussians: every tile of the rect, or for the
-// alt rasterizer the tiles alt_tile_keep leaves (rasterizer_impl.cu:147-179 of alt-rasterizer).  The block's
-// instances are numbered Gaussian by Gaussian (s_pre) and each thread takes one contiguous run of them, so a
-// Gaussian whose rect spans thousands of tiles is spread over the whole block instead of serialising one thread.
-template <int BG, typename F>
+// Calls f(idx, x, y, qm, dbits) for every binned instance (Gaussian idx, tile (x, y)) of the block's Gaussians: every
+// tile of the rect, or for the alt rasterizer the tiles alt_tile_keep leaves (rasterizer_impl.cu:147-179 of
+// alt-rasterizer).  KEYS: dbits = the Gaussian's depth bits (the sort key's high word); MASKS: qm = the instance's
+// footprint quadrant mask, from the masks the preprocess left in Geom::qmask (rect_tile_mask); otherwise 0.
+// Without wide rects each thread takes four Gaussians and loads everything they need before its first call, so the
+// key stores issued by f never have to drain for a later load (vmcnt counts loads and stores alike).  With a wide
+// rect the block's instances are numbered Gaussian by Gaussian (s_pre) and each thread takes one contiguous run of
+// them, so a Gaussian whose rect spans thousands of tiles is spread over the whole block instead of serialising one
+// thread.
+template <int BG, bool KEYS, bool MASKS, typename F>
 __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy, bool alt, const uint32_t* s_pre,
                                                   const uint32_t* s_w, F&& f)
 {
     const int g0 = blockIdx.x * BG;
+    struct GIn {
+        float2 xy;
+        int2 ext;
+        float4 co;
+        uint32_t masks, dbits;
+    };
+    auto gauss = [&](int idx, GIn& v) {
+        v.xy = g.means2D[idx];
+        v.ext = g.rects[idx];
+        v.co = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (alt) {
+            const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
+            v.co = make_float4(r0.z, r0.w, r1.x, r1.y);
+        }
+        v.masks = MASKS ? g.qmask[idx] : 0u;
+        v.dbits = KEYS ? __float_as_uint(g.depths[idx]) : 0u;
+    };
+    auto qmask = [&](uint32_t masks, uint32_t r) { return MASKS ? rect_tile_mask(masks, r) : 0u; };
     if (s_w[(BG / 4) / 64] <= kNarrowRect) {  // no wide rect in this block: one thread per Gaussian
-        for (int k = threadIdx.x; k < BG; k += (BG / 4)) {
-            if (s_pre[k + 1] == s_pre[k]) continue;
-            const int idx = g0 + k;
-            const float2 xy = g.means2D[idx];
-            const int2 ext = g.rects[idx];
+        constexpr int J = 4;  // Gaussians per thread
+        GIn in[J];
+        bool live[J];
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            const int k = threadIdx.x + j * (BG / 4);
+            live[j] = s_pre[k + 1] != s_pre[k];
+            if (live[j]) gauss(g0 + k, in[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (!live[j]) continue;
+            const int idx = g0 + threadIdx.x + j * (BG / 4);
+            const GIn& v = in[j];
             int x0, y0, x1, y1;
-            tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
+            tile_rect(v.xy.x, v.xy.y, v.ext.x, v.ext.y, gx, gy, x0, y0, x1, y1);
+            uint32_t r = 0;
             if (alt) {
-                const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
-                const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-                const float thr = alt_keep_threshold(co.w);
+                const float thr = alt_keep_threshold(v.co.w);
                 for (int y = y0; y < y1; y++)
-                    for (int x = x0; x < x1; x++)
-                        if (alt_tile_keep(xy.x, xy.y, co, thr, x, y)) f(idx, y * gx + x);
+                    for (int x = x0; x < x1; x++, r++)
+                        if (alt_tile_keep(v.xy.x, v.xy.y, v.co, thr, x, y)) f(idx, x, y, qmask(v.masks, r), v.dbits);
             } else {
                 for (int y = y0; y < y1; y++)
-                    for (int x = x0; x < x1; x++) f(idx, y * gx + x);
+                    for (int x = x0; x < x1; x++, r++) f(idx, x, y, qmask(v.masks, r), v.dbits);
             }
         }
         return;
@@ -402,25 +439,24 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
         const uint32_t b = s_pre[k], e = s_pre[k + 1];
         if (e == b) continue;
         const int idx = g0 + k;
-        const float2 xy = g.means2D[idx];
-        const int2 ext = g.rects[idx];
+        GIn v;
+        gauss(idx, v);
         int x0, y0, x1, y1;
-        tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
+        tile_rect(v.xy.x, v.xy.y, v.ext.x, v.ext.y, gx, gy, x0, y0, x1, y1);
         const int w = x1 - x0;
         const uint32_t local = i - b;
         int ty = (int)(local / (uint32_t)w), tx = (int)local - ty * w;
         const uint32_t stop = min(iend, e);
         if (alt) {
-            const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
-            const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            const float thr = alt_keep_threshold(co.w);
+            const float thr = alt_keep_threshold(v.co.w);
             for (; i < stop; i++) {
-                if (alt_tile_keep(xy.x, xy.y, co, thr, x0 + tx, y0 + ty)) f(idx, (y0 + ty) * gx + x0 + tx);
+                if (alt_tile_keep(v.xy.x, v.xy.y, v.co, thr, x0 + tx, y0 + ty))
+                    f(idx, x0 + tx, y0 + ty, qmask(v.masks, i - b), v.dbits);
                 if (++tx == w) { tx = 0; ty++; }
             }
         } else {
             for (; i < stop; i++) {
-                f(idx, (y0 + ty) * gx + x0 + tx);
+                f(idx, x0 + tx, y0 + ty, qmask(v.masks, i - b), v.dbits);
                 if (++tx == w) { tx = 0; ty++; }
             }
         }
@@ -444,7 +480,8 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     __syncthreads();
     block_rect_prefix<BG>(P, g, s_pre, s_w);
     if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[BG];
-    for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_hist[tile], 1u); });
+    for_each_instance<BG, false, false>(
+        g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t, uint32_t) { atomicAdd(&s_hist[y * gx + x], 1u); });
     __syncthreads();
     if (hist) {
         uint32_t* row = hist + (size_t)blockIdx.x * T;
@@ -516,7 +553,7 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hi
 // irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
 // hist != nullptr: the block's base inside each tile segment is ranges[t].x + its k_tile_offsets offset, so the block
 // walks its instances once (no count walk, no returning device atomics).
-template <int BG>
+template <int BG, bool PACK>
 __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
                                                                   uint64_t* __restrict__ keys, int gx, int gy, int alt,
@@ -546,7 +583,8 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         const uint32_t* row = hist + (size_t)blockIdx.x * T;
         for (int t = threadIdx.x; t < T; t += (BG / 4)) s_cnt[t] = ranges[t].x + row[t];
     } else {
-        for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int, int tile) { atomicAdd(&s_cnt[tile], 1u); });
+        for_each_instance<BG, false, false>(
+            g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t, uint32_t) { atomicAdd(&s_cnt[y * gx + x], 1u); });
         __syncthreads();
         for (int t = threadIdx.x; t < T; t += (BG / 4)) {
             const uint32_t c = s_cnt[t];
@@ -554,9 +592,11 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         }
     }
     __syncthreads();
-    for_each_instance<BG>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int tile) {
+    for_each_instance<BG, true, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int x, int y, uint32_t qm, uint32_t dbits) {
+        const int tile = y * gx + x;
         const uint32_t r = atomicAdd(&s_rank[tile], 1u);
-        keys[s_cnt[tile] + r] = ((uint64_t)__float_as_uint(g.depths[idx]) << 32) | (uint32_t)idx;
+        const uint32_t entry = PACK ? ((uint32_t)idx << kEntryShift) | qm : (uint32_t)idx;
+        keys[s_cnt[tile] + r] = ((uint64_t)dbits << 32) | entry;
     });
 }
 
@@ -664,7 +704,8 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
 // One thread per Gaussian: drop (depth, index) keys into each touched tile's segment.
 __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restrict__ radii, Geom g,
                                                       const uint2* __restrict__ ranges, uint32_t* cursor,
-                                                      uint64_t* __restrict__ keys, int gx, int gy, int alt, Guard gd)
+                                                      uint64_t* __restrict__ keys, int gx, int gy, int alt, Guard gd,
+                                                      int pack)
 {
     if (guard_fail(gd)) return;
     const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -673,16 +714,19 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
     const int2 ext = g.rects[idx];
     int x0, y0, x1, y1;
     tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
-    const uint64_t key = ((uint64_t)__float_as_uint(g.depths[idx]) << 32) | (uint32_t)idx;
+    const uint64_t dkey = (uint64_t)__float_as_uint(g.depths[idx]) << 32;
     const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
     const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
     const float kthr = alt ? alt_keep_threshold(co.w) : 0.f;
+    const uint32_t masks = pack ? g.qmask[idx] : 0u;
+    uint32_t r = 0;
     for (int y = y0; y < y1; y++)
-        for (int x = x0; x < x1; x++) {
+        for (int x = x0; x < x1; x++, r++) {
             if (alt && !alt_tile_keep(xy.x, xy.y, co, kthr, x, y)) continue;
             const int tile = y * gx + x;
             const uint32_t slot = atomicAdd(&cursor[tile], 1u);
-            keys[ranges[tile].x + slot] = key;
+            keys[ranges[tile].x + slot] =
+                dkey | (pack ? ((uint32_t)idx << kEntryShift) | rect_tile_mask(masks, r) : (uint32_t)idx);
         }
 }
 
@@ -832,6 +876,7 @@ struct FwdArgs {
     float* out_invdepth;
     int* seen;
     float* split_state;  // Img::split_state (null: not sampled)
+    int pack;            // point_list entries are packed (pack_entries)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -899,15 +944,20 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 #if HLGS_FWD_PREFETCH_ID
         my_id = next_id;
         next_id = pos + 64 < range.y ? A.point_list[pos + 64] : 0u;
+#else
+        if (pos < range.y) my_id = A.point_list[pos];
 #endif
-        if (pos < range.y) {
-#if !HLGS_FWD_PREFETCH_ID
-            my_id = A.point_list[pos];
-#endif
+        // packed entries (pack_entries) carry the quadrant mask: only the splats reaching this quadrant are loaded
+        bool stage = pos < range.y;
+        if (A.pack) {
+            stage = stage && ((my_id >> q) & 1u);
+            my_id >>= kEntryShift;
+        }
+        if (stage) {
             const float4* rec = A.splat + 4 * (size_t)my_id;
             const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            hit = touches_quad(r0.x, r0.y, co, r3.w, fqx, fqy);
+            hit = A.pack || touches_quad(r0.x, r0.y, co, r3.w, fqx, fqy);
             s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, r3.w);
             s_co[lane] = conic_q(co);
             // .w: 1/kids in hierarchy mode, otherwise the splat's 1-based position in the tile list (n_contrib value)
@@ -1029,8 +1079,10 @@ static void allow_big_lds()
     const int dyn = 2 * (int)sizeof(uint32_t) * kBinMaxTiles;
     hipFuncSetAttribute((const void*)k_count_tiles<4096>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
     hipFuncSetAttribute((const void*)k_count_tiles<2048>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_scatter_keys_lds<4096>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_scatter_keys_lds<2048>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_scatter_keys_lds<4096, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_scatter_keys_lds<2048, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_scatter_keys_lds<4096, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_scatter_keys_lds<2048, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
     hipGetLastError();
     done = true;
 }
@@ -1124,17 +1176,17 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
     if (timing) stage_mark(s, 3, true);
     if (lds_binning(a.P, gx, gy)) {
         allow_big_lds();
-        if (bin_gauss(a.P) == 4096)
-            hipLaunchKernelGGL(k_scatter_keys_lds<4096>, dim3((a.P + 4095) / 4096), dim3(1024),
-                               2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys,
-                               gx, gy, alt, gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy));
-        else
-            hipLaunchKernelGGL(k_scatter_keys_lds<2048>, dim3((a.P + 2047) / 2048), dim3(512),
-                               2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys,
-                               gx, gy, alt, gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy));
+#define HLGS_SCATTER(BG, PK)                                                                                       \
+    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK>), dim3((a.P + BG - 1) / BG), dim3(BG / 4),                           \
+                       2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy, alt, \
+                       gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy))
+        const bool pk = pack_entries(a.P);
+        if (bin_gauss(a.P) == 4096) { if (pk) HLGS_SCATTER(4096, true); else HLGS_SCATTER(4096, false); }
+        else { if (pk) HLGS_SCATTER(2048, true); else HLGS_SCATTER(2048, false); }
+#undef HLGS_SCATTER
     } else
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
-                           im.tile_cursor, b.keys, gx, gy, alt, gd);
+                           im.tile_cursor, b.keys, gx, gy, alt, gd, (int)pack_entries(a.P));
     if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
     hipLaunchKernelGGL(k_tile_sort_wave, dim3(T), dim3(64), 0, s, im.ranges, b.keys, b.point_list, T, gd);
     if (max_count > (uint32_t)kWaveSortCap)
@@ -1159,7 +1211,7 @@ void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     const bool depth = out_invdepth != nullptr;
     FwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, T, g.splat, im.final_T, im.n_contrib, a.bg, out_color,
-              out_invdepth, seen, im.split_state};
+              out_invdepth, seen, im.split_state, (int)pack_entries(a.P)};
 #define HLGS_BLEND(I, Dp)                                                                                         \
     do {                                                                                                          \
         if (seen) hipLaunchKernelGGL((k_blend_fwd<I, Dp, true>), dim3(4 * T), dim3(64), 0, s, A, gd);           \

@@ -190,9 +190,12 @@ def _field(buf, offset, count, dtype):
     return buf[shift + offset: shift + offset + nbytes].view(dtype)
 
 
-def inspect_point_list(binningBuffer, R):
-    """Sorted per-tile Gaussian ids (tile-major, front to back) held in a forward's binning buffer."""
-    return _field(binningBuffer, L.load().hlgs_binning_point_list_offset(int(R)), int(R), torch.int32)
+def inspect_point_list(binningBuffer, R, P=0):
+    """Sorted per-tile Gaussian ids (tile-major, front to back) held in a forward's binning buffer of a P-Gaussian
+    forward (the stored entries carry a footprint quadrant mask below the id: hlgs_point_list_entry_shift)."""
+    lib = L.load()
+    raw = _field(binningBuffer, lib.hlgs_binning_point_list_offset(int(R)), int(R), torch.int32)
+    return (raw.to(torch.int64) & 0xFFFFFFFF) >> lib.hlgs_point_list_entry_shift(int(P))
 
 
 def inspect_ranges(imageBuffer, W, H):
