@@ -645,28 +645,37 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
     return woff + x - v;
 }
 
-// Scan of n counts by one 1024-thread block, each thread over a contiguous run of up to kPlanRun entries with
-// all its loads issued at once (one block-wide scan of the run totals instead of a loop of them).
+// Scan of n counts by one 1024-thread block, each thread over a contiguous run of up to kPlanRun entries (one
+// block-wide scan of the run totals instead of a loop of them).  plan_load issues a run's loads; both of k_plan's
+// inputs are loaded before either is scanned, so the block waits for one round trip, not two.
 constexpr int kPlanRun = 16;  // 16 x 1024 >= kBinMaxTiles
-template <typename F>
-__device__ __forceinline__ uint32_t plan_scan(const uint32_t* in, int n, uint32_t* s_w, uint32_t& mx, F&& emit)
-{
-    const int run = (n + 1023) / 1024;  // <= kPlanRun (checked by the launcher)
-    const int i0 = (int)threadIdx.x * run;
+struct PlanRun {
     uint32_t v[kPlanRun];
+    int i0, run, n;
+};
+__device__ __forceinline__ void plan_load(const uint32_t* in, int n, PlanRun& r)
+{
+    r.n = n;
+    r.run = (n + 1023) / 1024;  // <= kPlanRun (checked by the launcher)
+    r.i0 = (int)threadIdx.x * r.run;
+#pragma unroll
+    for (int k = 0; k < kPlanRun; k++) r.v[k] = (k < r.run && r.i0 + k < n) ? in[r.i0 + k] : 0u;
+}
+template <typename F>
+__device__ __forceinline__ uint32_t plan_scan(const PlanRun& r, uint32_t* s_w, uint32_t& mx, F&& emit)
+{
     uint32_t sum = 0;
 #pragma unroll
     for (int k = 0; k < kPlanRun; k++) {
-        v[k] = (k < run && i0 + k < n) ? in[i0 + k] : 0u;
-        sum += v[k];
-        mx = max(mx, v[k]);
+        sum += r.v[k];
+        mx = max(mx, r.v[k]);
     }
     uint32_t total;
     uint32_t ex = block_excl_scan(sum, s_w, total);
 #pragma unroll
     for (int k = 0; k < kPlanRun; k++) {
-        if (k < run && i0 + k < n) emit(i0 + k, ex, v[k]);
-        ex += v[k];
+        if (k < r.run && r.i0 + k < r.n) emit(r.i0 + k, ex, r.v[k]);
+        ex += r.v[k];
     }
     return total;
 }
@@ -679,9 +688,12 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_max;
     if (threadIdx.x == 0) s_max = 0;
+    PlanRun rb, rc;
+    plan_load(block_tot, nb, rb);
+    plan_load(count, T, rc);
     uint32_t mx = 0, unused = 0;
-    const uint32_t slots = plan_scan(block_tot, nb, s_w, unused, [&](int i, uint32_t ex, uint32_t) { block_tot[i] = ex; });
-    const uint32_t R = plan_scan(count, T, s_w, mx, [&](int t, uint32_t ex, uint32_t c) {
+    const uint32_t slots = plan_scan(rb, s_w, unused, [&](int i, uint32_t ex, uint32_t) { block_tot[i] = ex; });
+    const uint32_t R = plan_scan(rc, s_w, mx, [&](int t, uint32_t ex, uint32_t c) {
         ranges[t] = make_uint2(ex, ex + c);
         cursor[t] = 0;
     });
