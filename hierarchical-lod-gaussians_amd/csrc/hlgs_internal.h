@@ -21,8 +21,11 @@ constexpr int kBinMaxTiles = 16384; // tile grids up to this use LDS histograms 
 // more, shorter waves than tiles.  A chunk that is not the tile's last starts from the per-pixel state the forward
 // sampled at the chunk's end (Img::split_state): the transmittance there, and the colour and inverse depth blended
 // behind it (final - sampled), which give the back-to-front recursion's accumulators without replaying the back part.
+// Chunks of at least 192 entries (round 3; 128 before): a configs[1] tile (~300 entries) then has one boundary instead
+// of two, which halves the split state the forward writes (its write traffic was 137 MB per view, 83 MB of it split
+// state) at no measured cost (blend pair 538.6-538.9 against 535.2-536.7 us).
 #ifndef HLGS_BWD_CHUNK
-#define HLGS_BWD_CHUNK 128
+#define HLGS_BWD_CHUNK 192
 #endif
 #ifndef HLGS_BWD_SPLITS
 #define HLGS_BWD_SPLITS 2

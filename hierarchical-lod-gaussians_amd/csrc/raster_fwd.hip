@@ -313,6 +313,113 @@ __global__ void __launch_bounds__(64) k_preprocess_sh(hlgs_raster_args a, Geom g
     rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
 }
 
+// The same preprocess with two waves per 64 Gaussians (HLGS_PRE_SPLIT): wave 0 runs the geometry while wave 1 streams
+// the block's 64 SH rows (contiguous in the AoS input, culled rows included) into LDS; after a barrier wave 1
+// evaluates the colour and the direction Jacobian from LDS while wave 0 classifies the footprint quadrants, and
+// after a second barrier wave 0 writes the records.  The SH rows' HBM latency overlaps the geometry instead of
+// following it, and one 12.5 KB LDS stage now keeps two waves busy.  Same arithmetic, same outputs.
+#ifndef HLGS_PRE_SPLIT
+#define HLGS_PRE_SPLIT 1
+#endif
+template <int M3T>
+__device__ __forceinline__ void sh_rows_load_contig(const float* gbase, float* lds, int n, int lane, int m3)
+{
+    if constexpr (M3T > 0 && M3T % 4 == 0) {
+        constexpr int Q = M3T / 4;
+        float4 v[Q];
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const int f = lane + 64 * k;
+            v[k] = f < n * Q ? reinterpret_cast<const float4*>(gbase)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const int f = lane + 64 * k;
+            if (f < n * Q) {
+                const int r = f / Q, q = f - r * Q;
+                float* lp = lds + r * kShStride + 4 * q;
+                lp[0] = v[k].x; lp[1] = v[k].y; lp[2] = v[k].z; lp[3] = v[k].w;
+            }
+        }
+    } else {
+        const int M3 = M3T ? M3T : m3;
+        for (int f = lane; f < n * M3; f += 64) {
+            const int r = f / M3, q = f - r * M3;
+            lds[r * kShStride + q] = gbase[f];
+        }
+    }
+}
+
+template <bool ALT, int M3T>
+__global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
+                                                        int gy, float fx, float fy, ZeroJob z)
+{
+    __shared__ float s_rows[64 * kShStride];
+    __shared__ float4 s_col[64];  // r, g, b, clamp bits
+    __shared__ int s_need[64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t0 = blockIdx.x * 64, t_idx = t0 + lane;
+    const int M3 = 3 * a.M;
+    PreGeom o;
+    bool need = false;
+    if (wave == 0) {
+        zero_prelude(z, t_idx, gridDim.x * 64);
+        need = t_idx < a.P && preprocess_geom<ALT>(a, g, radii, t_idx, gx, gy, fx, fy, o);
+        s_need[lane] = need;
+    } else {
+        sh_rows_load_contig<M3T>(a.shs + (size_t)t0 * M3, s_rows, min(64, a.P - t0), lane, M3);
+    }
+    __syncthreads();
+    const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+    const bool interp = a.ts && a.kids;
+    float thr = 0.f, opacity = 0.f;
+    if (wave == 1) {
+        if (s_need[lane]) {
+            const float* row = s_rows + lane * kShStride;
+            const f3 mean_r = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
+            const float* d0 = ALT ? a.dc + 3 * (size_t)t_idx : nullptr;
+            auto shv = [&](int c) {
+                if (ALT) return c == 0 ? mk(d0[0], d0[1], d0[2]) : mk(row[3 * c - 3], row[3 * c - 2], row[3 * c - 1]);
+                return mk(row[3 * c], row[3 * c + 1], row[3 * c + 2]);
+            };
+            uint32_t cb = 0;
+            const f3 col = sh_to_rgb(a.D, shv, mean_r, campos, cb);
+            s_col[lane] = make_float4(col.x, col.y, col.z, __uint_as_float(cb));
+            if (HLGS_SH_JAC) {
+                const f3 d = sub(mean_r, campos);
+                const float len = sqrtf(dot(d, d));
+                f3 jx, jy, jz;
+                sh_dir_jacobian(a.D, shv, d.x / len, d.y / len, d.z / len, jx, jy, jz);
+                float* J = g.sh_jac + 9 * (size_t)t_idx;
+                J[0] = jx.x; J[1] = jx.y; J[2] = jx.z;
+                J[3] = jy.x; J[4] = jy.y; J[5] = jy.z;
+                J[6] = jz.x; J[7] = jz.y; J[8] = jz.z;
+            }
+        }
+    } else if (need) {
+        opacity = a.opacities[t_idx];
+        const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+        thr = alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr);
+        if (pack_entries(a.P))
+            g.qmask[t_idx] = rect_quad_masks(o.pix_x, o.pix_y, make_float4(o.conic_x, o.conic_y, o.conic_z,
+                                                                           opacity * o.h_scale), thr, o.x0, o.y0, o.x1, o.y1);
+    }
+    __syncthreads();
+    if (wave == 1 || !need) return;
+    const float4 c = s_col[lane];
+    g.clamped[t_idx] = __float_as_uint(c.w);
+    g.depths[t_idx] = o.depth;
+    radii[t_idx] = (int)o.radius;
+    g.means2D[t_idx] = make_float2(o.pix_x, o.pix_y);
+    g.tiles_touched[t_idx] = (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0);
+    const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+    float4* rec = g.splat + 4 * (size_t)t_idx;
+    rec[0] = make_float4(o.pix_x, o.pix_y, o.conic_x, o.conic_y);
+    rec[1] = make_float4(o.conic_z, opacity * o.h_scale, c.x, c.y);
+    rec[2] = make_float4(c.z, 1.f / o.depth, tt, fr);
+    rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Tile binning with block-level LDS histograms.  A block owns BG consecutive Gaussians (bin_gauss); its
 // instances are counted per tile in LDS and each non-empty bin costs one coalesced device atomic,
@@ -1146,7 +1253,13 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
     const bool alt = a.variant == HLGS_VARIANT_ALT;
     if (!a.indices && !a.colors_precomp && a.shs && a.M > 0 && !tile_count && a.M <= 16) {
         const dim3 g64((a.P + 63) / 64);
-#define HLGS_PSH(AL, M3) hipLaunchKernelGGL((k_preprocess_sh<AL, M3>), g64, dim3(64), 0, s, a, g, radii, gx, gy, fx, fy, z)
+#define HLGS_PSH(AL, M3)                                                                                           \
+    do {                                                                                                           \
+        if (HLGS_PRE_SPLIT)                                                                                        \
+            hipLaunchKernelGGL((k_preprocess_sh2<AL, M3>), g64, dim3(128), 0, s, a, g, radii, gx, gy, fx, fy, z);  \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_preprocess_sh<AL, M3>), g64, dim3(64), 0, s, a, g, radii, gx, gy, fx, fy, z);    \
+    } while (0)
         if (alt) {
             switch (a.M) {
             case 3: HLGS_PSH(true, 9); break;
