@@ -20,7 +20,7 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
                        const ZeroJob& z,
                        hipStream_t s);
 void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s);
-void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, hipStream_t s);
+void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, uint32_t seq, hipStream_t s);
 bool lds_binning(int P, int gx, int gy);
 uint32_t* bin_histogram(const Img& im, int P, int gx, int gy);
 void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
@@ -292,7 +292,7 @@ namespace hlgs {
 // binning the preprocess also clears tile_count and `seen`, and one k_plan block does both scans and the ranges and
 // mirrors misc into `host` (pinned, may be null); otherwise the generic path runs device-wide scans.
 static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int* radii, int* seen, uint32_t* host,
-                          hipStream_t s)
+                          uint32_t seq, hipStream_t s)
 {
     const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16, T = gx * gy;
     Geom g = carve_geom(aligned(geom), a->P, nullptr);
@@ -310,7 +310,7 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
         stage_mark(s, ST_COUNT_TILES, false);
         if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
         stage_mark(s, ST_SCAN, true);
-        launch_plan(a->P, g, im, T, host, s);
+        launch_plan(a->P, g, im, T, host, seq, s);
         stage_mark(s, ST_SCAN, false);
         return check_stage(s, a->debug, "scan");
     }
@@ -361,10 +361,25 @@ static int binning_capacity(size_t bytes)
 
 // Pinned read-back slot and event for the speculative forward, per thread and device.
 struct Readback {
-    uint32_t* host = nullptr;
+    uint32_t* host = nullptr;  // [0..2] = R, longest list, record slots; [3] = the frame's sequence number (k_plan)
     hipEvent_t ev = nullptr;
     uint32_t last_maxc = 0;  // longest tile list of the previous frame (plans the speculative sort)
+    uint32_t seq = 0;
 };
+// Wait until k_plan has mirrored the frame's words (host[3] == seq), polling the coherent pinned words rather than
+// synchronising on an event recorded after k_plan: an event is a queue barrier, ~6 us of idle GPU before the binning.
+// A stream that drains or fails without the words reports an error instead of spinning forever.
+static int wait_plan_words(const uint32_t* host, uint32_t seq, hipStream_t s)
+{
+    for (uint32_t n = 1;; n++) {
+        if (__atomic_load_n(&host[3], __ATOMIC_ACQUIRE) == seq) return HLGS_OK;
+        if ((n & 1023u) == 0u && hipStreamQuery(s) != hipErrorNotReady) {
+            if (__atomic_load_n(&host[3], __ATOMIC_ACQUIRE) == seq) return HLGS_OK;
+            return fail(HLGS_ERR_DEVICE, "the binning plan did not report its sizes");
+        }
+        __builtin_ia32_pause();
+    }
+}
 static int readback_for(hipStream_t s, Readback** out)
 {
     static thread_local Readback rb[64];
@@ -391,7 +406,7 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     info->num_binned = 0;
     if (a->P == 0) return HLGS_OK;
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = prepare_launch(a, geom, img, radii, nullptr, nullptr, s))) return rc;
+    if ((rc = prepare_launch(a, geom, img, radii, nullptr, nullptr, 0u, s))) return rc;
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     uint32_t misc[3];
     HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
@@ -438,9 +453,13 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     }
     Readback* rb;
     if ((rc = readback_for(s, &rb))) return rc;
-    if ((rc = prepare_launch(a, geom, img, radii, seen, rb->host, s))) return rc;
+    if (++rb->seq == 0u) rb->seq = 1u;
+    const uint32_t seq = rb->seq;
+    if ((rc = prepare_launch(a, geom, img, radii, seen, rb->host, seq, s))) return rc;
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
-    HLGS_TRY_HIP(hipEventRecord(rb->ev, s));
+    // the LDS-binning plan (k_plan) mirrors its words with the sequence number; the generic path copies them
+    const bool polled = lds_binning(a->P, (a->W + 15) / 16, (a->H + 15) / 16);
+    if (!polled) HLGS_TRY_HIP(hipEventRecord(rb->ev, s));
     // Queue the render before knowing R: it is sized for the caller's buffer and for lists the one-wave and
     // block sorts handle; the kernels exit at once if the frame exceeds either (Guard).
     const int capR = binning ? binning_capacity(binning_bytes) : 0;
@@ -449,7 +468,11 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     if (spec && (rc = render_launch(a, radii, geom, img, binning, capR, cap_n, out_color, out_invdepth, seen, s,
                                     Guard{im.misc, (uint32_t)capR, cap_n})))
         return rc;
-    HLGS_TRY_HIP(hipEventSynchronize(rb->ev));
+    if (polled) {
+        if ((rc = wait_plan_words(rb->host, seq, s))) return rc;
+    } else {
+        HLGS_TRY_HIP(hipEventSynchronize(rb->ev));
+    }
     const uint32_t R = rb->host[0], maxc = rb->host[1];
     rb->last_maxc = maxc;
     info->num_binned = (int)R;

@@ -790,7 +790,7 @@ __device__ __forceinline__ uint32_t plan_scan(const PlanRun& r, uint32_t* s_w, u
 __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot, int nb,
                                                const uint32_t* __restrict__ count, uint32_t* __restrict__ cursor,
                                                uint2* __restrict__ ranges, int T, uint32_t* __restrict__ misc,
-                                               uint32_t* host)
+                                               uint32_t* host, uint32_t seq)
 {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_max;
@@ -811,10 +811,12 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
         misc[0] = R;
         misc[1] = s_max;
         misc[2] = slots;
-        if (host) {
+        if (host) {  // host[3] = seq last: the host polls it instead of putting an event (a queue barrier) here
             host[0] = R;
             host[1] = s_max;
             host[2] = slots;
+            __threadfence_system();
+            host[3] = seq;
             __threadfence_system();
         }
     }
@@ -1236,12 +1238,12 @@ void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_c
     }
 }
 
-void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, hipStream_t s)
+void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, uint32_t seq, hipStream_t s)
 {
     static_assert(kPlanRun * 1024 >= kBinMaxTiles, "one k_plan block covers every LDS-binned tile grid");
 
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, (P + bin_gauss(P) - 1) / bin_gauss(P), im.tile_count,
-                       im.tile_cursor, im.ranges, T, im.misc, host);
+                       im.tile_cursor, im.ranges, T, im.misc, host, seq);
 }
 
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
