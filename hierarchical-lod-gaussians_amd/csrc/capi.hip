@@ -16,6 +16,8 @@
 #include "hlgs_internal.h"
 
 namespace hlgs {
+int g_entry_packing = HLGS_PACK_ENTRIES;  // hlgs_set_entry_packing
+bool pack_entries(int P) { return g_entry_packing && P < (1 << (32 - kEntryShift)); }
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
                        const ZeroJob& z,
                        hipStream_t s);
@@ -100,6 +102,7 @@ Geom carve_geom(void* base, int P, size_t* total)
     g.splat = take<float4>(p, 4 * (size_t)P);
     g.sh_jac = take<float>(p, 9 * (size_t)P);
     g.qmask = take<uint32_t>(p, (size_t)P);
+    g.pack = pack_entries(P) ? 1 : 0;
     g.scan_tmp = take<uint32_t>(p, scan_scratch_elems(P));
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return g;
@@ -269,6 +272,7 @@ size_t hlgs_backward_scratch_size(int P, int R)
 
 static void* aligned(const void* p) { return (void*)align_up((size_t)p); }
 
+void hlgs_set_entry_packing(int on) { g_entry_packing = on ? HLGS_PACK_ENTRIES : 0; }
 int hlgs_point_list_entry_shift(int P) { return pack_entries(P) ? kEntryShift : 0; }
 
 size_t hlgs_binning_point_list_offset(int R)

@@ -55,6 +55,7 @@ struct Geom {
     float4* splat;            // P x 4: the blend kernels' per-Gaussian record (see SplatRec)
     uint32_t* qmask;          // P: footprint quadrant masks of the first rect tiles (rect_quad_masks), written by the
                               // preprocess for the visible Gaussians when pack_entries; read by the key scatter
+    int pack;                 // pack_entries(P) of the frame this buffer is carved for
     float* sh_jac;            // P x 9: d colour / d view direction (dRGBdx, dRGBdy, dRGBdz), written by k_preprocess_sh
                               // for the visible Gaussians when sh_jac_written(); the SH backward then reads no SH rows
     uint32_t* scan_tmp;
@@ -76,11 +77,13 @@ bool lds_binning(int P, int gx, int gy);
 // 8x8 quadrant q of the tile (quad_mask), decided once by the key scatter so that the blends read it instead of
 // testing the footprint in every quadrant wave.  Otherwise the entry is idx and the blends test it themselves.
 // The low bits do not change the sort order: within a tile the (depth, idx) pairs are already distinct.
+// pack_entries(P) is decided on the host (capi.hip; hlgs_set_entry_packing turns it off for tests) and reaches the
+// kernels as Geom::pack / their pack argument.
 #ifndef HLGS_PACK_ENTRIES
 #define HLGS_PACK_ENTRIES 1
 #endif
 constexpr int kEntryShift = 4;
-__host__ __device__ inline bool pack_entries(int P) { return HLGS_PACK_ENTRIES && P < (1 << (32 - kEntryShift)); }
+bool pack_entries(int P);
 // Does the forward's preprocess (k_preprocess_sh) leave Geom::sh_jac for the SH backward?  Same condition as its launch.
 #ifndef HLGS_SH_JAC
 #define HLGS_SH_JAC 1  // 0: no Jacobian; the SH backward reads the SH rows again (A/B)

@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
         const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
         rec[2] = make_float4(cbl, 1.f / p_view.z, tt, fr);
         const float thr = alpha_e2_threshold(opacity * h_scale, interp, tt, fr);
-        if (pack_entries(a.P))
+        if (g.pack)
             g.qmask[t_idx] = rect_quad_masks(pix_x, pix_y, make_float4(conic_x, conic_y, conic_z, opacity * h_scale), thr,
                                              x0, y0, x1, y1);
         rec[3] = make_float4(0.f, __int_as_float(x0 | (y0 << 16)), __int_as_float(x1 - x0), thr);
@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(64) k_preprocess_sh(hlgs_raster_args a, Geom g
     const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
     rec[2] = make_float4(col.z, 1.f / o.depth, tt, fr);
     const float thr = alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr);
-    if (pack_entries(a.P))
+    if (g.pack)
         g.qmask[t_idx] = rect_quad_masks(o.pix_x, o.pix_y, make_float4(o.conic_x, o.conic_y, o.conic_z, opacity * o.h_scale),
                                          thr, o.x0, o.y0, o.x1, o.y1);
     rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
@@ -400,7 +400,7 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
         opacity = a.opacities[t_idx];
         const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
         thr = alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr);
-        if (pack_entries(a.P))
+        if (g.pack)
             g.qmask[t_idx] = rect_quad_masks(o.pix_x, o.pix_y, make_float4(o.conic_x, o.conic_y, o.conic_z,
                                                                            opacity * o.h_scale), thr, o.x0, o.y0, o.x1, o.y1);
     }

@@ -435,6 +435,8 @@ int hlgs_expand_to_target(int N, const int* nodes, int target, int* out, int cap
 size_t hlgs_binning_point_list_offset(int R);  /* uint32 point_list[R] */
 /* point_list entries of a P-Gaussian forward are (Gaussian index << shift) | footprint quadrant mask: the shift. */
 int hlgs_point_list_entry_shift(int P);
+/* Tests: on = 0 makes every following frame use plain index entries (the P >= 2^28 path); 1 restores the default. */
+void hlgs_set_entry_packing(int on);
 size_t hlgs_image_ranges_offset(int W, int H);  /* uint2 ranges[tiles] */
 size_t hlgs_geom_splat_offset(int P);           /* float4 splat[P][4]: x, y, conic a, b | conic c, opacity, r, g |
                                                    b, 1/depth, t, 1/kids | record base, tile x0, y0, width */

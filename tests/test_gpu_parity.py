@@ -208,3 +208,23 @@ def test_backward_chunks_from_sampled_state(P, deg, W, H, depth, op):
     assert nc.max() > 256, nc.max()
     if op[1] > 0.5:  # pixels stop (T would drop below 1e-4) inside the middle chunk
         assert 448 < np.median(nc) < 896 and nc.max() < counts.max()
+
+
+@pytest.mark.parametrize("case", ["dense", "long_lists"])
+def test_unpacked_tile_list_entries(case):
+    """The plain-index tile lists that frames of 2^28 or more Gaussians use (hlgs_set_entry_packing(0) forces them
+    here): the blends then test each splat's footprint themselves, with the same result."""
+    from hlgs_core import _lib as L
+    if case == "dense":
+        sc, cam = _scene(4000, 3, 128, 96, seed=77)
+    else:  # > 1,024 entries per tile around the centre: block LDS sort and merge passes
+        cam = S.make_camera(64, 64)
+        sc = S.make_gaussians(6000, 1, cam, seed=78, zmin=10.0, zmax=12.0, xy_spread=0.05, sigma_px=(1.0, 2.0))
+    lib = L.load()
+    lib.hlgs_set_entry_packing(0)
+    try:
+        assert lib.hlgs_point_list_entry_shift(1000) == 0
+        _compare(sc, cam)
+    finally:
+        lib.hlgs_set_entry_packing(1)
+    assert lib.hlgs_point_list_entry_shift(1000) == 4
