@@ -22,7 +22,7 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
                        const ZeroJob& z,
                        hipStream_t s);
 void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s);
-void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, uint32_t seq, hipStream_t s);
+void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s);
 bool lds_binning(int P, int gx, int gy);
 uint32_t* bin_histogram(const Img& im, int P, int gx, int gy);
 void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
@@ -314,7 +314,7 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
         stage_mark(s, ST_COUNT_TILES, false);
         if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
         stage_mark(s, ST_SCAN, true);
-        launch_plan(a->P, g, im, T, host, seq, s);
+        launch_plan(a->P, g, im, gx, gy, host, seq, s);
         stage_mark(s, ST_SCAN, false);
         return check_stage(s, a->debug, "scan");
     }

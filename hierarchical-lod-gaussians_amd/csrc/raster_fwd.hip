@@ -802,7 +802,7 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
     const uint32_t slots = plan_scan(rb, s_w, unused, [&](int i, uint32_t ex, uint32_t) { block_tot[i] = ex; });
     const uint32_t R = plan_scan(rc, s_w, mx, [&](int t, uint32_t ex, uint32_t c) {
         ranges[t] = make_uint2(ex, ex + c);
-        cursor[t] = 0;
+        if (cursor) cursor[t] = 0;  // only the atomic scatter (no histogram rows) hands out slots from cursors
     });
     for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
     if ((threadIdx.x & 63) == 0) atomicMax(&s_max, mx);
@@ -816,8 +816,7 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
             host[1] = s_max;
             host[2] = slots;
             __threadfence_system();
-            host[3] = seq;
-            __threadfence_system();
+            host[3] = seq;  // visible at the latest when the kernel completes
         }
     }
 }
@@ -1238,12 +1237,14 @@ void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_c
     }
 }
 
-void launch_plan(int P, const Geom& g, const Img& im, int T, uint32_t* host, uint32_t seq, hipStream_t s)
+void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s)
 {
+    const int T = gx * gy;
     static_assert(kPlanRun * 1024 >= kBinMaxTiles, "one k_plan block covers every LDS-binned tile grid");
 
+    uint32_t* cursor = bin_histogram(im, P, gx, gy) ? nullptr : im.tile_cursor;
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, (P + bin_gauss(P) - 1) / bin_gauss(P), im.tile_count,
-                       im.tile_cursor, im.ranges, T, im.misc, host, seq);
+                       cursor, im.ranges, T, im.misc, host, seq);
 }
 
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
