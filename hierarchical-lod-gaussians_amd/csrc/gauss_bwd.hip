@@ -491,6 +491,99 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
     sh_rows_copy<3 * MT, false>(o.dsh, s_rows, s_idx, n, lane, M3);
 }
 
+// The Jacobian SH backward (JAC) with two waves per 64 Gaussians (HLGS_SH_BWD_SPLIT): wave 0 does k_sh_bwd's per-Gaussian
+// work and builds the dsh rows in LDS, then both waves store the block's rows.  The 12.5 KB row stage then keeps two
+// waves per block instead of one (the stores, 192 B per Gaussian, are most of the kernel's traffic).  Same arithmetic.
+#ifndef HLGS_SH_BWD_SPLIT
+#define HLGS_SH_BWD_SPLIT 1
+#endif
+template <int MT, bool ALT>
+__global__ void __launch_bounds__(128) k_sh_bwd_jac2(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
+                                                    BwdScratch rec, hlgs_grads o)
+{
+    constexpr int OFF = ALT ? 1 : 0;  // full coefficient index of staged row 0
+    constexpr int MC = MT ? MT : (16 - OFF);
+    const int M = MT ? MT : a.M;
+    const int M3 = 3 * M;
+    __shared__ float s_rows[64 * kShStride];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t0 = blockIdx.x * 64;
+    const int n = min(64, a.P - t0);
+    const bool factored = o.drgb != nullptr;  // uniform
+    if (wave == 0) {
+        const int t_idx = t0 + lane, idx = t_idx;
+        const bool active = lane < n;
+        const bool vis = active && radii[t_idx] > 0;
+        float* row = s_rows + lane * kShStride;
+        if (!vis) {
+            for (int c = 0; c < M3; c++) row[c] = 0.f;  // invisible rows are zero
+            if (active && factored) {
+                o.drgb[3 * idx] = 0.f; o.drgb[3 * idx + 1] = 0.f; o.drgb[3 * idx + 2] = 0.f;
+            } else if (active && ALT) {
+                o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f;
+            }
+        } else {
+            const f3 m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+            const f3 dcol = mk(o.dcolor[3 * idx], o.dcolor[3 * idx + 1], o.dcolor[3 * idx + 2]);
+            const uint32_t cl = g.clamped[t_idx];
+            const float* J = g.sh_jac + 9 * (size_t)t_idx;
+            const f3 jx = mk(J[0], J[1], J[2]), jy = mk(J[3], J[4], J[5]), jz = mk(J[6], J[7], J[8]);
+            const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+            const f3 dir_orig = sub(m, campos);
+            const float len = sqrtf(dot(dir_orig, dir_orig));
+            const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+            const float dR = (cl & 1u) ? 0.f : dcol.x;
+            const float dG = (cl & 2u) ? 0.f : dcol.y;
+            const float dB = (cl & 4u) ? 0.f : dcol.z;
+            const int ncoef = (a.D + 1) * (a.D + 1);
+            float basis[MC + OFF];
+#pragma unroll
+            for (int c = 0; c < MC + OFF; c++) {
+                float gx, gy, gz;
+                basis[c] = c < ncoef ? sh_basis(c, x, y, z, gx, gy, gz) : 0.f;
+            }
+            const f3 d3 = mk(dR, dG, dB);
+            const float vx = dot(jx, d3), vy = dot(jy, d3), vz = dot(jz, d3);
+            if (factored) {
+                o.drgb[3 * idx] = dR; o.drgb[3 * idx + 1] = dG; o.drgb[3 * idx + 2] = dB;
+            } else if (ALT) {
+                o.ddc[3 * idx] = basis[0] * dR;
+                o.ddc[3 * idx + 1] = basis[0] * dG;
+                o.ddc[3 * idx + 2] = basis[0] * dB;
+            }
+#pragma unroll
+            for (int c = OFF; c < MC + OFF; c++) {
+                if (factored) break;
+                if (c - OFF >= M) break;
+                row[3 * (c - OFF)] = basis[c] * dR;
+                row[3 * (c - OFF) + 1] = basis[c] * dG;
+                row[3 * (c - OFF) + 2] = basis[c] * dB;
+            }
+            const f3 d = dnormvdv(dir_orig, mk(vx, vy, vz));
+            o.dmean3D[3 * idx] += d.x;
+            o.dmean3D[3 * idx + 1] += d.y;
+            o.dmean3D[3 * idx + 2] += d.z;
+        }
+    }
+    if (factored) return;  // block-uniform
+    __syncthreads();
+    // the block's rows are contiguous in dsh (non-hierarchy mode): both waves store them as float4 runs
+    float* gbase = o.dsh + (size_t)t0 * M3;
+    if constexpr (MT > 0 && (3 * MT) % 4 == 0) {
+        constexpr int Q = 3 * MT / 4;
+        for (int f = threadIdx.x; f < n * Q; f += 128) {
+            const int r = f / Q, q = f - r * Q;
+            const float* lp = s_rows + r * kShStride + 4 * q;
+            reinterpret_cast<float4*>(gbase)[f] = make_float4(lp[0], lp[1], lp[2], lp[3]);
+        }
+    } else {
+        for (int f = threadIdx.x; f < n * M3; f += 128) {
+            const int r = f / M3, q = f - r * M3;
+            gbase[f] = s_rows[r * kShStride + q];
+        }
+    }
+}
+
 // hlgs_sh_grad_from_colour: one thread per Gaussian rebuilds its averaged SH gradient row from the V views' colour
 // gradients, with the per-view products basis_c(dir_v) * dL/dRGB_v in k_sh_bwd's operation order, summed in view
 // order and scaled once; rows go out through LDS as contiguous float4 runs (as k_sh_bwd's).
@@ -605,7 +698,8 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
     const bool jac = sh_jac_written(a);  // the forward's preprocess left d colour / d direction (no SH row reads)
 #define HLGS_SHK(H, MT, AL)                                                                                \
     do {                                                                                                   \
-        if (!(H) && jac) hipLaunchKernelGGL((k_sh_bwd<false, MT, AL, true>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o); \
+        if (!(H) && jac && HLGS_SH_BWD_SPLIT) hipLaunchKernelGGL((k_sh_bwd_jac2<MT, AL>), grid_sh, dim3(128), 0, sl, a, radii, g, rs, o); \
+        else if (!(H) && jac) hipLaunchKernelGGL((k_sh_bwd<false, MT, AL, true>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o); \
         else hipLaunchKernelGGL((k_sh_bwd<H, MT, AL, false>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o); \
     } while (0)
 #define HLGS_SHB(H)                                                                                        \
