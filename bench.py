@@ -151,7 +151,7 @@ def _oracle_frame(O, sc, cam, g, gd, omp=False):
     gr = O.backward(fr, sc, g, gd)
     dt = time.perf_counter() - t0
     ref = dict(color=fr.color, invdepth=fr.invdepth, dmean3D=gr["dmean3D"], dmean2D=gr["dmean2D"],
-               dopacity=gr["dopacity"], dscale=gr["dscale"], drot=gr["drot"], dsh=gr["dsh"])
+               dopacity=gr["dopacity"], dscale=gr["dscale"], drot=gr["drot"], dsh=gr["dsh"], radii=fr.radii)
     return dt, ref
 
 
@@ -191,6 +191,39 @@ def cpu_baseline(P, deg, W, H, reference_order=True):
         for t in th:
             t.join()
     return summary, ref, ref_order
+
+
+def rotated_parity(P, deg, W, H, dev, cam_index=5):
+    """configs[1]'s workload (P Gaussians, SH deg, W x H, inverse depth) seen through one of the reference's own
+    cameras (cameras.json entry in tests/golden/golden_realcam.npz: rotated view matrix, fx != fy, kept at its own FoV
+    at W x H), GPU step against the serial oracle: the full-size check of computeCov2D's T = W J and the mean gradient
+    through the view matrix (forward.cu:141-176, backward.cu:285-312, 433-447)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from hlgs_core import synthetic as S
+    from oracle import oracle as O
+    entry = S.load_real_cameras()[cam_index]
+    cam = S.real_camera(entry, W=W, H=H)
+    host = S.make_gaussians(P, deg, cam, seed=0)
+    g, gd = S.upstream_grads(W, H, seed=1)
+    to = lambda a: torch.tensor(a, device=dev, requires_grad=True)  # noqa: E731
+    means3D, scales, rots, opac, shs = (to(host[k]) for k in ("means3D", "scales", "rotations", "opacities", "shs"))
+    means2D = torch.zeros_like(means3D, requires_grad=True)
+    color, radii, invd = GaussianRasterizer(settings_for(cam, deg, dev))(
+        means3D=means3D, means2D=means2D, opacities=opac, shs=shs, scales=scales, rotations=rots)
+    torch.autograd.backward([color, invd], [torch.tensor(g, device=dev), torch.tensor(gd, device=dev)])
+    npy = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    gpu = dict(color=npy(color), invdepth=npy(invd), dmean3D=npy(means3D.grad), dmean2D=npy(means2D.grad),
+               dopacity=npy(opac.grad), dscale=npy(scales.grad), dsh=npy(shs.grad), drot=npy(rots.grad))
+    gpu_radii = npy(radii)
+    del means3D, scales, rots, opac, shs, means2D, color, radii, invd
+    sc = {k: host[k] for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+    sc["sh_degree"] = deg
+    _, ref = _oracle_frame(O, sc, S.cam_numpy(cam), g, gd)
+    rep = parity_report(gpu, ref, f"oracle, same inputs, configs[1] workload through the reference's camera "
+                                  f"cameras.json id {entry['id']} ({entry['width']}x{entry['height']}, fx {entry['fx']:.2f}, "
+                                  f"fy {entry['fy']:.2f}) kept at its FoV at {W}x{H}")
+    rep["radii_equal"] = bool(np.array_equal(gpu_radii, ref["radii"]))
+    return rep
 
 
 def parity_report(gpu, ref, vs):
@@ -751,6 +784,9 @@ def main():
         parity["reference_variance"] = parity_report(
             ref_order["fma"], ref_order[False], "the reference order's own build-to-build variance: contracted vs "
                                                 "uncontracted oracle, same frame (no GPU involved)")
+        _mem("parity")
+        parity["reference_camera"] = rotated_parity(P, deg, W, H, dev)
+        _mem("parity, reference camera")
     if rank == 0:
         wl = (f"configs[1]: {P} Gaussians, SH deg {deg}, {W}x{H}, fwd+bwd with depth, one view" if world == 1 else
               f"configs[1] per GPU, view-data parallel: {P} Gaussians per replica, SH deg {deg}, {W}x{H}, fwd+bwd "

@@ -33,10 +33,12 @@ struct PixB {
 
 // 1 if o G <= 0.99, else 0: the reference's dL/dalpha = 0 above the alpha clamp (backward.cu:619, 693) as a factor.
 // fma(-2^40, ta, 2^40 next(0.99f)) is exactly 2^40 (next(0.99f) - ta) for ta near 0.99f (both operands scaled by a
-// power of two), so it is >= 2^16 for ta <= 0.99f and <= 0 for ta > 0.99f; the clamp makes it 1 or 0 (NaN -> 0).
+// power of two), so it is >= 2^16 (one ulp of 0.99f, scaled) for ta <= 0.99f and <= 0 for ta > 0.99f; the clamp makes
+// it 1 or 0 (NaN -> 0).  2^40 next(0.99f) = 1088516587520 is exact in float32 (tests/test_gpu_parity.py::
+// test_alpha_clamp_threshold_exact checks prev(0.99f), 0.99f, next(0.99f) and next(next(0.99f))).
 __device__ __forceinline__ float below_clamp(float test_alpha)
 {
-    return __builtin_amdgcn_fmed3f(fmaf(-1099511627776.0f, test_alpha, 1088516562944.0f + 65536.0f), 0.f, 1.f);
+    return __builtin_amdgcn_fmed3f(fmaf(-1099511627776.0f, test_alpha, 1088516587520.0f), 0.f, 1.f);
 }
 
 // 1/(1 - alpha) for alpha in [0, 0.99].  HLGS_BWD_RCP_NR > 0: that many Newton steps from the bit-pattern seed

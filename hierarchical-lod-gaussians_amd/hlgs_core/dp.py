@@ -334,28 +334,42 @@ class FlatGradExchange:
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             if self.cf is not None and self.cf.written:
                 _check_factored(self.cf)
+                self.join()  # the SH backward may still be writing this rank's row on the late stream
                 self.cf.gathered[0].copy_(self.cf.mine)
                 rebuild_sh(self.cf, 1)
+            elif self.cf is not None:
+                self._warn_unfactored()
             self.release()
             return
         world = dist.get_world_size(self.group)
-        cf_work = None
-        if self.cf is not None:
-            cf = self.cf
-            if cf.written:  # the rows of all ranks, gathered while the flat buffer is reduced below
+        cf = self.cf
+        cf_work = []
+
+        def start_gather():
+            """The rows of all ranks, gathered while the flat buffer is reduced; called once the late stream (which
+            writes this rank's row with the SH backward) is joined."""
+            if cf is None or not cf.written or cf_work:
+                return
+            if cf.gathered.shape[0] != world:  # sized at construction, possibly before init_process_group
+                cf.gathered = torch.empty((world, cf.row), dtype=torch.float32, device=cf.mine.device)
+            if cf.mine.is_cuda and dist.get_backend(self.group) != "nccl":
+                # gloo has no all_gather of device tensors (one-GPU rehearsals): each rank's row in its own slot
+                # of a zeroed buffer, summed -- the same rows, twice the bytes
+                me = dist.get_rank(self.group)
+                cf.gathered.zero_()
+                cf.gathered[me].copy_(cf.mine)
+                cf_work.append(dist.all_reduce(cf.gathered, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            elif dist.get_backend(self.group) == "nccl":  # RCCL writes the rows straight into the [world, row] buffer
+                cf_work.append(dist.all_gather_into_tensor(cf.gathered, cf.mine, group=self.group, async_op=True))
+            else:
+                cf_work.append(dist.all_gather(list(cf.gathered.unbind(0)), cf.mine, group=self.group, async_op=True))
+
+        if cf is not None:
+            if cf.written:
                 _check_factored(cf)
-                if cf.mine.is_cuda and dist.get_backend(self.group) != "nccl":
-                    # gloo has no all_gather of device tensors (one-GPU rehearsals): each rank's row in its own slot
-                    # of a zeroed buffer, summed -- the same rows, twice the bytes
-                    me = dist.get_rank(self.group)
-                    cf.gathered.zero_()
-                    cf.gathered[me].copy_(cf.mine)
-                    cf_work = dist.all_reduce(cf.gathered, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-                elif dist.get_backend(self.group) == "nccl":  # RCCL writes the rows straight into the [world, row] buffer
-                    cf_work = dist.all_gather_into_tensor(cf.gathered, cf.mine, group=self.group, async_op=True)
-                else:
-                    cf_work = dist.all_gather(list(cf.gathered.unbind(0)), cf.mine, group=self.group, async_op=True)
             else:  # the backward did not factor (no rasterizer call saw the exchange): plain averaged all-reduce
+                self._warn_unfactored()
+                self.join()
                 for t in (cf.sh, cf.dc):
                     if t is not None and t.grad is not None:
                         dist.all_reduce(t.grad, op=dist.ReduceOp.SUM, group=self.group)
@@ -380,11 +394,13 @@ class FlatGradExchange:
             spans = [(a, b) for a, b, lt in runs if not lt] + [None] + [(a, b) for a, b, lt in runs if lt]
         else:
             self.join()
+            start_gather()
             spans = [(0, self.flat.numel())] if in_place else self.buckets
-        self.last_collectives = sum(1 for sp in spans if sp is not None)
+        self.last_collectives = sum(1 for sp in spans if sp is not None) + (1 if cf is not None and cf.written else 0)
         for sp in spans:
             if sp is None:
                 self.join()
+                start_gather()
                 continue
             a, b = sp
             self._pack_range(a, b)
@@ -402,7 +418,22 @@ class FlatGradExchange:
             w.wait()
         if self.average and not native_avg:
             self.flat.mul_(1.0 / world)
-        if cf_work is not None:
-            cf_work.wait()
-            rebuild_sh(self.cf, world)
+        self.join()
+        start_gather()  # (split spans with no late run: nothing joined above)
+        if cf_work:
+            cf_work[0].wait()
+            rebuild_sh(cf, world)
         self.unpack()
+
+    def _warn_unfactored(self):
+        """Warns (once) when the SH leaves hold a gradient that did not come through the factored backward.
+        A colour-factored exchange whose round produced no colour row: the SH leaves' gradient came from elsewhere
+        (e.g. a fresh torch.cat of dc and rest each step, which the exchange cannot recognise), so it is exchanged by a
+        plain all-reduce -- correct, but without the factored exchange's bandwidth saving."""
+        if any(t is not None and t.grad is not None for t in (self.cf.sh, self.cf.dc)) and \
+                not getattr(self, "_warned_unfactored", False):
+            import warnings
+            warnings.warn("FlatGradExchange(colour_factor=...): no rasterizer backward wrote a colour row this round; "
+                          "the SH gradient is exchanged by a plain all-reduce (pass the SH parameter leaf itself to the "
+                          "rasterizer to factor it)", RuntimeWarning, stacklevel=3)
+            self._warned_unfactored = True

@@ -48,19 +48,63 @@ def _projection(znear, zfar, fovX, fovY, primx=0.5, primy=0.5):
     return P
 
 
-def make_camera(W, H, R=None, T=None, focal_scale=0.9, znear=0.01, zfar=100.0, bg=(0.0, 0.0, 0.0)):
-    """Camera dict with float32 CPU tensors laid out exactly as the reference passes them."""
+def make_camera(W, H, R=None, T=None, focal_scale=0.9, znear=0.01, zfar=100.0, bg=(0.0, 0.0, 0.0), fx=None, fy=None,
+                fovx=None, fovy=None, primx=0.5, primy=0.5):
+    """Camera dict with float32 CPU tensors laid out exactly as the reference passes them.
+
+    R is the camera-to-world rotation and T the world-to-camera translation (the reference's Camera.R / Camera.T,
+    scene/dataset_readers.py).  The field of view comes from fovx / fovy when given (a camera kept at its own FoV and
+    rendered at another resolution, as the reference's Camera does when its image is resized), else from the focal
+    lengths fx / fy (default focal_scale * W for both): FoVx = focal2fov(fx, W), FoVy = focal2fov(fy, H)
+    (scene/dataset_readers.py:87-101).  primx / primy: the principal point as a fraction of the image size
+    (getProjectionMatrix, utils/graphics_utils.py:51-77)."""
     R = np.eye(3) if R is None else np.asarray(R, dtype=np.float64)
     T = np.zeros(3) if T is None else np.asarray(T, dtype=np.float64)
-    fx = focal_scale * W
-    fy = focal_scale * W
-    fovx, fovy = focal2fov(fx, W), focal2fov(fy, H)
-    wv = torch.tensor(_world2view2(R, T)).transpose(0, 1).contiguous()
-    pr = _projection(znear, zfar, fovx, fovy).transpose(0, 1)
+    fx = focal_scale * W if fx is None else float(fx)
+    fy = focal_scale * W if fy is None else float(fy)
+    if fovx is None:
+        fovx = focal2fov(fx, W)
+    else:  # the focal length the rasterizer derives from the FoV at this width (rasterizer_impl.cu:246-247)
+        fovx, fx = float(fovx), W / (2 * math.tan(float(fovx) * 0.5))
+    if fovy is None:
+        fovy = focal2fov(fy, H)
+    else:
+        fovy, fy = float(fovy), H / (2 * math.tan(float(fovy) * 0.5))
+    wv_t = torch.tensor(_world2view2(R, T)).transpose(0, 1)  # a transposed view, as scene/cameras.py:102 holds it
+    wv = wv_t.contiguous()
+    pr = _projection(znear, zfar, fovx, fovy, primx, primy).transpose(0, 1)
     full = wv.unsqueeze(0).bmm(pr.unsqueeze(0)).squeeze(0).contiguous()
-    campos = wv.inverse()[3, :3].contiguous()
+    campos = wv_t.inverse()[3, :3].contiguous()  # :107 (the float32 inverse rounds by the operand's layout)
     return dict(W=int(W), H=int(H), tanfovx=math.tan(fovx * 0.5), tanfovy=math.tan(fovy * 0.5), fx=fx, fy=fy,
-                viewmatrix=wv, projmatrix=full, campos=campos, bg=torch.tensor(bg, dtype=torch.float32), R=R, T=T)
+                viewmatrix=wv, projmatrix=full, campos=campos, bg=torch.tensor(bg, dtype=torch.float32), R=R, T=T,
+                fovx=fovx, fovy=fovy)
+
+
+def real_camera(entry, W=None, H=None, **kw):
+    """A camera of the reference's own dataset from one cameras.json entry (utils/camera_utils.py:91-111 writes it:
+    `position` is the camera centre and `rotation` the camera-to-world rotation, i.e. Camera.R; fx / fy the focal
+    lengths at width x height).  T = -R^T position undoes camera_to_JSON's inversion.  W, H: render at another
+    resolution with the camera's own field of view (the reference's Camera keeps FoVx / FoVy when it resizes)."""
+    R = np.asarray(entry["rotation"], np.float64)
+    T = -R.T @ np.asarray(entry["position"], np.float64)
+    w0, h0 = int(entry["width"]), int(entry["height"])
+    fovx, fovy = focal2fov(float(entry["fx"]), w0), focal2fov(float(entry["fy"]), h0)
+    return make_camera(w0 if W is None else W, h0 if H is None else H, R=R, T=T, fovx=fovx, fovy=fovy, **kw)
+
+
+def load_real_cameras(path=None):
+    """The cameras.json entries committed in tests/golden/golden_realcam.npz (tests/golden/make_golden.py), as dicts
+    real_camera accepts."""
+    import os
+    path = path or os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                                "tests", "golden", "golden_realcam.npz")
+    z = np.load(path)
+    out = []
+    for i in range(int(z["count"])):
+        out.append(dict(id=int(z[f"id_{i}"]), rotation=z[f"rotation_{i}"], position=z[f"position_{i}"],
+                        fx=float(z[f"fxfy_{i}"][0]), fy=float(z[f"fxfy_{i}"][1]), width=int(z[f"WH_{i}"][0]),
+                        height=int(z[f"WH_{i}"][1])))
+    return out
 
 
 def ring_camera(W, H, k, n, radius=0.4, yaw_deg=3.0, **kw):

@@ -20,6 +20,12 @@ where /root/reference exists; the fixtures are committed so tests never need the
                      cut_hierarchy_on_condition (:184-404), extract_frustum_planes / frustum_cull_spheres (:55-103),
                      the coarse cut of train_post.py:330-343 for several cameras and distance multipliers, and
                      OurAdam._single_tensor_adam2 (:357-457) as train_post.py:802-818 calls it.
+  golden_realcam.npz 12 of the reference's own 1,499 real cameras (/root/reference/cameras.json: six physical cameras,
+                     ragged 1021-1028 x 686-690 images, arbitrary rotations, fx != fy), spread over the file, and their
+                     world_view_transform / full_proj_transform / camera_center built by utils/graphics_utils as
+                     scene/cameras.py:102-107 does -- at the native size, rendered at 1920x1080 with the camera's own
+                     FoV (a resized Camera keeps FoVx / FoVy), and with an off-centre principal point (primx 0.47,
+                     primy 0.53; cameras.json does not record it, dataset_readers.py:94-100 reads it from COLMAP).
 
 Device shim: the reference's Python hard-codes device='cuda' in a few tensor factories; _CudaToCpu (a torch
 function mode) allocates those on the CPU here.  The intended SPT cut (scene/gaussian_model.py:158-181) is
@@ -120,6 +126,40 @@ def main():
     cov3d_fixture(rng)
     lerp_fixture(rng)
     spt_fixture(rng)
+    realcam_fixture()
+
+
+def realcam_fixture():
+    """golden_realcam.npz: see the module docstring.  cameras.json is written by utils/camera_utils.camera_to_JSON
+    (:91-111): `position` = W2C[:3, 3] and `rotation` = W2C[:3, :3] of W2C = inv([R^T | T]), i.e. the camera centre
+    and Camera.R itself; so Camera.T = -R^T position.  FoVx / FoVy = focal2fov(fx, width) / focal2fov(fy, height)
+    (dataset_readers.py:87-101)."""
+    import json
+    from utils.graphics_utils import focal2fov, getProjectionMatrix, getWorld2View2
+    cams = json.load(open(os.path.join(REF, "cameras.json")))
+    idx = np.linspace(0, len(cams) - 1, 12).astype(int)
+    out = dict(count=np.int32(len(idx)))
+    for i, ci in enumerate(idx):
+        e = cams[ci]
+        R = np.array(e["rotation"], np.float64)
+        pos = np.array(e["position"], np.float64)
+        T = -R.T @ pos
+        W0, H0 = int(e["width"]), int(e["height"])
+        fovx, fovy = focal2fov(e["fx"], W0), focal2fov(e["fy"], H0)
+        out[f"id_{i}"] = np.int32(e["id"])
+        out[f"rotation_{i}"], out[f"position_{i}"] = R, pos
+        out[f"fxfy_{i}"], out[f"WH_{i}"] = np.array([e["fx"], e["fy"]], np.float64), np.array([W0, H0], np.int32)
+        for tag, (W, H, px, py) in dict(native=(W0, H0, 0.5, 0.5), hd=(1920, 1080, 0.5, 0.5),
+                                        pp=(W0, H0, 0.47, 0.53)).items():
+            wv = torch.tensor(getWorld2View2(R, T, np.array([0.0, 0.0, 0.0]), 1.0)).transpose(0, 1)
+            pr = getProjectionMatrix(znear=0.01, zfar=100.0, fovX=fovx, fovY=fovy, primx=px, primy=py).transpose(0, 1)
+            full = wv.unsqueeze(0).bmm(pr.unsqueeze(0)).squeeze(0)
+            out[f"view_{tag}_{i}"], out[f"proj_{tag}_{i}"] = wv.numpy(), full.numpy()
+            out[f"campos_{tag}_{i}"] = wv.inverse()[3, :3].numpy()
+            out[f"WH_{tag}_{i}"] = np.array([W, H], np.int32)
+            out[f"tanfov_{tag}_{i}"] = np.array([math.tan(fovx * 0.5), math.tan(fovy * 0.5)], np.float64)
+    np.savez_compressed(os.path.join(OUT, "golden_realcam.npz"), **out)
+    print("wrote golden_realcam.npz")
 
 
 class _CudaToCpu(torch.overrides.TorchFunctionMode):
@@ -373,4 +413,8 @@ def lerp_fixture(rng):
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:  # one fixture only, e.g. `python make_golden.py realcam`
+        sys.path.insert(0, REF)
+        {"realcam": realcam_fixture}[sys.argv[1]]()
+    else:
+        main()

@@ -66,16 +66,21 @@ def test_configs_frame_matches_oracle(P, deg, W, H):
     _check_frame(gpu_render(sc, cam, grads=g), oracle_render(sc, cam, grads=g))
 
 
-def test_configs2_lod_chain_1080p():
+@pytest.mark.parametrize("realcam", [None, 5], ids=["synthetic_cam", "reference_cam5"])
+def test_configs2_lod_chain_1080p(realcam):
+    """realcam: one of the reference's own cameras (tests/golden/golden_realcam.npz, rotated, fx != fy) at 1080p with
+    its own FoV; the hierarchy is built over leaves in front of it, and the view direction handed to the LOD
+    functions is world_view_transform[:3, :3] @ (0, 0, 1), as debug_utils.py:150-153 forms it."""
     import gaussian_hierarchy as GH
     from diff_gaussian_rasterization import GaussianRasterizer
     from helpers import settings_for
     W, H, deg, tau_px = 1920, 1080, 3, 6.0
-    cam = S.make_camera(W, H)
+    cam = S.make_camera(W, H) if realcam is None else S.real_camera(S.load_real_cameras()[realcam], W=W, H=H)
     h = S.make_dynamic_hierarchy(S.make_gaussians(1_000_000, deg, cam, seed=0), seed=0)
     N = h["nodes"].shape[0]
     tau = (2 * (tau_px + 0.5)) * cam["tanfovx"] / (0.5 * W)  # bench.py's config3 threshold
-    vp, vd = cam["campos"].numpy(), np.array([0.0, 0.0, 1.0], np.float32)
+    vp = cam["campos"].numpy()
+    vd = (cam["viewmatrix"][:3, :3] @ torch.tensor([0.0, 0.0, 1.0])).numpy().astype(np.float32)
     d = lambda a, **kw: torch.tensor(np.ascontiguousarray(a), device=DEV, **kw)  # noqa: E731
     nodes = d(h["nodes"])
     leaves = [d(h[k], requires_grad=True) for k in ("means3D", "scales", "rotations", "opacities", "shs")]

@@ -149,11 +149,12 @@ def test_overlap_two_renders_of_the_same_leaves_in_one_backward():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("alt", [False, True])
-def test_colour_factored_sh_exchange(alt):
+@pytest.mark.parametrize("alt,overlap", [(False, False), (True, False), (False, True), (True, True)])
+def test_colour_factored_sh_exchange(alt, overlap):
     """Colour-factored exchange (FlatGradExchange(colour_factor=...)): the backward hands the exchange dL/dRGB instead of
     the SH gradient and the exchange rebuilds it (hlgs_sh_grad_from_colour).  One view: every gradient bitwise the plain
-    backward's.  Two views' rows rebuilt together: the average of the two views' SH (and dc) gradients."""
+    backward's.  Two views' rows rebuilt together: the average of the two views' SH (and dc) gradients.  overlap=True:
+    the exchange joins any late SH-backward work before it reads this rank's colour row."""
     import ctypes as C
     from hlgs_core import _lib as L
     from hlgs_core.dp import FlatGradExchange
@@ -200,14 +201,14 @@ def test_colour_factored_sh_exchange(alt):
     for cam in cams:
         backward(cam)
         plain.append([p.grad.clone() for p in params])
-    ex = FlatGradExchange(params, colour_factor=factor)
+    ex = FlatGradExchange(params, colour_factor=factor, overlap=overlap)
     rows = []
     try:
         for cam, ref in zip(cams, plain):
             backward(cam)
             assert ex.cf.written, "the backward did not take the colour-factored path"
+            ex.allreduce()  # one rank: the rebuild from this view's row alone (joins the late stream first)
             rows.append(ex.cf.mine.clone())
-            ex.allreduce()  # one rank: the rebuild from this view's row alone
             for a, p in zip(ref, params):
                 assert torch.equal(a, p.grad)
     finally:

@@ -228,3 +228,38 @@ def test_unpacked_tile_list_entries(case):
     finally:
         lib.hlgs_set_entry_packing(1)
     assert lib.hlgs_point_list_entry_shift(1000) == 4
+
+
+def clamp_boundary_scene(step):
+    """One splat on the optical axis of an odd-sized image: it projects exactly onto pixel centre (32, 32), so there
+    dx = dy = 0, G = exp2(0) = 1 and the backward's test alpha o' G equals the record opacity o' = o h (h: the
+    anti-aliasing compensation, forward.cu).  o is searched so that o' is exactly the float `step` ulps from 0.99f.
+    The splat is wide (h ~ 0.996), so o < 1 and every float near 0.99f is some o h."""
+    from oracle import oracle as O
+    cam = S.make_camera(65, 65)
+    target = np.float32(0.99)
+    for _ in range(abs(step)):
+        target = np.nextafter(target, np.float32(2.0 if step > 0 else 0.0))
+    sc = dict(means3D=np.array([[0.0, 0.0, 4.0]], np.float32), scales=np.full((1, 3), 0.6, np.float32),
+              rotations=np.array([[1.0, 0.0, 0.0, 0.0]], np.float32), opacities=np.array([[0.5]], np.float32),
+              shs=np.full((1, 1, 3), 0.3, np.float32), sh_degree=0)
+    h = O.forward(sc, S.cam_numpy(cam)).conic_opacity[0, 3] / np.float32(0.5)
+    o = np.float32(target / h)
+    for _ in range(64):
+        sc["opacities"][0, 0] = o
+        got = O.forward(sc, S.cam_numpy(cam)).conic_opacity[0, 3]
+        if got == target:
+            return sc, cam, target
+        o = np.nextafter(o, np.float32(2.0 if got < target else 0.0))
+    raise AssertionError("no opacity gives the target record opacity")
+
+
+@pytest.mark.parametrize("step", [-1, 0, 1, 2])
+def test_alpha_clamp_threshold_exact(step):
+    """The backward zeroes dL/dalpha where o G > 0.99f (backward.cu:619, 693), decided exactly at the float boundary
+    (ADVICE r03): the centre pixel's test alpha is prev(0.99f), 0.99f, next(0.99f) or next(next(0.99f))
+    (clamp_boundary_scene); its dL/dalpha is kept for the first two and zeroed for the others, as the oracle does."""
+    sc, cam, target = clamp_boundary_scene(step)
+    gpu, ref = _compare(sc, cam)
+    fr = ref["frame"]
+    assert fr.means2D[0].tolist() == [32.0, 32.0] and fr.conic_opacity[0, 3] == target

@@ -37,6 +37,31 @@ def test_camera_matches_reference_graphics_utils():
         np.testing.assert_allclose(cam["campos"].numpy(), z[f"campos_{i}"], rtol=0, atol=1e-6)
 
 
+REALCAM_TAGS = dict(native=dict(), hd=dict(W=1920, H=1080), pp=dict(primx=0.47, primy=0.53))
+
+
+@pytest.mark.parametrize("tag", list(REALCAM_TAGS))
+def test_real_cameras_match_reference_graphics_utils(tag):
+    """The reference's own cameras (cameras.json: rotated, fx != fy, ragged sizes) through S.real_camera against the
+    matrices utils/graphics_utils builds for them (scene/cameras.py:102-107), bit for bit."""
+    z = np.load(os.path.join(GOLD, "golden_realcam.npz"))
+    cams = S.load_real_cameras()
+    assert len(cams) == int(z["count"]) >= 8
+    for i, e in enumerate(cams):
+        cam = S.real_camera(e, **REALCAM_TAGS[tag])
+        assert [cam["W"], cam["H"]] == list(z[f"WH_{tag}_{i}"])
+        np.testing.assert_array_equal(cam["viewmatrix"].numpy(), z[f"view_{tag}_{i}"])
+        np.testing.assert_array_equal(cam["projmatrix"].numpy(), z[f"proj_{tag}_{i}"])
+        np.testing.assert_allclose(cam["campos"].numpy(), z[f"campos_{tag}_{i}"], rtol=1e-6, atol=0)
+        np.testing.assert_allclose([cam["tanfovx"], cam["tanfovy"]], z[f"tanfov_{tag}_{i}"], rtol=1e-15)
+    assert len({(e["width"], e["height"]) for e in cams}) >= 4 and all(e["fx"] != e["fy"] for e in cams)
+
+
+def real_camera_small(i, W, H, bg=(0.0, 0.0, 0.0), **kw):
+    """Real camera i of the fixture, kept at its own FoV and rendered at W x H (small enough for float64 autograd)."""
+    return S.real_camera(S.load_real_cameras()[i], W=W, H=H, bg=bg, **kw)
+
+
 # ------------------------------------------------------------------------------------------------------
 # float64 autograd restatement
 # ------------------------------------------------------------------------------------------------------
@@ -199,22 +224,44 @@ def torch_render(sc, cam, fr, deg, alt=False, aa=True):
     return out
 
 
+def _fwd_tol_far(cam, sc):
+    """Forward tolerance of the float32 oracle against float64 for a camera far from the world origin.  The real
+    cameras sit up to ~133 units from it, so the float32 view transform p_view = R p + t cancels terms of that size
+    down to depths of 2-30: its rounding moves a splat centre by ~eps * |t| * f / z pixels (~2e-3 px here), which the
+    float64 restatement of the same float32 inputs does not have.  The bound scales 1e-5 by |t| / min depth (>= 1):
+    a wrong view matrix or a swapped focal length moves pixels by O(1), far above it."""
+    t = float(np.abs(cam["viewmatrix"].numpy()[3, :3]).max())
+    zmin = float((np.c_[sc["means3D"], np.ones(len(sc["means3D"]))] @ cam["viewmatrix"].numpy().astype(np.float64))[:, 2].min())
+    return 1e-5 * max(1.0, t / max(zmin, 1e-3))
+
+
 def _rel(a, b):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
 
 
-@pytest.mark.parametrize("P,deg,W,H,bg", [(250, 3, 64, 48, (0.0, 0.0, 0.0)), (300, 1, 48, 40, (0.2, 0.5, 0.8)),
-                                          (150, 0, 40, 40, (0.1, 0.1, 0.1))])
-def test_oracle_matches_float64_autograd(P, deg, W, H, bg):
-    cam = S.make_camera(W, H, bg=bg)
+@pytest.mark.parametrize("P,deg,W,H,bg,realcam", [(250, 3, 64, 48, (0.0, 0.0, 0.0), None),
+                                                  (300, 1, 48, 40, (0.2, 0.5, 0.8), None),
+                                                  (150, 0, 40, 40, (0.1, 0.1, 0.1), None),
+                                                  (250, 3, 60, 44, (0.3, 0.2, 0.1), 0),
+                                                  (300, 2, 52, 36, (0.0, 0.0, 0.0), 5),
+                                                  (250, 1, 47, 41, (0.6, 0.3, 0.2), 9)])
+def test_oracle_matches_float64_autograd(P, deg, W, H, bg, realcam):
+    """realcam: one of the reference's own cameras (rotated view matrix, fx != fy; camera 9 with an off-centre
+    principal point), so T = W J of computeCov2D (forward.cu:141-176) and the mean-gradient chain through the view
+    matrix (backward.cu:285-312, 433-447) are exercised with a non-identity W."""
+    if realcam is None:
+        cam = S.make_camera(W, H, bg=bg)
+    else:
+        cam = real_camera_small(realcam, W, H, bg=bg, **(dict(primx=0.47, primy=0.53) if realcam == 9 else {}))
     sc = S.make_gaussians(P, deg, cam, seed=P)
     fr = O.forward(sc, S.cam_numpy(cam))
     g, gd = S.upstream_grads(W, H)
     gr = O.backward(fr, sc, g, gd)
     tr = torch_render(sc, cam, fr, deg)
-    assert _rel(fr.color, tr["color"].detach().numpy()) < 1e-5
-    assert _rel(fr.invdepth, tr["invdepth"].detach().numpy()) < 1e-5
+    tol = 1e-5 if realcam is None else _fwd_tol_far(cam, sc)
+    assert _rel(fr.color, tr["color"].detach().numpy()) < tol
+    assert _rel(fr.invdepth, tr["invdepth"].detach().numpy()) < tol
     loss = (tr["color"] * torch.tensor(g, dtype=torch.float64)).sum() + \
         (tr["invdepth"] * torch.tensor(gd, dtype=torch.float64)).sum()
     loss.backward()
@@ -262,12 +309,15 @@ def alt_scene(sc, antialiasing=True):
     return out
 
 
-@pytest.mark.parametrize("P,deg,W,H,bg,aa", [(250, 3, 64, 48, (0.0, 0.0, 0.0), True),
-                                             (300, 2, 48, 40, (0.2, 0.5, 0.8), False),
-                                             (200, 1, 40, 40, (0.3, 0.1, 0.6), True)])
-def test_alt_oracle_matches_float64_autograd(P, deg, W, H, bg, aa):
-    """alt-rasterizer restatement (dc/rest split, optional AA, per-tile culling, its own backward)."""
-    cam = S.make_camera(W, H, bg=bg)
+@pytest.mark.parametrize("P,deg,W,H,bg,aa,realcam", [(250, 3, 64, 48, (0.0, 0.0, 0.0), True, None),
+                                                     (300, 2, 48, 40, (0.2, 0.5, 0.8), False, None),
+                                                     (200, 1, 40, 40, (0.3, 0.1, 0.6), True, None),
+                                                     (250, 3, 60, 44, (0.2, 0.4, 0.6), True, 3),
+                                                     (250, 1, 45, 39, (0.0, 0.0, 0.0), False, 7)])
+def test_alt_oracle_matches_float64_autograd(P, deg, W, H, bg, aa, realcam):
+    """alt-rasterizer restatement (dc/rest split, optional AA, per-tile culling, its own backward); realcam as in
+    test_oracle_matches_float64_autograd."""
+    cam = S.make_camera(W, H, bg=bg) if realcam is None else real_camera_small(realcam, W, H, bg=bg)
     sc = alt_scene(S.make_gaussians(P, deg, cam, seed=P + 7), aa)
     sc["opacities"][: P // 10] = 0.999  # some splats reach the 0.99 clamp
     fr = O.forward(sc, S.cam_numpy(cam))
@@ -275,8 +325,9 @@ def test_alt_oracle_matches_float64_autograd(P, deg, W, H, bg, aa):
     g, gd = S.upstream_grads(W, H)
     gr = O.backward(fr, sc, g, gd)
     tr = torch_render(sc, cam, fr, deg, alt=True, aa=aa)
-    assert _rel(fr.color, tr["color"].detach().numpy()) < 1e-5
-    assert _rel(fr.invdepth, tr["invdepth"].detach().numpy()) < 1e-5
+    tol = 1e-5 if realcam is None else _fwd_tol_far(cam, sc)
+    assert _rel(fr.color, tr["color"].detach().numpy()) < tol
+    assert _rel(fr.invdepth, tr["invdepth"].detach().numpy()) < tol
     loss = (tr["color"] * torch.tensor(g, dtype=torch.float64)).sum() + \
         (tr["invdepth"] * torch.tensor(gd, dtype=torch.float64)).sum()
     loss.backward()
