@@ -83,6 +83,7 @@ bool lds_binning(int P, int gx, int gy);
 #define HLGS_PACK_ENTRIES 1
 #endif
 constexpr int kEntryShift = 4;
+constexpr int kMiscPack = 3;  // Img::misc word holding the frame's pack_entries(P)
 bool pack_entries(int P);
 // Does the forward's preprocess (k_preprocess_sh) leave Geom::sh_jac for the SH backward?  Same condition as its launch.
 #ifndef HLGS_SH_JAC
@@ -103,7 +104,8 @@ struct Img {
     uint2* ranges;         // T: [start, end) into point_list
     uint32_t* tile_count;  // T
     uint32_t* tile_cursor; // T
-    uint32_t* misc;        // 16: [0] = binned instances, [1] = longest per-tile list, [2] = record slots (point_offsets[P-1])
+    uint32_t* misc;        // 16: [0] = binned instances, [1] = longest per-tile list, [2] = record slots (point_offsets[P-1]),
+                           // [kMiscPack] = the frame's pack_entries(P), read by the backward (not the process-wide switch)
     uint32_t* scan_tmp;
     float* split_state;    // T x kBwdSplits x kSplitFloats (see bwd_chunk_len)
 };

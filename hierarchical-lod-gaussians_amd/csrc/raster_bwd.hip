@@ -175,7 +175,7 @@ struct BwdArgs {
     const float* dL_dpixels;
     const float* dL_dinvdepths;
     BwdScratch rec;
-    int pack;  // point_list entries are packed (pack_entries)
+    const uint32_t* misc;  // Img::misc of the forward: [kMiscPack] says whether its point_list entries are packed
 };
 
 // One wave per (tile, chunk of the tile's list), back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8
@@ -204,6 +204,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     const float* __restrict__ dL_dpixels = A.dL_dpixels;
     const float* __restrict__ dL_dinvdepths = A.dL_dinvdepths;
     const BwdScratch& rec = A.rec;
+    const uint32_t pack = __builtin_amdgcn_readfirstlane(A.misc[kMiscPack]);  // as the forward packed them
     __shared__ float4 s_xy[64];   // x, y, 1/depth, unused
     __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
     __shared__ float4 s_col[64];  // r, g, b, alpha threshold on e2
@@ -275,7 +276,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         if (lane_valid) {
             const uint32_t pos = range.x + li_top - lane;
             uint32_t id = point_list[pos], pm = 0;
-            if (A.pack) {  // packed entry (pack_entries): the quadrant mask comes with it
+            if (pack) {  // packed entry (pack_entries): the quadrant mask comes with it
                 pm = id & ((1u << kEntryShift) - 1u);
                 id >>= kEntryShift;
             }
@@ -283,7 +284,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
             const uint32_t sbase = id ? g.point_offsets[id - 1] : 0u;
             const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            qm = A.pack ? pm : quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
+            qm = pack ? pm : quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
             s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
             s_q[lane] = conic_q(co);
             my_co = co;
@@ -375,7 +376,7 @@ void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
     const int T = gx * gy;
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     BwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, im.final_T, im.n_contrib, im.split_state, a.bg, dL_dpix,
-              dL_dinv, rs, (int)pack_entries(a.P)};
+              dL_dinv, rs, im.misc};
 #define HLGS_BB(I, Dp, Al) hipLaunchKernelGGL((k_blend_bwd<I, Dp, Al>), dim3((kBwdSplits + 1) * T), dim3(64), 0, s, A)
     if (a.variant == HLGS_VARIANT_ALT) { if (dL_dinv) HLGS_BB(false, true, true); else HLGS_BB(false, false, true); }
     else if (interp) { if (dL_dinv) HLGS_BB(true, true, false); else HLGS_BB(true, false, false); }

@@ -709,9 +709,10 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
 
 // ranges[t] = [incl[t] - count[t], incl[t]); misc[0] = R, misc[1] = max count; cursor reset for the scatter.
 // misc[2] = point_offsets[P - 1]: instances over all tile rects (record slots; == misc[0] unless culled).
+// misc[3] = pack_entries(P) of this frame (kMiscPack), so the backward decodes the lists as they were written.
 __global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict__ count, uint32_t* incl_and_cursor,
                                                      uint2* __restrict__ ranges, uint32_t* __restrict__ misc, int T,
-                                                     const uint32_t* __restrict__ point_offsets, int P)
+                                                     const uint32_t* __restrict__ point_offsets, int P, uint32_t pack)
 {
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t >= T) return;
@@ -721,6 +722,7 @@ __global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict_
     if (t == T - 1) {
         misc[0] = e;
         misc[2] = P > 0 ? point_offsets[P - 1] : 0u;
+        misc[kMiscPack] = pack;
     }
     if (c) atomicMax(&misc[1], c);
 }
@@ -790,7 +792,7 @@ __device__ __forceinline__ uint32_t plan_scan(const PlanRun& r, uint32_t* s_w, u
 __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot, int nb,
                                                const uint32_t* __restrict__ count, uint32_t* __restrict__ cursor,
                                                uint2* __restrict__ ranges, int T, uint32_t* __restrict__ misc,
-                                               uint32_t* host, uint32_t seq)
+                                               uint32_t* host, uint32_t seq, uint32_t pack)
 {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_max;
@@ -811,6 +813,7 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
         misc[0] = R;
         misc[1] = s_max;
         misc[2] = slots;
+        misc[kMiscPack] = pack;
         if (host) {  // host[3] = seq last: the host polls it instead of putting an event (a queue barrier) here
             host[0] = R;
             host[1] = s_max;
@@ -1244,7 +1247,7 @@ void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* 
 
     uint32_t* cursor = bin_histogram(im, P, gx, gy) ? nullptr : im.tile_cursor;
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, (P + bin_gauss(P) - 1) / bin_gauss(P), im.tile_count,
-                       cursor, im.ranges, T, im.misc, host, seq);
+                       cursor, im.ranges, T, im.misc, host, seq, (uint32_t)g.pack);
 }
 
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
@@ -1293,7 +1296,7 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
 void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s)
 {
     hipLaunchKernelGGL(k_tile_ranges, dim3((T + 255) / 256), dim3(256), 0, s, im.tile_count, im.tile_cursor,
-                       im.ranges, im.misc, T, point_offsets, P);
+                       im.ranges, im.misc, T, point_offsets, P, (uint32_t)pack_entries(P));
 }
 
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b,

@@ -647,6 +647,49 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
     free(thr);
 }
 
+/* Diagnostics (tests/test_gpu_refparity.py, tools/ref_flips.py): the threshold decisions of one pixel's pairs in both
+ * alpha modes, on a frame whose point_list / ranges are set (they do not depend on the mode).  For each of the
+ * pixel's tile-list entries k < cap, front to back: keep[2k + m] = 1 if mode m (0: the shared contract A-17, 1: the
+ * reference's float order) keeps the pair (power <= 0 and alpha >= 1/255), alpha[2k + m] its alpha (0 if skipped).
+ * last[m] = the n_contrib of the forward walk in mode m (its T < 1e-4 stop included).  Returns the list length. */
+int orc_pixel_pairs(const orc_args *a, const orc_geom *g, const orc_img *im, int px, int py, int cap, int *keep,
+                    float *alpha_out, int *last)
+{
+    const int gx = (a->W + TILE - 1) / TILE;
+    const int t = (py / TILE) * gx + px / TILE;
+    const uint32_t rs = im->ranges[2 * t], re = im->ranges[2 * t + 1];
+    float *thr = alpha_thresholds(a, g);
+    const int saved = g_ref_order;
+    const int do_interp = (a->ts != NULL && a->kids != NULL);
+    for (int m = 0; m < 2; m++) {
+        g_ref_order = m;
+        float Tt = 1.0f;
+        int stopped = 0;
+        last[m] = 0;
+        for (uint32_t j = rs; j < re; j++) {
+            const int k = (int)(j - rs);
+            const uint32_t id = im->point_list[j];
+            const float dx = g->means2D[2 * id] - (float)px, dy = g->means2D[2 * id + 1] - (float)py;
+            const int ip = do_interp && (int)id < a->P;
+            float G, my_alpha, al = 0.0f;
+            const int kp = pair_alpha(g->conic_opacity + 4 * id, dx, dy, thr[id], ip, ip ? a->ts[id] : 0.0f,
+                                      ip ? 1.0f / (float)a->kids[id] : 0.0f, 1, &G, &my_alpha, &al);
+            if (k < cap) {
+                keep[2 * k + m] = kp;
+                alpha_out[2 * k + m] = kp ? al : 0.0f;
+            }
+            if (!kp || stopped) continue;
+            const float test_T = Tt * (1 - al);
+            if (test_T < 0.0001f) { stopped = 1; continue; }
+            Tt = test_T;
+            last[m] = k + 1;
+        }
+    }
+    g_ref_order = saved;
+    free(thr);
+    return (int)(re - rs);
+}
+
 /* Backward gradient outputs; every array has P_full rows and must be zero on entry. */
 typedef struct {
     float *dmean2D;  /* x3 */

@@ -99,6 +99,9 @@ def lib(omp=False):
         L.orc_lod_interp_backward.argtypes = [C.c_int, C.c_int, C.c_int, _i, _i, _f, _f, _f, _f, _f, _f,
                                               _f, _f, _f, _f, _f, _f]
         L.orc_sh_colors.argtypes = [C.c_int, C.c_int, C.c_int, _f, _f, _f, _f, _b]
+        L.orc_pixel_pairs.restype = C.c_int
+        L.orc_pixel_pairs.argtypes = [C.POINTER(_Args), C.POINTER(_Geom), C.POINTER(_Img), C.c_int, C.c_int, C.c_int,
+                                      _i, _f, _i]
         _libs[omp] = L
     return L
 
@@ -233,6 +236,23 @@ def backward(fr, scene, dL_dcolor, dL_dinvdepth=None):
     if fr.P:
         L.orc_backward(C.byref(fr.args), C.byref(fr.geom), C.byref(fr.img), fr.R, _p(dpix), _p(dinv), C.byref(gr))
     return g
+
+
+def pixel_pairs(fr, px, py, cap=4096):
+    """Diagnostics: the threshold decisions of pixel (px, py)'s pairs on frame fr in both alpha modes (orc_pixel_pairs):
+    dict(ids, keep (n, 2), alpha (n, 2), last (2,)) -- column 0 the shared contract (A-17), column 1 the reference's
+    float order; last = each mode's n_contrib."""
+    L = lib(getattr(fr, "omp", False))
+    keep = np.zeros((cap, 2), np.int32)
+    alpha = np.zeros((cap, 2), np.float32)
+    last = np.zeros(2, np.int32)
+    n = L.orc_pixel_pairs(C.byref(fr.args), C.byref(fr.geom), C.byref(fr.img), int(px), int(py), int(cap),
+                          _p(keep, _i), _p(alpha), _p(last, _i))
+    gx = (fr.W + 15) // 16
+    t = (py // 16) * gx + px // 16
+    rs = int(fr.ranges[t, 0])
+    m = min(n, cap)
+    return dict(ids=fr.point_list[rs:rs + m].copy(), keep=keep[:m], alpha=alpha[:m], last=last)
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

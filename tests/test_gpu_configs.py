@@ -45,16 +45,23 @@ def _check_frame(gpu, ref, row_rtol=0.0):
 ILL = ("d_scales", "d_rotations")  # gradients behind the ill-conditioned conic -> cov3D backward of wide splats
 
 
+VARIANCE_CEILING = 40.0  # element-wise ratio; the oracle builds' own measured ~33 (d_rotations) / ~30 (d_scales)
+
+
 def _assert_grad_within_variance(name, a, b, b_alt, row_rtol=1e-3):
     """north_star's per-tensor rule (max|a - b| / max|b| <= 1e-3) always; element-wise, grad_check with the per-Gaussian
-    floor, or else no further from the oracle b than b_alt -- the same oracle source built with FMA contraction -- is."""
+    floor, or else no further from the oracle b than b_alt -- the same oracle source built with FMA contraction -- is,
+    and never above VARIANCE_CEILING: the builds' variance comes from an x86 contraction pattern, not from the
+    reference's nvcc build, so it may not loosen the gate without bound.  Measured on the configs[2] frame
+    (tools/diag/lod_chain_variance.py): the builds differ by ~33 (d_rotations) and ~30 (d_scales); the GPU by less."""
     e = rel_err(a, b)
     assert e <= 1e-3, f"{name}: rel err {e}"
     ratio, ok = grad_check(a, b, row_rtol=row_rtol)
     if not ok:
         var, _ = grad_check(b_alt, b, row_rtol=row_rtol)
         print(f"{name}: element-wise ratio {ratio:.3f} (GPU vs oracle), {var:.3f} (oracle builds)")
-        assert ratio <= var, f"{name}: element-wise ratio {ratio} above the oracle builds' own {var}"
+        assert ratio <= min(var, VARIANCE_CEILING), \
+            f"{name}: element-wise ratio {ratio} above the oracle builds' own {var} (ceiling {VARIANCE_CEILING})"
 
 
 @pytest.mark.parametrize("P,deg,W,H", [(10_000, 0, 256, 256), (1_000_000, 3, 1920, 1080)],

@@ -263,3 +263,28 @@ def test_alpha_clamp_threshold_exact(step):
     gpu, ref = _compare(sc, cam)
     fr = ref["frame"]
     assert fr.means2D[0].tolist() == [32.0, 32.0] and fr.conic_opacity[0, 3] == target
+
+
+def test_packing_switch_between_forward_and_backward():
+    """The backward decodes the tile lists as the forward wrote them (the frame's packing decision travels in the image
+    buffer, Img::misc[kMiscPack]), so turning hlgs_set_entry_packing off between a forward and its backward changes
+    nothing."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from helpers import settings_for
+    from hlgs_core import _lib as L
+    sc, cam = _scene(3000, 2, 128, 96, seed=91)
+    g, gd = S.upstream_grads(128, 96, seed=3)
+    ref = gpu_render(sc, cam, grads=(g, gd))
+    t = lambda a: torch.tensor(np.ascontiguousarray(a), device="cuda", requires_grad=True)  # noqa: E731
+    m, s_, r, o, sh = (t(sc[k]) for k in ("means3D", "scales", "rotations", "opacities", "shs"))
+    m2 = torch.zeros_like(m, requires_grad=True)
+    color, _, inv = GaussianRasterizer(settings_for(cam, 2, "cuda"))(means3D=m, means2D=m2, opacities=o, shs=sh,
+                                                                      scales=s_, rotations=r)
+    lib = L.load()
+    lib.hlgs_set_entry_packing(0)
+    try:
+        torch.autograd.backward([color, inv], [torch.tensor(g, device="cuda"), torch.tensor(gd, device="cuda")])
+    finally:
+        lib.hlgs_set_entry_packing(1)
+    for k, v in (("dmean3D", m), ("dopacity", o), ("d_shs", sh), ("d_scales", s_), ("d_rotations", r)):
+        np.testing.assert_array_equal(v.grad.cpu().numpy(), ref[k], err_msg=k)

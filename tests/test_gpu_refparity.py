@@ -12,10 +12,16 @@ three distances on the full 1M-Gaussian, 1920x1080 frame:
   gpu vs ref_fma  the GPU against the same oracle source with a*b+c contracted (gcc -ffp-contract=fast -mfma)
   ref_fma vs ref  the reference order's own build-to-build variance
 
-and fails if the GPU is further from either reference-order build than a fixed bound: at most 10 pixels above
-north_star's 1e-4, colour / inverse-depth L-inf <= 1e-3, and every gradient tensor within north_star's 1e-3
-(max|d| / max|ref|).  The build-to-build variance is asserted to be of the same order (it is what makes the 1e-4
-per-pixel bound unattainable for any reimplementation of this float order), and all three reports are printed.
+and gates the GPU's distance on the measured build-to-build variance:
+  - pixels above 1e-4: at most the builds' own count + 2;
+  - colour L-inf: at most 2x the builds' mutual colour L-inf; inverse-depth L-inf <= 1e-3;
+  - max per-tensor gradient error (max|d| / max|ref|): at most 2x the builds' own, and <= north_star's 1e-3;
+  - every pixel above 1e-4 is explained: one of its pairs is kept by one order and skipped by the other (alpha within
+    float rounding of 1/255, oracle.pixel_pairs), or the two forward walks stop at different contributors.
+On the configs[1] frame (tools/ref_flips.py) each of the 3 pixels is one pair whose alpha rounds to 1/255f exactly in
+the reference's order while its exact value is below 1/255 (or the reverse); the largest, pixel (668, 1033), is such a
+pair that BOTH reference builds keep, so it is absent from their mutual variance, which is why the GPU's colour L-inf
+(7.2e-4) exceeds the builds' mutual 3.9e-4.
 """
 import json
 import threading
@@ -36,14 +42,16 @@ GRAD_KEYS = {"dmean3D": "dmean3D", "dmean2D": "dmean2D", "dopacity": "dopacity",
 
 
 def _reference_order_frames(sc, cam, g, gd):
-    """Both reference-order oracle frames, each on its own thread (ctypes releases the GIL)."""
+    """Both reference-order oracle frames (and the frame objects, for pixel_pairs), each on its own thread (ctypes
+    releases the GIL)."""
     cn = S.cam_numpy(cam)
-    out = {}
+    out, frs = {}, {}
 
     def run(key):
         with O.reference_order(omp=key):
             fr = O.forward(sc, cn, do_depth=True, omp=key)
             gr = O.backward(fr, sc, g, gd)
+        frs[key] = fr
         out[key] = dict(color=fr.color, invdepth=fr.invdepth, dmean3D=gr["dmean3D"], dmean2D=gr["dmean2D"],
                         dopacity=gr["dopacity"], dscale=gr["dscale"], drot=gr["drot"], dsh=gr["dsh"])
     th = [threading.Thread(target=run, args=(k,)) for k in (False, "fma")]
@@ -51,7 +59,20 @@ def _reference_order_frames(sc, cam, g, gd):
         t.start()
     for t in th:
         t.join()
-    return out[False], out["fma"]
+    return out[False], out["fma"], frs[False], frs["fma"]
+
+
+def _unexplained(gpu, ref, fr_contract_lists, fr_ref, tol=1e-4):
+    """Pixels where the GPU (bit-exact with the shared contract) and a reference-order frame differ by more than tol
+    without a threshold flip: no pair kept by one order and skipped by the other, and equal walk lengths."""
+    d = np.maximum(np.abs(gpu["color"] - ref["color"]).max(0), np.abs(gpu["invdepth"] - ref["invdepth"]).max(0))
+    bad = []
+    for y, x in zip(*np.nonzero(d > tol)):
+        pc, pr = O.pixel_pairs(fr_contract_lists, int(x), int(y)), O.pixel_pairs(fr_ref, int(x), int(y))
+        flips = np.nonzero(pc["keep"][:, 0] != pr["keep"][:, 1])[0]
+        if not len(flips) and pc["last"][0] == pr["last"][1]:
+            bad.append((int(x), int(y), float(d[y, x])))
+    return bad
 
 
 def _report(a, b):
@@ -73,14 +94,19 @@ def test_configs1_reference_order_within_bound():
     g, gd = S.upstream_grads(W, H, seed=1)
     out = gpu_render(sc, cam, grads=(g, gd))
     gpu = dict(color=out["color"], invdepth=out["invdepth"], **{k: out[v] for k, v in GRAD_KEYS.items()})
-    ref, fma = _reference_order_frames(sc, cam, g, gd)
+    ref, fma, fr_ref, fr_fma = _reference_order_frames(sc, cam, g, gd)
     reps = {"gpu_vs_ref": _report(gpu, ref), "gpu_vs_ref_fma": _report(gpu, fma), "ref_fma_vs_ref": _report(fma, ref)}
     print(json.dumps(reps, indent=1))
-    for name in ("gpu_vs_ref", "gpu_vs_ref_fma"):
-        r = reps[name]
-        assert r["pixels_above_1e_4"] <= PIX_BOUND, (name, reps)
-        assert max(r["color_linf"], r["invdepth_linf"]) <= LINF_BOUND, (name, reps)
-        assert max(r["grad_rel"].values()) <= GRAD_REL, (name, reps)
-    # the reference order's own variance is of the same order as the GPU's distance from it
     v = reps["ref_fma_vs_ref"]
-    assert v["pixels_above_1e_4"] <= PIX_BOUND and max(v["grad_rel"].values()) <= GRAD_REL, reps
+    v_grad = max(v["grad_rel"].values())
+    assert v["pixels_above_1e_4"] <= PIX_BOUND and v_grad <= GRAD_REL, reps
+    for name, fr_b in (("gpu_vs_ref", fr_ref), ("gpu_vs_ref_fma", fr_fma)):
+        r = reps[name]
+        assert r["pixels_above_1e_4"] <= v["pixels_above_1e_4"] + 2, (name, reps)
+        assert r["color_linf"] <= 2 * v["color_linf"], (name, reps)
+        assert r["invdepth_linf"] <= LINF_BOUND, (name, reps)
+        assert max(r["grad_rel"].values()) <= min(2 * v_grad, GRAD_REL), (name, reps)
+        # the serial reference-order frame's build also decides in the shared contract (mode 0): its lists are the
+        # GPU's (bit-exact), so its mode-0 decisions are the GPU's
+        bad = _unexplained(gpu, ref if fr_b is fr_ref else fma, fr_ref, fr_b)
+        assert not bad, (name, "pixels above 1e-4 without a threshold flip", bad)
