@@ -608,4 +608,59 @@ __device__ __forceinline__ float wave_reduce10_rs(const float (&v)[10])
     return w;
 }
 
+// Reduce-scatter of two splats' ten moments each (a = values 0-9, b = values 10-19) in one pass: FOLD8 of the ten
+// pairs, FOLD4 of five, permlane32 swaps fold 5 -> 3, permlane16 swaps 3 -> 2, quad_perm adds finish both.  34 DPP adds,
+// 5 permlane swaps and 5 adds, where two wave_reduce10_rs take 36, 6 and 6 (and 8 s_nop).  Every lane of row rho, bank
+// beta ends with the total of value reduce20_index(rho, beta, 0) in w0 and of reduce20_index(rho, beta, 1) in w1
+// (-1: none); the mapping was derived by simulating the lane operations (tools/diag/reduce_layout.py).
+__device__ __forceinline__ int reduce20_index(int rho, int beta, int reg)
+{
+    const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
+    if (reg == 1) return rho == 0 ? 16 + cb : -1;
+    return rho == 0 ? cb : rho == 1 ? 8 + cb : rho == 2 ? 4 + cb : 12 + cb;
+}
+__device__ __forceinline__ void wave_reduce20_rs(const float (&a)[10], const float (&b)[10], float& w0, float& w1)
+{
+    float s[10], t[5], z, z2;
+#define HLGS_FOLD8(d, x, y)                                                                                        \
+    "v_add_f32_dpp " d ", " x ", " x " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
+    "v_add_f32_dpp " d ", " y ", " y " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+#define HLGS_FOLD4(d, x, y)                                                                                        \
+    "v_add_f32_dpp " d ", " x ", " x " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
+    "v_add_f32_dpp " d ", " y ", " y " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
+    asm volatile("s_nop 1\n\t"
+                 HLGS_FOLD8("%0", "%19", "%20") HLGS_FOLD8("%1", "%21", "%22") HLGS_FOLD8("%2", "%23", "%24")
+                 HLGS_FOLD8("%3", "%25", "%26") HLGS_FOLD8("%4", "%27", "%28") HLGS_FOLD8("%5", "%29", "%30")
+                 HLGS_FOLD8("%6", "%31", "%32") HLGS_FOLD8("%7", "%33", "%34") HLGS_FOLD8("%8", "%35", "%36")
+                 HLGS_FOLD8("%9", "%37", "%38")
+                 "v_mov_b32 %15, 0\n\t"
+                 "v_mov_b32 %16, 0\n\t"
+                 HLGS_FOLD4("%10", "%0", "%1") HLGS_FOLD4("%11", "%2", "%3") HLGS_FOLD4("%12", "%4", "%5")
+                 HLGS_FOLD4("%13", "%6", "%7") HLGS_FOLD4("%14", "%8", "%9")
+                 "v_permlane32_swap_b32 %10, %11\n\t"  // t1 written six instructions back
+                 "v_add_f32 %10, %10, %11\n\t"         // rows 0-1: t0, rows 2-3: t1
+                 "v_permlane32_swap_b32 %12, %13\n\t"
+                 "v_add_f32 %12, %12, %13\n\t"         // rows 0-1: t2, rows 2-3: t3
+                 "v_permlane32_swap_b32 %14, %15\n\t"
+                 "v_add_f32 %14, %14, %15\n\t"         // rows 0-1: t4, rows 2-3: 0
+                 "v_permlane16_swap_b32 %10, %12\n\t"  // t2 written two instructions back
+                 "v_add_f32 %17, %10, %12\n\t"         // rows: t0, t2, t1, t3
+                 "v_permlane16_swap_b32 %14, %16\n\t"
+                 "v_add_f32 %18, %14, %16\n\t"         // row 0: t4
+                 "v_add_f32_dpp %17, %17, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 0\n\t"
+                 "v_add_f32_dpp %18, %18, %18 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "v_add_f32_dpp %17, %17, %17 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 0\n\t"
+                 "v_add_f32_dpp %18, %18, %18 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                 : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5]), "=&v"(s[6]),
+                   "=&v"(s[7]), "=&v"(s[8]), "=&v"(s[9]), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]),
+                   "=&v"(t[4]), "=&v"(z), "=&v"(z2), "=&v"(w0), "=&v"(w1)
+                 : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
+                   "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]),
+                   "v"(b[8]), "v"(b[9]));
+#undef HLGS_FOLD8
+#undef HLGS_FOLD4
+}
+
 }  // namespace hlgs

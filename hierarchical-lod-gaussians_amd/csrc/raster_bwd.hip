@@ -186,6 +186,35 @@ struct BwdArgs {
 // 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
 // whose n_contrib lies behind it) run bwd_pass, the ten moments are folded over the wave, and one record per
 // (tile, splat) is stored after the batch.
+// Traffic-attribution switches (tools/ab_fetch.sh, timing and counters only; each breaks parity): skip the
+// point_offsets gather, the per-pixel inputs, the split-state reads, or the record stores.
+#ifndef HLGS_BWD_NT_LOAD
+#define HLGS_BWD_NT_LOAD 0
+#endif
+#ifndef HLGS_BWD_NT_STORE
+#define HLGS_BWD_NT_STORE 0
+#endif
+#ifndef HLGS_DIAG_BWD_FAKE_SBASE
+#define HLGS_DIAG_BWD_FAKE_SBASE 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_GATHER
+#define HLGS_DIAG_BWD_NO_GATHER 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_PIXIN
+#define HLGS_DIAG_BWD_NO_PIXIN 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_SPLIT
+#define HLGS_DIAG_BWD_NO_SPLIT 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_STORE
+#define HLGS_DIAG_BWD_NO_STORE 0
+#endif
+#ifndef HLGS_BWD_PAIR
+#define HLGS_BWD_PAIR 0  // two visited splats per loop iteration, one twenty-moment reduction (wave_reduce20_rs)
+#endif
+#ifndef HLGS_BWD_MSTRIDE
+#define HLGS_BWD_MSTRIDE 65
+#endif
 #ifndef HLGS_BWD_WAVES
 #define HLGS_BWD_WAVES 5  // waves per SIMD: 96 VGPRs
 #endif
@@ -209,7 +238,11 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
     __shared__ float4 s_col[64];  // r, g, b, alpha threshold on e2
     __shared__ float2 s_tf[64];   // interpolation t, 1/kids
-    __shared__ float s_m[64 * 11];  // reduced moments per splat (+ a spare row the non-storing lanes write)
+    // reduced moments per splat (+ a spare row the non-storing lanes write), rows padded to kMStride = 65 floats: the
+    // ten lanes holding totals store moment v of splat j at kMStride v + j, on ten different banks ((v + j) mod 32),
+    // where a 64-float stride put all ten (and the spare row) on bank j mod 32
+    constexpr int kMStride = HLGS_BWD_MSTRIDE;
+    __shared__ float s_m[kMStride * 11];
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
     const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
@@ -225,9 +258,22 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
     const float lx = (float)(tx0 + (lane & 7)), ly = (float)(ty0 + (lane >> 3));
     // the reduced moment this lane stores (wave_reduce10_rs layout) as an offset into s_m; lanes holding no total
-    // store into the spare row s_m[640..703]
+    // store into the spare row s_m[10 kMStride ..]
     const int wm_i = (lane & 3) ? -1 : reduce10_index(lane >> 4, (lane >> 2) & 3);
-    const int wmd = wm_i < 0 ? 640 : 64 * wm_i;
+    const int wmd = wm_i < 0 ? 10 * kMStride : kMStride * wm_i;
+#if HLGS_BWD_PAIR
+    // wave_reduce20_rs layout: this lane's two totals, each a moment of the pair's first (A) or second (B) splat
+    int wmd0, wmd1;
+    bool w0b, w1b;
+    {
+        const int v0 = (lane & 3) ? -1 : reduce20_index(lane >> 4, (lane >> 2) & 3, 0);
+        const int v1 = (lane & 3) ? -1 : reduce20_index(lane >> 4, (lane >> 2) & 3, 1);
+        wmd0 = v0 < 0 ? 10 * kMStride : kMStride * (v0 % 10);
+        wmd1 = v1 < 0 ? 10 * kMStride : kMStride * (v1 % 10);
+        w0b = v0 >= 10;
+        w1b = v1 >= 10;
+    }
+#endif
 
     // lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant k
     PixB ps[4];
@@ -238,6 +284,12 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         const bool inside = px < W && py < H;
         const size_t pid = (size_t)W * py + px;
         PixB& p = ps[k];
+#if HLGS_DIAG_BWD_NO_PIXIN  // traffic attribution only (tools/ab_fetch.sh): no per-pixel input reads, parity broken
+        const float tf = inside ? 0.5f : 0.f;
+        p.T = tf;
+        p.last = inside ? count : 0u;
+        p.dr = p.dg = p.db = p.dinv = inside ? 0.1f : 0.f;
+#else
         const float tf = inside ? final_Ts[pid] : 0.f;
         p.T = tf;
         p.last = inside ? n_contrib[pid] : 0u;
@@ -245,6 +297,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         p.dg = inside ? dL_dpixels[HW + pid] : 0.f;
         p.db = inside ? dL_dpixels[2 * HW + pid] : 0.f;
         p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
+#endif
         float bgd = 0.f;
         bgd += bg[0] * p.dr;
         bgd += bg[1] * p.dg;
@@ -253,7 +306,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         // (alt-rasterizer backward.cu:608, 619): the background enters dL/dalpha twice
         if (ALT) bgd *= 2.f;
         p.ARD = bgd;  // T_final <bg, dL/dpixel> / T_final
-        if (p.last > cnt) {  // still blending at the chunk's end (so the forward sampled it there, with T >= 1e-4)
+        if (p.last > cnt && !HLGS_DIAG_BWD_NO_SPLIT) {  // still blending at the chunk's end (so the forward sampled it there)
             const float* sk = st + k * 5 * 64;
             p.T = sk[0];
             float behind = sk[64] * p.dr + sk[128] * p.dg + sk[192] * p.db;
@@ -281,8 +334,21 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                 id >>= kEntryShift;
             }
             const float4* sr = g.splat + 4 * (size_t)id;
-            const uint32_t sbase = id ? g.point_offsets[id - 1] : 0u;
+#if HLGS_DIAG_BWD_FAKE_SBASE  // traffic attribution: slots spread by id, no point_offsets gather (parity broken)
+            const uint32_t sbase = id;
+#else
+            const uint32_t sbase = (id && !HLGS_DIAG_BWD_NO_GATHER) ? g.point_offsets[id - 1] : 0u;
+#endif
+#if HLGS_BWD_NT_LOAD  // records streamed past L2 (no reuse across tile waves), so point_offsets stays resident
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            const v4f* srv = reinterpret_cast<const v4f*>(sr);
+            const v4f q0 = __builtin_nontemporal_load(srv), q1 = __builtin_nontemporal_load(srv + 1),
+                      q2 = __builtin_nontemporal_load(srv + 2), q3 = __builtin_nontemporal_load(srv + 3);
+            const float4 r0 = make_float4(q0.x, q0.y, q0.z, q0.w), r1 = make_float4(q1.x, q1.y, q1.z, q1.w),
+                         r2 = make_float4(q2.x, q2.y, q2.z, q2.w), r3 = make_float4(q3.x, q3.y, q3.z, q3.w);
+#else
             const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
+#endif
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
             qm = pack ? pm : quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
             s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
@@ -296,7 +362,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
             slot = sbase + (uint32_t)((ty - y0) * w + (tx - x0));
         }
 #pragma unroll
-        for (int v = 0; v < 10; v++) s_m[64 * v + lane] = 0.f;
+        for (int v = 0; v < 10; v++) s_m[kMStride * v + lane] = 0.f;
         __syncthreads();
         // a batch entirely behind every pixel's last contributor leaves its records zero
         const uint32_t li_bot = li_top - (uint32_t)(n - 1);
@@ -322,11 +388,10 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                 int j = __builtin_ctzll(todo);
                 float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
                 float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
-                while (true) {
-                    int jn;  // s_ff1: -1 once todo is empty
-                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
-                    const uint32_t li = li_top - (uint32_t)j;
-                    float acc[10];
+                // the quadrants splat jj visits, in quadrant order (uniform branches), into acc
+                auto passes = [&](int jj, const float4& pxy, const float4& pco, const float4& pcol, const float2& ptf,
+                                  float(&acc)[10]) {
+                    const uint32_t li = li_top - (uint32_t)jj;
 #pragma unroll
                     for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
                         uint64_t z;
@@ -334,11 +399,49 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                         acc[v] = __uint_as_float((uint32_t)z);
                         acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
                     }
-                    // uniform branches: the quadrants this splat visits, in quadrant order
-                    if ((qv[0] >> j) & 1u) bwd_pass<INTERP, DEPTH, ALT, 0>(ps, li, lx, ly, xy, co, col, tf, acc);
-                    if ((qv[1] >> j) & 1u) bwd_pass<INTERP, DEPTH, ALT, 1>(ps, li, lx, ly, xy, co, col, tf, acc);
-                    if ((qv[2] >> j) & 1u) bwd_pass<INTERP, DEPTH, ALT, 2>(ps, li, lx, ly, xy, co, col, tf, acc);
-                    if ((qv[3] >> j) & 1u) bwd_pass<INTERP, DEPTH, ALT, 3>(ps, li, lx, ly, xy, co, col, tf, acc);
+                    if ((qv[0] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 0>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+                    if ((qv[1] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 1>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+                    if ((qv[2] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 2>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+                    if ((qv[3] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 3>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+                };
+#if HLGS_BWD_PAIR
+                // Two visited splats per iteration, their twenty moments folded by one reduce-scatter
+                // (wave_reduce20_rs): 34 DPP adds and 5 permlane swaps where two ten-moment reductions take 36 and 6
+                while (true) {
+                    int jn;  // s_ff1: -1 once todo is empty
+                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
+                    float accA[10];
+                    passes(j, xy, co, col, tf, accA);
+                    if (jn < 0) {
+                        s_m[wmd + j] = wave_reduce10_rs(accA);
+                        break;
+                    }
+                    float accB[10];
+                    {
+                        const float4 xyB = s_xy[jn], coB = s_q[jn], colB = s_col[jn];
+                        const float2 tfB = INTERP ? s_tf[jn] : make_float2(0.f, 0.f);
+                        int jn2;
+                        asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn2) : "s"(jn));
+                        passes(jn, xyB, coB, colB, tfB, accB);
+                        const int jl = jn2 < 0 ? 0 : jn2;  // the next pair's first splat, read ahead of the reduction
+                        xy = s_xy[jl];
+                        co = s_q[jl];
+                        col = s_col[jl];
+                        if (INTERP) tf = s_tf[jl];
+                        float w0, w1;
+                        wave_reduce20_rs(accA, accB, w0, w1);
+                        s_m[wmd0 + (w0b ? jn : j)] = w0;
+                        s_m[wmd1 + (w1b ? jn : j)] = w1;
+                        if (jn2 < 0) break;
+                        j = jn2;
+                    }
+                }
+#else
+                while (true) {
+                    int jn;  // s_ff1: -1 once todo is empty
+                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
+                    float acc[10];
+                    passes(j, xy, co, col, tf, acc);
                     const int jl = jn < 0 ? 0 : jn;  // the next visited splat's LDS reads ahead of the reduction
                     xy = s_xy[jl];
                     co = s_q[jl];
@@ -349,20 +452,29 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                     if (jn < 0) break;
                     j = jn;
                 }
+#endif
             }
         }
         __syncthreads();
-        if (lane_valid) {
+        if (lane_valid && !HLGS_DIAG_BWD_NO_STORE) {
             float m[10];
 #pragma unroll
-            for (int v = 0; v < 10; v++) m[v] = s_m[64 * v + lane];
+            for (int v = 0; v < 10; v++) m[v] = s_m[kMStride * v + lane];
             float4 ra, rb;
             float2 rc;
             finish_record(m, my_co, ddelx_dx, ddely_dy, ra, rb, rc);
             float4* r = rec.rec + 3 * (size_t)slot;
+#if HLGS_BWD_NT_STORE
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            v4f* rv = reinterpret_cast<v4f*>(r);
+            __builtin_nontemporal_store(v4f{ra.x, ra.y, ra.z, ra.w}, rv);
+            __builtin_nontemporal_store(v4f{rb.x, rb.y, rb.z, rb.w}, rv + 1);
+            __builtin_nontemporal_store(v4f{rc.x, rc.y, 0.f, 0.f}, rv + 2);
+#else
             r[0] = ra;
             r[1] = rb;
             r[2] = make_float4(rc.x, rc.y, 0.f, 0.f);
+#endif
         }
         __syncthreads();
     }

@@ -41,6 +41,34 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
+def launch_timing(trace_csv, bench_line, kernel="k_blend_bwd<false, true, false>"):
+    """Durations of one kernel from the kernel trace of the bench command, cut into the phases its JSON line's
+    launch_plan names (warm-up, stage-timing pass, timed steps, and the last `evented` timed steps whose launches the
+    bench brackets with HIP events), beside the bench's own event time for those launches (roofline.kernel_ms): the
+    reconciliation of the event time with the rocprof averages."""
+    rows = []
+    for r in csv.DictReader(open(trace_csv)):
+        if kernel in r["Kernel_Name"]:
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    rows.sort()
+    us = [(e - b) / 1e3 for b, e in rows]
+    plan = bench_line.get("launch_plan") or {}
+    w, st, k, ev = (int(plan.get(x, 0)) for x in ("warmup", "stage_timing", "timed", "evented"))
+    st += int(plan.get("settle", 0))  # the clock-settle steps run between the stage pass and the timed steps
+    avg = lambda v: round(sum(v) / len(v), 2) if v else None  # noqa: E731
+    timed = us[w + st:w + st + k]
+    out = dict(kernel=kernel, launches=len(us), all_avg_us=avg(us), warmup_avg_us=avg(us[:w]),
+               stage_and_settle_avg_us=avg(us[w:w + st]), settle_steps=int(plan.get("settle", 0)), timed_avg_us=avg(timed), timed_min_us=min(timed) if timed else None,
+               timed_max_us=max(timed) if timed else None, evented_avg_us=avg(timed[k - ev:]) if ev else None,
+               after_timed_avg_us=avg(us[w + st + k:]),
+               bench_event_us=round(1e3 * bench_line["roofline"]["kernel_ms"], 2) if bench_line.get("roofline") else None,
+               timed_gaps_us=None)
+    if len(rows) >= w + st + k and k > 1:
+        seg = rows[w + st:w + st + k]
+        out["timed_gaps_us"] = avg([(seg[i + 1][0] - seg[i][1]) / 1e3 for i in range(len(seg) - 1)])
+    return out
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
@@ -58,6 +86,9 @@ def main(src, dst):
     if os.path.exists(traced):
         line = [l for l in open(traced).read().splitlines() if l.startswith("{")][-1]
         open(os.path.join(dst, "bench_line_under_rocprof.json"), "w").write(line + "\n")
+        tr = os.path.join(src, "trace", "run_kernel_trace.csv")
+        if os.path.exists(tr):
+            json.dump(launch_timing(tr, json.loads(line)), open(os.path.join(dst, "timing.json"), "w"), indent=1)
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     sqp = os.path.join(src, "sq", "run_counter_collection.csv")
