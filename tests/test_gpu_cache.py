@@ -246,3 +246,43 @@ def test_spt_cache_view_batches_match_restatement(views):
     # the union cut of a batch holds at least as many Gaussians as the cut of its first view alone
     single = _Oracle(b, storage, sky, 0.9, 10 ** 9)
     assert sizes[0] >= len(single.step(batches[0][0])["render_indices"])
+
+
+_UNION_SCENE = []
+
+
+def _union_scene():
+    if not _UNION_SCENE:
+        import bench
+        _UNION_SCENE.append(bench.merged_two_chunk_scene(200_000)[:2])
+    return _UNION_SCENE[0]
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_union_cut_semantics_and_cost(G):
+    """What the config #5 union cut does to each rank's view, pinned at a reduced size
+    of bench.py's config5 workload (a 2-chunk merged hierarchy over 200k leaves; the views of its N > 1 leg, rank r's
+    camera offset 0.4 units sideways).  Measured at the bench's 1M leaves (profiles/r04/union_cut.json, G = 8): the union
+    resident set is 1.009x the mean of the views' own cuts, raster time +1-4%, cache rows moved +6%, and every view
+    rendered from the union set is within 43-46 dB PSNR of its own cut's image.  Here: a one-view batch is the view's own
+    cut bit for bit; the union holds at most 3% more Gaussians than the largest own cut; rendered from the union set each
+    view stays above 38 dB PSNR of its own cut's image (the finest LOD any view needs replaces coarser nodes)."""
+    from tools_free_render import render_alt
+    from hlgs_core.spt_cache import SPTCache
+    b, storage = _union_scene()
+    cache = SPTCache(storage, b, 0, reuse_tolerance=0.9, device=DEV)
+    W, H = 480, 270
+    cams = [S.make_camera(W, H, T=np.array([0.09 + 0.4 * r, 0.03, 0.2 * np.sin(0.9)])) for r in range(G)]
+    batch = lambda cs: (torch.stack([c["projmatrix"] for c in cs]).to(DEV),  # noqa: E731
+                        torch.stack([c["campos"] for c in cs]).to(DEV))
+    union = cache.plan(*batch(cams))["render_indices"]
+    own = [cache.plan(*batch([c]))["render_indices"] for c in cams]
+    np.testing.assert_array_equal(cache.plan(*batch(cams[:1]))["render_indices"].cpu().numpy(), own[0].cpu().numpy())
+    assert union.numel() <= 1.03 * max(o.numel() for o in own), (union.numel(), [o.numel() for o in own])
+    gather = lambda idx: {k: storage[k][idx.long().cpu()].to(DEV).contiguous() for k in NAMES}  # noqa: E731
+    pu = gather(union)
+    for c, o in zip(cams, own):
+        iu, io = render_alt(pu, c, DEV), render_alt(gather(o), c, DEV)
+        mse = float(((iu.clamp(0, 1) - io.clamp(0, 1)) ** 2).mean())
+        psnr = 10 * np.log10(1.0 / max(mse, 1e-12))
+        assert psnr >= 38.0, psnr
