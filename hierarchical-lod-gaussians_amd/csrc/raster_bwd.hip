@@ -12,6 +12,17 @@
 #include "hlgs_internal.h"
 #include "hlgs_math.h"
 
+#ifndef HLGS_BWD_ZERO_LDS
+#define HLGS_BWD_ZERO_LDS 1  // accumulators zeroed by LDS reads, not v_mov_b64 (the VALU pipe is the limit)
+#endif
+#ifndef HLGS_BWD_OPQ
+#define HLGS_BWD_OPQ 0  // 1: the 0.99-clamp factor only for splats whose opacity exceeds 0.99f (a uniform branch per
+                        // pass: 358.8-359.1 against 356.4-356.8 us without it; not kept)
+#endif
+#ifndef HLGS_BWD_PK
+#define HLGS_BWD_PK 0  // packed-FP32 moment updates (v_pk_mul / v_pk_add / v_pk_fma on moment pairs)
+#endif
+
 namespace hlgs {
 
 // Per-pixel state of the back-to-front replay (backward.cu:549-572).  The reference keeps the
@@ -79,8 +90,11 @@ struct BwdFront {
     uint64_t ok;  // wave mask: alpha >= 1/255 (alpha_e2_threshold)
 };
 
+// clampable: wave-uniform, the splat's opacity exceeds 0.99f.  Otherwise o G <= o <= 0.99f for every kept pair
+// (G = exp2(e2) <= 1 for e2 <= 0), below_clamp is 1, and the two VALU it costs per pass are skipped (HLGS_BWD_OPQ).
 template <bool INTERP, bool ALT>
-__device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& q, float tt, float fr, float thr)
+__device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& q, float tt, float fr, float thr,
+                                              bool clampable = true)
 {
     BwdFront f;
     f.dx = dx;
@@ -88,11 +102,20 @@ __device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& 
     const float e2 = splat_e2(q, dx, dy);  // power * log2(e)
     float G = __builtin_amdgcn_exp2f(e2);
     const float test_alpha = q.w * G;
+#if HLGS_BWD_OPQ
+    // min(0.99f, o G) as one v_min_f32 (fminf across the clamp branch below otherwise gets a canonicalising v_max)
+    asm("v_min_f32 %0, 0x3f7d70a4, %1" : "=v"(f.my_alpha) : "v"(test_alpha));
+#else
     f.my_alpha = fminf(0.99f, test_alpha);
+#endif
     f.alpha = f.my_alpha;
     if (INTERP) f.alpha = tt * f.my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - f.my_alpha, fr));
     f.r1m = rcp_one_minus(f.alpha);
-    if (!ALT) G *= below_clamp(test_alpha);
+    if (!ALT && clampable) {
+        float b = below_clamp(test_alpha);
+        asm volatile("" : "+v"(b));  // not speculatable: a scalar branch around two VALU, not a select after them
+        G *= b;
+    }
     f.G = G;
     // as wave masks: one v_cmp per test, combined in SALU (the wave is full)
     f.ok = ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < thr);
@@ -116,12 +139,37 @@ __device__ __forceinline__ void bwd_back(PixB& p, uint32_t li, const BwdFront& f
         if (DEPTH) cd += invz * p.dinv;
         const float raw = cd - p.ARD;
         p.ARD = fmaf(alpha, raw, p.ARD);
-        acc[6] = fmaf(weight, p.dr, acc[6]);
-        acc[7] = fmaf(weight, p.dg, acc[7]);
-        acc[8] = fmaf(weight, p.db, acc[8]);
-        if (DEPTH) acc[9] = fmaf(weight, p.dinv, acc[9]);
+#if HLGS_BWD_PK
+        if (!INTERP && DEPTH) {
+            typedef float v2f __attribute__((ext_vector_type(2)));
+            v2f a67 = {acc[6], acc[7]}, a89 = {acc[8], acc[9]};
+            a67 = __builtin_elementwise_fma(v2f{weight, weight}, v2f{p.dr, p.dg}, a67);
+            a89 = __builtin_elementwise_fma(v2f{weight, weight}, v2f{p.db, p.dinv}, a89);
+            acc[6] = a67.x; acc[7] = a67.y; acc[8] = a89.x; acc[9] = a89.y;
+        } else
+#endif
+        {
+            acc[6] = fmaf(weight, p.dr, acc[6]);
+            acc[7] = fmaf(weight, p.dg, acc[7]);
+            acc[8] = fmaf(weight, p.db, acc[8]);
+            if (DEPTH) acc[9] = fmaf(weight, p.dinv, acc[9]);
+        }
         const float dL_dalpha = raw * p.T;
         const float w = f.G * dL_dalpha;
+#if HLGS_BWD_PK
+        if (!INTERP) {  // the same IEEE products and sums, two per instruction
+            typedef float v2f __attribute__((ext_vector_type(2)));
+            const v2f dxy = {dx, dy};
+            const v2f wd = v2f{w, w} * dxy;
+            v2f a01 = {acc[0], acc[1]}, a23 = {acc[2], acc[3]};
+            a01 += wd;
+            a23 = __builtin_elementwise_fma(v2f{wd.x, wd.x}, dxy, a23);
+            acc[0] = a01.x; acc[1] = a01.y; acc[2] = a23.x; acc[3] = a23.y;
+            acc[4] = fmaf(wd.y, dy, acc[4]);
+            acc[5] += w;
+            return;
+        }
+#endif
         const float wdx = w * dx, wdy = w * dy;
         acc[0] += wdx;
         acc[1] += wdy;
@@ -137,9 +185,10 @@ __device__ __forceinline__ void bwd_back(PixB& p, uint32_t li, const BwdFront& f
 // transcendental latency overlaps the compare -> SALU -> exec chain that decides the branch instead of following it.
 template <bool INTERP, bool DEPTH, bool ALT, int K>
 __device__ __forceinline__ void bwd_pass(PixB (&ps)[4], uint32_t li, float lx, float ly, const float4& xy, const float4& q,
-                                         const float4& col, float2 tf, float (&acc)[10])
+                                         const float4& col, float2 tf, float (&acc)[10], bool clampable)
 {
-    BwdFront f = bwd_front<INTERP, ALT>(xy.x - (lx + 8.f * (K & 1)), xy.y - (ly + 8.f * (K >> 1)), q, tf.x, tf.y, col.w);
+    BwdFront f = bwd_front<INTERP, ALT>(xy.x - (lx + 8.f * (K & 1)), xy.y - (ly + 8.f * (K >> 1)), q, tf.x, tf.y, col.w,
+                                        clampable);
 #if HLGS_BWD_HOIST
     asm volatile("" : "+v"(f.G), "+v"(f.r1m), "+v"(f.alpha));  // keep them above the branch
 #endif
@@ -209,6 +258,9 @@ struct BwdArgs {
 #ifndef HLGS_DIAG_BWD_NO_STORE
 #define HLGS_DIAG_BWD_NO_STORE 0
 #endif
+#ifndef HLGS_DIAG_BWD_NO_ZERO
+#define HLGS_DIAG_BWD_NO_ZERO 0
+#endif
 #ifndef HLGS_BWD_PAIR
 #define HLGS_BWD_PAIR 0  // two visited splats per loop iteration, one twenty-moment reduction (wave_reduce20_rs)
 #endif
@@ -243,6 +295,10 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     // where a 64-float stride put all ten (and the spare row) on bank j mod 32
     constexpr int kMStride = HLGS_BWD_MSTRIDE;
     __shared__ float s_m[kMStride * 11];
+#if HLGS_BWD_ZERO_LDS
+    __shared__ float4 s_zero[3];
+    if (threadIdx.x < 3) s_zero[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);  // ordered by the batch barrier
+#endif
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
     const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
@@ -381,6 +437,8 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                 qv[k] = m;
             }
             uint64_t todo = qv[0] | qv[1] | qv[2] | qv[3];
+            // the batch's splats whose opacity can reach the 0.99 clamp (bit j: splat j)
+            const uint64_t opq = __ballot(lane_valid && my_co.w > 0.99f);
             // Splat loop with the least scalar bookkeeping: the visited bit is cleared (s_bitset0), the next visited
             // splat found by s_ff1 (-1 once none is left; its LDS reads use index 0 then), and every visited splat
             // is reduced (0.15% of them have no valid pair), so no per-pass wave-mask tracking.
@@ -392,6 +450,20 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                 auto passes = [&](int jj, const float4& pxy, const float4& pco, const float4& pcol, const float2& ptf,
                                   float(&acc)[10]) {
                     const uint32_t li = li_top - (uint32_t)jj;
+#if HLGS_BWD_ZERO_LDS
+                    // the ten accumulators zeroed by three LDS reads of a zero block (the LDS pipe, ~29% busy here)
+                    // instead of five v_mov_b64 on the VALU pipe, which this kernel saturates
+                    {
+                        typedef float v4f __attribute__((ext_vector_type(4)));
+                        typedef __attribute__((address_space(3))) const volatile v4f lds_v4f;  // stays a ds_read
+                        lds_v4f* vz = (lds_v4f*)(s_zero);
+                        const v4f z0 = vz[0], z1 = vz[1], z2 = vz[2];
+                        acc[0] = z0.x; acc[1] = z0.y; acc[2] = z0.z; acc[3] = z0.w;
+                        acc[4] = z1.x; acc[5] = z1.y; acc[6] = z1.z; acc[7] = z1.w;
+                        acc[8] = z2.x; acc[9] = z2.y;
+                    }
+#elif HLGS_DIAG_BWD_NO_ZERO  // timing only: accumulators not reset between splats (parity broken)
+#else
 #pragma unroll
                     for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
                         uint64_t z;
@@ -399,10 +471,13 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                         acc[v] = __uint_as_float((uint32_t)z);
                         acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
                     }
-                    if ((qv[0] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 0>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
-                    if ((qv[1] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 1>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
-                    if ((qv[2] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 2>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
-                    if ((qv[3] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 3>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+#endif
+                    // wave-uniform (scalar mask); the hierarchy-mode kernels keep the factor (no VGPRs for the branch)
+                    const bool clampable = !HLGS_BWD_OPQ || INTERP || ((opq >> jj) & 1u);
+                    if ((qv[0] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 0>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
+                    if ((qv[1] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 1>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
+                    if ((qv[2] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 2>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
+                    if ((qv[3] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 3>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
                 };
 #if HLGS_BWD_PAIR
                 // Two visited splats per iteration, their twenty moments folded by one reduce-scatter
@@ -437,10 +512,13 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
                     }
                 }
 #else
+                float acc[10];  // (reset by passes() for every splat)
+#if HLGS_DIAG_BWD_NO_ZERO
+                for (int v = 0; v < 10; v++) acc[v] = 0.f;
+#endif
                 while (true) {
                     int jn;  // s_ff1: -1 once todo is empty
                     asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
-                    float acc[10];
                     passes(j, xy, co, col, tf, acc);
                     const int jl = jn < 0 ? 0 : jn;  // the next visited splat's LDS reads ahead of the reduction
                     xy = s_xy[jl];

@@ -12,12 +12,15 @@
 constexpr int ITERS = 1024;
 
 enum Kind { FMA, FMAC, MUL_SGPR, CNDMASK_VCC, CMP_SGPR, DPP_ADD, EXP, PERMLANE32, MIX_SALU, MIX_EXP, MIX_DPP, MIX_CMP,
-            MIX_CND, MOV, CND_E64, CND_VCC_SET, CND_E64_SET, PK_FMA, PK_MUL, DPP_BCAST31, PERMLANE16, MIX_PK, NKINDS };
+            MIX_CND, MOV, CND_E64, CND_VCC_SET, CND_E64_SET, PK_FMA, PK_MUL, DPP_BCAST31, PERMLANE16, MIX_PK,
+            FMA_HALF_LO, FMA_HALF_HI, FMA_QUARTER, FMA_ODD, EXP_HALF, NKINDS };
 static const char* kNames[] = {"v_fma_f32", "v_fmac_f32", "v_mul_f32 sgpr", "v_cndmask vcc", "v_cmp->sgpr",
                                "v_add_f32_dpp", "v_exp_f32", "v_permlane32_swap", "fma+s_and 1:1", "fma+exp 3:1",
                                "fma+dpp 1:1", "fma+cmp 1:1", "fma+cndmask 1:1", "v_mov_b32", "v_cndmask_e64 s[10:11]",
                                "v_cndmask vcc (vcc set)", "v_cndmask_e64 (mask set)", "v_pk_fma_f32",
-                               "v_pk_mul_f32", "v_add_f32_dpp row_bcast:31", "v_permlane16_swap", "fma+pk_fma 1:1"};
+                               "v_pk_mul_f32", "v_add_f32_dpp row_bcast:31", "v_permlane16_swap", "fma+pk_fma 1:1",
+                               "v_fma_f32 exec=lanes 0-31", "v_fma_f32 exec=lanes 32-63", "v_fma_f32 exec=lanes 0-15",
+                               "v_fma_f32 exec=odd lanes", "v_exp_f32 exec=lanes 0-31"};
 
 #define R8(op) op(0) op(1) op(2) op(3) op(4) op(5) op(6) op(7)
 
@@ -33,6 +36,13 @@ __global__ void __launch_bounds__(64) k_issue(float* out, float b, float c)
     const f2 pb = {b, b}, pc = {c, c};
     const uint64_t msk = __builtin_amdgcn_ballot_w64(threadIdx.x & 1);
     if constexpr (K == CND_VCC_SET) asm volatile("v_cmp_lt_f32 vcc, %0, %1\n\ts_nop 4" : : "v"(a[0]), "v"(b) : "vcc");
+    // partial exec masks: the loop body runs under a lane predicate (does the SIMD skip an idle 32-lane half?)
+    bool on = true;
+    if constexpr (K == FMA_HALF_LO || K == EXP_HALF) on = threadIdx.x < 32;
+    if constexpr (K == FMA_HALF_HI) on = threadIdx.x >= 32;
+    if constexpr (K == FMA_QUARTER) on = threadIdx.x < 16;
+    if constexpr (K == FMA_ODD) on = threadIdx.x & 1;
+    if (on)
     for (int it = 0; it < ITERS; it++) {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -86,7 +96,10 @@ __global__ void __launch_bounds__(64) k_issue(float* out, float b, float c)
     if constexpr (K == PERMLANE16) {                                                                              \
         if ((i) & 1) asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(a[((i) + 7) & 7]), "+v"(a[i]));         \
     }                                                                                                             \
-    if constexpr (K == CND_E64_SET) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "s"(msk));
+    if constexpr (K == CND_E64_SET) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "s"(msk));  \
+    if constexpr (K == FMA_HALF_LO || K == FMA_HALF_HI || K == FMA_QUARTER || K == FMA_ODD)                       \
+        asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));                                 \
+    if constexpr (K == EXP_HALF) asm volatile("v_exp_f32 %0, %0" : "+v"(a[i]));
             R8(OP)
 #undef OP
         }
@@ -143,8 +156,15 @@ int main()
     printf("# %s, %d CUs, nominal %.1f GHz\n", p.gcnArchName, p.multiProcessorCount, clk);
     float* out;
     CHK(hipMalloc(&out, (size_t)simds * 8 * 64 * sizeof(float)));
-    if (sweep<FMA>(out, simds, clk) || sweep<PK_FMA>(out, simds, clk) || sweep<PK_MUL>(out, simds, clk) ||
-        sweep<MIX_PK>(out, simds, clk) || sweep<DPP_BCAST31>(out, simds, clk) || sweep<PERMLANE16>(out, simds, clk))
+    if (sweep<FMA_HALF_LO>(out, simds, clk) || sweep<FMA_HALF_HI>(out, simds, clk) ||
+        sweep<FMA_QUARTER>(out, simds, clk) || sweep<FMA_ODD>(out, simds, clk) || sweep<EXP_HALF>(out, simds, clk) ||
+        sweep<EXP>(out, simds, clk) ||
+        sweep<FMA>(out, simds, clk) || sweep<FMAC>(out, simds, clk) || sweep<CMP_SGPR>(out, simds, clk) ||
+        sweep<DPP_ADD>(out, simds, clk) || sweep<EXP>(out, simds, clk) || sweep<PERMLANE32>(out, simds, clk) ||
+        sweep<MIX_SALU>(out, simds, clk) || sweep<MIX_EXP>(out, simds, clk) || sweep<MIX_DPP>(out, simds, clk) ||
+        sweep<MIX_CMP>(out, simds, clk) || sweep<MOV>(out, simds, clk) || sweep<PK_FMA>(out, simds, clk) ||
+        sweep<PK_MUL>(out, simds, clk) || sweep<MIX_PK>(out, simds, clk) || sweep<DPP_BCAST31>(out, simds, clk) ||
+        sweep<PERMLANE16>(out, simds, clk))
         return 1;
     CHK(hipFree(out));
     return 0;
