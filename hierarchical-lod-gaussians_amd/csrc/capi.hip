@@ -373,12 +373,29 @@ struct Readback {
 // Wait until k_plan has mirrored the frame's words (host[3] == seq), polling the coherent pinned words rather than
 // synchronising on an event recorded after k_plan: an event is a queue barrier, ~6 us of idle GPU before the binning.
 // A stream that drains or fails without the words reports an error instead of spinning forever.
-static int wait_plan_words(const uint32_t* host, uint32_t seq, hipStream_t s)
+// HLGS_PLAN_TAGGED: words[i] = the three tagged 64-bit words' low halves once all of them carry seq.
+static bool plan_words_ready(const uint32_t* host, uint32_t seq, uint32_t* words)
+{
+#if HLGS_PLAN_TAGGED
+    const uint64_t* h = reinterpret_cast<const uint64_t*>(host);
+    for (int i = 0; i < 3; i++) {
+        const uint64_t v = __atomic_load_n(&h[i], __ATOMIC_ACQUIRE);
+        if ((uint32_t)(v >> 32) != seq) return false;
+        words[i] = (uint32_t)v;
+    }
+    return true;
+#else
+    if (__atomic_load_n(&host[3], __ATOMIC_ACQUIRE) != seq) return false;
+    for (int i = 0; i < 3; i++) words[i] = host[i];
+    return true;
+#endif
+}
+static int wait_plan_words(const uint32_t* host, uint32_t seq, hipStream_t s, uint32_t* words)
 {
     for (uint32_t n = 1;; n++) {
-        if (__atomic_load_n(&host[3], __ATOMIC_ACQUIRE) == seq) return HLGS_OK;
+        if (plan_words_ready(host, seq, words)) return HLGS_OK;
         if ((n & 1023u) == 0u && hipStreamQuery(s) != hipErrorNotReady) {
-            if (__atomic_load_n(&host[3], __ATOMIC_ACQUIRE) == seq) return HLGS_OK;
+            if (plan_words_ready(host, seq, words)) return HLGS_OK;
             return fail(HLGS_ERR_DEVICE, "the binning plan did not report its sizes");
         }
         __builtin_ia32_pause();
@@ -472,15 +489,17 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     if (spec && (rc = render_launch(a, radii, geom, img, binning, capR, cap_n, out_color, out_invdepth, seen, s,
                                     Guard{im.misc, (uint32_t)capR, cap_n})))
         return rc;
+    uint32_t words[3];
     if (polled) {
-        if ((rc = wait_plan_words(rb->host, seq, s))) return rc;
+        if ((rc = wait_plan_words(rb->host, seq, s, words))) return rc;
     } else {
         HLGS_TRY_HIP(hipEventSynchronize(rb->ev));
+        for (int i = 0; i < 3; i++) words[i] = rb->host[i];
     }
-    const uint32_t R = rb->host[0], maxc = rb->host[1];
+    const uint32_t R = words[0], maxc = words[1];
     rb->last_maxc = maxc;
     info->num_binned = (int)R;
-    info->num_rendered = (int)rb->host[2];
+    info->num_rendered = (int)words[2];
     info->max_tile_count = (int)maxc;
     if (R == 0 && !alt) {  // rasterizer_impl.cu:332-333: the output stays 0 (not bg)
         HLGS_TRY_HIP(hipMemsetAsync(out_color, 0, 3 * sizeof(float) * HW, s));

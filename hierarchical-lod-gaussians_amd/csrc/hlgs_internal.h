@@ -83,7 +83,15 @@ bool lds_binning(int P, int gx, int gy);
 #define HLGS_PACK_ENTRIES 1
 #endif
 constexpr int kEntryShift = 4;
-constexpr int kMiscPack = 3;  // Img::misc word holding the frame's pack_entries(P)
+constexpr int kMiscPack = 3;
+// k_plan's words for the host (R, longest list, record slots) in the pinned read-back slot.  HLGS_PLAN_TAGGED: three
+// 64-bit words, each carrying the frame's sequence number in its high half, written by single-copy-atomic 64-bit stores,
+// so the host waits until all three carry it and the kernel needs no system-scope release (buffer_wbl2: a write-back
+// of the whole L2) to order them.  0: three words, then the sequence number after a system fence.
+#ifndef HLGS_PLAN_TAGGED
+#define HLGS_PLAN_TAGGED 1
+#endif
+  // Img::misc word holding the frame's pack_entries(P)
 bool pack_entries(int P);
 // Does the forward's preprocess (k_preprocess_sh) leave Geom::sh_jac for the SH backward?  Same condition as its launch.
 #ifndef HLGS_SH_JAC

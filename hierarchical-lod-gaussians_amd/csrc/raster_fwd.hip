@@ -814,12 +814,20 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
         misc[1] = s_max;
         misc[2] = slots;
         misc[kMiscPack] = pack;
-        if (host) {  // host[3] = seq last: the host polls it instead of putting an event (a queue barrier) here
+        if (host) {  // the host polls these words instead of putting an event (a queue barrier) here
+#if HLGS_PLAN_TAGGED
+            uint64_t* h = reinterpret_cast<uint64_t*>(host);
+            const uint64_t tag = (uint64_t)seq << 32;
+            h[0] = tag | R;
+            h[1] = tag | s_max;
+            h[2] = tag | slots;
+#else
             host[0] = R;
             host[1] = s_max;
             host[2] = slots;
             __threadfence_system();
             host[3] = seq;  // visible at the latest when the kernel completes
+#endif
         }
     }
 }
@@ -1015,6 +1023,9 @@ struct FwdArgs {
 #ifndef HLGS_FWD_PREFETCH_ID
 #define HLGS_FWD_PREFETCH_ID 1
 #endif
+#ifndef HLGS_FWD_PREFETCH_REC
+#define HLGS_FWD_PREFETCH_REC 1
+#endif
 #ifndef HLGS_FWD_BITSET
 #define HLGS_FWD_BITSET 1
 #endif
@@ -1046,10 +1057,35 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
     // per-lane predicates are kept as wave masks (the wave is always full): compares are ballots of one v_cmp
     // each, their combinations scalar mask operations, and selects read them back with inverse_ballot
     uint64_t done = __builtin_amdgcn_ballot_w64(!(px < A.W && py < A.H));
-#if HLGS_FWD_PREFETCH_ID
+#if HLGS_FWD_PREFETCH_ID && !HLGS_FWD_PREFETCH_REC
     // each batch's list entries are loaded one batch ahead, so a batch waits for one dependent load (its records),
     // not two
     uint32_t next_id = range.x + lane < range.y ? A.point_list[range.x + lane] : 0u;
+#endif
+#if HLGS_FWD_PREFETCH_REC
+    // Software pipeline over batches: while batch b is blended, the records of batch b+1 and the list entries of
+    // batch b+2 are in flight.  Every lane issues every load (a lane with nothing to stage reads record 0, a lane
+    // past the list end re-reads the list's last entry), so the loads retire in a fixed order and the wait at the top
+    // of a batch is for the records alone, not for everything in flight as after a branch round a load.
+    const bool any = range.x < range.y;  // wave-uniform
+    const uint32_t lastpos = any ? range.y - 1 : range.x;
+    auto entry_at = [&](uint32_t p) -> uint32_t { return any ? A.point_list[p < range.y ? p : lastpos] : 0u; };
+    auto decode = [&](uint32_t e, uint32_t p, uint32_t& id) -> bool {
+        bool s = p < range.y;
+        if (A.pack) {
+            s = s && ((e >> q) & 1u);
+            e >>= kEntryShift;
+        }
+        id = e;
+        return s;
+    };
+    uint32_t cur_id, nxt_entry = entry_at(range.x + 64 + lane);
+    bool cur_stage = decode(entry_at(range.x + lane), range.x + lane, cur_id);
+    float4 R0, R1, R2, R3;
+    {
+        const float4* rec = A.splat + 4 * (size_t)(cur_stage ? cur_id : 0u);
+        R0 = rec[0]; R1 = rec[1]; R2 = rec[2]; R3 = rec[3];
+    }
 #endif
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if (done == ~0ull) break;
@@ -1064,6 +1100,22 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
         const uint32_t pos = base + lane;
         uint32_t my_id = 0;
         bool hit = false;
+#if HLGS_FWD_PREFETCH_REC
+        {
+            my_id = cur_id;
+            const float4 co = make_float4(R0.z, R0.w, R1.x, R1.y);
+            hit = cur_stage && (A.pack || touches_quad(R0.x, R0.y, co, R3.w, fqx, fqy));
+            // unconditional: lanes that stage nothing write slots no lane visits
+            s_xy[lane] = make_float4(R0.x, R0.y, DEPTH ? R2.y : 0.f, R3.w);
+            s_co[lane] = conic_q(co);
+            s_col[lane] = make_float4(R1.z, R1.w, R2.x, INTERP ? R2.w : __uint_as_float(base - range.x + lane + 1));
+            if (INTERP) s_t[lane] = R2.z;
+            cur_stage = decode(nxt_entry, pos + 64, cur_id);
+            const float4* rec = A.splat + 4 * (size_t)(cur_stage ? cur_id : 0u);
+            R0 = rec[0]; R1 = rec[1]; R2 = rec[2]; R3 = rec[3];
+            nxt_entry = entry_at(pos + 128);
+        }
+#else
 #if HLGS_FWD_PREFETCH_ID
         my_id = next_id;
         next_id = pos + 64 < range.y ? A.point_list[pos + 64] : 0u;
@@ -1087,6 +1139,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             s_col[lane] = make_float4(r1.z, r1.w, r2.x, INTERP ? r2.w : __uint_as_float(base - range.x + lane + 1));
             if (INTERP) s_t[lane] = r2.z;
         }
+#endif
         uint64_t todo = __ballot(hit);
         __syncthreads();
         uint64_t seen_mask = 0;
