@@ -25,7 +25,7 @@ void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int
 void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s);
 bool lds_binning(int P, int gx, int gy);
 uint32_t* bin_histogram(const Img& im, int P, int gx, int gy);
-void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
+void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, int gx, int gy, bool alt,
                         hipStream_t s, uint32_t* hist);
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
                     int gy, uint32_t max_count, hipStream_t s, bool timing, Guard gd);
@@ -34,7 +34,8 @@ void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
 void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, const BwdScratch& rs,
                       int gx, int gy, const float* dL_dpix, const float* dL_dinv, hipStream_t s);
 void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
-                      const hlgs_grads& o, bool has_depth, hipStream_t s, hipStream_t late, hipEvent_t ev);
+                      const hlgs_grads& o, bool has_depth, hipStream_t s, hipStream_t late, hipEvent_t ev,
+                      const uint32_t* misc);
 void launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t s);
 void launch_sh_from_colour(int P, int V, int D, int M, bool alt, const float* means, const float* campos,
                            const float* drgb, int64_t stride, float scale, float* dsh, float* ddc, hipStream_t s);
@@ -274,6 +275,7 @@ static void* aligned(const void* p) { return (void*)align_up((size_t)p); }
 
 void hlgs_set_entry_packing(int on) { g_entry_packing = on ? HLGS_PACK_ENTRIES : 0; }
 int hlgs_point_list_entry_shift(int P) { return pack_entries(P) ? kEntryShift : 0; }
+int hlgs_point_list_drops_empty(int P) { return pack_entries(P) && HLGS_DROP_EMPTY ? 1 : 0; }
 
 size_t hlgs_binning_point_list_offset(int R)
 {
@@ -310,7 +312,7 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
         launch_preprocess(*a, g, radii, nullptr, gx, gy, ZeroJob{im.tile_count, T, seen, a->P}, s);
         stage_mark(s, ST_PRE, false);
         stage_mark(s, ST_COUNT_TILES, true);
-        launch_count_tiles(a->P, radii, g, im.tile_count, gx, gy, alt, s, bin_histogram(im, a->P, gx, gy));
+        launch_count_tiles(a->P, radii, g, im, gx, gy, alt, s, bin_histogram(im, a->P, gx, gy));
         stage_mark(s, ST_COUNT_TILES, false);
         if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
         stage_mark(s, ST_SCAN, true);
@@ -432,6 +434,7 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     uint32_t misc[3];
     HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipStreamSynchronize(s));
+    if (misc[0] == ~0u) return fail(HLGS_ERR_DEVICE, "the binning plan's look-back timed out");
     info->num_binned = (int)misc[0];
     info->max_tile_count = (int)misc[1];
     info->num_rendered = (int)misc[2];
@@ -497,6 +500,7 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
         for (int i = 0; i < 3; i++) words[i] = rb->host[i];
     }
     const uint32_t R = words[0], maxc = words[1];
+    if (R == ~0u) return fail(HLGS_ERR_DEVICE, "the binning plan's look-back timed out");
     rb->last_maxc = maxc;
     info->num_binned = (int)R;
     info->num_rendered = (int)words[2];
@@ -574,7 +578,7 @@ int hlgs_rasterize_backward_split(const hlgs_raster_args* a, const int* radii, c
     hipEvent_t ev = nullptr;
     if (late && !(ev = handover_event())) return fail(HLGS_ERR_DEVICE, "hipEventCreateWithFlags failed");
     stage_mark(s, ST_GAUSS_BWD, true);
-    launch_gauss_bwd(*a, radii, g, rs, *out, dL_dinvdepth != nullptr, s, late, ev);
+    launch_gauss_bwd(*a, radii, g, rs, *out, dL_dinvdepth != nullptr, s, late, ev, R > 0 ? im.misc : nullptr);
     stage_mark(s, ST_GAUSS_BWD, false);
     if (late && (rc = check_stage(late, a->debug, "sh_bwd"))) return rc;
     return check_stage(s, a->debug, "gauss_bwd");

@@ -52,8 +52,12 @@ __device__ __forceinline__ void cov3d_exact(f3 scale, float mod, float4 q, float
 // backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
 template <bool HIER, bool ALT>
 __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
-                                                   BwdScratch rec, hlgs_grads o, float fx, float fy, int has_depth)
+                                                   BwdScratch rec, hlgs_grads o, float fx, float fy, int has_depth,
+                                                   const uint32_t* __restrict__ misc)
 {
+    // the forward packed its entries (misc[kMiscPack]), so Geom::qmask holds this frame's quadrant masks: a slot whose
+    // mask is 0 holds no record (HLGS_DROP_EMPTY: never binned) or a zero one, and is skipped (rect_tile_mask)
+    const bool masked = misc && misc[kMiscPack];
     const int t_idx = blockIdx.x * 256 + threadIdx.x;
     const bool vis = t_idx < a.P && radii[t_idx] > 0;
     // Gaussians with more than kWide record slots (rects over many tiles) are summed by their whole wave, lane-
@@ -66,6 +70,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
         r_start = r_end - g.tiles_touched[t_idx];
     }
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f, s8 = 0.f, s9 = 0.f;
+    const uint32_t qmasks = (vis && masked) ? g.qmask[t_idx] : 0xFFFFFFFFu;
     {
         uint64_t wide = __ballot(vis && r_end - r_start > kWide);
         const int lane = threadIdx.x & 63;
@@ -87,8 +92,10 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
                 ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
                 kw = __float_as_int(r3.z);
             }
+            const uint32_t wq = (uint32_t)__shfl((int)qmasks, src, 64);
             float p[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             for (uint32_t r = ws + lane; r < we; r += 64) {
+                if (!rect_tile_mask(wq, r - ws)) continue;
                 if (ALT) {
                     const int k = (int)(r - ws);
                     if (!alt_tile_keep(kx, ky, kco, kthr, kx0 + k % kw, ky0 + k / kw)) continue;
@@ -162,7 +169,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t r = r0 + k;
-            use[k] = r < end;
+            use[k] = r < end && rect_tile_mask(qmasks, r - start);
             if (alt && use[k]) {
                 const int kk = (int)(r - start);
                 use[k] = alt_tile_keep(kx, ky, kco, kthr, kx0 + kk % kw, ky0 + kk / kw);
@@ -683,7 +690,8 @@ __global__ void __launch_bounds__(256) k_parent_mean_add(int P, const int* __res
 // hierarchy parent add) run on `late` behind an event on `s`, and are not joined back into `s`: the opacity, scale and
 // rotation gradients are final on `s` while the SH backward still runs (hlgs_rasterize_backward_split).
 void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g, const BwdScratch& rs,
-                      const hlgs_grads& o, bool has_depth, hipStream_t s, hipStream_t late, hipEvent_t ev)
+                      const hlgs_grads& o, bool has_depth, hipStream_t s, hipStream_t late, hipEvent_t ev,
+                      const uint32_t* misc)
 {
     const float fy = a.H / (2.0f * a.tanfovy);
     const float fx = a.W / (2.0f * a.tanfovx);
@@ -711,7 +719,7 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
     default: HLGS_SHK(H, 0, false); break;                                                                 \
     }
     if (a.indices) {
-        hipLaunchKernelGGL((k_gauss_bwd<true, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth);
+        hipLaunchKernelGGL((k_gauss_bwd<true, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy, (int)has_depth, misc);
         hand_over();
         if (a.shs) HLGS_SHB(true)
         if (a.parent_indices)
@@ -720,10 +728,10 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
     } else {
         if (a.variant == HLGS_VARIANT_ALT)
             hipLaunchKernelGGL((k_gauss_bwd<false, true>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy,
-                               (int)has_depth);
+                               (int)has_depth, misc);
         else
             hipLaunchKernelGGL((k_gauss_bwd<false, false>), grid, dim3(256), 0, s, a, radii, g, rs, o, fx, fy,
-                               (int)has_depth);
+                               (int)has_depth, misc);
         hand_over();
         if (a.shs && a.variant == HLGS_VARIANT_ALT) {
             switch (a.M) {  // rest coefficients of degree 1, 2, 3

@@ -83,15 +83,21 @@ bool lds_binning(int P, int gx, int gy);
 #define HLGS_PACK_ENTRIES 1
 #endif
 constexpr int kEntryShift = 4;
-constexpr int kMiscPack = 3;
+constexpr int kMiscPack = 3;  // Img::misc word holding the frame's pack_entries(P)
 // k_plan's words for the host (R, longest list, record slots) in the pinned read-back slot.  HLGS_PLAN_TAGGED: three
 // 64-bit words, each carrying the frame's sequence number in its high half, written by single-copy-atomic 64-bit stores,
 // so the host waits until all three carry it and the kernel needs no system-scope release (buffer_wbl2: a write-back
 // of the whole L2) to order them.  0: three words, then the sequence number after a system fence.
+// HLGS_DROP_EMPTY: with packed entries, an instance whose quadrant mask is 0 (its footprint reaches none of the tile's
+// four 8x8 quadrants, so no pixel of the tile blends it) is not binned: the tile lists, the sort and the blends' staging
+// skip it.  Its record slot stays (point_offsets and num_rendered are unchanged) and is never written; k_gauss_bwd
+// skips the slots whose mask is 0 (their records would be zero).
+#ifndef HLGS_DROP_EMPTY
+#define HLGS_DROP_EMPTY 0
+#endif
 #ifndef HLGS_PLAN_TAGGED
 #define HLGS_PLAN_TAGGED 1
 #endif
-  // Img::misc word holding the frame's pack_entries(P)
 bool pack_entries(int P);
 // Does the forward's preprocess (k_preprocess_sh) leave Geom::sh_jac for the SH backward?  Same condition as its launch.
 #ifndef HLGS_SH_JAC

@@ -231,6 +231,7 @@ struct SplatFoot {
 // Q <= -2 ln2 thr = 2 ln(255 o) (or the lerped bound in hierarchy mode), so the log is already in hand.
 __device__ __forceinline__ SplatFoot splat_foot(float x, float y, float4 co, float thr)
 {
+#pragma clang fp contract(off)
     SplatFoot f;
     f.x = x; f.y = y; f.a = co.x; f.b = co.y; f.c = co.z;
     f.kv = f.ku = f.t = 0.f;
@@ -279,16 +280,20 @@ __device__ __forceinline__ uint32_t quad_mask(float x, float y, float4 co, float
 // The same footprint test in band form, for the key scatter, which classifies every (Gaussian, tile) instance: per
 // 8-row band of the tile, the exact x-extent of the footprint ellipse Q <= t inside the band (the ellipse's
 // rightmost / leftmost point clamped into the band, where the concave chord ends peak), widened by a tolerance far
-// above the rounding of the hardware square roots and reciprocals used here; an 8x8 block is reached iff that extent
-// overlaps its columns.  det = ac - b^2 is formed with Kahan's compensated product so it does not cancel for
-// elongated splats.  The extents are set up once per tile row of the rect (row_bands), so a tile costs four interval
-// tests instead of sixteen edge minimisations.  tools/cull_check.py checks it against brute force like foot_touches.
+// above the rounding of the float operations; an 8x8 block is reached iff that extent overlaps its columns.
+// det = ac - b^2 is formed with Kahan's compensated product so it does not cancel for elongated splats.  The extents
+// are set up once per tile row of the rect (row_bands), so a tile costs four interval tests instead of sixteen edge
+// minimisations.  tools/cull_check.py checks it against brute force like foot_touches.
+// Every operation is IEEE-rounded (correctly rounded square roots and divisions, no contraction; fmaf where written),
+// so the oracle's restatement (oracle/hlgs_oracle.c rect_quad_masks) computes the same masks bit for bit: with
+// HLGS_DROP_EMPTY the masks decide which instances are binned, and the oracle's tile lists must match.
 struct SplatBands {
     float x, y, nb, det, at, ia, vmax, vr, tol;
     int mode;  // as SplatFoot
 };
 __device__ __forceinline__ SplatBands splat_bands(float x, float y, float4 co, float thr)
 {
+#pragma clang fp contract(off)
     const SplatFoot f = splat_foot(x, y, co, thr);
     SplatBands s;
     s.x = x; s.y = y;
@@ -299,25 +304,26 @@ __device__ __forceinline__ SplatBands splat_bands(float x, float y, float4 co, f
     const float bb = b * b, e = fmaf(-b, b, bb);  // e = bb - b^2 exactly
     const float det = fmaf(a, c, -bb) + e;
     if (!(det > 0.f)) { s.mode = 1; return s; }
-    const float idet = __builtin_amdgcn_rcpf(det);
-    s.ia = __builtin_amdgcn_rcpf(a);
-    const float vmax = __builtin_amdgcn_sqrtf(a * t * idet);
+    const float idet = 1.0f / det;
+    s.ia = 1.0f / a;
+    const float vmax = sqrtf(a * t * idet);
     s.nb = -b;
     s.det = det;
     s.at = a * t;
     s.vmax = fmaf(vmax, 1e-4f, vmax) + 1e-3f;
-    s.vr = -b * __builtin_amdgcn_sqrtf(t * idet * __builtin_amdgcn_rcpf(c));
-    s.tol = 2e-3f * (__builtin_amdgcn_sqrtf(s.at) + fabsf(b) * vmax) * s.ia + 2e-3f;
+    s.vr = -b * sqrtf(t * idet * (1.0f / c));
+    s.tol = 2e-3f * (sqrtf(s.at) + fabsf(b) * vmax) * s.ia + 2e-3f;
     return s;
 }
 // The footprint's x-extent [umin, umax] (offsets from the centre) inside the band v in [v0, v0 + 7]; empty: +-3e38.
 __device__ __forceinline__ void band_extent(const SplatBands& s, float v0, float& umin, float& umax)
 {
+#pragma clang fp contract(off)
     const float lo = fmaxf(v0, -s.vmax), hi = fminf(v0 + 7.f, s.vmax);
     if (!(lo <= hi)) { umin = 3e38f; umax = -3e38f; return; }  // empty: overlaps no column
     const float vR = __builtin_amdgcn_fmed3f(s.vr, lo, hi), vL = __builtin_amdgcn_fmed3f(-s.vr, lo, hi);
-    umax = fmaf(s.nb, vR, __builtin_amdgcn_sqrtf(fmaxf(fmaf(-s.det * vR, vR, s.at), 0.f))) * s.ia + s.tol;
-    umin = fmaf(s.nb, vL, -__builtin_amdgcn_sqrtf(fmaxf(fmaf(-s.det * vL, vL, s.at), 0.f))) * s.ia - s.tol;
+    umax = fmaf(s.nb, vR, sqrtf(fmaxf(fmaf(-s.det * vR, vR, s.at), 0.f))) * s.ia + s.tol;
+    umin = fmaf(s.nb, vL, -sqrtf(fmaxf(fmaf(-s.det * vL, vL, s.at), 0.f))) * s.ia - s.tol;
 }
 // One tile row of a Gaussian's rect: the extents in its two 8-row bands, set up once for every tile of the row.
 struct RowBands {
@@ -326,6 +332,7 @@ struct RowBands {
 };
 __device__ __forceinline__ RowBands row_bands(const SplatBands& s, int ty)
 {
+#pragma clang fp contract(off)
     RowBands r;
     r.cx = s.x;
     r.mode = s.mode;
@@ -340,6 +347,7 @@ __device__ __forceinline__ RowBands row_bands(const SplatBands& s, int ty)
 // Quadrant mask of tile column tx in that row: bit q set iff band q >> 1 reaches columns of half q & 1.
 __device__ __forceinline__ uint32_t row_quad_mask(const RowBands& r, int tx)
 {
+#pragma clang fp contract(off)
     if (r.mode) return r.mode == 1 ? 0xFu : 0u;
     const float u0 = (float)(tx * HLGS_TILE) - r.cx, u7 = u0 + 7.f, u8 = u0 + 8.f, u15 = u0 + 15.f;
     return (r.hi0 >= u0 && r.lo0 <= u7 ? 1u : 0u) | (r.hi0 >= u8 && r.lo0 <= u15 ? 2u : 0u) |

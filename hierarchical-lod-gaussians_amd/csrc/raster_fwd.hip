@@ -153,6 +153,7 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
     float opacity = a.opacities[r_idx];
     if (HIER && use_parent) opacity = t * opacity + (1.0f - t) * a.opacities[p_idx];
     g.tiles_touched[t_idx] = area;
+    uint32_t masks = 0xFFFFFFFFu;
     {
         const float cr = col.x, cg = col.y, cbl = col.z;
         const bool interp = a.ts && a.kids;
@@ -163,16 +164,20 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
         rec[2] = make_float4(cbl, 1.f / p_view.z, tt, fr);
         const float thr = alpha_e2_threshold(opacity * h_scale, interp, tt, fr);
         if (g.pack)
-            g.qmask[t_idx] = rect_quad_masks(pix_x, pix_y, make_float4(conic_x, conic_y, conic_z, opacity * h_scale), thr,
-                                             x0, y0, x1, y1);
+            masks = rect_quad_masks(pix_x, pix_y, make_float4(conic_x, conic_y, conic_z, opacity * h_scale), thr, x0, y0,
+                                    x1, y1);
+        if (g.pack) g.qmask[t_idx] = masks;
         rec[3] = make_float4(0.f, __int_as_float(x0 | (y0 << 16)), __int_as_float(x1 - x0), thr);
     }
     if (tile_count) {  // only when the tile grid is too large for the LDS-histogram binning
         const float4 co = make_float4(conic_x, conic_y, conic_z, opacity * h_scale);
         const float kthr = alt ? alt_keep_threshold(co.w) : 0.f;
+        uint32_t r = 0;
         for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++)
-                if (!alt || alt_tile_keep(pix_x, pix_y, co, kthr, x, y)) atomicAdd(&tile_count[y * gx + x], 1u);
+            for (int x = x0; x < x1; x++, r++)
+                if ((!alt || alt_tile_keep(pix_x, pix_y, co, kthr, x, y)) &&
+                    !(g.pack && HLGS_DROP_EMPTY && !rect_tile_mask(masks, r)))
+                    atomicAdd(&tile_count[y * gx + x], 1u);
     }
 }
 
@@ -573,10 +578,11 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
 // hist != nullptr (bin_histogram): the block's per-tile counts are stored as row blockIdx.x of hist (coalesced), and
 // k_tile_offsets turns the rows into per-(block, tile) offsets and tile totals; otherwise they are added to
 // tile_count with one device atomic per non-empty tile.
-template <int BG>
+template <int BG, bool DROP>
 __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
                                                              uint32_t* __restrict__ tile_count, int gx, int gy, int alt,
-                                                             uint32_t* __restrict__ block_tot, uint32_t* __restrict__ hist)
+                                                             uint32_t* __restrict__ block_tot, uint32_t* __restrict__ hist,
+                                                             uint32_t* __restrict__ zero_words, int n_zero)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_pre[BG + 1];
@@ -587,8 +593,11 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     __syncthreads();
     block_rect_prefix<BG>(P, g, s_pre, s_w);
     if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[BG];
-    for_each_instance<BG, false, false>(
-        g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t, uint32_t) { atomicAdd(&s_hist[y * gx + x], 1u); });
+    if (zero_words && blockIdx.x == 0)  // k_tile_offsets_plan's look-back words
+        for (int i = threadIdx.x; i < n_zero; i += BG / 4) zero_words[i] = 0u;
+    for_each_instance<BG, false, DROP>(g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t qm, uint32_t) {
+        if (!DROP || qm) atomicAdd(&s_hist[y * gx + x], 1u);
+    });
     __syncthreads();
     if (hist) {
         uint32_t* row = hist + (size_t)blockIdx.x * T;
@@ -690,8 +699,9 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         const uint32_t* row = hist + (size_t)blockIdx.x * T;
         for (int t = threadIdx.x; t < T; t += (BG / 4)) s_cnt[t] = ranges[t].x + row[t];
     } else {
-        for_each_instance<BG, false, false>(
-            g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t, uint32_t) { atomicAdd(&s_cnt[y * gx + x], 1u); });
+        for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t qm, uint32_t) {
+            if (!(PACK && HLGS_DROP_EMPTY && !qm)) atomicAdd(&s_cnt[y * gx + x], 1u);
+        });
         __syncthreads();
         for (int t = threadIdx.x; t < T; t += (BG / 4)) {
             const uint32_t c = s_cnt[t];
@@ -700,6 +710,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
     }
     __syncthreads();
     for_each_instance<BG, true, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int x, int y, uint32_t qm, uint32_t dbits) {
+        if (PACK && HLGS_DROP_EMPTY && !qm) return;  // the footprint reaches none of the tile's quadrants
         const int tile = y * gx + x;
         const uint32_t r = atomicAdd(&s_rank[tile], 1u);
         const uint32_t entry = PACK ? ((uint32_t)idx << kEntryShift) | qm : (uint32_t)idx;
@@ -832,6 +843,134 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
     }
 }
 
+// k_tile_offsets and k_plan in one launch (HLGS_FUSED_PLAN): each block turns its 32 tiles' histogram columns into
+// block offsets as k_tile_offsets does, publishes its tiles' total and longest list in one 64-bit word (flags[b]:
+// high half 1 << 31 | max, low half total; zeroed by k_count_tiles), and sums its predecessors' published totals for
+// its ranges (a decoupled look-back: every block publishes before it waits, and blocks are dispatched in order, so a
+// waiting block's predecessors are all running or done).  Block 0 scans the count blocks' totals into the scatter's
+// block bases; the last block, which sees every predecessor's word, writes misc and the host words.  One launch and
+// one dependent round trip instead of two launches, the second a single block.
+constexpr uint32_t kPlanPolls = 1u << 20;  // ~0.1 s of polling per word
+__global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict__ hist, int nb, int T,
+                                                            uint32_t* __restrict__ tile_count, uint2* __restrict__ ranges,
+                                                            uint32_t* __restrict__ block_tot, uint64_t* flags,
+                                                            uint32_t* __restrict__ misc, uint32_t* host, uint32_t seq,
+                                                            uint32_t pack)
+{
+    __shared__ uint32_t s_part[32][33];
+    __shared__ uint32_t s_ex[32];
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_sum, s_max, s_agg, s_bmax, s_fail;
+    const int c = threadIdx.x & 31, r = threadIdx.x >> 5;
+    const int t = blockIdx.x * 32 + c;
+    const int NB = (T + 31) / 32;
+    const int run = (nb + 31) / 32, b0 = r * run, b1 = min(nb, b0 + run);
+    constexpr int K = 8;
+    uint32_t v[K];
+    uint32_t sum = 0;
+    if (threadIdx.x == 0) { s_sum = 0; s_max = 0; s_fail = 0; }
+    if (t < T) {
+        if (run <= K) {
+#pragma unroll
+            for (int k = 0; k < K; k++) v[k] = b0 + k < b1 ? hist[(size_t)(b0 + k) * T + t] : 0u;
+#pragma unroll
+            for (int k = 0; k < K; k++) sum += v[k];
+        } else {
+            for (int b = b0; b < b1; b++) sum += hist[(size_t)b * T + t];
+        }
+    }
+    s_part[r][c] = sum;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        const uint32_t x = s_part[i][c];
+        if (i < r) off += x;
+        tot += x;
+    }
+    if (threadIdx.x == 0) {  // the block's 32 tile totals: exclusive prefix, total and longest list, published at once
+        uint32_t a = 0, m = 0;
+        for (int i = 0; i < 32; i++) {
+            uint32_t x = 0;
+            for (int k = 0; k < 32; k++) x += s_part[k][i];
+            if (blockIdx.x * 32 + i >= T) x = 0;
+            s_ex[i] = a;
+            a += x;
+            m = max(m, x);
+        }
+        s_agg = a;
+        s_bmax = m;
+        __hip_atomic_store(&flags[blockIdx.x], ((uint64_t)(0x80000000u | m) << 32) | a, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t < T) {
+        if (run <= K) {
+#pragma unroll
+            for (int k = 0; k < K; k++)
+                if (b0 + k < b1) {
+                    hist[(size_t)(b0 + k) * T + t] = off;
+                    off += v[k];
+                }
+        } else {
+            for (int b = b0; b < b1; b++) {
+                uint32_t* h = hist + (size_t)b * T + t;
+                const uint32_t x = *h;
+                *h = off;
+                off += x;
+            }
+        }
+        if (r == 0) tile_count[t] = tot;
+    }
+    // look-back: thread i < blockIdx.x polls block i's word (sc1 loads, bounded: a word that never arrives marks the
+    // frame failed instead of hanging the queue)
+    if ((int)threadIdx.x < (int)blockIdx.x) {
+        uint64_t w = 0;
+        for (uint32_t n = 0; n < kPlanPolls; n++) {
+            w = __hip_atomic_load(&flags[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (w >> 63) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!(w >> 63)) s_fail = 1u;
+        atomicAdd(&s_sum, (uint32_t)w);
+        atomicMax(&s_max, (uint32_t)(w >> 32) & 0x7fffffffu);
+    }
+    __syncthreads();
+    const uint32_t E = s_sum;
+    if (r == 0 && t < T) ranges[t] = make_uint2(E + s_ex[c], E + s_ex[c] + tot);
+    if (blockIdx.x == 0 || (int)blockIdx.x == NB - 1) {
+        // block 0: the count blocks' totals -> their exclusive bases (the scatter's block_base), in place; the last
+        // block only needs their sum (record slots)
+        PlanRun rb;
+        plan_load(block_tot, nb, rb);
+        uint32_t unused = 0;
+        const bool first = blockIdx.x == 0;
+        const uint32_t slots = plan_scan(rb, s_w, unused, [&](int i, uint32_t ex, uint32_t) { if (first) block_tot[i] = ex; });
+        if ((int)blockIdx.x == NB - 1 && threadIdx.x == 0) {
+            // a failed look-back reports R = ~0u, which the host turns into an error
+            const uint32_t R = s_fail ? ~0u : E + s_agg, mx = max(s_max, s_bmax);
+            misc[0] = R;
+            misc[1] = mx;
+            misc[2] = slots;
+            misc[kMiscPack] = pack;
+            if (host) {
+#if HLGS_PLAN_TAGGED
+                uint64_t* h = reinterpret_cast<uint64_t*>(host);
+                const uint64_t tag = (uint64_t)seq << 32;
+                h[0] = tag | R;
+                h[1] = tag | mx;
+                h[2] = tag | slots;
+#else
+                host[0] = R;
+                host[1] = mx;
+                host[2] = slots;
+                __threadfence_system();
+                host[3] = seq;
+#endif
+            }
+        }
+    }
+}
+
 // One thread per Gaussian: drop (depth, index) keys into each touched tile's segment.
 __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restrict__ radii, Geom g,
                                                       const uint2* __restrict__ ranges, uint32_t* cursor,
@@ -854,6 +993,7 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
     for (int y = y0; y < y1; y++)
         for (int x = x0; x < x1; x++, r++) {
             if (alt && !alt_tile_keep(xy.x, xy.y, co, kthr, x, y)) continue;
+            if (pack && HLGS_DROP_EMPTY && !rect_tile_mask(masks, r)) continue;
             const int tile = y * gx + x;
             const uint32_t slot = atomicAdd(&cursor[tile], 1u);
             keys[ranges[tile].x + slot] =
@@ -1017,6 +1157,9 @@ struct FwdArgs {
 // set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
 // visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
 // ------------------------------------------------------------------------------------------------
+#ifndef HLGS_FUSED_PLAN
+#define HLGS_FUSED_PLAN 1  // k_tile_offsets + k_plan as one launch (k_tile_offsets_plan)
+#endif
 #ifndef HLGS_BIN_HIST
 #define HLGS_BIN_HIST 1  // atomic-free binning through stored per-block histograms (0: device atomics)
 #endif
@@ -1253,8 +1396,10 @@ static void allow_big_lds()
     if (done) return;
     // the kernels' static LDS (the block's rect prefix, ~16 KiB) comes out of the same 160 KiB
     const int dyn = 2 * (int)sizeof(uint32_t) * kBinMaxTiles;
-    hipFuncSetAttribute((const void*)k_count_tiles<4096>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_count_tiles<2048>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_count_tiles<4096, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_count_tiles<2048, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_count_tiles<4096, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    hipFuncSetAttribute((const void*)k_count_tiles<2048, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
     hipFuncSetAttribute((const void*)k_scatter_keys_lds<4096, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
     hipFuncSetAttribute((const void*)k_scatter_keys_lds<2048, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
     hipFuncSetAttribute((const void*)k_scatter_keys_lds<4096, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
@@ -1275,19 +1420,27 @@ uint32_t* bin_histogram(const Img& im, int P, int gx, int gy)
     return nullptr;
 }
 
-void launch_count_tiles(int P, const int* radii, const Geom& g, uint32_t* tile_count, int gx, int gy, bool alt,
+// The fused plan's look-back words live in the tile cursors (unused by the histogram binning): ceil(T / 32) 64-bit
+// words, within the cursors' align_up(4 T) bytes for every T >= 1.
+static uint64_t* plan_flags(const Img& im) { return reinterpret_cast<uint64_t*>(im.tile_cursor); }
+
+void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, int gx, int gy, bool alt,
                         hipStream_t s, uint32_t* hist)
 {
+    uint32_t* tile_count = im.tile_count;
     const size_t lds = sizeof(uint32_t) * (size_t)gx * gy;
     allow_big_lds();
     const int bg = bin_gauss(P);
-    if (bg == 4096)
-        hipLaunchKernelGGL(k_count_tiles<4096>, dim3((P + 4095) / 4096), dim3(1024), lds, s, P, radii, g, tile_count, gx,
-                           gy, (int)alt, g.scan_tmp, hist);
-    else
-        hipLaunchKernelGGL(k_count_tiles<2048>, dim3((P + 2047) / 2048), dim3(512), lds, s, P, radii, g, tile_count, gx,
-                           gy, (int)alt, g.scan_tmp, hist);
-    if (hist) {
+    const bool fused = hist && HLGS_FUSED_PLAN;
+    uint32_t* zw = fused ? im.tile_cursor : nullptr;
+    const int nz = fused ? 2 * ((gx * gy + 31) / 32) : 0;
+    const bool drop = g.pack && HLGS_DROP_EMPTY;
+#define HLGS_CNT(BG, D) hipLaunchKernelGGL((k_count_tiles<BG, D>), dim3((P + BG - 1) / BG), dim3(BG / 4), lds, s, P, radii, g, \
+                                          tile_count, gx, gy, (int)alt, g.scan_tmp, hist, zw, nz)
+    if (bg == 4096) { if (drop) HLGS_CNT(4096, true); else HLGS_CNT(4096, false); }
+    else { if (drop) HLGS_CNT(2048, true); else HLGS_CNT(2048, false); }
+#undef HLGS_CNT
+    if (hist && !fused) {
         const int T = gx * gy, nb = (P + bin_gauss(P) - 1) / bin_gauss(P);
         hipLaunchKernelGGL(k_tile_offsets, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, tile_count);
     }
@@ -1298,7 +1451,14 @@ void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* 
     const int T = gx * gy;
     static_assert(kPlanRun * 1024 >= kBinMaxTiles, "one k_plan block covers every LDS-binned tile grid");
 
-    uint32_t* cursor = bin_histogram(im, P, gx, gy) ? nullptr : im.tile_cursor;
+    uint32_t* hist = bin_histogram(im, P, gx, gy);
+    const int nb = (P + bin_gauss(P) - 1) / bin_gauss(P);
+    if (hist && HLGS_FUSED_PLAN) {
+        hipLaunchKernelGGL(k_tile_offsets_plan, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count,
+                           im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack);
+        return;
+    }
+    uint32_t* cursor = hist ? nullptr : im.tile_cursor;
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, (P + bin_gauss(P) - 1) / bin_gauss(P), im.tile_count,
                        cursor, im.ranges, T, im.misc, host, seq, (uint32_t)g.pack);
 }

@@ -135,6 +135,7 @@ _SIGS = {
     "hlgs_lod_interp_backward": (_i, [_i, _i, _i, _i] + [_vp] * 16),
     "hlgs_binning_point_list_offset": (_sz, [_i]),
     "hlgs_point_list_entry_shift": (_i, [_i]),
+    "hlgs_point_list_drops_empty": (_i, [_i]),
     "hlgs_set_entry_packing": (None, [_i]),
     "hlgs_image_ranges_offset": (_sz, [_i, _i]),
     "hlgs_geom_splat_offset": (_sz, [_i]),

@@ -435,6 +435,9 @@ int hlgs_expand_to_target(int N, const int* nodes, int target, int* out, int cap
 size_t hlgs_binning_point_list_offset(int R);  /* uint32 point_list[R] */
 /* point_list entries of a P-Gaussian forward are (Gaussian index << shift) | footprint quadrant mask: the shift. */
 int hlgs_point_list_entry_shift(int P);
+/* 1 if a P-Gaussian forward bins no instance whose quadrant mask is 0 (packed entries with HLGS_DROP_EMPTY): its tile
+ * lists and n_contrib then match the oracle run with drop_empty (oracle/hlgs_oracle.c rect_quad_masks). */
+int hlgs_point_list_drops_empty(int P);
 /* Tests: on = 0 makes every following frame use plain index entries (the P >= 2^28 path); 1 restores the default. */
 void hlgs_set_entry_packing(int on);
 size_t hlgs_image_ranges_offset(int W, int H);  /* uint2 ranges[tiles] */

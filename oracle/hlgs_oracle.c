@@ -242,6 +242,10 @@ typedef struct {
     const float *dc;
     int antialiasing;
     int alt;
+    /* not the reference's: bin no instance whose quadrant mask (rect_quad_masks) is 0, as the HIP binning does with
+     * packed entries and HLGS_DROP_EMPTY (hlgs_point_list_drops_empty).  Such an instance reaches no pixel of its tile
+     * with alpha >= 1/255, so the images and gradients do not change; the tile lists and n_contrib positions do. */
+    int drop_empty;
 } orc_args;
 
 /* Per-Gaussian geometry produced by the forward preprocess (HR/rasterizer_impl.h:29-45) */
@@ -439,6 +443,79 @@ static int alt_tile_keep(float mx, float my, const float *co, int tx, int ty)
     return power <= thr;
 }
 
+/* Footprint quadrant masks of the first 8 tiles of a Gaussian's rect, restated operation for operation from the HIP
+ * preprocess (hlgs_math.h splat_foot, splat_bands, band_extent, row_bands, row_quad_mask, rect_quad_masks): IEEE
+ * square roots and divisions, no contraction (the serial and OpenMP builds; the contracted variance build never
+ * drops), fmaf where the kernels write it -- so the masks, and with drop_empty the binned instances, are
+ * bit-identical.  The test itself: an 8x8 block can hold a pixel with alpha >= 1/255 only if
+ * the ellipse Q(u, v) = a u^2 + 2 b u v + c v^2 <= t (t = -2 ln2 thr, widened) overlaps it; per 8-row band the
+ * ellipse's x-extent is compared with the block's columns, widened by a tolerance far above the float rounding. */
+typedef struct { float x, y, nb, det, at, ia, vmax, vr, tol; int mode; } orc_bands;
+static inline float med3f(float v, float lo, float hi) { return fmaxf(fminf(v, lo), fminf(fmaxf(v, lo), hi)); }
+static orc_bands splat_bands(float x, float y, const float *co, float thr)
+{
+    orc_bands s;
+    s.x = x; s.y = y;
+    s.nb = s.det = s.at = s.ia = s.vmax = s.vr = s.tol = 0.f;
+    s.mode = 0;
+    const float o = co[3];
+    if (o != o || co[0] != co[0] || co[1] != co[1] || co[2] != co[2] || x != x || y != y) { s.mode = 1; return s; }
+    if (o < (1.0f / 255.0f) * 0.999f) { s.mode = 2; return s; }
+    const float det0 = co[0] * co[2] - co[1] * co[1]; /* splat_foot's */
+    if (!(det0 > 0.f) || !(co[0] > 0.f) || !(co[2] > 0.f)) { s.mode = 1; return s; }
+    const float t = fmaxf(-1.3862944f * thr, 0.f) * 1.002f + 2e-3f;
+    const float a = co[0], b = co[1], c = co[2];
+    const float bb = b * b, e = fmaf(-b, b, bb);
+    const float det = fmaf(a, c, -bb) + e;
+    if (!(det > 0.f)) { s.mode = 1; return s; }
+    const float idet = 1.0f / det;
+    s.ia = 1.0f / a;
+    const float vmax = sqrtf(a * t * idet);
+    s.nb = -b;
+    s.det = det;
+    s.at = a * t;
+    s.vmax = fmaf(vmax, 1e-4f, vmax) + 1e-3f;
+    s.vr = -b * sqrtf(t * idet * (1.0f / c));
+    s.tol = 2e-3f * (sqrtf(s.at) + fabsf(b) * vmax) * s.ia + 2e-3f;
+    return s;
+}
+static void band_extent(const orc_bands *s, float v0, float *umin, float *umax)
+{
+    const float lo = fmaxf(v0, -s->vmax), hi = fminf(v0 + 7.f, s->vmax);
+    if (!(lo <= hi)) { *umin = 3e38f; *umax = -3e38f; return; }
+    const float vR = med3f(s->vr, lo, hi), vL = med3f(-s->vr, lo, hi);
+    *umax = fmaf(s->nb, vR, sqrtf(fmaxf(fmaf(-s->det * vR, vR, s->at), 0.f))) * s->ia + s->tol;
+    *umin = fmaf(s->nb, vL, -sqrtf(fmaxf(fmaf(-s->det * vL, vL, s->at), 0.f))) * s->ia - s->tol;
+}
+static uint32_t rect_quad_masks(float x, float y, const float *co, float thr, int x0, int y0, int x1, int y1)
+{
+    const orc_bands s = splat_bands(x, y, co, thr);
+    const int w = x1 - x0, n = (x1 - x0) * (y1 - y0) < 8 ? (x1 - x0) * (y1 - y0) : 8;
+    uint32_t m = 0;
+    float lo0 = 3e38f, hi0 = -3e38f, lo1 = 3e38f, hi1 = -3e38f;
+    for (int r = 0; r < n; r++) {
+        const int ty = y0 + r / w, tx = x0 + r % w;
+        if (r == 0 || tx == x0) { /* row_bands */
+            lo0 = lo1 = 3e38f;
+            hi0 = hi1 = -3e38f;
+            if (!s.mode) {
+                const float v0 = (float)(ty * TILE) - s.y;
+                band_extent(&s, v0, &lo0, &hi0);
+                band_extent(&s, v0 + 8.f, &lo1, &hi1);
+            }
+        }
+        uint32_t q; /* row_quad_mask */
+        if (s.mode) q = s.mode == 1 ? 0xFu : 0u;
+        else {
+            const float u0 = (float)(tx * TILE) - s.x, u7 = u0 + 7.f, u8 = u0 + 8.f, u15 = u0 + 15.f;
+            q = (hi0 >= u0 && lo0 <= u7 ? 1u : 0u) | (hi0 >= u8 && lo0 <= u15 ? 2u : 0u) |
+                (hi1 >= u0 && lo1 <= u7 ? 4u : 0u) | (hi1 >= u8 && lo1 <= u15 ? 8u : 0u);
+        }
+        m |= q << (4 * r);
+    }
+    return m;
+}
+
 /* Forward phase 2: duplicate, stable sort, ranges, blend (HR/rasterizer_impl.cu:335-399, HR/forward.cu:450-596) */
 
 /* Splat falloff and the alpha >= 1/255 test (forward.cu:539-560, backward.cu:614-643), restated so
@@ -537,6 +614,7 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
     memset(im->ranges, 0, sizeof(uint32_t) * 2 * (size_t)T);
     if (R == 0 && !a->alt) return; /* A-7: output stays 0, not bg (the alt rasterizer renders bg) */
     kv *buf = (kv *)malloc(sizeof(kv) * (size_t)(R > 0 ? R : 1));
+    float *thr = alpha_thresholds(a, g);
     /* duplicateWithKeys, HR/rasterizer_impl.cu:70-115; AR/rasterizer_impl.cu:120-191 adds the per-tile
      * culling: a culled instance gets the sentinel key (tile 0xFFFFFFFF, depth FLT_MAX) and sorts last */
     const float fltmax = FLT_MAX;
@@ -551,10 +629,15 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
         get_rect(g->means2D[2 * i], g->means2D[2 * i + 1], g->rects[2 * i], g->rects[2 * i + 1], gx, gy, &x0, &y0, &x1, &y1);
         uint32_t dbits;
         memcpy(&dbits, &g->depths[i], 4);
+        const uint32_t qm = a->drop_empty ? rect_quad_masks(g->means2D[2 * i], g->means2D[2 * i + 1],
+                                                            g->conic_opacity + 4 * i, thr[i], x0, y0, x1, y1)
+                                          : 0xFFFFFFFFu;
+        uint32_t r = 0;
         for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) {
+            for (int x = x0; x < x1; x++, r++) {
                 if (a->alt && !alt_tile_keep(g->means2D[2 * i], g->means2D[2 * i + 1], g->conic_opacity + 4 * i, x, y))
                     continue;
+                if (r < 8 && !((qm >> (4 * r)) & 0xFu)) continue; /* drop_empty: reaches none of the quadrants */
                 buf[off].key = ((uint64_t)(uint32_t)(y * gx + x) << 32) | dbits;
                 buf[off].pos = off;
                 buf[off].val = (uint32_t)i;
@@ -606,7 +689,6 @@ void orc_forward_render(const orc_args *a, const orc_geom *g, orc_img *im, int R
     free(buf);
     const float *feat = a->colors_precomp ? a->colors_precomp : g->rgb;
     int do_interp = (a->ts != NULL && a->kids != NULL);
-    float *thr = alpha_thresholds(a, g);
     /* renderCUDA<3> per pixel, HR/forward.cu:450-596 (AR/forward.cu:282-430) */
 #pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ty++)

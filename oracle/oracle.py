@@ -46,7 +46,7 @@ class _Args(C.Structure):
                 ("scales", _f), ("rotations", _f), ("cov3D_precomp", _f), ("viewmatrix", _f),
                 ("projmatrix", _f), ("campos", _f), ("scale_modifier", C.c_float), ("tanfovx", C.c_float),
                 ("tanfovy", C.c_float), ("indices", _i), ("parent_indices", _i), ("ts", _f), ("kids", _i),
-                ("dc", _f), ("antialiasing", C.c_int), ("alt", C.c_int)]
+                ("dc", _f), ("antialiasing", C.c_int), ("alt", C.c_int), ("drop_empty", C.c_int)]
 
 
 class _Geom(C.Structure):
@@ -176,11 +176,14 @@ def _make_args(scene, cam, keep):
     return a, P
 
 
-def forward(scene, cam, do_depth=True, omp=False):
-    """Full forward: returns a Frame with color (3,H,W), radii, invdepth, seen and all intermediates."""
+def forward(scene, cam, do_depth=True, omp=False, drop_empty=False):
+    """Full forward: returns a Frame with color (3,H,W), radii, invdepth, seen and all intermediates.
+    drop_empty: bin no instance whose footprint quadrant mask is 0, as the HIP binning does when
+    hlgs_point_list_drops_empty(P) (not the reference's binning: same images and gradients, shorter tile lists)."""
     L = lib(omp)
     keep = []
     a, P = _make_args(scene, cam, keep)
+    a.drop_empty = int(bool(drop_empty))
     W, H = int(cam["W"]), int(cam["H"])
     fr = Frame()
     fr.keep = keep

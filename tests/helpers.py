@@ -54,9 +54,23 @@ def gpu_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_cov=
     return out
 
 
-def oracle_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_cov=False, lib=False):
+def drops_empty(P):
+    """Whether the HIP binning of a P-Gaussian frame leaves out the instances whose quadrant mask is 0
+    (hlgs_point_list_drops_empty): an oracle frame whose tile lists or n_contrib are compared with the GPU's is run
+    with the same drop_empty.  Images and gradients do not depend on it."""
+    from hlgs_core import _lib as L
+    return bool(L.load().hlgs_point_list_drops_empty(int(P)))
+
+
+def binned(fr):
+    """Entries an oracle frame binned: the tile lists' total, without the sentinel entries of culled or dropped
+    instances that sort behind them (compare this many point_list entries)."""
+    return int((fr.ranges[:, 1].astype(np.int64) - fr.ranges[:, 0].astype(np.int64)).sum())
+
+
+def oracle_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_cov=False, lib=False, drop_empty=False):
     """lib: the oracle build (False: the serial reference of every parity check; "fma": the same source with FMA
-    contraction, for build-to-build variance)."""
+    contraction, for build-to-build variance).  drop_empty: see drops_empty."""
     from oracle import oracle as O
     sc = dict(means3D=scene["means3D"], opacities=scene["opacities"], sh_degree=scene.get("sh_degree", 0))
     if use_colors:
@@ -69,7 +83,7 @@ def oracle_render(scene, cam, do_depth=True, grads=None, use_colors=False, use_c
         sc["scales"] = scene["scales"]
         sc["rotations"] = scene["rotations"]
     camn = S.cam_numpy(cam)
-    fr = O.forward(sc, camn, do_depth=do_depth, omp=lib)
+    fr = O.forward(sc, camn, do_depth=do_depth, omp=lib, drop_empty=drop_empty)
     out = dict(color=fr.color, radii=fr.radii, invdepth=fr.invdepth, frame=fr)
     if grads is not None:
         g, gd = grads

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from hlgs_core import synthetic as S
-from helpers import assert_grad, image_check, rel_err
+from helpers import assert_grad, drops_empty, image_check, rel_err
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -126,7 +126,7 @@ def test_alt_tile_culling_lists_bit_exact(P, W, H, stretch):
     if stretch > 1.0:
         sc["scales"][::3, 0] *= stretch
         sc["opacities"][::3] = 0.9
-    fr = O.forward(dict(sc), S.cam_numpy(cam))
+    fr = O.forward(dict(sc), S.cam_numpy(cam), drop_empty=drops_empty(sc["means3D"].shape[0]))
     t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
     e = torch.empty(0, device=DEV)
     out = _C.rasterize_gaussians(cam["bg"], t(sc["means3D"]), e, t(sc["opacities"]), t(sc["scales"]),

@@ -7,7 +7,7 @@ import torch
 
 from hlgs_core import synthetic as S
 from oracle import oracle as O
-from helpers import assert_grad, gpu_render, oracle_render, rel_err, settings_for, image_check
+from helpers import assert_grad, binned, drops_empty, gpu_render, oracle_render, rel_err, settings_for, image_check
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -26,7 +26,7 @@ def test_point_list_and_ranges_bit_exact(P, W, H, band):
     cam = S.make_camera(W, H)
     sc = S.make_gaussians(P, 1, cam, seed=11)
     sc["means3D"][::7, 2] = 9.0  # depth ties
-    fr = O.forward(dict(sc), S.cam_numpy(cam))
+    fr = O.forward(dict(sc), S.cam_numpy(cam), drop_empty=drops_empty(P))
     counts = fr.ranges[:, 1] - fr.ranges[:, 0]
     assert counts.max() <= band and (band == 64 or counts.max() > band // 2), counts.max()
     t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
@@ -36,10 +36,11 @@ def test_point_list_and_ranges_bit_exact(P, W, H, band):
                                  cam["tanfovy"], H, W, t(sc["shs"]), 1, cam["campos"], False, True, True)
     R = out[0]
     assert R == fr.R
-    pl = _C.inspect_point_list(out[4], R).cpu().numpy().astype(np.uint32)
+    kept = binned(fr)
+    pl = _C.inspect_point_list(out[4], kept).cpu().numpy().astype(np.uint32)
     rg = _C.inspect_ranges(out[5], W, H).cpu().numpy().astype(np.uint32)
     np.testing.assert_array_equal(rg, fr.ranges)
-    np.testing.assert_array_equal(pl, fr.point_list[:R])
+    np.testing.assert_array_equal(pl, fr.point_list[:kept])
     np.testing.assert_array_equal(out[7].cpu().numpy(), fr.seen)
 
 
@@ -54,7 +55,7 @@ def test_decisions_bit_exact_for_elongated_splats(deg):
     rng = np.random.default_rng(5)
     sc["scales"] = np.ascontiguousarray(sc["scales"] * np.exp(rng.uniform(-2.5, 2.5, sc["scales"].shape))
                                         .astype(np.float32))
-    fr = O.forward(dict(sc), S.cam_numpy(cam))
+    fr = O.forward(dict(sc), S.cam_numpy(cam), drop_empty=drops_empty(6000))
     t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
     e = torch.empty(0, device=DEV)
     out = _C.rasterize_gaussians(cam["bg"], e, e, e, e, t(sc["means3D"]), e, t(sc["opacities"]), t(sc["scales"]),
@@ -62,8 +63,9 @@ def test_decisions_bit_exact_for_elongated_splats(deg):
                                  cam["tanfovy"], H, W, t(sc["shs"]), deg, cam["campos"], False, False, True)
     R = out[0]
     assert R == fr.R
-    np.testing.assert_array_equal(_C.inspect_point_list(out[4], R).cpu().numpy().astype(np.uint32),
-                                  fr.point_list[:R])
+    kept = binned(fr)
+    np.testing.assert_array_equal(_C.inspect_point_list(out[4], kept).cpu().numpy().astype(np.uint32),
+                                  fr.point_list[:kept])
     N = W * H
     n_contrib = _C._field(out[5], (4 * N + 255) // 256 * 256, N, torch.int32).cpu().numpy()
     np.testing.assert_array_equal(n_contrib, fr.n_contrib.astype(np.int32))

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from hlgs_core import synthetic as S
-from helpers import assert_grad, gpu_render, image_check, oracle_render, rel_err
+from helpers import assert_grad, drops_empty, gpu_render, image_check, oracle_render, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -25,7 +25,8 @@ def _scene(P, deg, W, H, seed=0, bg=(0.0, 0.0, 0.0), **kw):
 def _compare(sc, cam, do_depth=True, use_colors=False, use_cov=False, grads=True):
     g = S.upstream_grads(cam["W"], cam["H"], seed=1, depth=do_depth) if grads else None
     gpu = gpu_render(sc, cam, do_depth=do_depth, grads=g, use_colors=use_colors, use_cov=use_cov)
-    ref = oracle_render(sc, cam, do_depth=do_depth, grads=g, use_colors=use_colors, use_cov=use_cov)
+    ref = oracle_render(sc, cam, do_depth=do_depth, grads=g, use_colors=use_colors, use_cov=use_cov,
+                        drop_empty=drops_empty(sc["means3D"].shape[0]))
     np.testing.assert_array_equal(gpu["radii"], ref["radii"])
     mx, nbad, ok = image_check(gpu["color"], ref["color"], FWD_TOL)
     assert ok, f"color L-inf {mx} ({nbad} pixels over {FWD_TOL})"

@@ -20,7 +20,7 @@ import pytest
 import torch
 
 from hlgs_core import synthetic as S
-from helpers import assert_grad, gpu_render, image_check, oracle_render
+from helpers import assert_grad, binned, drops_empty, gpu_render, image_check, oracle_render
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -51,7 +51,7 @@ def _check_lists_and_records(sc, cam, deg):
     """The forward's integer outputs and the per-Gaussian splat records against the oracle frame, bit for bit."""
     from diff_gaussian_rasterization import _C
     W, H = cam["W"], cam["H"]
-    fr = O.forward(dict(sc), S.cam_numpy(cam))
+    fr = O.forward(dict(sc), S.cam_numpy(cam), drop_empty=drops_empty(sc["means3D"].shape[0]))
     t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
     e = torch.empty(0, device=DEV)
     out = _C.rasterize_gaussians(cam["bg"], e, e, e, e, t(sc["means3D"]), e, t(sc["opacities"]), t(sc["scales"]),
@@ -61,8 +61,9 @@ def _check_lists_and_records(sc, cam, deg):
     P = sc["means3D"].shape[0]
     assert R == fr.R and R > 0
     np.testing.assert_array_equal(_C.inspect_ranges(out[5], W, H).cpu().numpy().astype(np.uint32), fr.ranges)
-    np.testing.assert_array_equal(_C.inspect_point_list(out[4], R, P).cpu().numpy().astype(np.uint32),
-                                  fr.point_list[:R])
+    kept = binned(fr)
+    np.testing.assert_array_equal(_C.inspect_point_list(out[4], kept, P).cpu().numpy().astype(np.uint32),
+                                  fr.point_list[:kept])
     N = W * H
     n_contrib = _C._field(out[5], (4 * N + 255) // 256 * 256, N, torch.int32).cpu().numpy()
     np.testing.assert_array_equal(n_contrib, fr.n_contrib.astype(np.int32))

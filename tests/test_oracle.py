@@ -355,6 +355,44 @@ def test_alt_oracle_culls_tiles_and_renders_bg_when_empty():
     np.testing.assert_array_equal(fr.color, np.broadcast_to(np.float32([0.5, 0.25, 0.75])[:, None, None], (3, 64, 64)))
 
 
+@pytest.mark.parametrize("P,deg,W,H,alt,elong", [(3000, 3, 160, 112, False, 0.0), (2500, 1, 128, 96, True, 0.0),
+                                                 (3000, 2, 144, 96, False, 2.5)])
+def test_drop_empty_changes_lists_not_images(P, deg, W, H, alt, elong):
+    """drop_empty (the HIP binning with packed entries and HLGS_DROP_EMPTY) bins no instance whose footprint quadrant
+    mask is 0.  The mask test is conservative (tools/cull_check.py), so such an instance reaches no pixel of its tile:
+    the image, inverse depth, transmittance and every gradient stay bit-identical, the lists get shorter, num_rendered
+    (record slots) stays, and every pixel's last contributor is the same Gaussian."""
+    cam = S.make_camera(W, H, bg=(0.1, 0.2, 0.3))
+    sc = S.make_gaussians(P, deg, cam, seed=P + deg)
+    if elong:  # strongly anisotropic splats: the band test's widest cases
+        rng = np.random.default_rng(7)
+        sc["scales"] = np.ascontiguousarray(sc["scales"] * np.exp(rng.uniform(-elong, elong, sc["scales"].shape))
+                                            .astype(np.float32))
+    if alt:
+        sc = alt_scene(sc)
+    g = S.upstream_grads(W, H, seed=2)
+    a = O.forward(dict(sc), S.cam_numpy(cam))
+    b = O.forward(dict(sc), S.cam_numpy(cam), drop_empty=True)
+    ka = int((a.ranges[:, 1].astype(np.int64) - a.ranges[:, 0]).sum())
+    kb = int((b.ranges[:, 1].astype(np.int64) - b.ranges[:, 0]).sum())
+    # the alt rasterizer's exact per-tile culling already removes nearly every such instance
+    assert a.R == b.R and (kb <= ka if alt else kb < 0.95 * ka), (a.R, ka, kb)
+    for k in ("color", "invdepth", "final_T", "radii", "seen"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+    ga, gb = O.backward(a, dict(sc), *g), O.backward(b, dict(sc), *g)
+    for k in ga:
+        if ga[k] is not None:
+            np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
+    gx = (W + 15) // 16
+    pix = np.arange(W * H)
+    tile = (pix // W // 16) * gx + (pix % W) // 16
+    live = (a.n_contrib > 0) & (b.n_contrib > 0)
+    assert np.array_equal(a.n_contrib > 0, b.n_contrib > 0)
+    la = a.point_list[a.ranges[tile[live], 0] + a.n_contrib[live] - 1]
+    lb = b.point_list[b.ranges[tile[live], 0] + b.n_contrib[live] - 1]
+    np.testing.assert_array_equal(la, lb)
+
+
 # ------------------------------------------------------------------------------------------------------
 # Reference-run fixtures for the Python pieces of the path (tests/golden/make_golden.py)
 
