@@ -48,6 +48,9 @@ __device__ __forceinline__ void cov3d_exact(f3 scale, float mod, float4 q, float
     out[3] = Sig.m[1][1]; out[4] = Sig.m[1][2]; out[5] = Sig.m[2][2];
 }
 
+#ifndef HLGS_GAUSS_SKIP
+#define HLGS_GAUSS_SKIP 1  // skip zero-mask record slots also when they were written (always with HLGS_DROP_EMPTY)
+#endif
 // One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
 // backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
 template <bool HIER, bool ALT>
@@ -57,20 +60,25 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
 {
     // the forward packed its entries (misc[kMiscPack]), so Geom::qmask holds this frame's quadrant masks: a slot whose
     // mask is 0 holds no record (HLGS_DROP_EMPTY: never binned) or a zero one, and is skipped (rect_tile_mask)
-    const bool masked = misc && misc[kMiscPack];
+    const bool masked = (HLGS_GAUSS_SKIP || HLGS_DROP_EMPTY) && misc && misc[kMiscPack];
     const int t_idx = blockIdx.x * 256 + threadIdx.x;
-    const bool vis = t_idx < a.P && radii[t_idx] > 0;
+    // the slot range and the masks are loaded with the radius, not behind it (an invisible Gaussian's tiles_touched
+    // is 0, so its range is empty; its qmask word is stale and never used)
+    uint32_t r_end = 0, r_start = 0, qraw = 0xFFFFFFFFu;
+    bool vis = false;
+    if (t_idx < a.P) {
+        vis = radii[t_idx] > 0;
+        r_end = g.point_offsets[t_idx];
+        r_start = r_end - g.tiles_touched[t_idx];
+        qraw = g.qmask[t_idx];
+    }
+    if (!vis) r_start = r_end;
     // Gaussians with more than kWide record slots (rects over many tiles) are summed by their whole wave, lane-
     // strided, with a fixed butterfly at the end -- deterministic, and one wide splat no longer serialises a lane
     // over thousands of slots.  Done before any lane leaves, so every lane of the wave takes part.
     constexpr uint32_t kWide = 32;
-    uint32_t r_end = 0, r_start = 0;
-    if (vis) {
-        r_end = g.point_offsets[t_idx];
-        r_start = r_end - g.tiles_touched[t_idx];
-    }
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f, s8 = 0.f, s9 = 0.f;
-    const uint32_t qmasks = (vis && masked) ? g.qmask[t_idx] : 0xFFFFFFFFu;
+    const uint32_t qmasks = (vis && masked) ? qraw : 0xFFFFFFFFu;
     {
         uint64_t wide = __ballot(vis && r_end - r_start > kWide);
         const int lane = threadIdx.x & 63;

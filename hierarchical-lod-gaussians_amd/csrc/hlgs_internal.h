@@ -93,7 +93,7 @@ constexpr int kMiscPack = 3;  // Img::misc word holding the frame's pack_entries
 // skip it.  Its record slot stays (point_offsets and num_rendered are unchanged) and is never written; k_gauss_bwd
 // skips the slots whose mask is 0 (their records would be zero).
 #ifndef HLGS_DROP_EMPTY
-#define HLGS_DROP_EMPTY 0
+#define HLGS_DROP_EMPTY 1
 #endif
 #ifndef HLGS_PLAN_TAGGED
 #define HLGS_PLAN_TAGGED 1

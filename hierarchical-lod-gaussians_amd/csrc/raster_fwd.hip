@@ -673,11 +673,12 @@ template <int BG, bool PACK>
 __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
                                                                   uint64_t* __restrict__ keys, int gx, int gy, int alt,
-                                                                  Guard gd, const uint32_t* __restrict__ block_base,
+                                                                  Guard gd, const uint32_t* __restrict__ block_tot,
                                                                   const uint32_t* __restrict__ hist)
 {
     if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+    __shared__ uint32_t s_base;
     __shared__ uint32_t s_pre[BG + 1];
     __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
     const int T = gx * gy;
@@ -687,9 +688,16 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
     if (threadIdx.x == 0) s_w[(BG / 4) / 64] = 0;
     __syncthreads();
     block_rect_prefix<BG>(P, g, s_pre, s_w);
-    {  // point_offsets (the inclusive scan of tiles_touched) = the block's base (k_plan) + the block-local prefix
+    {  // point_offsets (the inclusive scan of tiles_touched) = the block's base + the block-local prefix; the base is
+       // the sum of the preceding count blocks' totals (k_count_tiles), at most 16 per thread
+        if (threadIdx.x == 0) s_base = 0;
+        __syncthreads();
+        uint32_t part = 0;
+        for (int i = threadIdx.x; i < (int)blockIdx.x; i += BG / 4) part += block_tot[i];
+        if (part) atomicAdd(&s_base, part);
+        __syncthreads();
         const int g0 = blockIdx.x * BG, g1 = min(P, g0 + BG);
-        const uint32_t base = block_base[blockIdx.x];
+        const uint32_t base = s_base;
         for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += (BG / 4)) {
             const int k = idx - g0;
             g.point_offsets[idx] = base + s_pre[k + 1];
@@ -738,9 +746,9 @@ __global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict_
     if (c) atomicMax(&misc[1], c);
 }
 
-// Binning plan of the LDS-histogram path, one 1024-thread block: the exclusive scan of the count blocks'
-// instance totals (block_tot -> block bases, in place; k_scatter_keys_lds adds its local prefix to form
-// point_offsets), the tile ranges from the per-tile counts, cursor reset, and misc[0..2] = R, longest list,
+// Binning plan of the LDS-histogram path, one 1024-thread block: the sum of the count blocks' instance totals
+// (record slots; each k_scatter_keys_lds block sums its predecessors' totals for its base and adds its local prefix to
+// form point_offsets), the tile ranges from the per-tile counts, cursor reset, and misc[0..2] = R, longest list,
 // record slots -- mirrored into the caller's pinned host words, so the host reads R without a copy.
 // Replaces two device-wide scans, k_tile_ranges and the read-back copy (seven launches).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t& total)
@@ -812,7 +820,7 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
     plan_load(block_tot, nb, rb);
     plan_load(count, T, rc);
     uint32_t mx = 0, unused = 0;
-    const uint32_t slots = plan_scan(rb, s_w, unused, [&](int i, uint32_t ex, uint32_t) { block_tot[i] = ex; });
+    const uint32_t slots = plan_scan(rb, s_w, unused, [&](int, uint32_t, uint32_t) {});  // the scatter sums its own base
     const uint32_t R = plan_scan(rc, s_w, mx, [&](int t, uint32_t ex, uint32_t c) {
         ranges[t] = make_uint2(ex, ex + c);
         if (cursor) cursor[t] = 0;  // only the atomic scatter (no histogram rows) hands out slots from cursors
@@ -847,9 +855,10 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
 // block offsets as k_tile_offsets does, publishes its tiles' total and longest list in one 64-bit word (flags[b]:
 // high half 1 << 31 | max, low half total; zeroed by k_count_tiles), and sums its predecessors' published totals for
 // its ranges (a decoupled look-back: every block publishes before it waits, and blocks are dispatched in order, so a
-// waiting block's predecessors are all running or done).  Block 0 scans the count blocks' totals into the scatter's
-// block bases; the last block, which sees every predecessor's word, writes misc and the host words.  One launch and
-// one dependent round trip instead of two launches, the second a single block.
+// waiting block's predecessors are all running or done).  The last block, which sees every predecessor's word, also
+// sums the count blocks' totals (record slots) and writes misc and the host words; the totals stay as they are (each
+// scatter block sums its predecessors' for its base), so no block reads what another rewrites.  One launch and one
+// dependent round trip instead of two launches, the second a single block.
 constexpr uint32_t kPlanPolls = 1u << 20;  // ~0.1 s of polling per word
 __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict__ hist, int nb, int T,
                                                             uint32_t* __restrict__ tile_count, uint2* __restrict__ ranges,
@@ -888,15 +897,17 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
         if (i < r) off += x;
         tot += x;
     }
-    if (threadIdx.x == 0) {  // the block's 32 tile totals: exclusive prefix, total and longest list, published at once
-        uint32_t a = 0, m = 0;
+    if (r == 0) s_ex[c] = t < T ? tot : 0u;  // the block's 32 tile totals
+    __syncthreads();
+    if (threadIdx.x == 0) {  // their exclusive prefix, total and longest list, published at once
+        uint32_t x[32], a = 0, m = 0;
+#pragma unroll
+        for (int i = 0; i < 32; i++) x[i] = s_ex[i];
+#pragma unroll
         for (int i = 0; i < 32; i++) {
-            uint32_t x = 0;
-            for (int k = 0; k < 32; k++) x += s_part[k][i];
-            if (blockIdx.x * 32 + i >= T) x = 0;
             s_ex[i] = a;
-            a += x;
-            m = max(m, x);
+            a += x[i];
+            m = max(m, x[i]);
         }
         s_agg = a;
         s_bmax = m;
@@ -937,15 +948,12 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
     __syncthreads();
     const uint32_t E = s_sum;
     if (r == 0 && t < T) ranges[t] = make_uint2(E + s_ex[c], E + s_ex[c] + tot);
-    if (blockIdx.x == 0 || (int)blockIdx.x == NB - 1) {
-        // block 0: the count blocks' totals -> their exclusive bases (the scatter's block_base), in place; the last
-        // block only needs their sum (record slots)
+    if ((int)blockIdx.x == NB - 1) {  // the count blocks' totals summed: record slots (the scatter sums its own base)
         PlanRun rb;
         plan_load(block_tot, nb, rb);
         uint32_t unused = 0;
-        const bool first = blockIdx.x == 0;
-        const uint32_t slots = plan_scan(rb, s_w, unused, [&](int i, uint32_t ex, uint32_t) { if (first) block_tot[i] = ex; });
-        if ((int)blockIdx.x == NB - 1 && threadIdx.x == 0) {
+        const uint32_t slots = plan_scan(rb, s_w, unused, [&](int, uint32_t, uint32_t) {});
+        if (threadIdx.x == 0) {
             // a failed look-back reports R = ~0u, which the host turns into an error
             const uint32_t R = s_fail ? ~0u : E + s_agg, mx = max(s_max, s_bmax);
             misc[0] = R;
