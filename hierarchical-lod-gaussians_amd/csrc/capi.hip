@@ -25,6 +25,7 @@ void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int
 void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s);
 bool lds_binning(int P, int gx, int gy);
 uint32_t* bin_histogram(const Img& im, int P, int gx, int gy);
+bool two_level(const Img& im, int P, int gx, int gy);
 void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, int gx, int gy, bool alt,
                         hipStream_t s, uint32_t* hist);
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
@@ -134,6 +135,7 @@ Bin carve_bin(void* base, int R, size_t* total)
     b.point_list = take<uint32_t>(p, R);  // first: its offset does not depend on R
     b.keys = take<uint64_t>(p, R);
     b.keys2 = take<uint64_t>(p, R);
+    b.tile_local = take<uint8_t>(p, R);
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return b;
 }
@@ -359,8 +361,8 @@ static int render_launch(const hlgs_raster_args* a, const int* radii, void* geom
 // Largest R whose binning layout fits in `bytes`.
 static int binning_capacity(size_t bytes)
 {
-    if (bytes <= 4 * kAlign) return 0;
-    long r = (long)((bytes - 4 * kAlign) / 20);
+    if (bytes <= 5 * kAlign) return 0;
+    long r = (long)((bytes - 5 * kAlign) / 21);
     while (r > 0 && hlgs_binning_buffer_size((int)r) > bytes) r--;
     return (int)std::min<long>(r, 0x7fffffff);
 }
@@ -488,7 +490,11 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     // block sorts handle; the kernels exit at once if the frame exceeds either (Guard).
     const int capR = binning ? binning_capacity(binning_bytes) : 0;
     const bool spec = capR > 0;
-    const uint32_t cap_n = rb->last_maxc <= (uint32_t)kWaveSortCap ? (uint32_t)kWaveSortCap : (uint32_t)kSortCap;
+    // the two-level binning sorts lists of any length on the device (k_supertile_sort, k_big_tile_sort); otherwise the
+    // queued sorts are the ones the previous frame's longest list needed
+    const bool any_len = two_level(im, a->P, (a->W + 15) / 16, (a->H + 15) / 16);
+    const uint32_t cap_n = any_len ? ~0u
+                           : rb->last_maxc <= (uint32_t)kWaveSortCap ? (uint32_t)kWaveSortCap : (uint32_t)kSortCap;
     if (spec && (rc = render_launch(a, radii, geom, img, binning, capR, cap_n, out_color, out_invdepth, seen, s,
                                     Guard{im.misc, (uint32_t)capR, cap_n})))
         return rc;

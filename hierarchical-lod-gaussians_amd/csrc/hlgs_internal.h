@@ -84,6 +84,15 @@ bool lds_binning(int P, int gx, int gy);
 #endif
 constexpr int kEntryShift = 4;
 constexpr int kMiscPack = 3;  // Img::misc word holding the frame's pack_entries(P)
+constexpr int kMiscBig = 4;   // Img::misc word: tiles k_supertile_sort left to k_big_tile_sort (two-level binning)
+// Two-level binning (HLGS_TWO_LEVEL): the key scatter bins instances into super-tiles of kSuperTiles consecutive tiles
+// (tile-major order, so a super-tile's segment is its tiles' lists back to back), with runs long enough to be written
+// as whole sectors; k_supertile_sort then splits each segment into its tiles in LDS and sorts them.
+#ifndef HLGS_TWO_LEVEL
+#define HLGS_TWO_LEVEL 0  // measured slower: an option
+#endif
+constexpr int kSuperTiles = 16;
+__host__ __device__ inline int super_tiles(int T) { return (T + kSuperTiles - 1) / kSuperTiles; }
 // k_plan's words for the host (R, longest list, record slots) in the pinned read-back slot.  HLGS_PLAN_TAGGED: three
 // 64-bit words, each carrying the frame's sequence number in its high half, written by single-copy-atomic 64-bit stores,
 // so the host waits until all three carry it and the kernel needs no system-scope release (buffer_wbl2: a write-back
@@ -130,6 +139,7 @@ struct Bin {
     uint64_t* keys;
     uint64_t* keys2;
     uint32_t* point_list;  // R, tile-major then front-to-back
+    uint8_t* tile_local;   // R: the two-level binning's tile index inside the super-tile of keys2[i]
 };
 Bin carve_bin(void* base, int R, size_t* total);
 

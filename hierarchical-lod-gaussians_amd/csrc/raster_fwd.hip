@@ -577,8 +577,9 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
 
 // hist != nullptr (bin_histogram): the block's per-tile counts are stored as row blockIdx.x of hist (coalesced), and
 // k_tile_offsets turns the rows into per-(block, tile) offsets and tile totals; otherwise they are added to
-// tile_count with one device atomic per non-empty tile.
-template <int BG, bool DROP>
+// tile_count with one device atomic per non-empty tile.  SUPER: the bins are super-tiles of kSuperTiles consecutive
+// tiles (the two-level binning, k_supertile_sort), not tiles.
+template <int BG, bool DROP, bool SUPER>
 __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
                                                              uint32_t* __restrict__ tile_count, int gx, int gy, int alt,
                                                              uint32_t* __restrict__ block_tot, uint32_t* __restrict__ hist,
@@ -587,7 +588,7 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_pre[BG + 1];
     __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
-    const int T = gx * gy;
+    const int T = SUPER ? super_tiles(gx * gy) : gx * gy;  // bins
     for (int t = threadIdx.x; t < T; t += (BG / 4)) s_hist[t] = 0;
     if (threadIdx.x == 0) s_w[(BG / 4) / 64] = 0;
     __syncthreads();
@@ -596,7 +597,7 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     if (zero_words && blockIdx.x == 0)  // k_tile_offsets_plan's look-back words
         for (int i = threadIdx.x; i < n_zero; i += BG / 4) zero_words[i] = 0u;
     for_each_instance<BG, false, DROP>(g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t qm, uint32_t) {
-        if (!DROP || qm) atomicAdd(&s_hist[y * gx + x], 1u);
+        if (!DROP || qm) atomicAdd(&s_hist[SUPER ? (y * gx + x) / kSuperTiles : y * gx + x], 1u);
     });
     __syncthreads();
     if (hist) {
@@ -669,19 +670,23 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hi
 // irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
 // hist != nullptr: the block's base inside each tile segment is ranges[t].x + its k_tile_offsets offset, so the block
 // walks its instances once (no count walk, no returning device atomics).
-template <int BG, bool PACK>
+// SUPER (the two-level binning): the bins are super-tiles; ranges are the super-tiles' segments (k_tile_offsets_plan),
+// each key goes to its super-tile's segment and its tile's index inside the super-tile to tile_local at the same
+// position, for k_supertile_sort.
+template <int BG, bool PACK, bool SUPER>
 __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
                                                                   uint64_t* __restrict__ keys, int gx, int gy, int alt,
                                                                   Guard gd, const uint32_t* __restrict__ block_tot,
-                                                                  const uint32_t* __restrict__ hist)
+                                                                  const uint32_t* __restrict__ hist,
+                                                                  uint8_t* __restrict__ tile_local)
 {
     if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_base;
     __shared__ uint32_t s_pre[BG + 1];
     __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
-    const int T = gx * gy;
+    const int T = SUPER ? super_tiles(gx * gy) : gx * gy;  // bins
     uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
     uint32_t* s_rank = s_hist + T; // per-tile running rank
     for (int t = threadIdx.x; t < T; t += (BG / 4)) { s_cnt[t] = 0; s_rank[t] = 0; }
@@ -719,10 +724,12 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
     __syncthreads();
     for_each_instance<BG, true, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int x, int y, uint32_t qm, uint32_t dbits) {
         if (PACK && HLGS_DROP_EMPTY && !qm) return;  // the footprint reaches none of the tile's quadrants
-        const int tile = y * gx + x;
-        const uint32_t r = atomicAdd(&s_rank[tile], 1u);
+        const int tile = y * gx + x, bin = SUPER ? tile / kSuperTiles : tile;
+        const uint32_t r = atomicAdd(&s_rank[bin], 1u);
         const uint32_t entry = PACK ? ((uint32_t)idx << kEntryShift) | qm : (uint32_t)idx;
-        keys[s_cnt[tile] + r] = ((uint64_t)dbits << 32) | entry;
+        const uint32_t pos = s_cnt[bin] + r;
+        keys[pos] = ((uint64_t)dbits << 32) | entry;
+        if (SUPER) tile_local[pos] = (uint8_t)(tile % kSuperTiles);
     });
 }
 
@@ -860,11 +867,14 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
 // scatter block sums its predecessors' for its base), so no block reads what another rewrites.  One launch and one
 // dependent round trip instead of two launches, the second a single block.
 constexpr uint32_t kPlanPolls = 1u << 20;  // ~0.1 s of polling per word
+// super != 0 (the two-level binning): the columns are super-tiles, ranges their segments, tile_count unused; misc[1]
+// is left 0 for k_supertile_sort to raise to the longest tile list, and the host's word is the longest super-tile
+// segment (a bound on it); the big-tile list count misc[kMiscBig] is reset.
 __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict__ hist, int nb, int T,
                                                             uint32_t* __restrict__ tile_count, uint2* __restrict__ ranges,
                                                             uint32_t* __restrict__ block_tot, uint64_t* flags,
                                                             uint32_t* __restrict__ misc, uint32_t* host, uint32_t seq,
-                                                            uint32_t pack)
+                                                            uint32_t pack, int super_)
 {
     __shared__ uint32_t s_part[32][33];
     __shared__ uint32_t s_ex[32];
@@ -930,7 +940,7 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
                 off += x;
             }
         }
-        if (r == 0) tile_count[t] = tot;
+        if (r == 0 && tile_count) tile_count[t] = tot;
     }
     // look-back: thread i < blockIdx.x polls block i's word (sc1 loads, bounded: a word that never arrives marks the
     // frame failed instead of hanging the queue)
@@ -957,9 +967,10 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
             // a failed look-back reports R = ~0u, which the host turns into an error
             const uint32_t R = s_fail ? ~0u : E + s_agg, mx = max(s_max, s_bmax);
             misc[0] = R;
-            misc[1] = mx;
+            misc[1] = super_ ? 0u : mx;
             misc[2] = slots;
             misc[kMiscPack] = pack;
+            misc[kMiscBig] = 0u;
             if (host) {
 #if HLGS_PLAN_TAGGED
                 uint64_t* h = reinterpret_cast<uint64_t*>(host);
@@ -1049,16 +1060,16 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
 // Per-tile sort of up to 64 * KPL keys by one wave, entirely in registers: lane l holds elements
 // l * KPL .. l * KPL + KPL - 1; bitonic stages with partner distance < KPL are compare-exchanges inside
 // a lane, longer ones exchange with lane l ^ (j / KPL).  No LDS, no barriers.
-template <int KPL>
-__device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list,
-                                               uint32_t base, uint32_t n, int lane)
+// The keys are read through ld(e), e < n, and the entries (low words) written to out[0 .. n).
+template <int KPL, typename LD>
+__device__ __forceinline__ void wave_sort_keys(LD&& ld, uint32_t n, uint32_t* __restrict__ out, int lane)
 {
     constexpr uint32_t NP = 64u * KPL;
     uint64_t v[KPL];
 #pragma unroll
     for (int i = 0; i < KPL; i++) {
         const uint32_t e = (uint32_t)lane * KPL + i;
-        v[i] = e < n ? keys[base + e] : ~0ull;
+        v[i] = e < n ? ld(e) : ~0ull;
     }
 #pragma unroll
     for (uint32_t kk = 2; kk <= NP; kk <<= 1) {
@@ -1093,8 +1104,25 @@ __device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ keys, uint
 #pragma unroll
     for (int i = 0; i < KPL; i++) {
         const uint32_t e = (uint32_t)lane * KPL + i;
-        if (e < n) point_list[base + e] = (uint32_t)v[i];
+        if (e < n) out[e] = (uint32_t)v[i];
     }
+}
+template <int KPL>
+__device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list,
+                                               uint32_t base, uint32_t n, int lane)
+{
+    wave_sort_keys<KPL>([&](uint32_t e) { return keys[base + e]; }, n, point_list + base, lane);
+}
+// n <= kWaveSortCap keys, the smallest register layout that holds them
+template <typename LD>
+__device__ __forceinline__ void wave_sort_any(LD&& ld, uint32_t n, uint32_t* __restrict__ out, int lane)
+{
+    if (n == 0) return;
+    if (n <= 64) wave_sort_keys<1>(ld, n, out, lane);
+    else if (n <= 128) wave_sort_keys<2>(ld, n, out, lane);
+    else if (n <= 256) wave_sort_keys<4>(ld, n, out, lane);
+    else if (n <= 512) wave_sort_keys<8>(ld, n, out, lane);
+    else wave_sort_keys<16>(ld, n, out, lane);
 }
 
 // Tiles of up to kWaveSortCap instances: one wave each (k_tile_sort handles the longer ones).
@@ -1112,6 +1140,142 @@ __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__
     else if (n <= 256) wave_sort_tile<4>(keys, point_list, r.x, n, lane);
     else if (n <= 512) wave_sort_tile<8>(keys, point_list, r.x, n, lane);
     else wave_sort_tile<16>(keys, point_list, r.x, n, lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Two-level binning, second level (HLGS_TWO_LEVEL).  One 512-thread block per super-tile: the segment the key scatter
+// filled (keys2, with each key's tile index inside the super-tile in tile_local) is counted per tile, which gives the
+// tiles' ranges (the segment's start plus the tile's prefix: tile-major order, as a one-level binning has it), then
+// split into its tiles in LDS (a segment of up to kSuperCap keys; longer ones through keys in global memory), and each
+// tile of up to kWaveSortCap keys is sorted by one wave in registers and written to point_list.  Longer tiles are left
+// unsorted in keys at their range and listed for k_big_tile_sort.  Every tile list is (depth, entry)-ordered, the same
+// total order the one-level sort gives, so point_list is identical.
+// ------------------------------------------------------------------------------------------------
+constexpr int kSuperCap = 8192;  // 64 KiB of LDS
+__global__ void __launch_bounds__(512) k_supertile_sort(const uint2* __restrict__ st_ranges, int T,
+                                                        const uint64_t* __restrict__ src, const uint8_t* __restrict__ tl,
+                                                        uint64_t* __restrict__ dst, uint32_t* __restrict__ point_list,
+                                                        uint2* __restrict__ ranges, uint32_t* misc,
+                                                        uint32_t* __restrict__ big, Guard gd)
+{
+    if (guard_fail(gd)) return;
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
+    __shared__ uint32_t s_cnt[kSuperTiles], s_off[kSuperTiles], s_cur[kSuperTiles];
+    const int st = blockIdx.x;
+    const uint2 seg = st_ranges[st];
+    const uint32_t n = seg.y - seg.x;
+    const int t0 = st * kSuperTiles, nt = min(kSuperTiles, T - t0);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid < kSuperTiles) s_cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += 512) atomicAdd(&s_cnt[tl[seg.x + i]], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t a = 0;
+        for (int k = 0; k < kSuperTiles; k++) {
+            s_off[k] = a;
+            s_cur[k] = a;
+            a += s_cnt[k];
+        }
+    }
+    __syncthreads();
+    if (tid < nt) {
+        const uint32_t b = seg.x + s_off[tid];
+        ranges[t0 + tid] = make_uint2(b, b + s_cnt[tid]);
+        atomicMax(&misc[1], s_cnt[tid]);  // the longest tile list (k_tile_offsets_plan left it 0)
+    }
+    const bool staged = n <= (uint32_t)kSuperCap;
+    for (uint32_t i = tid; i < n; i += 512) {
+        const uint32_t p = atomicAdd(&s_cur[tl[seg.x + i]], 1u);  // order inside a tile is irrelevant: sorted below
+        const uint64_t key = src[seg.x + i];
+        if (staged) s_keys[p] = key;
+        else dst[seg.x + p] = key;
+    }
+    if (!staged) __threadfence_block();  // this block's own global stores, read back below
+    __syncthreads();
+    for (int k = w; k < nt; k += 512 / 64) {
+        const uint32_t c = s_cnt[k], o = s_off[k];
+        if (c <= (uint32_t)kWaveSortCap) {
+            if (staged) wave_sort_any([&](uint32_t e) { return s_keys[o + e]; }, c, point_list + seg.x + o, lane);
+            else wave_sort_any([&](uint32_t e) { return dst[seg.x + o + e]; }, c, point_list + seg.x + o, lane);
+        } else {
+            if (staged)
+                for (uint32_t e = lane; e < c; e += 64) dst[seg.x + o + e] = s_keys[o + e];
+            if (lane == 0) big[atomicAdd(&misc[kMiscBig], 1u)] = (uint32_t)(t0 + k);
+        }
+    }
+}
+
+// Tiles longer than kWaveSortCap that k_supertile_sort listed (misc[kMiscBig] of them, in big[]), keys unsorted at their
+// range in keys: a few persistent blocks take them in turn; runs of kSortCap are sorted in LDS (bitonic, as
+// k_tile_sort), then merged pairwise through keys2 (each key's rank in the partner run by binary search, as
+// k_merge_runs) until one run is left, written to point_list.
+__global__ void __launch_bounds__(256) k_big_tile_sort(const uint2* __restrict__ ranges, uint64_t* keys, uint64_t* keys2,
+                                                       uint32_t* __restrict__ point_list, const uint32_t* misc,
+                                                       const uint32_t* __restrict__ big, Guard gd)
+{
+    if (guard_fail(gd)) return;
+    __shared__ uint64_t s[kSortCap];
+    const uint32_t nbig = misc[kMiscBig];
+    const int tid = threadIdx.x;
+    for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+        const uint2 r = ranges[big[bi]];
+        const uint32_t cnt = r.y - r.x;
+        const bool multi = cnt > (uint32_t)kSortCap;
+        for (uint32_t c0 = 0; c0 < cnt; c0 += kSortCap) {
+            const uint32_t n = min((uint32_t)kSortCap, cnt - c0);
+            uint32_t np = 2;
+            while (np < n) np <<= 1;
+            for (uint32_t i = tid; i < np; i += 256) s[i] = i < n ? keys[r.x + c0 + i] : ~0ull;
+            __syncthreads();
+            for (uint32_t kk = 2; kk <= np; kk <<= 1)
+                for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                    for (uint32_t i = tid; i < np / 2; i += 256) {
+                        const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                        const bool asc = (lo & kk) == 0;
+                        const uint64_t x = s[lo], y = s[hi];
+                        if ((x > y) == asc) { s[lo] = y; s[hi] = x; }
+                    }
+                    __syncthreads();
+                }
+            for (uint32_t i = tid; i < n; i += 256) {
+                if (multi) keys[r.x + c0 + i] = s[i];
+                else point_list[r.x + c0 + i] = (uint32_t)s[i];
+            }
+            __syncthreads();
+        }
+        if (!multi) continue;
+        uint64_t* from = keys;
+        uint64_t* to = keys2;
+        for (uint32_t L = kSortCap; L < cnt; L <<= 1) {
+            __threadfence_block();
+            __syncthreads();
+            const bool last = (L << 1) >= cnt;
+            for (uint32_t i = tid; i < cnt; i += 256) {
+                const uint64_t key = from[r.x + i];
+                const uint32_t run = i / L, a = i - run * L, prun = run ^ 1u;
+                uint32_t out = i;
+                const uint64_t pstart64 = (uint64_t)prun * L;
+                if (pstart64 < cnt) {
+                    const uint32_t ps = (uint32_t)pstart64, pe = min(cnt, ps + L);
+                    uint32_t lo = ps, hi = pe;  // partner keys < key (keys are unique)
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (from[r.x + mid] < key) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    out = min(run, prun) * L + a + (lo - ps);
+                }
+                to[r.x + out] = key;
+                if (last) point_list[r.x + out] = (uint32_t)key;
+            }
+            uint64_t* t = from;
+            from = to;
+            to = t;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
 }
 
 // Merge pass for long tiles: element of run r finds its rank in the partner run by binary search.
@@ -1390,7 +1554,10 @@ __global__ void __launch_bounds__(256) k_relocation(int P, const float* __restri
 // LDS-histogram binning with the one-block plan: tile grids up to kBinMaxTiles and up to kPlanRun * 1024 blocks of
 // bin_gauss(P) Gaussians (67M); anything larger takes the generic per-Gaussian path.
 // Gaussians per binning block: 4,096, or 2,048 when that would leave fewer than ~200 blocks for the 256 CUs
-int bin_gauss(int P) { return P >= 200 * 4096 ? 4096 : 2048; }
+#ifndef HLGS_BIN_GAUSS
+#define HLGS_BIN_GAUSS 0  // 0: by P as above; 2048 or 4096: that size always (A/B)
+#endif
+int bin_gauss(int P) { return HLGS_BIN_GAUSS ? HLGS_BIN_GAUSS : P >= 200 * 4096 ? 4096 : 2048; }
 
 bool lds_binning(int P, int gx, int gy)
 {
@@ -1404,14 +1571,18 @@ static void allow_big_lds()
     if (done) return;
     // the kernels' static LDS (the block's rect prefix, ~16 KiB) comes out of the same 160 KiB
     const int dyn = 2 * (int)sizeof(uint32_t) * kBinMaxTiles;
-    hipFuncSetAttribute((const void*)k_count_tiles<4096, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_count_tiles<2048, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_count_tiles<4096, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_count_tiles<2048, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_scatter_keys_lds<4096, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_scatter_keys_lds<2048, true>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_scatter_keys_lds<4096, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    hipFuncSetAttribute((const void*)k_scatter_keys_lds<2048, false>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
+#define HLGS_BIG(...) (void)hipFuncSetAttribute((const void*)__VA_ARGS__, A, dyn)
+    HLGS_BIG(k_count_tiles<4096, false, false>); HLGS_BIG(k_count_tiles<2048, false, false>);
+    HLGS_BIG(k_count_tiles<4096, true, false>); HLGS_BIG(k_count_tiles<2048, true, false>);
+    HLGS_BIG(k_count_tiles<4096, false, true>); HLGS_BIG(k_count_tiles<2048, false, true>);
+    HLGS_BIG(k_count_tiles<4096, true, true>); HLGS_BIG(k_count_tiles<2048, true, true>);
+    HLGS_BIG(k_scatter_keys_lds<4096, true, false>); HLGS_BIG(k_scatter_keys_lds<2048, true, false>);
+    HLGS_BIG(k_scatter_keys_lds<4096, false, false>); HLGS_BIG(k_scatter_keys_lds<2048, false, false>);
+    HLGS_BIG(k_scatter_keys_lds<4096, true, true>); HLGS_BIG(k_scatter_keys_lds<2048, true, true>);
+    HLGS_BIG(k_scatter_keys_lds<4096, false, true>); HLGS_BIG(k_scatter_keys_lds<2048, false, true>);
+#undef HLGS_BIG
+    (void)hipFuncSetAttribute((const void*)k_supertile_sort, A, (int)sizeof(uint64_t) * kSuperCap);
     hipGetLastError();
     done = true;
 }
@@ -1431,22 +1602,37 @@ uint32_t* bin_histogram(const Img& im, int P, int gx, int gy)
 // The fused plan's look-back words live in the tile cursors (unused by the histogram binning): ceil(T / 32) 64-bit
 // words, within the cursors' align_up(4 T) bytes for every T >= 1.
 static uint64_t* plan_flags(const Img& im) { return reinterpret_cast<uint64_t*>(im.tile_cursor); }
+// The two-level binning applies (the LDS binning with histogram rows and the fused plan): the count, plan and scatter
+// work on super-tiles, and k_supertile_sort forms the tiles.  Its super-tile segments follow the look-back words in the
+// tile cursors: 8 ceil(NST / 32) + 8 NST bytes, NST = ceil(T / 16), within align_up(4 T) for every T >= 1.
+bool two_level(const Img& im, int P, int gx, int gy)
+{
+    return HLGS_TWO_LEVEL && HLGS_FUSED_PLAN && bin_histogram(im, P, gx, gy) != nullptr;
+}
+static uint2* super_ranges(const Img& im, int T)
+{
+    return reinterpret_cast<uint2*>(im.tile_cursor + 2 * ((super_tiles(T) + 31) / 32));
+}
 
 void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, int gx, int gy, bool alt,
                         hipStream_t s, uint32_t* hist)
 {
     uint32_t* tile_count = im.tile_count;
-    const size_t lds = sizeof(uint32_t) * (size_t)gx * gy;
+    const bool sup = two_level(im, P, gx, gy);
+    const int bins = sup ? super_tiles(gx * gy) : gx * gy;
+    const size_t lds = sizeof(uint32_t) * (size_t)bins;
     allow_big_lds();
     const int bg = bin_gauss(P);
     const bool fused = hist && HLGS_FUSED_PLAN;
     uint32_t* zw = fused ? im.tile_cursor : nullptr;
-    const int nz = fused ? 2 * ((gx * gy + 31) / 32) : 0;
+    const int nz = fused ? 2 * ((bins + 31) / 32) : 0;
     const bool drop = g.pack && HLGS_DROP_EMPTY;
-#define HLGS_CNT(BG, D) hipLaunchKernelGGL((k_count_tiles<BG, D>), dim3((P + BG - 1) / BG), dim3(BG / 4), lds, s, P, radii, g, \
-                                          tile_count, gx, gy, (int)alt, g.scan_tmp, hist, zw, nz)
-    if (bg == 4096) { if (drop) HLGS_CNT(4096, true); else HLGS_CNT(4096, false); }
-    else { if (drop) HLGS_CNT(2048, true); else HLGS_CNT(2048, false); }
+#define HLGS_CNT(BG, D, S) hipLaunchKernelGGL((k_count_tiles<BG, D, S>), dim3((P + BG - 1) / BG), dim3(BG / 4), lds, s, P, \
+                                             radii, g, tile_count, gx, gy, (int)alt, g.scan_tmp, hist, zw, nz)
+#define HLGS_CNT2(BG, S) do { if (drop) HLGS_CNT(BG, true, S); else HLGS_CNT(BG, false, S); } while (0)
+    if (sup) { if (bg == 4096) HLGS_CNT2(4096, true); else HLGS_CNT2(2048, true); }
+    else { if (bg == 4096) HLGS_CNT2(4096, false); else HLGS_CNT2(2048, false); }
+#undef HLGS_CNT2
 #undef HLGS_CNT
     if (hist && !fused) {
         const int T = gx * gy, nb = (P + bin_gauss(P) - 1) / bin_gauss(P);
@@ -1461,9 +1647,15 @@ void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* 
 
     uint32_t* hist = bin_histogram(im, P, gx, gy);
     const int nb = (P + bin_gauss(P) - 1) / bin_gauss(P);
+    if (two_level(im, P, gx, gy)) {  // columns = super-tiles
+        const int C = super_tiles(T);
+        hipLaunchKernelGGL(k_tile_offsets_plan, dim3((C + 31) / 32), dim3(1024), 0, s, hist, nb, C, nullptr,
+                           super_ranges(im, T), g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, 1);
+        return;
+    }
     if (hist && HLGS_FUSED_PLAN) {
         hipLaunchKernelGGL(k_tile_offsets_plan, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count,
-                           im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack);
+                           im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, 0);
         return;
     }
     uint32_t* cursor = hist ? nullptr : im.tile_cursor;
@@ -1526,12 +1718,33 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
     const int T = gx * gy;
     const int alt = a.variant == HLGS_VARIANT_ALT;
     if (timing) stage_mark(s, 3, true);
+    if (two_level(im, a.P, gx, gy)) {
+        // first level: keys into their super-tiles' segments (keys2) with their tile inside it (tile_local)
+        allow_big_lds();
+        const int C = super_tiles(T);
+#define HLGS_SCATTER(BG, PK)                                                                                       \
+    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK, true>), dim3((a.P + BG - 1) / BG), dim3(BG / 4),                     \
+                       2 * sizeof(uint32_t) * (size_t)C, s, a.P, radii, g, super_ranges(im, T), nullptr, b.keys2, gx, gy, \
+                       alt, gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy), b.tile_local)
+        const bool pk = pack_entries(a.P);
+        if (bin_gauss(a.P) == 4096) { if (pk) HLGS_SCATTER(4096, true); else HLGS_SCATTER(4096, false); }
+        else { if (pk) HLGS_SCATTER(2048, true); else HLGS_SCATTER(2048, false); }
+#undef HLGS_SCATTER
+        if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
+        // second level: tiles, their ranges and their sorted lists; tiles past kWaveSortCap through k_big_tile_sort
+        hipLaunchKernelGGL(k_supertile_sort, dim3(C), dim3(512), sizeof(uint64_t) * kSuperCap, s, super_ranges(im, T), T,
+                           b.keys2, b.tile_local, b.keys, b.point_list, im.ranges, im.misc, im.tile_count, gd);
+        hipLaunchKernelGGL(k_big_tile_sort, dim3(64), dim3(256), 0, s, im.ranges, b.keys, b.keys2, b.point_list, im.misc,
+                           im.tile_count, gd);
+        if (timing) stage_mark(s, 4, false);
+        return;
+    }
     if (lds_binning(a.P, gx, gy)) {
         allow_big_lds();
 #define HLGS_SCATTER(BG, PK)                                                                                       \
-    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK>), dim3((a.P + BG - 1) / BG), dim3(BG / 4),                           \
+    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK, false>), dim3((a.P + BG - 1) / BG), dim3(BG / 4),                    \
                        2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy, alt, \
-                       gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy))
+                       gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy), nullptr)
         const bool pk = pack_entries(a.P);
         if (bin_gauss(a.P) == 4096) { if (pk) HLGS_SCATTER(4096, true); else HLGS_SCATTER(4096, false); }
         else { if (pk) HLGS_SCATTER(2048, true); else HLGS_SCATTER(2048, false); }
