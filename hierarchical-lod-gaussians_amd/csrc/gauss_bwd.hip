@@ -53,8 +53,16 @@ __device__ __forceinline__ void cov3d_exact(f3 scale, float mod, float4 q, float
 #endif
 // One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
 // backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
+#ifndef HLGS_GBWD_WAVES
+#define HLGS_GBWD_WAVES 0  // > 0: ask for that many waves per SIMD (a VGPR cap; 120 VGPRs give 4)
+#endif
+#if HLGS_GBWD_WAVES > 0
+#define HLGS_GBWD_BOUNDS __launch_bounds__(256, HLGS_GBWD_WAVES)
+#else
+#define HLGS_GBWD_BOUNDS __launch_bounds__(256)
+#endif
 template <bool HIER, bool ALT>
-__global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
+__global__ void HLGS_GBWD_BOUNDS k_gauss_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
                                                    BwdScratch rec, hlgs_grads o, float fx, float fy, int has_depth,
                                                    const uint32_t* __restrict__ misc)
 {
