@@ -355,8 +355,16 @@ __device__ __forceinline__ void sh_rows_load_contig(const float* gbase, float* l
     }
 }
 
+#ifndef HLGS_PRE_WAVES
+#define HLGS_PRE_WAVES 0  // > 0: ask for that many waves per SIMD (a VGPR cap; 102 VGPRs give 4; measured no gain)
+#endif
+#if HLGS_PRE_WAVES > 0
+#define HLGS_PRE_BOUNDS __launch_bounds__(128, HLGS_PRE_WAVES)
+#else
+#define HLGS_PRE_BOUNDS __launch_bounds__(128)
+#endif
 template <bool ALT, int M3T>
-__global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
+__global__ void HLGS_PRE_BOUNDS k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
                                                         int gy, float fx, float fy, ZeroJob z)
 {
     __shared__ float s_rows[64 * kShStride];
