@@ -559,6 +559,22 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// Its inverse: the workgroup whose xcd_remap is i (the i-th in XCD-grouped order).
+__device__ __forceinline__ int xcd_unmap(int i, int nwg)
+{
+    const int q = nwg / 8, r = nwg % 8;
+    int x, k;
+    if (i < r * (q + 1)) {
+        x = i / (q + 1);
+        k = i - x * (q + 1);
+    } else {
+        const int j = i - r * (q + 1);
+        x = r + j / q;
+        k = j - (x - r) * q;
+    }
+    return x + 8 * k;
+}
+
 // One DPP lane permutation of v (ctrl: quad_perm / row_ror / row_bcast encodings).
 template <int CTRL, int ROW, bool BC>
 __device__ __forceinline__ float dpp(float v)

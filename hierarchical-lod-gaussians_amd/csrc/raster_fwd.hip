@@ -619,6 +619,31 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     }
 }
 
+// HLGS_XCD_RUNS: a tile segment holds the count blocks' runs in XCD-grouped block order (xcd_unmap), not in block order,
+// so that the runs next to each other in memory are written by scatter blocks of the same XCD (workgroups go to XCDs
+// round robin): their partial lines meet in that XCD's L2 and leave it whole, instead of as partial lines from eight
+// L2s.  The order inside a segment is free (k_tile_sort orders it).
+#ifndef HLGS_XCD_RUNS
+#define HLGS_XCD_RUNS 1
+#endif
+// The histogram rows of logical positions i, i + 1, ... in that order, stepped without a division per row.
+struct HistRows {
+    int i, x, k, q, r;
+    __device__ HistRows(int i0, int nb) : i(i0), x(0), k(0), q(nb / 8), r(nb % 8)
+    {
+        if (HLGS_XCD_RUNS) {
+            const int b = xcd_unmap(i0, nb);
+            x = b % 8;
+            k = b / 8;
+        }
+    }
+    __device__ int row() const { return HLGS_XCD_RUNS ? x + 8 * k : i; }
+    __device__ void next()
+    {
+        i++;
+        if (++k == (x < r ? q + 1 : q)) { x++; k = 0; }
+    }
+};
 // The count blocks' histogram rows (nb x T) -> in place, each block's exclusive offset inside every tile's segment (the
 // blocks in order), and tile_count[t] = the tile's total.  32 tiles per workgroup (128-byte row segments), 32 row
 // groups of 32 threads; each thread takes a contiguous run of blocks down its tile's column, issues all of a run's
@@ -634,15 +659,23 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hi
     const int run = (nb + 31) / 32, b0 = r * run, b1 = min(nb, b0 + run);
     constexpr int K = 8;
     uint32_t v[K];
+    int rows[K];
     uint32_t sum = 0;
     if (t < T) {
         if (run <= K) {
+            HistRows it(b0, nb);
 #pragma unroll
-            for (int k = 0; k < K; k++) v[k] = b0 + k < b1 ? hist[(size_t)(b0 + k) * T + t] : 0u;
+            for (int k = 0; k < K; k++) {
+                rows[k] = it.row();
+                it.next();
+            }
+#pragma unroll
+            for (int k = 0; k < K; k++) v[k] = b0 + k < b1 ? hist[(size_t)rows[k] * T + t] : 0u;
 #pragma unroll
             for (int k = 0; k < K; k++) sum += v[k];
         } else {
-            for (int b = b0; b < b1; b++) sum += hist[(size_t)b * T + t];
+            HistRows it(b0, nb);
+            for (int b = b0; b < b1; b++, it.next()) sum += hist[(size_t)it.row() * T + t];
         }
     }
     s_part[r][c] = sum;
@@ -659,12 +692,13 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hi
 #pragma unroll
         for (int k = 0; k < K; k++)
             if (b0 + k < b1) {
-                hist[(size_t)(b0 + k) * T + t] = off;
+                hist[(size_t)rows[k] * T + t] = off;
                 off += v[k];
             }
     } else {
-        for (int b = b0; b < b1; b++) {
-            uint32_t* h = hist + (size_t)b * T + t;
+        HistRows it(b0, nb);
+        for (int b = b0; b < b1; b++, it.next()) {
+            uint32_t* h = hist + (size_t)it.row() * T + t;
             const uint32_t x = *h;
             *h = off;
             off += x;
@@ -673,6 +707,9 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hi
     if (r == 0) tile_count[t] = tot;
 }
 
+#ifndef HLGS_SCATTER_BATCH
+#define HLGS_SCATTER_BATCH 1  // key scatter: four rank atomics in flight per thread (narrow rects)
+#endif
 // Same block -> Gaussian mapping as k_count_tiles: reserve the block's run inside every tile segment
 // with one returning atomic per bin, then hand out slots from LDS.  Slot order inside a tile is
 // irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
@@ -730,6 +767,61 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         }
     }
     __syncthreads();
+#if HLGS_SCATTER_BATCH
+    if (!alt && s_w[(BG / 4) / 64] <= kNarrowRect) {
+        // Narrow rects (for_each_instance's one-thread-per-Gaussian path): each thread's instances in groups of four,
+        // the four rank atomics issued together and then the four key stores -- one at a time, every store waits for
+        // its atomic's return.
+        const int g0 = blockIdx.x * BG;
+        constexpr int J = 4;
+        float2 gxy[J];
+        int2 gext[J];
+        uint32_t gmask[J], gdb[J];
+        bool live[J];
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            const int k = threadIdx.x + j * (BG / 4);
+            live[j] = s_pre[k + 1] != s_pre[k];
+            if (live[j]) {
+                gxy[j] = g.means2D[g0 + k];
+                gext[j] = g.rects[g0 + k];
+                gmask[j] = PACK ? g.qmask[g0 + k] : 0u;
+                gdb[j] = __float_as_uint(g.depths[g0 + k]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (!live[j]) continue;
+            const uint32_t idx = (uint32_t)(g0 + threadIdx.x + j * (BG / 4));
+            int x0, y0, x1, y1;
+            tile_rect(gxy[j].x, gxy[j].y, gext[j].x, gext[j].y, gx, gy, x0, y0, x1, y1);
+            const int w = x1 - x0, n = w * (y1 - y0);
+            int tx = 0, ty = 0;
+            for (int c = 0; c < n; c += 4) {
+                uint32_t pos[4], ent[4], loc[4];
+                bool use[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int r = c + u;
+                    const uint32_t qm = PACK ? rect_tile_mask(gmask[j], (uint32_t)r) : 0u;
+                    use[u] = r < n && !(PACK && HLGS_DROP_EMPTY && !qm);
+                    const int tile = (y0 + ty) * gx + x0 + tx, bin = SUPER ? tile / kSuperTiles : tile;
+                    if (use[u]) pos[u] = s_cnt[bin] + atomicAdd(&s_rank[bin], 1u);
+                    ent[u] = PACK ? (idx << kEntryShift) | qm : idx;
+                    loc[u] = (uint32_t)(tile % kSuperTiles);
+                    if (++tx == w) { tx = 0; ty++; }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (use[u]) {
+                        keys[pos[u]] = ((uint64_t)gdb[j] << 32) | ent[u];
+                        if (SUPER) tile_local[pos[u]] = (uint8_t)loc[u];
+                    }
+            }
+        }
+        return;
+    }
+#endif
     for_each_instance<BG, true, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int x, int y, uint32_t qm, uint32_t dbits) {
         if (PACK && HLGS_DROP_EMPTY && !qm) return;  // the footprint reaches none of the tile's quadrants
         const int tile = y * gx + x, bin = SUPER ? tile / kSuperTiles : tile;
@@ -894,16 +986,24 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
     const int run = (nb + 31) / 32, b0 = r * run, b1 = min(nb, b0 + run);
     constexpr int K = 8;
     uint32_t v[K];
+    int rows[K];
     uint32_t sum = 0;
     if (threadIdx.x == 0) { s_sum = 0; s_max = 0; s_fail = 0; }
     if (t < T) {
         if (run <= K) {
+            HistRows it(b0, nb);
 #pragma unroll
-            for (int k = 0; k < K; k++) v[k] = b0 + k < b1 ? hist[(size_t)(b0 + k) * T + t] : 0u;
+            for (int k = 0; k < K; k++) {
+                rows[k] = it.row();
+                it.next();
+            }
+#pragma unroll
+            for (int k = 0; k < K; k++) v[k] = b0 + k < b1 ? hist[(size_t)rows[k] * T + t] : 0u;
 #pragma unroll
             for (int k = 0; k < K; k++) sum += v[k];
         } else {
-            for (int b = b0; b < b1; b++) sum += hist[(size_t)b * T + t];
+            HistRows it(b0, nb);
+            for (int b = b0; b < b1; b++, it.next()) sum += hist[(size_t)it.row() * T + t];
         }
     }
     s_part[r][c] = sum;
@@ -937,12 +1037,13 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
 #pragma unroll
             for (int k = 0; k < K; k++)
                 if (b0 + k < b1) {
-                    hist[(size_t)(b0 + k) * T + t] = off;
+                    hist[(size_t)rows[k] * T + t] = off;
                     off += v[k];
                 }
         } else {
-            for (int b = b0; b < b1; b++) {
-                uint32_t* h = hist + (size_t)b * T + t;
+            HistRows it(b0, nb);
+            for (int b = b0; b < b1; b++, it.next()) {
+                uint32_t* h = hist + (size_t)it.row() * T + t;
                 const uint32_t x = *h;
                 *h = off;
                 off += x;
