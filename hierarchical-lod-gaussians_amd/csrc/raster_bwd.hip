@@ -264,6 +264,9 @@ struct BwdArgs {
 #ifndef HLGS_BWD_PAIR
 #define HLGS_BWD_PAIR 0  // two visited splats per loop iteration, one twenty-moment reduction (wave_reduce20_rs)
 #endif
+#ifndef HLGS_BWD_TILE_MAJOR
+#define HLGS_BWD_TILE_MAJOR 0  // 0: chunk-major (the front chunks, where most pixels are live, start first)
+#endif
 #ifndef HLGS_BWD_MSTRIDE
 #define HLGS_BWD_MSTRIDE 65
 #endif
@@ -273,8 +276,15 @@ struct BwdArgs {
 template <bool INTERP, bool DEPTH, bool ALT>
 __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
 {
+#if HLGS_BWD_TILE_MAJOR
+    // a tile's chunk waves next to each other in dispatch order and on one XCD, so the second and third read of the
+    // tile's per-pixel inputs hit that XCD's L2
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = L / (kBwdSplits + 1), part = L - tile * (kBwdSplits + 1);
+#else
     const int part = blockIdx.x / A.T;
     const int tile = xcd_remap(blockIdx.x - part * A.T, A.T);
+#endif
     const uint2* __restrict__ ranges = A.ranges;
     const uint32_t* __restrict__ point_list = A.point_list;
     const int W = A.W, H = A.H, gx = A.gx;
