@@ -1051,6 +1051,13 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
         }
         if (r == 0 && tile_count) tile_count[t] = tot;
     }
+    uint32_t slots = 0;
+    if ((int)blockIdx.x == NB - 1) {  // the count blocks' totals summed (record slots), ahead of the look-back wait
+        PlanRun rb;
+        plan_load(block_tot, nb, rb);
+        uint32_t unused = 0;
+        slots = plan_scan(rb, s_w, unused, [&](int, uint32_t, uint32_t) {});
+    }
     // look-back: thread i < blockIdx.x polls block i's word (sc1 loads, bounded: a word that never arrives marks the
     // frame failed instead of hanging the queue)
     if ((int)threadIdx.x < (int)blockIdx.x) {
@@ -1067,11 +1074,7 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
     __syncthreads();
     const uint32_t E = s_sum;
     if (r == 0 && t < T) ranges[t] = make_uint2(E + s_ex[c], E + s_ex[c] + tot);
-    if ((int)blockIdx.x == NB - 1) {  // the count blocks' totals summed: record slots (the scatter sums its own base)
-        PlanRun rb;
-        plan_load(block_tot, nb, rb);
-        uint32_t unused = 0;
-        const uint32_t slots = plan_scan(rb, s_w, unused, [&](int, uint32_t, uint32_t) {});
+    if ((int)blockIdx.x == NB - 1) {  // misc and the host words (the scatter sums its own base)
         if (threadIdx.x == 0) {
             // a failed look-back reports R = ~0u, which the host turns into an error
             const uint32_t R = s_fail ? ~0u : E + s_agg, mx = max(s_max, s_bmax);
