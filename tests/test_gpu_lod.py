@@ -46,6 +46,36 @@ def test_point_list_and_ranges_bit_exact(P, W, H, band):
     np.testing.assert_array_equal(out[7].cpu().numpy(), fr.seen)
 
 
+@pytest.mark.parametrize("W,H", [(2048, 2048), (2064, 2048)])
+def test_tile_grid_limits_lists_bit_exact(W, H):
+    """The largest tile grid the LDS binning takes (128 x 128 = 16,384 tiles: 512 look-back blocks in the fused plan)
+    and the next width up, which takes the generic path (device-atomic tile counts in the preprocess, one thread per
+    Gaussian in the key scatter): ranges, point_list, n_contrib and seen against the oracle, with the zero-mask
+    instances left out by both paths alike."""
+    from diff_gaussian_rasterization import _C
+    P = 150_000
+    cam = S.make_camera(W, H)
+    sc = S.make_gaussians(P, 1, cam, seed=23)
+    fr = O.forward(dict(sc), S.cam_numpy(cam), drop_empty=drops_empty(P))
+    t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
+    e = torch.empty(0, device=DEV)
+    out = _C.rasterize_gaussians(cam["bg"], e, e, e, e, t(sc["means3D"]), e, t(sc["opacities"]), t(sc["scales"]),
+                                 t(sc["rotations"]), 1.0, e, cam["viewmatrix"], cam["projmatrix"], cam["tanfovx"],
+                                 cam["tanfovy"], H, W, t(sc["shs"]), 1, cam["campos"], False, True, True)
+    R = out[0]
+    assert R == fr.R
+    kept = binned(fr)
+    np.testing.assert_array_equal(_C.inspect_ranges(out[5], W, H).cpu().numpy().astype(np.uint32), fr.ranges)
+    np.testing.assert_array_equal(_C.inspect_point_list(out[4], kept, P).cpu().numpy().astype(np.uint32),
+                                  fr.point_list[:kept])
+    N = W * H
+    n_contrib = _C._field(out[5], (4 * N + 255) // 256 * 256, N, torch.int32).cpu().numpy()
+    np.testing.assert_array_equal(n_contrib, fr.n_contrib.astype(np.int32))
+    np.testing.assert_array_equal(out[7].cpu().numpy(), fr.seen)
+    mx, nbad, ok = image_check(out[1].cpu().numpy(), fr.color)
+    assert ok, (mx, nbad)
+
+
 @pytest.mark.parametrize("deg", [0, 3])
 def test_decisions_bit_exact_for_elongated_splats(deg):
     """Strongly anisotropic splats (the float quadratic form cancels): the GPU keeps and skips exactly the
