@@ -76,6 +76,23 @@ def test_tile_grid_limits_lists_bit_exact(W, H):
     assert ok, (mx, nbad)
 
 
+def test_generic_binning_path_backward():
+    """Forward and backward through the generic binning path (a tile grid above the LDS binning's 16,384 tiles), with
+    the zero-mask instances dropped: the Gaussian backward skips their never-written record slots."""
+    W, H, P = 2064, 2048, 60_000
+    cam = S.make_camera(W, H)
+    sc = S.make_gaussians(P, 3, cam, seed=29)
+    g = S.upstream_grads(W, H, seed=4)
+    gpu = gpu_render(sc, cam, grads=g)
+    ref = oracle_render(sc, cam, grads=g, drop_empty=drops_empty(P))
+    np.testing.assert_array_equal(gpu["radii"], ref["radii"])
+    mx, nbad, ok = image_check(gpu["color"], ref["color"])
+    assert ok, (mx, nbad)
+    for k in ref:
+        if k.startswith("d"):
+            assert_grad(k, gpu[k][..., :ref[k].shape[-1]], ref[k])
+
+
 @pytest.mark.parametrize("deg", [0, 3])
 def test_decisions_bit_exact_for_elongated_splats(deg):
     """Strongly anisotropic splats (the float quadratic form cancels): the GPU keeps and skips exactly the
