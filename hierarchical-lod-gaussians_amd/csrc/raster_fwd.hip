@@ -1172,9 +1172,9 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
 // Per-tile sort of up to 64 * KPL keys by one wave, entirely in registers: lane l holds elements
 // l * KPL .. l * KPL + KPL - 1; bitonic stages with partner distance < KPL are compare-exchanges inside
 // a lane, longer ones exchange with lane l ^ (j / KPL).  No LDS, no barriers.
-// The keys are read through ld(e), e < n, and the entries (low words) written to out[0 .. n).
-template <int KPL, typename LD>
-__device__ __forceinline__ void wave_sort_keys(LD&& ld, uint32_t n, uint32_t* __restrict__ out, int lane)
+// The keys are read through ld(e), e < n, and each sorted key handed to st(e, key).
+template <int KPL, typename LD, typename ST>
+__device__ __forceinline__ void wave_sort_keys_st(LD&& ld, uint32_t n, ST&& st, int lane)
 {
     constexpr uint32_t NP = 64u * KPL;
     uint64_t v[KPL];
@@ -1216,7 +1216,58 @@ __device__ __forceinline__ void wave_sort_keys(LD&& ld, uint32_t n, uint32_t* __
 #pragma unroll
     for (int i = 0; i < KPL; i++) {
         const uint32_t e = (uint32_t)lane * KPL + i;
-        if (e < n) out[e] = (uint32_t)v[i];
+        if (e < n) st(e, v[i]);
+    }
+}
+// ... with the entries (low words) written to out[0 .. n)
+template <int KPL, typename LD>
+__device__ __forceinline__ void wave_sort_keys(LD&& ld, uint32_t n, uint32_t* __restrict__ out, int lane)
+{
+    wave_sort_keys_st<KPL>(ld, n, [&](uint32_t e, uint64_t v) { out[e] = (uint32_t)v; }, lane);
+}
+// n <= 64 KMAX keys with the fewest keys per lane that hold them
+template <int KMAX, typename LD, typename ST>
+__device__ __forceinline__ void wave_sort_upto(LD&& ld, uint32_t n, ST&& st, int lane)
+{
+    if (n <= 64) { wave_sort_keys_st<1>(ld, n, st, lane); return; }
+    if constexpr (KMAX >= 2) if (n <= 128) { wave_sort_keys_st<2>(ld, n, st, lane); return; }
+    if constexpr (KMAX >= 4) if (n <= 256) { wave_sort_keys_st<4>(ld, n, st, lane); return; }
+    if constexpr (KMAX >= 8) if (n <= 512) { wave_sort_keys_st<8>(ld, n, st, lane); return; }
+    if constexpr (KMAX >= 16) wave_sort_keys_st<16>(ld, n, st, lane);
+}
+// HLGS_SORT_SPLIT: n in (64 KH, 128 KH]: the first 64 KH keys sorted with KH keys per lane and the other n - 64 KH
+// with the fewest that hold them, both into LDS, then merged -- each lane finds the start of its run of ceil(n / 64)
+// outputs on the merge path (binary search) and merges the run.  A 300-key tile then costs a 256-key and a 64-key
+// register sort instead of a 512-key one (the mean configs[1] list is 258 keys).  Keys are unique, so the merge is
+// the same total order.
+#ifndef HLGS_SORT_SPLIT
+#define HLGS_SORT_SPLIT 1
+#endif
+template <int KH>
+__device__ __forceinline__ void wave_sort_split(const uint64_t* __restrict__ keys, uint32_t base, uint32_t n,
+                                                uint32_t* __restrict__ out, int lane, uint64_t* s)
+{
+    constexpr uint32_t A = 64u * KH;
+    const uint32_t m = n - A;  // 1 .. A
+    wave_sort_keys_st<KH>([&](uint32_t e) { return keys[base + e]; }, A, [&](uint32_t e, uint64_t v) { s[e] = v; },
+                          lane);
+    wave_sort_upto<KH>([&](uint32_t e) { return keys[base + A + e]; }, m, [&](uint32_t e, uint64_t v) { s[A + e] = v; },
+                       lane);
+    __syncthreads();  // one wave: the LDS stores before the loads
+    const uint32_t per = (n + 63u) / 64u, k0 = min(n, (uint32_t)lane * per), k1 = min(n, k0 + per);
+    uint32_t lo = k0 > m ? k0 - m : 0u, hi = min(k0, A);  // A keys among the first k0 outputs
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s[mid] < s[A + (k0 - mid - 1)]) lo = mid + 1;
+        else hi = mid;
+    }
+    uint32_t i = lo, j = k0 - lo;
+    for (uint32_t k = k0; k < k1; k++) {
+        const bool takeA = j >= m || (i < A && s[i] < s[A + j]);
+        const uint64_t v = takeA ? s[i] : s[A + j];
+        out[base + k] = (uint32_t)v;
+        if (takeA) i++;
+        else j++;
     }
 }
 template <int KPL>
@@ -1247,6 +1298,15 @@ __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__
     const uint32_t n = r.y - r.x;
     const int lane = threadIdx.x;
     if (n == 0 || n > (uint32_t)kWaveSortCap) return;
+#if HLGS_SORT_SPLIT
+    __shared__ uint64_t s_sort[kWaveSortCap + 1];  // + 1: the merge may read one past the second run
+    if (n <= 64) wave_sort_tile<1>(keys, point_list, r.x, n, lane);
+    else if (n <= 128) wave_sort_split<1>(keys, r.x, n, point_list, lane, s_sort);
+    else if (n <= 256) wave_sort_split<2>(keys, r.x, n, point_list, lane, s_sort);
+    else if (n <= 512) wave_sort_split<4>(keys, r.x, n, point_list, lane, s_sort);
+    else wave_sort_split<8>(keys, r.x, n, point_list, lane, s_sort);
+    return;
+#endif
     if (n <= 64) wave_sort_tile<1>(keys, point_list, r.x, n, lane);
     else if (n <= 128) wave_sort_tile<2>(keys, point_list, r.x, n, lane);
     else if (n <= 256) wave_sort_tile<4>(keys, point_list, r.x, n, lane);
