@@ -16,18 +16,21 @@
 #include "hlgs_internal.h"
 
 namespace hlgs {
-int g_entry_packing = HLGS_PACK_ENTRIES;  // hlgs_set_entry_packing
+int g_entry_packing = 1;  // hlgs_set_entry_packing
+int g_drop_empty = 1;     // hlgs_set_drop_empty
+extern uint32_t g_plan_polls;  // hlgs_set_plan_polls (raster_fwd.hip)
 bool pack_entries(int P) { return g_entry_packing && P < (1 << (32 - kEntryShift)); }
+bool drop_empty(int P) { return g_drop_empty && pack_entries(P); }
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
                        const ZeroJob& z,
                        hipStream_t s);
 void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s);
-void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s);
+void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s,
+                 bool fused);
 bool lds_binning(int P, int gx, int gy);
 uint32_t* bin_histogram(const Img& im, int P, int gx, int gy);
-bool two_level(const Img& im, int P, int gx, int gy);
 void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, int gx, int gy, bool alt,
-                        hipStream_t s, uint32_t* hist);
+                        hipStream_t s, uint32_t* hist, bool fused);
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b, int gx,
                     int gy, uint32_t max_count, hipStream_t s, bool timing, Guard gd);
 void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, int gx, int gy,
@@ -105,6 +108,7 @@ Geom carve_geom(void* base, int P, size_t* total)
     g.sh_jac = take<float>(p, 9 * (size_t)P);
     g.qmask = take<uint32_t>(p, (size_t)P);
     g.pack = pack_entries(P) ? 1 : 0;
+    g.drop = drop_empty(P) ? 1 : 0;
     g.scan_tmp = take<uint32_t>(p, scan_scratch_elems(P));
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return g;
@@ -135,7 +139,6 @@ Bin carve_bin(void* base, int R, size_t* total)
     b.point_list = take<uint32_t>(p, R);  // first: its offset does not depend on R
     b.keys = take<uint64_t>(p, R);
     b.keys2 = take<uint64_t>(p, R);
-    b.tile_local = take<uint8_t>(p, R);
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return b;
 }
@@ -275,9 +278,11 @@ size_t hlgs_backward_scratch_size(int P, int R)
 
 static void* aligned(const void* p) { return (void*)align_up((size_t)p); }
 
-void hlgs_set_entry_packing(int on) { g_entry_packing = on ? HLGS_PACK_ENTRIES : 0; }
+void hlgs_set_entry_packing(int on) { g_entry_packing = on ? 1 : 0; }
+void hlgs_set_drop_empty(int on) { g_drop_empty = on ? 1 : 0; }
+void hlgs_set_plan_polls(unsigned polls) { g_plan_polls = polls; }
 int hlgs_point_list_entry_shift(int P) { return pack_entries(P) ? kEntryShift : 0; }
-int hlgs_point_list_drops_empty(int P) { return pack_entries(P) && HLGS_DROP_EMPTY ? 1 : 0; }
+int hlgs_point_list_drops_empty(int P) { return drop_empty(P) ? 1 : 0; }
 
 size_t hlgs_binning_point_list_offset(int R)
 {
@@ -300,7 +305,7 @@ namespace hlgs {
 // binning the preprocess also clears tile_count and `seen`, and one k_plan block does both scans and the ranges and
 // mirrors misc into `host` (pinned, may be null); otherwise the generic path runs device-wide scans.
 static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int* radii, int* seen, uint32_t* host,
-                          uint32_t seq, hipStream_t s)
+                          uint32_t seq, hipStream_t s, bool fused = true)
 {
     const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16, T = gx * gy;
     Geom g = carve_geom(aligned(geom), a->P, nullptr);
@@ -314,11 +319,11 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
         launch_preprocess(*a, g, radii, nullptr, gx, gy, ZeroJob{im.tile_count, T, seen, a->P}, s);
         stage_mark(s, ST_PRE, false);
         stage_mark(s, ST_COUNT_TILES, true);
-        launch_count_tiles(a->P, radii, g, im, gx, gy, alt, s, bin_histogram(im, a->P, gx, gy));
+        launch_count_tiles(a->P, radii, g, im, gx, gy, alt, s, bin_histogram(im, a->P, gx, gy), fused);
         stage_mark(s, ST_COUNT_TILES, false);
         if ((rc = check_stage(s, a->debug, "preprocess"))) return rc;
         stage_mark(s, ST_SCAN, true);
-        launch_plan(a->P, g, im, gx, gy, host, seq, s);
+        launch_plan(a->P, g, im, gx, gy, host, seq, s, fused);
         stage_mark(s, ST_SCAN, false);
         return check_stage(s, a->debug, "scan");
     }
@@ -341,6 +346,22 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
     return HLGS_OK;
 }
 
+// The binning plan again with the two launches that need no inter-block wait (k_tile_offsets + k_plan), for a frame
+// whose fused plan reported a timed-out look-back (k_tile_offsets_plan: R = ~0u).  The preprocess outputs are intact;
+// the count kernel rewrites the histogram rows the failed plan had partly turned into offsets.
+static int replan_launch(const hlgs_raster_args* a, void* geom, void* img, const int* radii, uint32_t* host,
+                         uint32_t seq, hipStream_t s)
+{
+    const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16;
+    Geom g = carve_geom(aligned(geom), a->P, nullptr);
+    Img im = carve_img(aligned(img), a->W, a->H, nullptr);
+    hipGetLastError();
+    launch_count_tiles(a->P, radii, g, im, gx, gy, a->variant == HLGS_VARIANT_ALT, s, bin_histogram(im, a->P, gx, gy),
+                       false);
+    launch_plan(a->P, g, im, gx, gy, host, seq, s, false);
+    return check_stage(s, a->debug, "re-plan");
+}
+
 static int render_launch(const hlgs_raster_args* a, const int* radii, void* geom, void* img, void* binning, int R_carve,
                          uint32_t max_count, float* out_color, float* out_invdepth, int* seen, hipStream_t s, Guard gd)
 {
@@ -361,15 +382,15 @@ static int render_launch(const hlgs_raster_args* a, const int* radii, void* geom
 // Largest R whose binning layout fits in `bytes`.
 static int binning_capacity(size_t bytes)
 {
-    if (bytes <= 5 * kAlign) return 0;
-    long r = (long)((bytes - 5 * kAlign) / 21);
+    if (bytes <= 4 * kAlign) return 0;
+    long r = (long)((bytes - 4 * kAlign) / 20);
     while (r > 0 && hlgs_binning_buffer_size((int)r) > bytes) r--;
     return (int)std::min<long>(r, 0x7fffffff);
 }
 
 // Pinned read-back slot and event for the speculative forward, per thread and device.
 struct Readback {
-    uint32_t* host = nullptr;  // [0..2] = R, longest list, record slots; [3] = the frame's sequence number (k_plan)
+    uint32_t* host = nullptr;  // three 64-bit words: the frame's sequence number | R, longest list, record slots (k_plan)
     hipEvent_t ev = nullptr;
     uint32_t last_maxc = 0;  // longest tile list of the previous frame (plans the speculative sort)
     uint32_t seq = 0;
@@ -377,10 +398,9 @@ struct Readback {
 // Wait until k_plan has mirrored the frame's words (host[3] == seq), polling the coherent pinned words rather than
 // synchronising on an event recorded after k_plan: an event is a queue barrier, ~6 us of idle GPU before the binning.
 // A stream that drains or fails without the words reports an error instead of spinning forever.
-// HLGS_PLAN_TAGGED: words[i] = the three tagged 64-bit words' low halves once all of them carry seq.
+// words[i] = the three tagged 64-bit words' low halves once all of them carry seq (plan_host_words, raster_fwd.hip).
 static bool plan_words_ready(const uint32_t* host, uint32_t seq, uint32_t* words)
 {
-#if HLGS_PLAN_TAGGED
     const uint64_t* h = reinterpret_cast<const uint64_t*>(host);
     for (int i = 0; i < 3; i++) {
         const uint64_t v = __atomic_load_n(&h[i], __ATOMIC_ACQUIRE);
@@ -388,11 +408,6 @@ static bool plan_words_ready(const uint32_t* host, uint32_t seq, uint32_t* words
         words[i] = (uint32_t)v;
     }
     return true;
-#else
-    if (__atomic_load_n(&host[3], __ATOMIC_ACQUIRE) != seq) return false;
-    for (int i = 0; i < 3; i++) words[i] = host[i];
-    return true;
-#endif
 }
 static int wait_plan_words(const uint32_t* host, uint32_t seq, hipStream_t s, uint32_t* words)
 {
@@ -436,7 +451,12 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     uint32_t misc[3];
     HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipStreamSynchronize(s));
-    if (misc[0] == ~0u) return fail(HLGS_ERR_DEVICE, "the binning plan's look-back timed out");
+    if (misc[0] == ~0u) {  // the fused plan's look-back timed out: plan again without inter-block waits
+        if ((rc = replan_launch(a, geom, img, radii, nullptr, 0u, s))) return rc;
+        HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
+        HLGS_TRY_HIP(hipStreamSynchronize(s));
+        if (misc[0] == ~0u) return fail(HLGS_ERR_DEVICE, "the binning plan failed twice");
+    }
     info->num_binned = (int)misc[0];
     info->max_tile_count = (int)misc[1];
     info->num_rendered = (int)misc[2];
@@ -490,11 +510,8 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     // block sorts handle; the kernels exit at once if the frame exceeds either (Guard).
     const int capR = binning ? binning_capacity(binning_bytes) : 0;
     const bool spec = capR > 0;
-    // the two-level binning sorts lists of any length on the device (k_supertile_sort, k_big_tile_sort); otherwise the
-    // queued sorts are the ones the previous frame's longest list needed
-    const bool any_len = two_level(im, a->P, (a->W + 15) / 16, (a->H + 15) / 16);
-    const uint32_t cap_n = any_len ? ~0u
-                           : rb->last_maxc <= (uint32_t)kWaveSortCap ? (uint32_t)kWaveSortCap : (uint32_t)kSortCap;
+    // the queued sorts are the ones the previous frame's longest list needed
+    const uint32_t cap_n = rb->last_maxc <= (uint32_t)kWaveSortCap ? (uint32_t)kWaveSortCap : (uint32_t)kSortCap;
     if (spec && (rc = render_launch(a, radii, geom, img, binning, capR, cap_n, out_color, out_invdepth, seen, s,
                                     Guard{im.misc, (uint32_t)capR, cap_n})))
         return rc;
@@ -505,8 +522,17 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
         HLGS_TRY_HIP(hipEventSynchronize(rb->ev));
         for (int i = 0; i < 3; i++) words[i] = rb->host[i];
     }
+    bool replanned = false;
+    if (words[0] == ~0u) {
+        // The fused plan's look-back timed out (k_tile_offsets_plan): the speculative render exited at once (R exceeds
+        // every capacity); plan again with the two launches that need no inter-block wait, then render.
+        if (++rb->seq == 0u) rb->seq = 1u;
+        if ((rc = replan_launch(a, geom, img, radii, rb->host, rb->seq, s))) return rc;
+        if ((rc = wait_plan_words(rb->host, rb->seq, s, words))) return rc;
+        if (words[0] == ~0u) return fail(HLGS_ERR_DEVICE, "the binning plan failed twice");
+        replanned = true;
+    }
     const uint32_t R = words[0], maxc = words[1];
-    if (R == ~0u) return fail(HLGS_ERR_DEVICE, "the binning plan's look-back timed out");
     rb->last_maxc = maxc;
     info->num_binned = (int)R;
     info->num_rendered = (int)words[2];
@@ -518,7 +544,7 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
         return HLGS_OK;
     }
     if (R > (uint32_t)capR) return HLGS_OK;  // caller allocates hlgs_binning_buffer_size(R), calls _render
-    if (!spec || maxc > cap_n) {
+    if (!spec || maxc > cap_n || replanned) {
         if ((rc = render_launch(a, radii, geom, img, binning, capR, maxc, out_color, out_invdepth, seen, s,
                                 Guard{nullptr, 0u, 0u})))
             return rc;

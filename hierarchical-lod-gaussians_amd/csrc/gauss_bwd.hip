@@ -48,27 +48,16 @@ __device__ __forceinline__ void cov3d_exact(f3 scale, float mod, float4 q, float
     out[3] = Sig.m[1][1]; out[4] = Sig.m[1][2]; out[5] = Sig.m[2][2];
 }
 
-#ifndef HLGS_GAUSS_SKIP
-#define HLGS_GAUSS_SKIP 1  // skip zero-mask record slots also when they were written (always with HLGS_DROP_EMPTY)
-#endif
 // One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
 // backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
-#ifndef HLGS_GBWD_WAVES
-#define HLGS_GBWD_WAVES 0  // > 0: ask for that many waves per SIMD (a VGPR cap; 120 VGPRs give 4)
-#endif
-#if HLGS_GBWD_WAVES > 0
-#define HLGS_GBWD_BOUNDS __launch_bounds__(256, HLGS_GBWD_WAVES)
-#else
-#define HLGS_GBWD_BOUNDS __launch_bounds__(256)
-#endif
 template <bool HIER, bool ALT>
-__global__ void HLGS_GBWD_BOUNDS k_gauss_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
+__global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
                                                    BwdScratch rec, hlgs_grads o, float fx, float fy, int has_depth,
                                                    const uint32_t* __restrict__ misc)
 {
     // the forward packed its entries (misc[kMiscPack]), so Geom::qmask holds this frame's quadrant masks: a slot whose
-    // mask is 0 holds no record (HLGS_DROP_EMPTY: never binned) or a zero one, and is skipped (rect_tile_mask)
-    const bool masked = (HLGS_GAUSS_SKIP || HLGS_DROP_EMPTY) && misc && misc[kMiscPack];
+    // mask is 0 holds no record (drop_empty: never binned) or a zero one, and is skipped (rect_tile_mask)
+    const bool masked = misc && misc[kMiscPack];
     const int t_idx = blockIdx.x * 256 + threadIdx.x;
     // the slot range and the masks are loaded with the radius, not behind it (an invisible Gaussian's tiles_touched
     // is 0, so its range is empty; its qmask word is stale and never used)
@@ -391,14 +380,12 @@ __device__ __forceinline__ float sh_basis(int c, float x, float y, float z, floa
 // parent-deferred share (backward.cu:458-494).
 // ALT (alt-rasterizer backward.cu:23-146): coefficient 0 is the separate dc row (gradient to ddc), and the
 // staged rows hold the M higher-order coefficients 1..M.
-// JAC: the forward left d colour / d view direction in Geom::sh_jac (sh_jac_written), so no SH row is read: the view
-// direction term is dot(dRGBd{x,y,z}, dL/dRGB) in the reference's order (backward.cu:139-141) and the dsh rows are
-// basis x dL/dRGB, built in LDS and stored as contiguous float4 runs.
-template <bool HIER, int MT, bool ALT, bool JAC>  // MT = 0: staged row count a.M known only at run time (up to 16)
+// When the forward left d colour / d view direction in Geom::sh_jac (sh_jac_written), k_sh_bwd_jac2 below runs instead
+// and reads no SH row.
+template <bool HIER, int MT, bool ALT>  // MT = 0: staged row count a.M known only at run time (up to 16)
 __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
                                                BwdScratch rec, hlgs_grads o)
 {
-    static_assert(!(JAC && HIER), "the hierarchy-mode preprocess leaves no Jacobian");
     constexpr int OFF = ALT ? 1 : 0;  // full coefficient index of staged row 0
     constexpr int MC = MT ? MT : (16 - OFF);
     const int M = MT ? MT : a.M;
@@ -416,27 +403,16 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
     s_idx[lane] = idx;
     s_vis[lane] = vis;
     // the visible Gaussian's own inputs, issued before the row copy so both latencies overlap
-    f3 m = mk(0.f, 0.f, 0.f), dcol = mk(0.f, 0.f, 0.f), jx = m, jy = m, jz = m;
+    f3 m = mk(0.f, 0.f, 0.f), dcol = mk(0.f, 0.f, 0.f);
     uint32_t cl = 0;
     if (vis) {
         m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
         dcol = mk(o.dcolor[3 * idx], o.dcolor[3 * idx + 1], o.dcolor[3 * idx + 2]);
         cl = g.clamped[t_idx];
-        if (JAC) {
-            const float* J = g.sh_jac + 9 * (size_t)t_idx;
-            jx = mk(J[0], J[1], J[2]);
-            jy = mk(J[3], J[4], J[5]);
-            jz = mk(J[6], J[7], J[8]);
-        }
     }
-    if (JAC) {  // invisible rows are zero
-        if (!vis)
-            for (int c = 0; c < M3; c++) s_rows[lane * kShStride + c] = 0.f;
-    } else {
-        __syncthreads();
-        // rows of invisible Gaussians are not read: they arrive as zeros, which is their dsh row
-        sh_rows_load<3 * MT>(a.shs, s_rows, s_idx, n, lane, M3, s_vis);
-    }
+    __syncthreads();
+    // rows of invisible Gaussians are not read: they arrive as zeros, which is their dsh row
+    sh_rows_load<3 * MT>(a.shs, s_rows, s_idx, n, lane, M3, s_vis);
     // colour-factored mode (o.drgb, view-data-parallel exchange): the masked dL/dRGB row replaces dsh / ddc
     const bool factored = o.drgb != nullptr;  // uniform
     __syncthreads();
@@ -464,19 +440,13 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
             for (int c = 0; c < MC + OFF; c++) {
                 float gx, gy, gz;
                 basis[c] = c < ncoef ? sh_basis(c, x, y, z, gx, gy, gz) : 0.f;
-                if (!JAC && c > 0 && c < ncoef) {
+                if (c > 0 && c < ncoef) {
                     const float* sc = row + 3 * (c - OFF);
                     const float proj = sc[0] * dR + sc[1] * dG + sc[2] * dB;
                     vx += proj * gx;
                     vy += proj * gy;
                     vz += proj * gz;
                 }
-            }
-            if (JAC) {
-                const f3 d = mk(dR, dG, dB);
-                vx = dot(jx, d);
-                vy = dot(jy, d);
-                vz = dot(jz, d);
             }
             if (factored) {
                 o.drgb[3 * idx] = dropped ? 0.f : dR;
@@ -514,12 +484,11 @@ __global__ void __launch_bounds__(64) k_sh_bwd(hlgs_raster_args a, const int* __
     sh_rows_copy<3 * MT, false>(o.dsh, s_rows, s_idx, n, lane, M3);
 }
 
-// The Jacobian SH backward (JAC) with two waves per 64 Gaussians (HLGS_SH_BWD_SPLIT): wave 0 does k_sh_bwd's per-Gaussian
-// work and builds the dsh rows in LDS, then both waves store the block's rows.  The 12.5 KB row stage then keeps two
+// The Jacobian SH backward: the forward left d colour / d view direction in Geom::sh_jac (sh_jac_written), so no SH row
+// is read: the view direction term is dot(dRGBd{x,y,z}, dL/dRGB) in the reference's order (backward.cu:139-141) and the
+// dsh rows are basis x dL/dRGB, built in LDS and stored as contiguous float4 runs.  Two waves per 64 Gaussians: wave 0
+// does the per-Gaussian work and builds the dsh rows in LDS, then both waves store the block's rows.  The 12.5 KB row stage then keeps two
 // waves per block instead of one (the stores, 192 B per Gaussian, are most of the kernel's traffic).  Same arithmetic.
-#ifndef HLGS_SH_BWD_SPLIT
-#define HLGS_SH_BWD_SPLIT 1
-#endif
 template <int MT, bool ALT>
 __global__ void __launch_bounds__(128) k_sh_bwd_jac2(hlgs_raster_args a, const int* __restrict__ radii, Geom g,
                                                     BwdScratch rec, hlgs_grads o)
@@ -722,9 +691,8 @@ void launch_gauss_bwd(const hlgs_raster_args& a, const int* radii, const Geom& g
     const bool jac = sh_jac_written(a);  // the forward's preprocess left d colour / d direction (no SH row reads)
 #define HLGS_SHK(H, MT, AL)                                                                                \
     do {                                                                                                   \
-        if (!(H) && jac && HLGS_SH_BWD_SPLIT) hipLaunchKernelGGL((k_sh_bwd_jac2<MT, AL>), grid_sh, dim3(128), 0, sl, a, radii, g, rs, o); \
-        else if (!(H) && jac) hipLaunchKernelGGL((k_sh_bwd<false, MT, AL, true>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o); \
-        else hipLaunchKernelGGL((k_sh_bwd<H, MT, AL, false>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o); \
+        if (!(H) && jac) hipLaunchKernelGGL((k_sh_bwd_jac2<MT, AL>), grid_sh, dim3(128), 0, sl, a, radii, g, rs, o); \
+        else hipLaunchKernelGGL((k_sh_bwd<H, MT, AL>), grid_sh, dim3(64), 0, sl, a, radii, g, rs, o); \
     } while (0)
 #define HLGS_SHB(H)                                                                                        \
     switch (a.M) {                                                                                         \

@@ -97,11 +97,18 @@ int hlgs_hier_info_read(const char* path, int dynamic, hlgs_hier_info* info)
     File F;
     F.f = fopen(path, "rb");
     if (!F.f) return fail_msg(HLGS_ERR_ARG, "File not found!");
+    // The header counts are checked against the file's size before anything is sized by them: the reference's loader
+    // trusts them (hierarchy_loader.cpp:39-65, 129-189), which lets a malformed file drive huge or negative sizes.
+    if (fseek(F.f, 0, SEEK_END) != 0) return fail_msg(HLGS_ERR_ARG, "unreadable hierarchy file");
+    const long long fsize = (long long)ftell(F.f);
+    if (fsize < 0 || fseek(F.f, 0, SEEK_SET) != 0) return fail_msg(HLGS_ERR_ARG, "unreadable hierarchy file");
     int32_t a = 0, b = 0;
     if (!rd(F.f, &a, 4)) return fail_msg(HLGS_ERR_ARG, "truncated hierarchy file");
     if (dynamic) {
         if (!rd(F.f, &b, 4)) return fail_msg(HLGS_ERR_ARG, "truncated hierarchy file");
         if (a < 0 || b < 0 || b > 3) return fail_msg(HLGS_ERR_ARG, "not a dynamic hierarchy (.dhier) file");
+        const long long need = 8 + (long long)a * (12 + 16 + 12 + 4 + 12LL * kShSize[b]) + 4 + (long long)a * 24;
+        if (need > fsize) return fail_msg(HLGS_ERR_ARG, "truncated hierarchy file");
         info->format = HLGS_HIER_DYNAMIC;
         info->G = a;
         info->sh_degree = b;
@@ -111,8 +118,11 @@ int hlgs_hier_info_read(const char* path, int dynamic, hlgs_hier_info* info)
     const bool half = a < 0;
     const long long P = half ? -(long long)a : a;
     const long long per = half ? 12 + 2 * (4 + 3 + 1 + 48) : 12 + 16 + 12 + 4 + 4 * 48;
-    if (fseek(F.f, (long)(4 + P * per), SEEK_SET) != 0 || !rd(F.f, &b, 4))
+    if (4 + P * per + 4 > fsize || fseek(F.f, (long)(4 + P * per), SEEK_SET) != 0 || !rd(F.f, &b, 4))
         return fail_msg(HLGS_ERR_ARG, "truncated hierarchy file");
+    if (b < 0) return fail_msg(HLGS_ERR_ARG, "negative node count in hierarchy file");
+    const long long node_bytes = half ? 12 + 8 + 16 : 28 + 32;  // (Half)Node + (Half)Box
+    if (4 + P * per + 4 + (long long)b * node_bytes > fsize) return fail_msg(HLGS_ERR_ARG, "truncated hierarchy file");
     info->format = half ? HLGS_HIER_HALF : HLGS_HIER_FULL;
     info->G = (int)P;
     info->N = b;

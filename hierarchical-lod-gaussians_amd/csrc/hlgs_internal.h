@@ -24,14 +24,8 @@ constexpr int kBinMaxTiles = 16384; // tile grids up to this use LDS histograms 
 // Chunks of at least 192 entries (round 3; 128 before): a configs[1] tile (~300 entries) then has one boundary instead
 // of two, which halves the split state the forward writes (its write traffic was 137 MB per view, 83 MB of it split
 // state) at no measured cost (blend pair 538.6-538.9 against 535.2-536.7 us).
-#ifndef HLGS_BWD_CHUNK
-#define HLGS_BWD_CHUNK 192
-#endif
-#ifndef HLGS_BWD_SPLITS
-#define HLGS_BWD_SPLITS 2
-#endif
-constexpr int kBwdChunk = HLGS_BWD_CHUNK;
-constexpr int kBwdSplits = HLGS_BWD_SPLITS;
+constexpr int kBwdChunk = 192;
+constexpr int kBwdSplits = 2;
 constexpr int kSplitFloats = 4 * 5 * 64;  // per (tile, split): [quadrant][T, dC r, g, b, dD][lane]
 __host__ __device__ inline uint32_t bwd_chunk_len(uint32_t cnt)
 {
@@ -56,6 +50,7 @@ struct Geom {
     uint32_t* qmask;          // P: footprint quadrant masks of the first rect tiles (rect_quad_masks), written by the
                               // preprocess for the visible Gaussians when pack_entries; read by the key scatter
     int pack;                 // pack_entries(P) of the frame this buffer is carved for
+    int drop;                 // drop_empty(P): instances whose quadrant mask is 0 are not binned
     float* sh_jac;            // P x 9: d colour / d view direction (dRGBdx, dRGBdy, dRGBdz), written by k_preprocess_sh
                               // for the visible Gaussians when sh_jac_written(); the SH backward then reads no SH rows
     uint32_t* scan_tmp;
@@ -79,42 +74,23 @@ bool lds_binning(int P, int gx, int gy);
 // The low bits do not change the sort order: within a tile the (depth, idx) pairs are already distinct.
 // pack_entries(P) is decided on the host (capi.hip; hlgs_set_entry_packing turns it off for tests) and reaches the
 // kernels as Geom::pack / their pack argument.
-#ifndef HLGS_PACK_ENTRIES
-#define HLGS_PACK_ENTRIES 1
-#endif
 constexpr int kEntryShift = 4;
 constexpr int kMiscPack = 3;  // Img::misc word holding the frame's pack_entries(P)
-constexpr int kMiscBig = 4;   // Img::misc word: tiles k_supertile_sort left to k_big_tile_sort (two-level binning)
-// Two-level binning (HLGS_TWO_LEVEL): the key scatter bins instances into super-tiles of kSuperTiles consecutive tiles
-// (tile-major order, so a super-tile's segment is its tiles' lists back to back), with runs long enough to be written
-// as whole sectors; k_supertile_sort then splits each segment into its tiles in LDS and sorts them.
-#ifndef HLGS_TWO_LEVEL
-#define HLGS_TWO_LEVEL 0  // measured slower: an option
-#endif
-constexpr int kSuperTiles = 16;
-__host__ __device__ inline int super_tiles(int T) { return (T + kSuperTiles - 1) / kSuperTiles; }
-// k_plan's words for the host (R, longest list, record slots) in the pinned read-back slot.  HLGS_PLAN_TAGGED: three
-// 64-bit words, each carrying the frame's sequence number in its high half, written by single-copy-atomic 64-bit stores,
-// so the host waits until all three carry it and the kernel needs no system-scope release (buffer_wbl2: a write-back
-// of the whole L2) to order them.  0: three words, then the sequence number after a system fence.
-// HLGS_DROP_EMPTY: with packed entries, an instance whose quadrant mask is 0 (its footprint reaches none of the tile's
+constexpr int kMiscFail = 5;  // Img::misc word: a block of the fused plan timed out in its look-back (k_tile_offsets_plan)
+constexpr int kMiscDone = 6;  // Img::misc word: blocks of the fused plan done with their ranges
+// drop_empty(P): with packed entries, an instance whose quadrant mask is 0 (its footprint reaches none of the tile's
 // four 8x8 quadrants, so no pixel of the tile blends it) is not binned: the tile lists, the sort and the blends' staging
 // skip it.  Its record slot stays (point_offsets and num_rendered are unchanged) and is never written; k_gauss_bwd
-// skips the slots whose mask is 0 (their records would be zero).
-#ifndef HLGS_DROP_EMPTY
-#define HLGS_DROP_EMPTY 1
-#endif
-#ifndef HLGS_PLAN_TAGGED
-#define HLGS_PLAN_TAGGED 1
-#endif
+// skips the slots whose mask is 0 (their records would be zero).  On by default; hlgs_set_drop_empty(0) bins every
+// instance, so point_list and n_contrib are laid out exactly as the reference's binning lays them out.
+// k_plan's words for the host (R, longest list, record slots) in the pinned read-back slot: three 64-bit words, each
+// carrying the frame's sequence number in its high half, written by single-copy-atomic 64-bit stores, so the host
+// waits until all three carry it and the kernel needs no system-scope release (a write-back of the whole L2).
 bool pack_entries(int P);
-// Does the forward's preprocess (k_preprocess_sh) leave Geom::sh_jac for the SH backward?  Same condition as its launch.
-#ifndef HLGS_SH_JAC
-#define HLGS_SH_JAC 1  // 0: no Jacobian; the SH backward reads the SH rows again (A/B)
-#endif
+bool drop_empty(int P);
+// Does the forward's preprocess (k_preprocess_sh2) leave Geom::sh_jac for the SH backward?  Same condition as its launch.
 inline bool sh_jac_written(const hlgs_raster_args& a)
 {
-    if (!HLGS_SH_JAC) return false;
     const int gx = (a.W + 15) / 16, gy = (a.H + 15) / 16;
     return !a.indices && !a.colors_precomp && a.shs && a.M > 0 && a.M <= 16 && lds_binning(a.P, gx, gy);
 }
@@ -128,7 +104,8 @@ struct Img {
     uint32_t* tile_count;  // T
     uint32_t* tile_cursor; // T
     uint32_t* misc;        // 16: [0] = binned instances, [1] = longest per-tile list, [2] = record slots (point_offsets[P-1]),
-                           // [kMiscPack] = the frame's pack_entries(P), read by the backward (not the process-wide switch)
+                           // [kMiscPack] = the frame's pack_entries(P), read by the backward (not the process-wide switch),
+                           // [kMiscFail], [kMiscDone]: the fused plan's failure and completion words
     uint32_t* scan_tmp;
     float* split_state;    // T x kBwdSplits x kSplitFloats (see bwd_chunk_len)
 };
@@ -139,7 +116,6 @@ struct Bin {
     uint64_t* keys;
     uint64_t* keys2;
     uint32_t* point_list;  // R, tile-major then front-to-back
-    uint8_t* tile_local;   // R: the two-level binning's tile index inside the super-tile of keys2[i]
 };
 Bin carve_bin(void* base, int R, size_t* total);
 

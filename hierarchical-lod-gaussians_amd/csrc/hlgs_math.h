@@ -315,11 +315,12 @@ __device__ __forceinline__ SplatBands splat_bands(float x, float y, float4 co, f
     s.tol = 2e-3f * (sqrtf(s.at) + fabsf(b) * vmax) * s.ia + 2e-3f;
     return s;
 }
-// The footprint's x-extent [umin, umax] (offsets from the centre) inside the band v in [v0, v0 + 7]; empty: +-3e38.
-__device__ __forceinline__ void band_extent(const SplatBands& s, float v0, float& umin, float& umax)
+// The footprint's x-extent [umin, umax] (offsets from the centre) inside the band v in [v0, v0 + h] (h = 7: an 8-row
+// band); empty: +-3e38.
+__device__ __forceinline__ void band_extent(const SplatBands& s, float v0, float& umin, float& umax, float h = 7.f)
 {
 #pragma clang fp contract(off)
-    const float lo = fmaxf(v0, -s.vmax), hi = fminf(v0 + 7.f, s.vmax);
+    const float lo = fmaxf(v0, -s.vmax), hi = fminf(v0 + h, s.vmax);
     if (!(lo <= hi)) { umin = 3e38f; umax = -3e38f; return; }  // empty: overlaps no column
     const float vR = __builtin_amdgcn_fmed3f(s.vr, lo, hi), vL = __builtin_amdgcn_fmed3f(-s.vr, lo, hi);
     umax = fmaf(s.nb, vR, sqrtf(fmaxf(fmaf(-s.det * vR, vR, s.at), 0.f))) * s.ia + s.tol;
@@ -370,6 +371,36 @@ __device__ __forceinline__ uint32_t rect_quad_masks(float x, float y, float4 co,
     }
     return m;
 }
+// The blend backward's 4x4 sub-block masks of one tile (origin tx0, ty0 in pixels): bit 4 k + g is set iff the footprint
+// reaches sub-block g (x half g & 1, y half g >> 1) of 8x8 quadrant k -- per 4-row band the footprint's x-extent (the
+// band form above with 4-row bands: the same tolerances, so just as conservative; tools/cull_check.py checks both
+// block sizes against brute force), tested against the band's four 4-column blocks.  Only a culling superset: the
+// backward decides every pair with the exact e2 >= thr test.
+__device__ __forceinline__ uint32_t sub_block_mask(const SplatBands& s, int tx0, int ty0)
+{
+#pragma clang fp contract(off)
+    if (s.mode) return s.mode == 1 ? 0xFFFFu : 0u;
+    const float u0 = (float)tx0 - s.x;
+    uint32_t m = 0;
+#pragma unroll
+    for (int band = 0; band < 4; band++) {
+        float lo, hi;
+        band_extent(s, (float)(ty0 + 4 * band) - s.y, lo, hi, 3.f);
+#pragma unroll
+        for (int col = 0; col < 4; col++) {
+            const float c0 = u0 + (float)(4 * col);
+            const int k = (col >> 1) + 2 * (band >> 1), g = (col & 1) + 2 * (band & 1);
+            if (hi >= c0 && lo <= c0 + 3.f) m |= 1u << (4 * k + g);
+        }
+    }
+    return m;
+}
+// The quadrant bits of a 4-bit mask spread over their four sub-block bits (bit k -> bits 4 k .. 4 k + 3).
+__device__ __forceinline__ uint32_t quad_to_sub(uint32_t qm)
+{
+    return ((qm & 1u) ? 0xFu : 0u) | ((qm & 2u) ? 0xF0u : 0u) | ((qm & 4u) ? 0xF00u : 0u) | ((qm & 8u) ? 0xF000u : 0u);
+}
+
 // The quadrant mask of rect tile r from the record's masks; tiles past kRectMasks take every quadrant (conservative).
 __device__ __forceinline__ uint32_t rect_tile_mask(uint32_t masks, uint32_t r)
 {
@@ -563,6 +594,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg)
 __device__ __forceinline__ int xcd_unmap(int i, int nwg)
 {
     const int q = nwg / 8, r = nwg % 8;
+    if (q == 0) return i;  // fewer than 8 workgroups: the identity (and no division by q for positions past nwg)
     int x, k;
     if (i < r * (q + 1)) {
         x = i / (q + 1);
@@ -582,109 +614,43 @@ __device__ __forceinline__ float dpp(float v)
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW, 0xF, BC));
 }
 
-// Reduce-scatter of ten per-lane values over the wave, cheapest stages first (issue costs measured by
-// tools/issue_probe.hip: a DPP add 4.2 cycles per wave instruction, a permlane swap 8.3).  Each fold halves the number
-// of registers: within each 16-lane row, bank-masked DPP adds fold lanes l and l^8 (values 2i into lanes 0-7, 2i+1 into
-// lanes 8-15), then l and l^4 (per 4-lane bank); permlane32 / permlane16 swaps fold the halves and the row pairs; a
-// quad_perm full reduction finishes each bank.  18 DPP + 3 permlane swaps, where ten full-wave reductions take
-// 12 DPP + 8 permlane swaps.  (row_ror:n: lane l reads lane l - n of its row.)  The result w holds, in every lane of
-// row rho and bank beta (lane = 16 rho + 4 beta + i), the total of value reduce10_index(rho, beta), or nothing for
-// rho = 3.
-__device__ __forceinline__ int reduce10_index(int rho, int beta)
+// Ten per-lane values summed over each 16-lane row of the wave (rows independently: in the blend backward each row is one
+// 4x4 sub-block working on its own splat).  Bank-masked DPP adds fold lanes l and l^8 (values 2i into banks 0-1, 2i+1
+// into banks 2-3), then l and l^4 (FOLD4: five values into three), and two quad_perm adds finish each bank: 22 DPP
+// adds.  Every lane of bank beta then holds t0 = the row total of value {0, 2, 1, 3}[beta], t1 = of {4, 6, 5, 7}[beta]
+// and t2 = of {8, 8, 9, 9}[beta] (tools/diag/reduce_layout.py simulates the lane operations).  A row whose lanes are
+// inactive (exec) is left alone: DPP row operations read within the row only.
+__device__ __forceinline__ void row_reduce10(const float (&v)[10], float& t0, float& t1, float& t2)
 {
-    const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
-    return rho == 0 ? cb : rho == 2 ? 4 + cb : rho == 1 ? ((beta & 1) ? -1 : 8 + (beta >> 1)) : -1;
-}
-// One instruction stream, ordered so that every DPP / permlane-swap source was written at least two instructions
-// earlier where the sequence allows it (the gfx950 VALU-write -> DPP-read and -> permlane-swap-read hazards need two
-// wait states): 4 s_nop where the builtin-and-asm version took 7.
-__device__ __forceinline__ float wave_reduce10_rs(const float (&v)[10])
-{
-    float s0, s1, s2, s3, s4, t0, t1, t2, z, w;
+    float s0, s1, s2, s3, s4;
 #define HLGS_FOLD8(d, a, b)                                                                                        \
     "v_add_f32_dpp " d ", " a ", " a " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
     "v_add_f32_dpp " d ", " b ", " b " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
 #define HLGS_FOLD4(d, a, b)                                                                                        \
     "v_add_f32_dpp " d ", " a ", " a " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
     "v_add_f32_dpp " d ", " b ", " b " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
-    asm volatile("s_nop 0\n\t"
-                 "v_mov_b32 %8, 0\n\t"
-                 HLGS_FOLD8("%0", "%10", "%11") HLGS_FOLD8("%1", "%12", "%13") HLGS_FOLD8("%2", "%14", "%15")
-                 HLGS_FOLD8("%3", "%16", "%17") HLGS_FOLD8("%4", "%18", "%19")
-                 HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%7", "%4", "%4")
-                 "v_permlane32_swap_b32 %5, %6\n\t"   // t0 (written two instructions back), t1
-                 "v_add_f32 %5, %5, %6\n\t"           // rows 0-1: t0, rows 2-3: t1
-                 "v_permlane32_swap_b32 %7, %8\n\t"   // t2 (two back), 0
-                 "v_add_f32 %7, %7, %8\n\t"           // rows 0-1: t2, rows 2-3: 0
-                 "s_nop 1\n\t"
-                 "v_permlane16_swap_b32 %5, %7\n\t"
-                 "v_add_f32 %9, %5, %7\n\t"           // row 0: t0, row 1: t2, row 2: t1, row 3: 0
-                 "s_nop 1\n\t"
-                 "v_add_f32_dpp %9, %9, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 1\n\t"
-                 "v_add_f32_dpp %9, %9, %9 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
-                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(z),
-                   "=&v"(w)
+#define HLGS_QUAD(d, p) "v_add_f32_dpp " d ", " d ", " d " quad_perm:" p " row_mask:0xf bank_mask:0xf\n\t"
+    // every DPP source was written at least two instructions earlier (the VALU-write -> DPP-read hazard), except the
+    // inputs, hence the leading s_nop
+    asm volatile("s_nop 1\n\t"
+                 HLGS_FOLD8("%0", "%8", "%9") HLGS_FOLD8("%1", "%10", "%11") HLGS_FOLD8("%2", "%12", "%13")
+                 HLGS_FOLD8("%3", "%14", "%15") HLGS_FOLD8("%4", "%16", "%17")
+                 HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%7", "%4", "%4")
+                 HLGS_QUAD("%5", "[1,0,3,2]") HLGS_QUAD("%6", "[1,0,3,2]") HLGS_QUAD("%7", "[1,0,3,2]")
+                 HLGS_QUAD("%5", "[2,3,0,1]") HLGS_QUAD("%6", "[2,3,0,1]") HLGS_QUAD("%7", "[2,3,0,1]")
+                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2)
                  : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]),
                    "v"(v[9]));
 #undef HLGS_FOLD8
 #undef HLGS_FOLD4
-    return w;
+#undef HLGS_QUAD
 }
-
-// Reduce-scatter of two splats' ten moments each (a = values 0-9, b = values 10-19) in one pass: FOLD8 of the ten
-// pairs, FOLD4 of five, permlane32 swaps fold 5 -> 3, permlane16 swaps 3 -> 2, quad_perm adds finish both.  34 DPP adds,
-// 5 permlane swaps and 5 adds, where two wave_reduce10_rs take 36, 6 and 6 (and 8 s_nop).  Every lane of row rho, bank
-// beta ends with the total of value reduce20_index(rho, beta, 0) in w0 and of reduce20_index(rho, beta, 1) in w1
-// (-1: none); the mapping was derived by simulating the lane operations (tools/diag/reduce_layout.py).
-__device__ __forceinline__ int reduce20_index(int rho, int beta, int reg)
+// The moment whose row total lane position (bank beta = (l >> 2) & 3, p = l & 3) stores after row_reduce10: p = 0 -> t0,
+// p = 1 -> t1, p = 2 -> t2 in banks 0 and 2; -1: none.
+__host__ __device__ inline int row_reduce10_index(int beta, int p)
 {
     const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
-    if (reg == 1) return rho == 0 ? 16 + cb : -1;
-    return rho == 0 ? cb : rho == 1 ? 8 + cb : rho == 2 ? 4 + cb : 12 + cb;
-}
-__device__ __forceinline__ void wave_reduce20_rs(const float (&a)[10], const float (&b)[10], float& w0, float& w1)
-{
-    float s[10], t[5], z, z2;
-#define HLGS_FOLD8(d, x, y)                                                                                        \
-    "v_add_f32_dpp " d ", " x ", " x " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
-    "v_add_f32_dpp " d ", " y ", " y " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
-#define HLGS_FOLD4(d, x, y)                                                                                        \
-    "v_add_f32_dpp " d ", " x ", " x " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
-    "v_add_f32_dpp " d ", " y ", " y " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
-    asm volatile("s_nop 1\n\t"
-                 HLGS_FOLD8("%0", "%19", "%20") HLGS_FOLD8("%1", "%21", "%22") HLGS_FOLD8("%2", "%23", "%24")
-                 HLGS_FOLD8("%3", "%25", "%26") HLGS_FOLD8("%4", "%27", "%28") HLGS_FOLD8("%5", "%29", "%30")
-                 HLGS_FOLD8("%6", "%31", "%32") HLGS_FOLD8("%7", "%33", "%34") HLGS_FOLD8("%8", "%35", "%36")
-                 HLGS_FOLD8("%9", "%37", "%38")
-                 "v_mov_b32 %15, 0\n\t"
-                 "v_mov_b32 %16, 0\n\t"
-                 HLGS_FOLD4("%10", "%0", "%1") HLGS_FOLD4("%11", "%2", "%3") HLGS_FOLD4("%12", "%4", "%5")
-                 HLGS_FOLD4("%13", "%6", "%7") HLGS_FOLD4("%14", "%8", "%9")
-                 "v_permlane32_swap_b32 %10, %11\n\t"  // t1 written six instructions back
-                 "v_add_f32 %10, %10, %11\n\t"         // rows 0-1: t0, rows 2-3: t1
-                 "v_permlane32_swap_b32 %12, %13\n\t"
-                 "v_add_f32 %12, %12, %13\n\t"         // rows 0-1: t2, rows 2-3: t3
-                 "v_permlane32_swap_b32 %14, %15\n\t"
-                 "v_add_f32 %14, %14, %15\n\t"         // rows 0-1: t4, rows 2-3: 0
-                 "v_permlane16_swap_b32 %10, %12\n\t"  // t2 written two instructions back
-                 "v_add_f32 %17, %10, %12\n\t"         // rows: t0, t2, t1, t3
-                 "v_permlane16_swap_b32 %14, %16\n\t"
-                 "v_add_f32 %18, %14, %16\n\t"         // row 0: t4
-                 "v_add_f32_dpp %17, %17, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 0\n\t"
-                 "v_add_f32_dpp %18, %18, %18 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                 "v_add_f32_dpp %17, %17, %17 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 0\n\t"
-                 "v_add_f32_dpp %18, %18, %18 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
-                 : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5]), "=&v"(s[6]),
-                   "=&v"(s[7]), "=&v"(s[8]), "=&v"(s[9]), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]),
-                   "=&v"(t[4]), "=&v"(z), "=&v"(z2), "=&v"(w0), "=&v"(w1)
-                 : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
-                   "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]),
-                   "v"(b[8]), "v"(b[9]));
-#undef HLGS_FOLD8
-#undef HLGS_FOLD4
+    return p == 0 ? cb : p == 1 ? 4 + cb : (p == 2 && !(beta & 1)) ? 8 + (beta >> 1) : -1;
 }
 
 }  // namespace hlgs

@@ -4,24 +4,18 @@
 //   k_blend_bwd  <- renderCUDA<3> backward      backward.cu:498-721
 //
 // The reference issues one global float atomic per (pixel, Gaussian, gradient component)
-// (backward.cu:669-718).  Here each wave owns one tile: every lane folds its four pixels, a
-// permlane/DPP reduce-scatter folds the 64 lanes, and the per-(tile, Gaussian) partial is stored once -- with
-// a plain store -- into a Gaussian-major record slot (the Gaussian's point_offsets range, indexed by
-// the tile's position inside its rect).  k_gauss_bwd then sums each Gaussian's contiguous records
-// in a fixed order, so the backward has no float atomics and is bitwise reproducible.
+// (backward.cu:669-718).  Here each wave owns one tile (one chunk of its list): every 16-lane row folds its pixels'
+// moments with DPP adds, the rows' totals meet in LDS, and the per-(tile, Gaussian) partial is stored once -- with a
+// plain store -- into a Gaussian-major record slot (the Gaussian's point_offsets range, indexed by the tile's position
+// inside its rect).  k_gauss_bwd then sums each Gaussian's contiguous records in a fixed order, so the backward has
+// no global float atomics and is bitwise reproducible.
+//
+// The measured variants of rounds 1-4 (wave-wide quadrant passes, two splats per reduction, opacity-uniform clamp
+// branches, packed moments, Newton reciprocals, tile-major chunk order, non-temporal loads and stores, and the
+// traffic-attribution builds) are kept outside the product source as tools/variants/raster_bwd_r04.hip, built for A/B
+// by tools/build_variant.py; DESIGN.md section 5 records each result.
 #include "hlgs_internal.h"
 #include "hlgs_math.h"
-
-#ifndef HLGS_BWD_ZERO_LDS
-#define HLGS_BWD_ZERO_LDS 1  // accumulators zeroed by LDS reads, not v_mov_b64 (the VALU pipe is the limit)
-#endif
-#ifndef HLGS_BWD_OPQ
-#define HLGS_BWD_OPQ 0  // 1: the 0.99-clamp factor only for splats whose opacity exceeds 0.99f (a uniform branch per
-                        // pass: 358.8-359.1 against 356.4-356.8 us without it; not kept)
-#endif
-#ifndef HLGS_BWD_PK
-#define HLGS_BWD_PK 0  // packed-FP32 moment updates (v_pk_mul / v_pk_add / v_pk_fma on moment pairs)
-#endif
 
 namespace hlgs {
 
@@ -52,27 +46,6 @@ __device__ __forceinline__ float below_clamp(float test_alpha)
     return __builtin_amdgcn_fmed3f(fmaf(-1099511627776.0f, test_alpha, 1088516587520.0f), 0.f, 1.f);
 }
 
-// 1/(1 - alpha) for alpha in [0, 0.99].  HLGS_BWD_RCP_NR > 0: that many Newton steps from the bit-pattern seed
-// instead of v_rcp_f32 (A/B of the transcendental's issue cost, tools/valu_probe.hip).
-#ifndef HLGS_BWD_HOIST
-#define HLGS_BWD_HOIST 1
-#endif
-#ifndef HLGS_BWD_RCP_NR
-#define HLGS_BWD_RCP_NR 0
-#endif
-__device__ __forceinline__ float rcp_one_minus(float alpha)
-{
-    const float d = 1.f - alpha;
-#if HLGS_BWD_RCP_NR > 0
-    float r = __int_as_float(0x7EF311C3 - __float_as_int(d));
-#pragma unroll
-    for (int i = 0; i < HLGS_BWD_RCP_NR; i++) r = r * fmaf(-d, r, 2.f);
-    return r;
-#else
-    return __builtin_amdgcn_rcpf(d);
-#endif
-}
-
 // One (pixel, splat) step of renderCUDA backward (backward.cu:601-718).  The splat's gradient terms
 // are linear in w = G * dL/dalpha and its moments over the pixels,
 //   dL/dmean2D = -o * (conic * [Sum w dx, Sum w dy]) * (W/2, H/2),
@@ -90,11 +63,8 @@ struct BwdFront {
     uint64_t ok;  // wave mask: alpha >= 1/255 (alpha_e2_threshold)
 };
 
-// clampable: wave-uniform, the splat's opacity exceeds 0.99f.  Otherwise o G <= o <= 0.99f for every kept pair
-// (G = exp2(e2) <= 1 for e2 <= 0), below_clamp is 1, and the two VALU it costs per pass are skipped (HLGS_BWD_OPQ).
 template <bool INTERP, bool ALT>
-__device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& q, float tt, float fr, float thr,
-                                              bool clampable = true)
+__device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& q, float tt, float fr, float thr)
 {
     BwdFront f;
     f.dx = dx;
@@ -102,22 +72,17 @@ __device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& 
     const float e2 = splat_e2(q, dx, dy);  // power * log2(e)
     float G = __builtin_amdgcn_exp2f(e2);
     const float test_alpha = q.w * G;
-#if HLGS_BWD_OPQ
-    // min(0.99f, o G) as one v_min_f32 (fminf across the clamp branch below otherwise gets a canonicalising v_max)
-    asm("v_min_f32 %0, 0x3f7d70a4, %1" : "=v"(f.my_alpha) : "v"(test_alpha));
-#else
     f.my_alpha = fminf(0.99f, test_alpha);
-#endif
     f.alpha = f.my_alpha;
     if (INTERP) f.alpha = tt * f.my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - f.my_alpha, fr));
-    f.r1m = rcp_one_minus(f.alpha);
-    if (!ALT && clampable) {
+    f.r1m = __builtin_amdgcn_rcpf(1.f - f.alpha);
+    if (!ALT) {
         float b = below_clamp(test_alpha);
         asm volatile("" : "+v"(b));  // not speculatable: a scalar branch around two VALU, not a select after them
         G *= b;
     }
     f.G = G;
-    // as wave masks: one v_cmp per test, combined in SALU (the wave is full)
+    // as wave masks: one v_cmp per test, combined in SALU
     f.ok = ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < thr);
     return f;
 }
@@ -139,37 +104,12 @@ __device__ __forceinline__ void bwd_back(PixB& p, uint32_t li, const BwdFront& f
         if (DEPTH) cd += invz * p.dinv;
         const float raw = cd - p.ARD;
         p.ARD = fmaf(alpha, raw, p.ARD);
-#if HLGS_BWD_PK
-        if (!INTERP && DEPTH) {
-            typedef float v2f __attribute__((ext_vector_type(2)));
-            v2f a67 = {acc[6], acc[7]}, a89 = {acc[8], acc[9]};
-            a67 = __builtin_elementwise_fma(v2f{weight, weight}, v2f{p.dr, p.dg}, a67);
-            a89 = __builtin_elementwise_fma(v2f{weight, weight}, v2f{p.db, p.dinv}, a89);
-            acc[6] = a67.x; acc[7] = a67.y; acc[8] = a89.x; acc[9] = a89.y;
-        } else
-#endif
-        {
-            acc[6] = fmaf(weight, p.dr, acc[6]);
-            acc[7] = fmaf(weight, p.dg, acc[7]);
-            acc[8] = fmaf(weight, p.db, acc[8]);
-            if (DEPTH) acc[9] = fmaf(weight, p.dinv, acc[9]);
-        }
+        acc[6] = fmaf(weight, p.dr, acc[6]);
+        acc[7] = fmaf(weight, p.dg, acc[7]);
+        acc[8] = fmaf(weight, p.db, acc[8]);
+        if (DEPTH) acc[9] = fmaf(weight, p.dinv, acc[9]);
         const float dL_dalpha = raw * p.T;
         const float w = f.G * dL_dalpha;
-#if HLGS_BWD_PK
-        if (!INTERP) {  // the same IEEE products and sums, two per instruction
-            typedef float v2f __attribute__((ext_vector_type(2)));
-            const v2f dxy = {dx, dy};
-            const v2f wd = v2f{w, w} * dxy;
-            v2f a01 = {acc[0], acc[1]}, a23 = {acc[2], acc[3]};
-            a01 += wd;
-            a23 = __builtin_elementwise_fma(v2f{wd.x, wd.x}, dxy, a23);
-            acc[0] = a01.x; acc[1] = a01.y; acc[2] = a23.x; acc[3] = a23.y;
-            acc[4] = fmaf(wd.y, dy, acc[4]);
-            acc[5] += w;
-            return;
-        }
-#endif
         const float wdx = w * dx, wdy = w * dy;
         acc[0] += wdx;
         acc[1] += wdy;
@@ -179,20 +119,6 @@ __device__ __forceinline__ void bwd_back(PixB& p, uint32_t li, const BwdFront& f
         if (INTERP) acc[5] += (tt - powf(1.0f - f.my_alpha, fr - 1.0f) * (tt - 1.0f) * fr) * w;
         else acc[5] += w;
     }
-}
-
-// One quadrant pass: the front is computed for every lane ahead of the validity branch (HLGS_BWD_HOIST), so its
-// transcendental latency overlaps the compare -> SALU -> exec chain that decides the branch instead of following it.
-template <bool INTERP, bool DEPTH, bool ALT, int K>
-__device__ __forceinline__ void bwd_pass(PixB (&ps)[4], uint32_t li, float lx, float ly, const float4& xy, const float4& q,
-                                         const float4& col, float2 tf, float (&acc)[10], bool clampable)
-{
-    BwdFront f = bwd_front<INTERP, ALT>(xy.x - (lx + 8.f * (K & 1)), xy.y - (ly + 8.f * (K >> 1)), q, tf.x, tf.y, col.w,
-                                        clampable);
-#if HLGS_BWD_HOIST
-    asm volatile("" : "+v"(f.G), "+v"(f.r1m), "+v"(f.alpha));  // keep them above the branch
-#endif
-    bwd_back<INTERP, DEPTH>(ps[K], li, f, col, xy.z, tf.x, tf.y, acc);
 }
 
 // Per-splat record from the reduced moments (see bwd_back); co = conic and opacity of the splat.
@@ -227,64 +153,30 @@ struct BwdArgs {
     const uint32_t* misc;  // Img::misc of the forward: [kMiscPack] says whether its point_list entries are packed
 };
 
-// One wave per (tile, chunk of the tile's list), back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8
-// quadrant.  Chunk c covers list entries [c clen, min(count, (c + 1) clen)) (bwd_chunk_len); blocks are ordered
-// chunk-major, so the front chunks, where most pixels are still live, start first.  A pixel whose last contributor
-// lies behind the chunk's end starts from the forward's sample there (transmittance, and what was blended behind
-// it), otherwise from its final state, as the reference's single back-to-front pass has it at that point.  Each
-// 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
-// whose n_contrib lies behind it) run bwd_pass, the ten moments are folded over the wave, and one record per
-// (tile, splat) is stored after the batch.
-// Traffic-attribution switches (tools/ab_fetch.sh, timing and counters only; each breaks parity): skip the
-// point_offsets gather, the per-pixel inputs, the split-state reads, or the record stores.
-#ifndef HLGS_BWD_NT_LOAD
-#define HLGS_BWD_NT_LOAD 0
-#endif
-#ifndef HLGS_BWD_NT_STORE
-#define HLGS_BWD_NT_STORE 0
-#endif
-#ifndef HLGS_DIAG_BWD_FAKE_SBASE
-#define HLGS_DIAG_BWD_FAKE_SBASE 0
-#endif
-#ifndef HLGS_DIAG_BWD_NO_GATHER
-#define HLGS_DIAG_BWD_NO_GATHER 0
-#endif
-#ifndef HLGS_DIAG_BWD_NO_PIXIN
-#define HLGS_DIAG_BWD_NO_PIXIN 0
-#endif
-#ifndef HLGS_DIAG_BWD_NO_SPLIT
-#define HLGS_DIAG_BWD_NO_SPLIT 0
-#endif
-#ifndef HLGS_DIAG_BWD_NO_STORE
-#define HLGS_DIAG_BWD_NO_STORE 0
-#endif
-#ifndef HLGS_DIAG_BWD_NO_ZERO
-#define HLGS_DIAG_BWD_NO_ZERO 0
-#endif
-#ifndef HLGS_BWD_PAIR
-#define HLGS_BWD_PAIR 0  // two visited splats per loop iteration, one twenty-moment reduction (wave_reduce20_rs)
-#endif
-#ifndef HLGS_BWD_TILE_MAJOR
-#define HLGS_BWD_TILE_MAJOR 0  // 0: chunk-major (the front chunks, where most pixels are live, start first)
-#endif
-#ifndef HLGS_BWD_MSTRIDE
-#define HLGS_BWD_MSTRIDE 65
-#endif
-#ifndef HLGS_BWD_WAVES
-#define HLGS_BWD_WAVES 5  // waves per SIMD: 96 VGPRs
-#endif
+// One wave per (tile, chunk of the tile's list), back to front.  Chunk c covers list entries [c clen, min(count,
+// (c + 1) clen)) (bwd_chunk_len); blocks are ordered chunk-major, so the front chunks, where most pixels are still live,
+// start first.  A pixel whose last contributor lies behind the chunk's end starts from the forward's sample there
+// (transmittance, and what was blended behind it), otherwise from its final state, as the reference's single
+// back-to-front pass has it at that point.
+//
+// Lanes and sub-blocks.  Lane l owns one pixel of each 8x8 quadrant k: 16-lane row g = l >> 4 is the 4x4 sub-block g of
+// the quadrant (x half g & 1, y half g >> 1) and l & 15 the pixel inside it.  Each 64-splat batch is staged in LDS with
+// a 16-bit sub-block mask per splat (sub_block_mask, intersected with the list entry's quadrant mask); per quadrant and
+// sub-block, the splats that reach it and lie in front of its furthest contributor are listed in LDS, back to front.
+// Then, per quadrant, every row walks its own sub-block's list: one iteration is one (splat, 4x4 sub-block) pair per row,
+// the ten moments are folded over the row (row_reduce10) and the totals added into the splat's moments in LDS.  Rows
+// whose list is done idle until the quadrant's longest list ends.  Against 8x8 passes with one wave-wide reduction
+// per splat (round 4), this keeps 61% of the pass lanes busy instead of 36% (configs[1] frame, tools/fold_stats.py),
+// and one row reduction costs 22 DPP adds where the wave reduction cost 24 instructions and 4 wait states.  After
+// the batch, lane j finishes splat j's record and stores it.
+// Moments of one splat meet by LDS float atomics (ds_add_f32).  Each is one instruction of one wave: the order in which
+// the rows' totals arrive is fixed by the lists, so the sums are the same on every run.
+constexpr int kMStride = 65;  // moment rows padded to 65 floats (moment v of splat j at v kMStride + j: distinct banks)
 template <bool INTERP, bool DEPTH, bool ALT>
-__global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
+__global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
 {
-#if HLGS_BWD_TILE_MAJOR
-    // a tile's chunk waves next to each other in dispatch order and on one XCD, so the second and third read of the
-    // tile's per-pixel inputs hit that XCD's L2
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int tile = L / (kBwdSplits + 1), part = L - tile * (kBwdSplits + 1);
-#else
     const int part = blockIdx.x / A.T;
     const int tile = xcd_remap(blockIdx.x - part * A.T, A.T);
-#endif
     const uint2* __restrict__ ranges = A.ranges;
     const uint32_t* __restrict__ point_list = A.point_list;
     const int W = A.W, H = A.H, gx = A.gx;
@@ -296,20 +188,13 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     const float* __restrict__ dL_dinvdepths = A.dL_dinvdepths;
     const BwdScratch& rec = A.rec;
     const uint32_t pack = __builtin_amdgcn_readfirstlane(A.misc[kMiscPack]);  // as the forward packed them
-    __shared__ float4 s_xy[64];   // x, y, 1/depth, unused
-    __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
-    __shared__ float4 s_col[64];  // r, g, b, alpha threshold on e2
-    __shared__ float2 s_tf[64];   // interpolation t, 1/kids
-    // reduced moments per splat (+ a spare row the non-storing lanes write), rows padded to kMStride = 65 floats: the
-    // ten lanes holding totals store moment v of splat j at kMStride v + j, on ten different banks ((v + j) mod 32),
-    // where a 64-float stride put all ten (and the spare row) on bank j mod 32
-    constexpr int kMStride = HLGS_BWD_MSTRIDE;
-    __shared__ float s_m[kMStride * 11];
-#if HLGS_BWD_ZERO_LDS
+    __shared__ float4 s_sp[3 * 64];   // splat j: [j] x, y, 1/depth, -; [64 + j] conic_q, opacity; [128 + j] r, g, b, thr
+    __shared__ float2 s_tf[64];       // interpolation t, 1/kids (hierarchy mode)
+    __shared__ float s_m[10 * kMStride];
+    __shared__ uint8_t s_list[16 * 64];  // per (quadrant k, sub-block g): the batch positions j, back to front
     __shared__ float4 s_zero[3];
     if (threadIdx.x < 3) s_zero[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);  // ordered by the batch barrier
-#endif
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x, grp = lane >> 4;
     const int tx = tile % gx, ty = tile / gx;
     const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
     const uint2 range = ranges[tile];
@@ -318,44 +203,27 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
     const uint32_t c0 = (uint32_t)part * clen;  // chunk = local list positions [c0, cnt)
     if (c0 >= count) return;
     const uint32_t cnt = min(count, c0 + clen);
+    // this lane's pixel inside each quadrant, and the forward's lane for it (its split-state column)
+    const int qxl = 4 * (grp & 1) + (lane & 3), qyl = 4 * (grp >> 1) + ((lane >> 2) & 3);
     const float* __restrict__ st =
-        cnt < count ? A.split_state + (size_t)(tile * kBwdSplits + part) * kSplitFloats + lane : nullptr;
+        cnt < count ? A.split_state + (size_t)(tile * kBwdSplits + part) * kSplitFloats + qxl + 8 * qyl : nullptr;
     const size_t HW = (size_t)H * W;
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
-    const float lx = (float)(tx0 + (lane & 7)), ly = (float)(ty0 + (lane >> 3));
-    // the reduced moment this lane stores (wave_reduce10_rs layout) as an offset into s_m; lanes holding no total
-    // store into the spare row s_m[10 kMStride ..]
-    const int wm_i = (lane & 3) ? -1 : reduce10_index(lane >> 4, (lane >> 2) & 3);
-    const int wmd = wm_i < 0 ? 10 * kMStride : kMStride * wm_i;
-#if HLGS_BWD_PAIR
-    // wave_reduce20_rs layout: this lane's two totals, each a moment of the pair's first (A) or second (B) splat
-    int wmd0, wmd1;
-    bool w0b, w1b;
-    {
-        const int v0 = (lane & 3) ? -1 : reduce20_index(lane >> 4, (lane >> 2) & 3, 0);
-        const int v1 = (lane & 3) ? -1 : reduce20_index(lane >> 4, (lane >> 2) & 3, 1);
-        wmd0 = v0 < 0 ? 10 * kMStride : kMStride * (v0 % 10);
-        wmd1 = v1 < 0 ? 10 * kMStride : kMStride * (v1 % 10);
-        w0b = v0 >= 10;
-        w1b = v1 >= 10;
-    }
-#endif
+    const float lx = (float)(tx0 + qxl), ly = (float)(ty0 + qyl);
+    // the row total this lane adds into s_m (row_reduce10 layout), or none
+    const int wm_i = row_reduce10_index((lane >> 2) & 3, lane & 3);
+    const bool has_total = wm_i >= 0;
+    const int wmd = has_total ? kMStride * wm_i : 0;
+    const int psel = lane & 3;  // which of t0, t1, t2 it adds
 
-    // lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant k
     PixB ps[4];
-    uint32_t qlast[4];  // wave-uniform per quadrant: furthest-back position any of its pixels needs
+    uint32_t slast[4];  // per quadrant, row-uniform: the furthest-back position any pixel of the row's sub-block needs
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int px = tx0 + 8 * (k & 1) + (lane & 7), py = ty0 + 8 * (k >> 1) + (lane >> 3);
+        const int px = tx0 + 8 * (k & 1) + qxl, py = ty0 + 8 * (k >> 1) + qyl;
         const bool inside = px < W && py < H;
         const size_t pid = (size_t)W * py + px;
         PixB& p = ps[k];
-#if HLGS_DIAG_BWD_NO_PIXIN  // traffic attribution only (tools/ab_fetch.sh): no per-pixel input reads, parity broken
-        const float tf = inside ? 0.5f : 0.f;
-        p.T = tf;
-        p.last = inside ? count : 0u;
-        p.dr = p.dg = p.db = p.dinv = inside ? 0.1f : 0.f;
-#else
         const float tf = inside ? final_Ts[pid] : 0.f;
         p.T = tf;
         p.last = inside ? n_contrib[pid] : 0u;
@@ -363,7 +231,6 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         p.dg = inside ? dL_dpixels[HW + pid] : 0.f;
         p.db = inside ? dL_dpixels[2 * HW + pid] : 0.f;
         p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
-#endif
         float bgd = 0.f;
         bgd += bg[0] * p.dr;
         bgd += bg[1] * p.dg;
@@ -372,7 +239,7 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         // (alt-rasterizer backward.cu:608, 619): the background enters dL/dalpha twice
         if (ALT) bgd *= 2.f;
         p.ARD = bgd;  // T_final <bg, dL/dpixel> / T_final
-        if (p.last > cnt && !HLGS_DIAG_BWD_NO_SPLIT) {  // still blending at the chunk's end (so the forward sampled it there)
+        if (p.last > cnt) {  // still blending at the chunk's end (so the forward sampled it there)
             const float* sk = st + k * 5 * 64;
             p.T = sk[0];
             float behind = sk[64] * p.dr + sk[128] * p.dg + sk[192] * p.db;
@@ -380,48 +247,43 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
             p.ARD = fmaf(tf, bgd, behind) / p.T;  // <accum_rec, dL/dpixel> (+ depth, + bg term) at the chunk's end
         }
         uint32_t m = min(p.last, cnt);
-        for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-        qlast[k] = __builtin_amdgcn_readfirstlane(m);
+        for (int off = 8; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        slast[k] = m;
     }
-    const uint32_t maxlast = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
+    // the same per (quadrant, sub-block) as scalars: sl[4 k + g]
+    uint32_t sl[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) sl[4 * k + r] = __builtin_amdgcn_readlane(slast[k], 16 * r);
+    uint32_t maxlast = 0;
+#pragma unroll
+    for (int b = 0; b < 16; b++) maxlast = max(maxlast, sl[b]);
 
     for (uint32_t b0 = 0; b0 < cnt - c0; b0 += 64) {
         // batch covers local positions cnt-1-b0 down to cnt-1-b0-(n-1), loaded back to front
         const int n = (int)min(64u, cnt - c0 - b0);
         const uint32_t li_top = cnt - 1 - b0;
         const bool lane_valid = lane < n;
-        uint32_t slot = 0, qm = 0;
+        uint32_t slot = 0, sbm = 0;
         float4 my_co = make_float4(0.f, 0.f, 0.f, 0.f);
         if (lane_valid) {
             const uint32_t pos = range.x + li_top - lane;
-            uint32_t id = point_list[pos], pm = 0;
+            uint32_t id = point_list[pos], qm = 0xFu;
             if (pack) {  // packed entry (pack_entries): the quadrant mask comes with it
-                pm = id & ((1u << kEntryShift) - 1u);
+                qm = id & ((1u << kEntryShift) - 1u);
                 id >>= kEntryShift;
             }
             const float4* sr = g.splat + 4 * (size_t)id;
-#if HLGS_DIAG_BWD_FAKE_SBASE  // traffic attribution: slots spread by id, no point_offsets gather (parity broken)
-            const uint32_t sbase = id;
-#else
-            const uint32_t sbase = (id && !HLGS_DIAG_BWD_NO_GATHER) ? g.point_offsets[id - 1] : 0u;
-#endif
-#if HLGS_BWD_NT_LOAD  // records streamed past L2 (no reuse across tile waves), so point_offsets stays resident
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            const v4f* srv = reinterpret_cast<const v4f*>(sr);
-            const v4f q0 = __builtin_nontemporal_load(srv), q1 = __builtin_nontemporal_load(srv + 1),
-                      q2 = __builtin_nontemporal_load(srv + 2), q3 = __builtin_nontemporal_load(srv + 3);
-            const float4 r0 = make_float4(q0.x, q0.y, q0.z, q0.w), r1 = make_float4(q1.x, q1.y, q1.z, q1.w),
-                         r2 = make_float4(q2.x, q2.y, q2.z, q2.w), r3 = make_float4(q3.x, q3.y, q3.z, q3.w);
-#else
+            const uint32_t sbase = id ? g.point_offsets[id - 1] : 0u;
             const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
-#endif
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            qm = pack ? pm : quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
-            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
-            s_q[lane] = conic_q(co);
-            my_co = co;
-            s_col[lane] = make_float4(r1.z, r1.w, r2.x, r3.w);
+            s_sp[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
+            s_sp[64 + lane] = conic_q(co);
+            s_sp[128 + lane] = make_float4(r1.z, r1.w, r2.x, r3.w);
             if (INTERP) s_tf[lane] = make_float2(r2.z, r2.w);
+            my_co = co;
+            sbm = sub_block_mask(splat_bands(r0.x, r0.y, co, r3.w), tx0, ty0) & quad_to_sub(qm);
             const int x0 = __float_as_int(r3.y) & 0xffff, y0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
             const int w = __float_as_int(r3.z);
             // the Gaussian's record slots start at the exclusive scan of the rect sizes (point_offsets is inclusive)
@@ -429,122 +291,62 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
         }
 #pragma unroll
         for (int v = 0; v < 10; v++) s_m[kMStride * v + lane] = 0.f;
-        __syncthreads();
         // a batch entirely behind every pixel's last contributor leaves its records zero
         const uint32_t li_bot = li_top - (uint32_t)(n - 1);
+        uint32_t nl[16];  // list lengths (scalars)
         if (li_bot < maxlast) {
-            // per quadrant, the wave-uniform set of the batch's splats to visit: footprint reaches the quadrant
-            // (quad_mask) and the splat lies in front of the quadrant's furthest contributor (li < qlast[k],
-            // i.e. j > li_top - qlast[k]); the loop then visits set bits only, with no LDS read to decide
-            uint64_t qv[4];
+            // splat j (this lane) goes to the list of sub-block b if its footprint reaches b and it lies in front of
+            // b's furthest contributor (li < sl[b]); lists are in ascending j, i.e. back to front
+            const uint32_t li = li_top - (uint32_t)lane;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                uint64_t m = __ballot((qm >> k) & 1u);
-                if (li_top >= qlast[k]) {
-                    const uint32_t d = li_top - qlast[k];  // splats 0..d are behind every pixel of quadrant k
-                    m = d >= 63 ? 0ull : m & (~0ull << (d + 1));
-                }
-                qv[k] = m;
-            }
-            uint64_t todo = qv[0] | qv[1] | qv[2] | qv[3];
-            // the batch's splats whose opacity can reach the 0.99 clamp (bit j: splat j)
-            const uint64_t opq = __ballot(lane_valid && my_co.w > 0.99f);
-            // Splat loop with the least scalar bookkeeping: the visited bit is cleared (s_bitset0), the next visited
-            // splat found by s_ff1 (-1 once none is left; its LDS reads use index 0 then), and every visited splat
-            // is reduced (0.15% of them have no valid pair), so no per-pass wave-mask tracking.
-            if (todo) {
-                int j = __builtin_ctzll(todo);
-                float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
-                float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
-                // the quadrants splat jj visits, in quadrant order (uniform branches), into acc
-                auto passes = [&](int jj, const float4& pxy, const float4& pco, const float4& pcol, const float2& ptf,
-                                  float(&acc)[10]) {
-                    const uint32_t li = li_top - (uint32_t)jj;
-#if HLGS_BWD_ZERO_LDS
-                    // the ten accumulators zeroed by three LDS reads of a zero block (the LDS pipe, ~29% busy here)
-                    // instead of five v_mov_b64 on the VALU pipe, which this kernel saturates
-                    {
-                        typedef float v4f __attribute__((ext_vector_type(4)));
-                        typedef __attribute__((address_space(3))) const volatile v4f lds_v4f;  // stays a ds_read
-                        lds_v4f* vz = (lds_v4f*)(s_zero);
-                        const v4f z0 = vz[0], z1 = vz[1], z2 = vz[2];
-                        acc[0] = z0.x; acc[1] = z0.y; acc[2] = z0.z; acc[3] = z0.w;
-                        acc[4] = z1.x; acc[5] = z1.y; acc[6] = z1.z; acc[7] = z1.w;
-                        acc[8] = z2.x; acc[9] = z2.y;
-                    }
-#elif HLGS_DIAG_BWD_NO_ZERO  // timing only: accumulators not reset between splats (parity broken)
-#else
-#pragma unroll
-                    for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
-                        uint64_t z;
-                        asm volatile("v_mov_b64 %0, 0" : "=v"(z));
-                        acc[v] = __uint_as_float((uint32_t)z);
-                        acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
-                    }
-#endif
-                    // wave-uniform (scalar mask); the hierarchy-mode kernels keep the factor (no VGPRs for the branch)
-                    const bool clampable = !HLGS_BWD_OPQ || INTERP || ((opq >> jj) & 1u);
-                    if ((qv[0] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 0>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
-                    if ((qv[1] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 1>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
-                    if ((qv[2] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 2>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
-                    if ((qv[3] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 3>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
-                };
-#if HLGS_BWD_PAIR
-                // Two visited splats per iteration, their twenty moments folded by one reduce-scatter
-                // (wave_reduce20_rs): 34 DPP adds and 5 permlane swaps where two ten-moment reductions take 36 and 6
-                while (true) {
-                    int jn;  // s_ff1: -1 once todo is empty
-                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
-                    float accA[10];
-                    passes(j, xy, co, col, tf, accA);
-                    if (jn < 0) {
-                        s_m[wmd + j] = wave_reduce10_rs(accA);
-                        break;
-                    }
-                    float accB[10];
-                    {
-                        const float4 xyB = s_xy[jn], coB = s_q[jn], colB = s_col[jn];
-                        const float2 tfB = INTERP ? s_tf[jn] : make_float2(0.f, 0.f);
-                        int jn2;
-                        asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn2) : "s"(jn));
-                        passes(jn, xyB, coB, colB, tfB, accB);
-                        const int jl = jn2 < 0 ? 0 : jn2;  // the next pair's first splat, read ahead of the reduction
-                        xy = s_xy[jl];
-                        co = s_q[jl];
-                        col = s_col[jl];
-                        if (INTERP) tf = s_tf[jl];
-                        float w0, w1;
-                        wave_reduce20_rs(accA, accB, w0, w1);
-                        s_m[wmd0 + (w0b ? jn : j)] = w0;
-                        s_m[wmd1 + (w1b ? jn : j)] = w1;
-                        if (jn2 < 0) break;
-                        j = jn2;
-                    }
-                }
-#else
-                float acc[10];  // (reset by passes() for every splat)
-#if HLGS_DIAG_BWD_NO_ZERO
-                for (int v = 0; v < 10; v++) acc[v] = 0.f;
-#endif
-                while (true) {
-                    int jn;  // s_ff1: -1 once todo is empty
-                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
-                    passes(j, xy, co, col, tf, acc);
-                    const int jl = jn < 0 ? 0 : jn;  // the next visited splat's LDS reads ahead of the reduction
-                    xy = s_xy[jl];
-                    co = s_q[jl];
-                    col = s_col[jl];
-                    if (INTERP) tf = s_tf[jl];
-                    // every lane stores (the spare row takes the non-totals), so no exec-mask change
-                    s_m[wmd + j] = wave_reduce10_rs(acc);
-                    if (jn < 0) break;
-                    j = jn;
-                }
-#endif
+            for (int b = 0; b < 16; b++) {
+                const bool in = ((sbm >> b) & 1u) && li < sl[b];
+                const uint64_t M = __builtin_amdgcn_ballot_w64(in);
+                nl[b] = (uint32_t)__popcll(M);
+                const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+                if (in) s_list[64 * b + rank] = (uint8_t)lane;
             }
         }
         __syncthreads();
-        if (lane_valid && !HLGS_DIAG_BWD_NO_STORE) {
+        if (li_bot < maxlast) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t n0 = nl[4 * k], n1 = nl[4 * k + 1], n2 = nl[4 * k + 2], n3 = nl[4 * k + 3];
+                const uint32_t nmax = max(max(n0, n1), max(n2, n3));
+                const uint32_t myn = grp == 0 ? n0 : grp == 1 ? n1 : grp == 2 ? n2 : n3;
+                const uint8_t* lst = s_list + 64 * (4 * k + grp);
+                for (uint32_t it = 0; it < nmax; it++) {
+                    if (it < myn) {
+                        const int j = lst[it];
+                        const float4 xy = s_sp[j], q = s_sp[64 + j], col = s_sp[128 + j];
+                        const float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
+                        float acc[10];
+                        {  // zeroed by three LDS reads of a zero block (the LDS pipe has room; the VALU pipe is the limit)
+                            typedef float v4f __attribute__((ext_vector_type(4)));
+                            typedef __attribute__((address_space(3))) const volatile v4f lds_v4f;  // stays a ds_read
+                            lds_v4f* vz = (lds_v4f*)(s_zero);
+                            const v4f z0 = vz[0], z1 = vz[1], z2 = vz[2];
+                            acc[0] = z0.x; acc[1] = z0.y; acc[2] = z0.z; acc[3] = z0.w;
+                            acc[4] = z1.x; acc[5] = z1.y; acc[6] = z1.z; acc[7] = z1.w;
+                            acc[8] = z2.x; acc[9] = z2.y;
+                        }
+                        BwdFront f = bwd_front<INTERP, ALT>(xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), q,
+                                                            tf.x, tf.y, col.w);
+                        // the front above the validity branch: its transcendental latency overlaps the compare -> SALU
+                        // -> exec chain that decides the branch instead of following it
+                        asm volatile("" : "+v"(f.G), "+v"(f.r1m), "+v"(f.alpha));
+                        bwd_back<INTERP, DEPTH>(ps[k], li_top - (uint32_t)j, f, col, xy.z, tf.x, tf.y, acc);
+                        float t0, t1, t2;
+                        row_reduce10(acc, t0, t1, t2);
+                        const float t = psel == 0 ? t0 : psel == 1 ? t1 : t2;
+                        if (has_total) atomicAdd(&s_m[wmd + j], t);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (lane_valid) {
             float m[10];
 #pragma unroll
             for (int v = 0; v < 10; v++) m[v] = s_m[kMStride * v + lane];
@@ -552,22 +354,13 @@ __global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
             float2 rc;
             finish_record(m, my_co, ddelx_dx, ddely_dy, ra, rb, rc);
             float4* r = rec.rec + 3 * (size_t)slot;
-#if HLGS_BWD_NT_STORE
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            v4f* rv = reinterpret_cast<v4f*>(r);
-            __builtin_nontemporal_store(v4f{ra.x, ra.y, ra.z, ra.w}, rv);
-            __builtin_nontemporal_store(v4f{rb.x, rb.y, rb.z, rb.w}, rv + 1);
-            __builtin_nontemporal_store(v4f{rc.x, rc.y, 0.f, 0.f}, rv + 2);
-#else
             r[0] = ra;
             r[1] = rb;
             r[2] = make_float4(rc.x, rc.y, 0.f, 0.f);
-#endif
         }
         __syncthreads();
     }
 }
-
 
 
 void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, const BwdScratch& rs,

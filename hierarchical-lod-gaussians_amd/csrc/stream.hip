@@ -191,21 +191,9 @@ __global__ void __launch_bounds__(1024) k_upper_cut(CutArgs a, int resume)
         parity = cs->parity;
         overflow = cs->overflow;
     }
-#ifdef HLGS_CUT_CLOCKS  // diagnostic build: per-level (realtime, core clock, size) at the unused tail of cut
-    int level = 0;
-#endif
     __syncthreads();
     while (size > 0 && !overflow) {
         if (!resume && size > kCutNarrow) break;  // hand off to k_cut_level
-#ifdef HLGS_CUT_CLOCKS
-        if (threadIdx.x == 0 && level < 40) {
-            long long* d = reinterpret_cast<long long*>(a.cut + a.capacity - 256) + 3 * level;
-            d[0] = (long long)__builtin_amdgcn_s_memrealtime();
-            d[1] = (long long)__builtin_amdgcn_s_memtime();
-            d[2] = size;
-        }
-        level++;
-#endif
         const int* front = parity ? a.front_b : a.front_a;
         int* next = parity ? a.front_a : a.front_b;
         const int K = (size + 1023) / 1024;
@@ -365,10 +353,7 @@ __global__ void __launch_bounds__(256) k_rows_multi(RowTabs tabs, int64_t n, con
     uint32_t* __restrict__ dst = static_cast<uint32_t*>(tb.dst);
     // lanes own U consecutive words (U = 4 for device-only tables, whose interior row chunks move as one 16-byte
     // access; 1 otherwise, since a 16-byte access to host memory may straddle a page)
-#ifndef HLGS_ROWS_WIDE
-#define HLGS_ROWS_WIDE 1  // 0: 4-byte lanes everywhere; 1: 16-byte lanes for device-only tables; 2: only if rows are whole 16-byte chunks
-#endif
-    const int U = (HLGS_ROWS_WIDE == 1 && tb.device_only) || (HLGS_ROWS_WIDE == 2 && tb.device_only && (words & 3) == 0) ? 4 : 1;
+    const int U = tb.device_only ? 4 : 1;  // 16-byte lanes for device-only tables, 4-byte lanes across the host link
     const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * U, S = (int64_t)gridDim.x * 256 * U;
     int64_t r = w0 / words, k = w0 - r * words;
     const int64_t dr = S / words, dk = S - dr * words;
@@ -474,12 +459,10 @@ void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, 
         pt.res[t] = resident ? resident[t] : nullptr;
         pt.words[t] = words[t];
     }
-#ifndef HLGS_WB_BLOCKS
-#define HLGS_WB_BLOCKS 128
-#endif
+    constexpr int64_t kWriteBackBlocks = 128;
     // 4 waves (rows) per block, grid-stride above.  The write-back is bound by the host link, not by waves: a
     // small grid moves it as fast and leaves the CUs to the compaction and load running beside it (SPTCache)
-    const int64_t blocks = std::min<int64_t>((n + 3) / 4, to_host ? HLGS_WB_BLOCKS : 2048);
+    const int64_t blocks = std::min<int64_t>((n + 3) / 4, to_host ? kWriteBackBlocks : 2048);
     if (blocks <= 0) return;
     if (to_host) hipLaunchKernelGGL(k_rows_packed<true>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw, (const int*)nullptr);
     else hipLaunchKernelGGL(k_rows_packed<false>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw, resident_of);
@@ -520,10 +503,7 @@ __global__ void __launch_bounds__(256) k_rows_compact(RowTabs tabs, int64_t n, c
 
 void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_rows, const int* dst_rows, hipStream_t s)
 {
-#ifndef HLGS_ROWS_COMPACT
-#define HLGS_ROWS_COMPACT 1
-#endif
-    bool compact = HLGS_ROWS_COMPACT && src_rows && !dst_rows;
+    bool compact = src_rows && !dst_rows;
     for (int t = 0; t < T && compact; t++)
         compact = tabs[t].device_only && (reinterpret_cast<uintptr_t>(tabs[t].dst) & 15u) == 0;
     if (compact) {

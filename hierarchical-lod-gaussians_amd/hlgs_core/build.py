@@ -42,8 +42,26 @@ def _compile(src, extra):
     return obj
 
 
+def variant_switches():
+    """Compile-time switches in the product sources (`#if[n]def HLGS_...` / `#if HLGS_...`): there are none.  Measured
+    variants live outside the product source (tools/variants/, built by tools/build_variant.py), so libhlgs.so is
+    exactly the tested configuration and no diagnostic or parity-breaking path can be compiled into it."""
+    import re
+    pat = re.compile(r"^\s*#\s*(ifdef|ifndef|if|elif)\b.*\bHLGS_", re.M)
+    hits = []
+    for f in sorted(os.listdir(CSRC)):
+        for m in pat.finditer(open(os.path.join(CSRC, f)).read()):
+            hits.append(f"{f}: {m.group(0).strip()}")
+    return hits
+
+
 def build(force=False, extra=None, verbose=False):
     extra = list(extra or [])
+    if any(f.startswith("-D") for f in extra):
+        raise ValueError("libhlgs.so is built without defines; experiment variants: tools/build_variant.py")
+    sw = variant_switches()
+    if sw:
+        raise RuntimeError("compile-time variant switches in the product sources:\n" + "\n".join(sw))
     os.makedirs(OBJDIR, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():

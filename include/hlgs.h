@@ -435,11 +435,19 @@ int hlgs_expand_to_target(int N, const int* nodes, int target, int* out, int cap
 size_t hlgs_binning_point_list_offset(int R);  /* uint32 point_list[R] */
 /* point_list entries of a P-Gaussian forward are (Gaussian index << shift) | footprint quadrant mask: the shift. */
 int hlgs_point_list_entry_shift(int P);
-/* 1 if a P-Gaussian forward bins no instance whose quadrant mask is 0 (packed entries with HLGS_DROP_EMPTY): its tile
- * lists and n_contrib then match the oracle run with drop_empty (oracle/hlgs_oracle.c rect_quad_masks). */
+/* 1 if a P-Gaussian forward bins no instance whose quadrant mask is 0 (packed entries, dropping on): its tile
+ * lists and n_contrib then match the oracle run with drop_empty (oracle/hlgs_oracle.c rect_quad_masks).  0: every
+ * instance of the reference's binning (rasterizer_impl.cu:70-115) is listed, and point_list / n_contrib are laid out as
+ * the reference lays them out. */
 int hlgs_point_list_drops_empty(int P);
 /* Tests: on = 0 makes every following frame use plain index entries (the P >= 2^28 path); 1 restores the default. */
 void hlgs_set_entry_packing(int on);
+/* on = 0: following frames bin every instance, including those whose footprint reaches none of their tile's quadrants
+ * (the reference's tile lists and n_contrib; images and gradients are the same either way); 1 (default) drops them. */
+void hlgs_set_drop_empty(int on);
+/* Tests: the bound on each look-back poll of the fused binning plan (default 2^20 polls, ~0.1 s).  A plan whose
+ * look-back times out is re-run with the two-launch plan that needs no inter-block wait; polls = 0 forces that path. */
+void hlgs_set_plan_polls(unsigned polls);
 size_t hlgs_image_ranges_offset(int W, int H);  /* uint2 ranges[tiles] */
 size_t hlgs_geom_splat_offset(int P);           /* float4 splat[P][4]: x, y, conic a, b | conic c, opacity, r, g |
                                                    b, 1/depth, t, 1/kids | record base, tile x0, y0, width */

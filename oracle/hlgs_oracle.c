@@ -32,14 +32,13 @@
 #endif
 
 /* The same source also builds the all-cores CPU baseline (oracle/build/libhlgs_oracle_omp.so, gcc -fopenmp):
- * preprocess and per-Gaussian backward over Gaussians, the blend over tiles, per-tile sorts in parallel; the
- * blend backward then accumulates its per-Gaussian sums with atomic adds (summation order, and so the last bits
- * of the gradients, vary from run to run -- the timing leg only; every parity check uses the serial build). */
-#ifdef _OPENMP
-#define ORC_ACC(lhs, rhs) do { const float v_ = (rhs); _Pragma("omp atomic") lhs += v_; } while (0)
-#else
-#define ORC_ACC(lhs, rhs) ((lhs) += (rhs))
-#endif
+ * preprocess and per-Gaussian backward over Gaussians, the blend and the blend backward over tiles, per-tile sorts
+ * in parallel.  The blend backward sums each (tile, Gaussian) pair's contributions over the tile's pixels into a
+ * record of its own (tile_records), and the records are added per Gaussian in tile order afterwards, serially: the
+ * reference adds its per-pixel contributions with float atomics in no fixed order (HR/backward.cu:669-718), and this
+ * fixed order makes the OpenMP build bitwise equal to the serial one (tests/test_oracle.py), so it can stand in for
+ * it on full-size frames. */
+
 
 /* Alpha decision mode:
  *   0 (default) -- the shared arithmetic contract (A-17): e2 = power log2(e) from the pre-scaled conic, G = exp2(e2),
@@ -787,6 +786,31 @@ typedef struct {
     float *ddc;      /* x3 (alt variant: gradient of the degree-0 coefficient) */
 } orc_grads;
 
+/* Record layout per tile-list position j (10 floats): dcolor r g b, dinvdepth, dmean2D x y, dconic 0 1 3, dopacity. */
+static void tile_records_add(const orc_img *im, int T, const int *indices, const float *rec, orc_grads *o)
+{
+    for (int t = 0; t < T; t++)
+        for (uint32_t j = im->ranges[2 * t]; j < im->ranges[2 * t + 1]; j++) {
+            const uint32_t id = im->point_list[j];
+            const int gid = indices ? indices[id] : (int)id;
+            const float *r = rec + 10 * (size_t)j;
+            for (int ch = 0; ch < 3; ch++) o->dcolor[3 * gid + ch] += r[ch];
+            if (o->dinvdepth) o->dinvdepth[gid] += r[3];
+            o->dmean2D[3 * gid] += r[4];
+            o->dmean2D[3 * gid + 1] += r[5];
+            o->dconic[4 * gid] += r[6];
+            o->dconic[4 * gid + 1] += r[7];
+            o->dconic[4 * gid + 3] += r[8];
+            o->dopacity[gid] += r[9];
+        }
+}
+static float *tile_records(const orc_img *im, int T)
+{
+    uint32_t n = 0;
+    for (int t = 0; t < T; t++) n = n > im->ranges[2 * t + 1] ? n : im->ranges[2 * t + 1];
+    return (float *)calloc(10 * (size_t)(n > 0 ? n : 1), sizeof(float));
+}
+
 /* HR/backward.cu:498-721 (renderCUDA<3> backward) */
 static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *im, const float *dL_dpix,
                            const float *dL_dinv, orc_grads *o)
@@ -797,6 +821,7 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
     const float *col = a->colors_precomp ? a->colors_precomp : g->rgb;
     int interp = (a->ts != NULL && a->kids != NULL);
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+    float *rec = tile_records(im, gx * gy);
 #pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ty++)
         for (int tx = 0; tx < gx; tx++) {
@@ -826,20 +851,20 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
                         T = T / (1.f - alpha);
                         const float weight = alpha * T;
                         float dL_dalpha = 0.0f;
-                        int gid = a->indices ? a->indices[id] : (int)id;
+                        float *r = rec + 10 * (size_t)j;
                         for (int ch = 0; ch < 3; ch++) {
                             const float c = col[3 * id + ch];
                             acc[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * acc[ch];
                             last_color[ch] = c;
                             dL_dalpha += (c - acc[ch]) * dpix[ch];
-                            ORC_ACC(o->dcolor[3 * gid + ch], weight * dpix[ch]);
+                            r[ch] += weight * dpix[ch];
                         }
                         if (dL_dinv) {
                             const float invd = 1.f / g->depths[id];
                             acc_inv = last_alpha * last_inv + (1.f - last_alpha) * acc_inv;
                             last_inv = invd;
                             dL_dalpha += (invd - acc_inv) * dinv;
-                            ORC_ACC(o->dinvdepth[gid], weight * dinv);
+                            r[3] += weight * dinv;
                         }
                         dL_dalpha *= T;
                         last_alpha = alpha;
@@ -851,17 +876,19 @@ static void blend_backward(const orc_args *a, const orc_geom *g, const orc_img *
                         const float gdx = G * dx, gdy = G * dy;
                         const float dG_ddelx = -gdx * co[0] - gdy * co[1];
                         const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                        ORC_ACC(o->dmean2D[3 * gid], dL_dG * dG_ddelx * ddelx_dx);
-                        ORC_ACC(o->dmean2D[3 * gid + 1], dL_dG * dG_ddely * ddely_dy);
-                        ORC_ACC(o->dconic[4 * gid], -0.5f * gdx * dx * dL_dG);
-                        ORC_ACC(o->dconic[4 * gid + 1], -0.5f * gdx * dy * dL_dG);
-                        ORC_ACC(o->dconic[4 * gid + 3], -0.5f * gdy * dy * dL_dG);
+                        r[4] += dL_dG * dG_ddelx * ddelx_dx;
+                        r[5] += dL_dG * dG_ddely * ddely_dy;
+                        r[6] += -0.5f * gdx * dx * dL_dG;
+                        r[7] += -0.5f * gdx * dy * dL_dG;
+                        r[8] += -0.5f * gdy * dy * dL_dG;
                         float mult = 1.0f;
                         if (interp) mult = tt - powf(1.0f - my_alpha, fr - 1.0f) * (tt - 1.0f) * fr;
-                        ORC_ACC(o->dopacity[gid], mult * G * dL_dalpha);
+                        r[9] += mult * G * dL_dalpha;
                     }
                 }
         }
+    tile_records_add(im, gx * gy, a->indices, rec, o);
+    free(rec);
     free(thr);
 }
 
@@ -881,6 +908,7 @@ static void blend_backward_alt(const orc_args *a, const orc_geom *g, const orc_i
     const size_t HW = (size_t)W * H;
     const float *col = a->colors_precomp ? a->colors_precomp : g->rgb;
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+    float *rec = tile_records(im, gx * gy);
 #pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ty++)
         for (int tx = 0; tx < gx; tx++) {
@@ -905,16 +933,17 @@ static void blend_backward_alt(const orc_args *a, const orc_geom *g, const orc_i
                         if (!pair_alpha(co, dx, dy, thr[id], 0, 0.0f, 0.0f, 0, &G, &my_alpha, &alpha)) continue;
                         const float weight = alpha * T;
                         float bg_dot = 0.0f, dL_dalpha = 0.0f;
+                        float *r = rec + 10 * (size_t)j;
                         for (int ch = 0; ch < 3; ch++) {
                             const float c = col[3 * id + ch];
                             ar[ch] += weight * c;
-                            ORC_ACC(o->dcolor[3 * id + ch], weight * dpix[ch]);
+                            r[ch] += weight * dpix[ch];
                             dL_dalpha += ((c * T) - (1.0f / (1.0f - alpha)) * (-ar[ch])) * dpix[ch];
                             bg_dot += a->bg[ch] * dpix[ch];
                         }
                         const float invd = 1.f / g->depths[id];
                         ard += weight * invd;
-                        if (o->dinvdepth) ORC_ACC(o->dinvdepth[id], weight * dinv);
+                        if (o->dinvdepth) r[3] += weight * dinv;
                         dL_dalpha += ((invd * T) - (1.0f / (1.0f - alpha)) * (-ard)) * dinv;
                         dL_dalpha += (-T_final / (1.0f - alpha)) * bg_dot;
                         T *= (1.0f - alpha);
@@ -922,15 +951,17 @@ static void blend_backward_alt(const orc_args *a, const orc_geom *g, const orc_i
                         const float gdx = G * dx, gdy = G * dy;
                         const float dG_ddelx = -gdx * co[0] - gdy * co[1];
                         const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                        ORC_ACC(o->dmean2D[3 * id], dL_dG * dG_ddelx * ddelx_dx);
-                        ORC_ACC(o->dmean2D[3 * id + 1], dL_dG * dG_ddely * ddely_dy);
-                        ORC_ACC(o->dconic[4 * id], -0.5f * gdx * dx * dL_dG);
-                        ORC_ACC(o->dconic[4 * id + 1], -0.5f * gdx * dy * dL_dG);
-                        ORC_ACC(o->dconic[4 * id + 3], -0.5f * gdy * dy * dL_dG);
-                        ORC_ACC(o->dopacity[id], G * dL_dalpha);
+                        r[4] += dL_dG * dG_ddelx * ddelx_dx;
+                        r[5] += dL_dG * dG_ddely * ddely_dy;
+                        r[6] += -0.5f * gdx * dx * dL_dG;
+                        r[7] += -0.5f * gdx * dy * dL_dG;
+                        r[8] += -0.5f * gdy * dy * dL_dG;
+                        r[9] += G * dL_dalpha;
                     }
                 }
         }
+    tile_records_add(im, gx * gy, NULL, rec, o);
+    free(rec);
     free(thr);
 }
 

@@ -73,7 +73,8 @@ def lib(omp=False):
     L = _libs.get(omp)
     if L is None:
         build()
-        L = C.CDLL(_LIB_FMA if omp == "fma" else _LIB_OMP if omp else _LIB)
+        # HLGS_ORACLE_LIB: the serial oracle built with other flags (tests/sanitize/build.py: ASan + UBSan)
+        L = C.CDLL(_LIB_FMA if omp == "fma" else _LIB_OMP if omp else os.environ.get("HLGS_ORACLE_LIB") or _LIB)
         L.orc_set_alpha_mode.argtypes = [C.c_int]
         L.orc_get_alpha_mode.restype = C.c_int
         L.orc_num_threads.restype = C.c_int

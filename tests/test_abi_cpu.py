@@ -117,3 +117,16 @@ def test_no_cpu_fallback():
     with pytest.raises(RuntimeError, match="means3D must have dimensions"):
         _C.rasterize_gaussians(torch.zeros(3), e, e, e, e, torch.zeros(4, 2), e, e, e, e, 1.0, e, torch.eye(4),
                                torch.eye(4), 0.5, 0.5, 16, 16, e, 0, torch.zeros(3), False, False, True)
+
+
+def test_product_sources_have_no_variant_switches():
+    """libhlgs.so is exactly the tested configuration: no `#if HLGS_...` switch (diagnostic or measured loser) in the
+    product sources -- the variants live in tools/variants/ and are built by tools/build_variant.py only."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        "hlgs_build", os.path.join(root, "hierarchical-lod-gaussians_amd", "hlgs_core", "build.py"))
+    B = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(B)
+    assert B.variant_switches() == []

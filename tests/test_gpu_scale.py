@@ -4,13 +4,16 @@ where the oracle finishes in seconds, against the oracle itself.
 - config #4 scale (4M Gaussians, SH 3, 1080p): the backward is bitwise deterministic, and scaling the upstream
   gradient by 2 scales every gradient by exactly 2 (every step of the backward is linear in it and a power-of-2
   scale commutes with float rounding), outputs are finite and the image is non-negative.
+- config #4 scale against the oracle itself: the full 4M-Gaussian 1080p frame, forward and backward, with the
+  OpenMP build of the oracle (bitwise equal to the serial one, tests/test_oracle.py::test_openmp_oracle_is_bitwise_serial):
+  radii bit-exact, every pixel within 1e-4, every gradient element within the element-wise bound.
 - a 3840x2160 frame (500k Gaussians): forward and backward against the oracle at the north-star tolerances.
 """
 import numpy as np
 import pytest
 
 from hlgs_core import synthetic as S
-from helpers import assert_grad, gpu_render, image_check, oracle_render, rel_err
+from helpers import assert_grad, drops_empty, gpu_render, image_check, oracle_render, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -33,6 +36,22 @@ def test_config4_scale_determinism_and_exact_linearity():
             np.testing.assert_array_equal(c[k], 2 * a[k], err_msg=f"{k} is not exactly linear in dL/dpixel")
         else:
             np.testing.assert_array_equal(c[k], a[k])
+
+
+def test_config4_full_frame_matches_oracle():
+    W, H, P = 1920, 1080, 4_000_000
+    cam = S.make_camera(W, H)
+    sc = S.make_gaussians(P, 3, cam, seed=4)
+    grads = S.upstream_grads(W, H, seed=1)
+    gpu = gpu_render(sc, cam, grads=grads)
+    ref = oracle_render(sc, cam, grads=grads, lib=True, drop_empty=drops_empty(P))
+    np.testing.assert_array_equal(gpu["radii"], ref["radii"])
+    for k in ("color", "invdepth"):
+        mx, nbad, ok = image_check(gpu[k], ref[k], 1e-4)
+        assert ok, f"{k} L-inf {mx} ({nbad} pixels)"
+    for k in ref:
+        if k.startswith("d"):
+            assert_grad(k, gpu[k][..., :ref[k].shape[-1]], ref[k])
 
 
 def test_uhd_frame_matches_oracle():

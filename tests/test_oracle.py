@@ -432,3 +432,31 @@ def test_lod_lerp_matches_reference_render_post(i):
     for k in keys:
         want = z[f"grad_{k}_{i}"]
         np.testing.assert_allclose(d[k].reshape(want.shape), want, rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("alt", [False, True])
+def test_openmp_oracle_is_bitwise_serial(alt):
+    """The OpenMP build (per-tile parallel blend and blend backward, per-Gaussian parallel preprocess and backward)
+    computes exactly what the serial build does -- every image, list and gradient bit -- because the blend backward sums
+    per (tile, Gaussian) record and adds the records in tile order (tile_records).  So the OpenMP build can stand in for
+    the serial oracle on full-size frames (tests/test_gpu_scale.py, configs[3] at 4M Gaussians)."""
+    from hlgs_core import synthetic as S
+    W, H = 320, 240
+    cam = S.cam_numpy(S.make_camera(W, H, bg=(0.2, 0.1, 0.3)))
+    sc = S.make_gaussians(30000, 3, cam, seed=41)
+    if alt:
+        sc = dict(sc, alt=True, antialiasing=True, dc=sc["shs"][:, :1].copy(), shs=sc["shs"][:, 1:].copy())
+    g, gd = S.upstream_grads(W, H, seed=5)
+    outs = []
+    for omp in (False, True):
+        fr = O.forward(sc, cam, do_depth=True, omp=omp, drop_empty=True)
+        gr = O.backward(fr, sc, g, gd)
+        outs.append((fr, gr))
+    (f0, g0), (f1, g1) = outs
+    for k in ("color", "invdepth", "final_T", "n_contrib", "ranges", "radii", "means2D", "conic_opacity"):
+        np.testing.assert_array_equal(getattr(f0, k), getattr(f1, k), err_msg=k)
+    np.testing.assert_array_equal(f0.point_list[:f0.R], f1.point_list[:f1.R])
+    for k, v in g0.items():
+        if v is not None:
+            np.testing.assert_array_equal(v.view(np.uint32), g1[k].view(np.uint32), err_msg=k)
+    assert O.num_threads(True) > 1  # the comparison means something only with several threads

@@ -5,7 +5,10 @@ tests/test_cull_check.py."""
 import numpy as np
 
 
-def run(N=400000, seed=0):
+def run(N=400000, seed=0, size=8):
+    """size = 8: the 8x8 quadrant blocks (foot_touches, the key scatter's bands); 4: the blend backward's 4x4
+    sub-blocks (sub_block_mask: the same band form with 4-row bands and 4-column blocks)."""
+    e = float(size - 1)
     rng = np.random.default_rng(seed)
     f32 = np.float32
     x = rng.uniform(-20, 28, N).astype(f32); y = rng.uniform(-20, 28, N).astype(f32)
@@ -18,7 +21,7 @@ def run(N=400000, seed=0):
     a = (cyy/det).astype(f32); b = (-cxy/det).astype(f32); cc = (cxx/det).astype(f32)
     o = rng.uniform(0.0, 1.0, N).astype(f32)
     # brute force over the 8x8 block at (0,0): any pixel with alpha >= 1/255 (float64 reference)
-    px, py = np.meshgrid(np.arange(8), np.arange(8))
+    px, py = np.meshgrid(np.arange(size), np.arange(size))
     px = px.ravel(); py = py.ravel()
     dx = x[:, None].astype(np.float64) - px; dy = y[:, None].astype(np.float64) - py
     power = -0.5*(a[:, None]*dx*dx + cc[:, None]*dy*dy) - b[:, None]*dx*dy
@@ -31,7 +34,7 @@ def run(N=400000, seed=0):
     thr = np.where(thr.astype(np.float64) < thr_exact, np.nextafter(thr, f32(np.inf)), thr).astype(f32)
     t = (np.maximum(f32(-1.3862944)*thr, f32(0)).astype(f32)*f32(1.002) + f32(2e-3)).astype(f32)
     kv = (-b/cc).astype(f32); ku = (-b/a).astype(f32)
-    u0 = (0 - x).astype(f32); u1 = u0 + f32(7); v0 = (0 - y).astype(f32); v1 = v0 + f32(7)
+    u0 = (0 - x).astype(f32); u1 = u0 + f32(e); v0 = (0 - y).astype(f32); v1 = v0 + f32(e)
     def qu(U):
         v = np.clip(kv*U, v0, v1); return U*(a*U + 2*b*v) + cc*v*v
     def qv(V):
@@ -46,8 +49,8 @@ def run(N=400000, seed=0):
     f64 = np.float64
     def fma32(p, q, r):
         return (p.astype(f64)*q.astype(f64) + r.astype(f64)).astype(f32)
-    bb = (b*b).astype(f32); e = fma32(-b, b, bb)
-    det = (fma32(a, cc, -bb) + e).astype(f32)
+    bb = (b*b).astype(f32); eb = fma32(-b, b, bb)
+    det = (fma32(a, cc, -bb) + eb).astype(f32)
     idet = (f32(1)/det).astype(f32); s_ia = (f32(1)/a).astype(f32)
     vmax = np.sqrt((a*t).astype(f32)*idet).astype(f32)
     s_nb = -b; s_det = det; s_at = (a*t).astype(f32)
@@ -66,6 +69,8 @@ def run(N=400000, seed=0):
 
 
 if __name__ == "__main__":
+    r4 = run(size=4)
+    print("4x4 sub-blocks, band form: missed (must be 0):", r4["band_missed"], " true:", r4["true"], " test:", r4["band_test"])
     r = run()
     print("missed (must be 0):", r["foot_missed"], " true:", r["true"], " test:", r["foot_test"])
     print("band form: missed (must be 0):", r["band_missed"], " test:", r["band_test"], " (foot form:", r["foot_test"], ")")

@@ -1,5 +1,6 @@
-"""Per-level clocks of k_upper_cut on bench.py's config5 scene (needs the HLGS_CUT_CLOCKS diagnostic build:
-python tools/build_variant.py CUTCLK --defs -DHLGS_CUT_CLOCKS; HLGS_LIBRARY=.../CUTCLK.so)."""
+"""Per-level clocks of k_upper_cut on bench.py's config5 scene (round 2-4 diagnostic: needs stream.hip with the
+HLGS_CUT_CLOCKS timer block, which round 5 removed from the product source -- `git show c236d54:hierarchical-lod-gaussians_amd/csrc/stream.hip`,
+built with tools/build_variant.py CUTCLK <that file> stream.hip after adding -DHLGS_CUT_CLOCKS; HLGS_LIBRARY=.../CUTCLK.so)."""
 import math, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "hierarchical-lod-gaussians_amd")]

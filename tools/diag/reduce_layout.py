@@ -1,6 +1,7 @@
-"""Lane-level simulation of the wave reduce-scatters in hlgs_math.h (wave_reduce10_rs, wave_reduce20_rs): DPP row_ror /
-quad_perm adds with bank masks and the gfx950 permlane32 / permlane16 swaps, on random per-lane values; prints which
-value's full 64-lane total every lane holds at the end (reduce10_index / reduce20_index are read off this).
+"""Lane-level simulation of the DPP reductions: hlgs_math.h row_reduce10 (the round-5 blend backward: ten values summed
+over each 16-lane row; row_reduce10_index is read off this), and the round-4 wave reduce-scatters (wave_reduce10_rs,
+wave_reduce20_rs, now in tools/variants/raster_bwd_r04.hip's header era): DPP row_ror / quad_perm adds with bank masks
+and the gfx950 permlane32 / permlane16 swaps, on random per-lane values; prints which value's total every lane holds.
 
     python tools/diag/reduce_layout.py
 """
@@ -65,3 +66,18 @@ r=check([w0,w1],X,None)
 print("20 w0:", [r[(0,l)] for l in range(0,64,4)])
 print("20 w1:", [r[(1,l)] for l in range(0,64,4)])
 print("all lanes of a bank agree:", all(r[(ri,l)]==r[(ri,l&~3)] for ri in (0,1) for l in range(64)))
+
+# row_reduce10: per 16-lane row
+V=10; X=rng.normal(size=(64,V))
+v=[X[:,i] for i in range(V)]
+s=[fold8(v[2*i],v[2*i+1]) for i in range(5)]
+t=[fold4(s[0],s[1]), fold4(s[2],s[3]), fold4(s[4],s[4])]
+for q in ([1,0,3,2],[2,3,0,1]): t=[quad(x,q) for x in t]
+ok=True
+for l in range(64):
+    row=l//16; tot=X[row*16:(row+1)*16].sum(0)
+    beta=(l>>2)&3
+    exp=[[0,2,1,3][beta],[4,6,5,7][beta],[8,8,9,9][beta]]
+    for ti in range(3):
+        ok &= abs(t[ti][l]-tot[exp[ti]])<1e-9
+print("row_reduce10 layout as row_reduce10_index says:", ok)

@@ -1,0 +1,7 @@
+# round 5: full -m gpu suite on the in-tree build, then rocprof A/B of the listed variants (C = in-tree)
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r5a.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_r5a.log
+[ $rc -eq 0 ] || [ "${CONTINUE_ON_FAIL:-0}" = 1 ] || exit $rc
+SKIP_TESTS=1 VARIANTS="${VARIANTS:-r04 C}" bash tools/ab_prof.sh

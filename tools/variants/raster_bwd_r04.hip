@@ -1,0 +1,698 @@
+// Round-4 blend backward (wave-wide 8x8 quadrant passes, one wave reduce-scatter per visited splat) with every
+// measured variant switch of rounds 1-4, kept outside the product source for A/B builds:
+//   python tools/build_variant.py r04 tools/variants/raster_bwd_r04.hip raster_bwd.hip
+// DESIGN.md section 5 records the result of each switch.  The wave reduce-scatters it uses are defined below.
+// raster_bwd.hip -- the blend backward for gfx950 (the per-Gaussian kernels are in gauss_bwd.hip).
+//
+// Reference semantics (submodules/hierarchy-rasterizer/cuda_rasterizer):
+//   k_blend_bwd  <- renderCUDA<3> backward      backward.cu:498-721
+//
+// The reference issues one global float atomic per (pixel, Gaussian, gradient component)
+// (backward.cu:669-718).  Here each wave owns one tile: every lane folds its four pixels, a
+// permlane/DPP reduce-scatter folds the 64 lanes, and the per-(tile, Gaussian) partial is stored once -- with
+// a plain store -- into a Gaussian-major record slot (the Gaussian's point_offsets range, indexed by
+// the tile's position inside its rect).  k_gauss_bwd then sums each Gaussian's contiguous records
+// in a fixed order, so the backward has no float atomics and is bitwise reproducible.
+#include "hlgs_internal.h"
+#include "hlgs_math.h"
+
+#ifndef HLGS_BWD_ZERO_LDS
+#define HLGS_BWD_ZERO_LDS 1  // accumulators zeroed by LDS reads, not v_mov_b64 (the VALU pipe is the limit)
+#endif
+#ifndef HLGS_BWD_OPQ
+#define HLGS_BWD_OPQ 0  // 1: the 0.99-clamp factor only for splats whose opacity exceeds 0.99f (a uniform branch per
+                        // pass: 358.8-359.1 against 356.4-356.8 us without it; not kept)
+#endif
+#ifndef HLGS_BWD_PK
+#define HLGS_BWD_PK 0  // packed-FP32 moment updates (v_pk_mul / v_pk_add / v_pk_fma on moment pairs)
+#endif
+
+namespace hlgs {
+
+// Reduce-scatter of ten per-lane values over the wave, cheapest stages first (issue costs measured by
+// tools/issue_probe.hip: a DPP add 4.2 cycles per wave instruction, a permlane swap 8.3).  Each fold halves the number
+// of registers: within each 16-lane row, bank-masked DPP adds fold lanes l and l^8 (values 2i into lanes 0-7, 2i+1 into
+// lanes 8-15), then l and l^4 (per 4-lane bank); permlane32 / permlane16 swaps fold the halves and the row pairs; a
+// quad_perm full reduction finishes each bank.  18 DPP + 3 permlane swaps, where ten full-wave reductions take
+// 12 DPP + 8 permlane swaps.  (row_ror:n: lane l reads lane l - n of its row.)  The result w holds, in every lane of
+// row rho and bank beta (lane = 16 rho + 4 beta + i), the total of value reduce10_index(rho, beta), or nothing for
+// rho = 3.
+__device__ __forceinline__ int reduce10_index(int rho, int beta)
+{
+    const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
+    return rho == 0 ? cb : rho == 2 ? 4 + cb : rho == 1 ? ((beta & 1) ? -1 : 8 + (beta >> 1)) : -1;
+}
+// One instruction stream, ordered so that every DPP / permlane-swap source was written at least two instructions
+// earlier where the sequence allows it (the gfx950 VALU-write -> DPP-read and -> permlane-swap-read hazards need two
+// wait states): 4 s_nop where the builtin-and-asm version took 7.
+__device__ __forceinline__ float wave_reduce10_rs(const float (&v)[10])
+{
+    float s0, s1, s2, s3, s4, t0, t1, t2, z, w;
+#define HLGS_FOLD8(d, a, b)                                                                                        \
+    "v_add_f32_dpp " d ", " a ", " a " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
+    "v_add_f32_dpp " d ", " b ", " b " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+#define HLGS_FOLD4(d, a, b)                                                                                        \
+    "v_add_f32_dpp " d ", " a ", " a " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
+    "v_add_f32_dpp " d ", " b ", " b " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
+    asm volatile("s_nop 0\n\t"
+                 "v_mov_b32 %8, 0\n\t"
+                 HLGS_FOLD8("%0", "%10", "%11") HLGS_FOLD8("%1", "%12", "%13") HLGS_FOLD8("%2", "%14", "%15")
+                 HLGS_FOLD8("%3", "%16", "%17") HLGS_FOLD8("%4", "%18", "%19")
+                 HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%7", "%4", "%4")
+                 "v_permlane32_swap_b32 %5, %6\n\t"   // t0 (written two instructions back), t1
+                 "v_add_f32 %5, %5, %6\n\t"           // rows 0-1: t0, rows 2-3: t1
+                 "v_permlane32_swap_b32 %7, %8\n\t"   // t2 (two back), 0
+                 "v_add_f32 %7, %7, %8\n\t"           // rows 0-1: t2, rows 2-3: 0
+                 "s_nop 1\n\t"
+                 "v_permlane16_swap_b32 %5, %7\n\t"
+                 "v_add_f32 %9, %5, %7\n\t"           // row 0: t0, row 1: t2, row 2: t1, row 3: 0
+                 "s_nop 1\n\t"
+                 "v_add_f32_dpp %9, %9, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\t"
+                 "v_add_f32_dpp %9, %9, %9 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(z),
+                   "=&v"(w)
+                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]),
+                   "v"(v[9]));
+#undef HLGS_FOLD8
+#undef HLGS_FOLD4
+    return w;
+}
+
+// Reduce-scatter of two splats' ten moments each (a = values 0-9, b = values 10-19) in one pass: FOLD8 of the ten
+// pairs, FOLD4 of five, permlane32 swaps fold 5 -> 3, permlane16 swaps 3 -> 2, quad_perm adds finish both.  34 DPP adds,
+// 5 permlane swaps and 5 adds, where two wave_reduce10_rs take 36, 6 and 6 (and 8 s_nop).  Every lane of row rho, bank
+// beta ends with the total of value reduce20_index(rho, beta, 0) in w0 and of reduce20_index(rho, beta, 1) in w1
+// (-1: none); the mapping was derived by simulating the lane operations (tools/diag/reduce_layout.py).
+__device__ __forceinline__ int reduce20_index(int rho, int beta, int reg)
+{
+    const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
+    if (reg == 1) return rho == 0 ? 16 + cb : -1;
+    return rho == 0 ? cb : rho == 1 ? 8 + cb : rho == 2 ? 4 + cb : 12 + cb;
+}
+__device__ __forceinline__ void wave_reduce20_rs(const float (&a)[10], const float (&b)[10], float& w0, float& w1)
+{
+    float s[10], t[5], z, z2;
+#define HLGS_FOLD8(d, x, y)                                                                                        \
+    "v_add_f32_dpp " d ", " x ", " x " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
+    "v_add_f32_dpp " d ", " y ", " y " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+#define HLGS_FOLD4(d, x, y)                                                                                        \
+    "v_add_f32_dpp " d ", " x ", " x " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
+    "v_add_f32_dpp " d ", " y ", " y " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
+    asm volatile("s_nop 1\n\t"
+                 HLGS_FOLD8("%0", "%19", "%20") HLGS_FOLD8("%1", "%21", "%22") HLGS_FOLD8("%2", "%23", "%24")
+                 HLGS_FOLD8("%3", "%25", "%26") HLGS_FOLD8("%4", "%27", "%28") HLGS_FOLD8("%5", "%29", "%30")
+                 HLGS_FOLD8("%6", "%31", "%32") HLGS_FOLD8("%7", "%33", "%34") HLGS_FOLD8("%8", "%35", "%36")
+                 HLGS_FOLD8("%9", "%37", "%38")
+                 "v_mov_b32 %15, 0\n\t"
+                 "v_mov_b32 %16, 0\n\t"
+                 HLGS_FOLD4("%10", "%0", "%1") HLGS_FOLD4("%11", "%2", "%3") HLGS_FOLD4("%12", "%4", "%5")
+                 HLGS_FOLD4("%13", "%6", "%7") HLGS_FOLD4("%14", "%8", "%9")
+                 "v_permlane32_swap_b32 %10, %11\n\t"  // t1 written six instructions back
+                 "v_add_f32 %10, %10, %11\n\t"         // rows 0-1: t0, rows 2-3: t1
+                 "v_permlane32_swap_b32 %12, %13\n\t"
+                 "v_add_f32 %12, %12, %13\n\t"         // rows 0-1: t2, rows 2-3: t3
+                 "v_permlane32_swap_b32 %14, %15\n\t"
+                 "v_add_f32 %14, %14, %15\n\t"         // rows 0-1: t4, rows 2-3: 0
+                 "v_permlane16_swap_b32 %10, %12\n\t"  // t2 written two instructions back
+                 "v_add_f32 %17, %10, %12\n\t"         // rows: t0, t2, t1, t3
+                 "v_permlane16_swap_b32 %14, %16\n\t"
+                 "v_add_f32 %18, %14, %16\n\t"         // row 0: t4
+                 "v_add_f32_dpp %17, %17, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 0\n\t"
+                 "v_add_f32_dpp %18, %18, %18 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "v_add_f32_dpp %17, %17, %17 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 0\n\t"
+                 "v_add_f32_dpp %18, %18, %18 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                 : "=&v"(s[0]), "=&v"(s[1]), "=&v"(s[2]), "=&v"(s[3]), "=&v"(s[4]), "=&v"(s[5]), "=&v"(s[6]),
+                   "=&v"(s[7]), "=&v"(s[8]), "=&v"(s[9]), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]),
+                   "=&v"(t[4]), "=&v"(z), "=&v"(z2), "=&v"(w0), "=&v"(w1)
+                 : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
+                   "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]),
+                   "v"(b[8]), "v"(b[9]));
+#undef HLGS_FOLD8
+#undef HLGS_FOLD4
+}
+
+
+// Per-pixel state of the back-to-front replay (backward.cu:549-572).  The reference keeps the
+// accumulated colour/inverse-depth behind the current splat and the previous splat's alpha and colour
+// (accum_rec, last_alpha, last_color) only to form dL/dalpha = <c - accum, dL/dpixel>, which is linear
+// in the accumulators; so one scalar ARD = <accum, dL/dpixel> (+ depth term), updated by the current
+// splat once its own step is done, carries the same information.
+//
+// The background term of dL/dalpha, -T_final <bg, dL/dpixel> / (1 - alpha) (backward.cu:688-691), rides along in ARD:
+// with ARD' = ARD + T_final <bg, dL/dpixel> / T_behind (T_behind = transmittance behind the current splat), the
+// recursion is unchanged (T_final bgd / T_i = (1 - alpha_i) T_final bgd / T_behind) and dL/dalpha = T (cd - ARD'),
+// so the step needs no product with 1/(1 - alpha) beyond the transmittance update.
+struct PixB {
+    float T;                 // transmittance in front of the current splat
+    float ARD;               // <accum_rec, dL/dpixel> + accum_invdepth * dL/dinvdepth + T_final <bg, dL/dpixel> / T_behind
+    float dr, dg, db, dinv;  // dL/dpixel, dL/dinvdepth
+    uint32_t last;           // n_contrib
+};
+
+// 1 if o G <= 0.99, else 0: the reference's dL/dalpha = 0 above the alpha clamp (backward.cu:619, 693) as a factor.
+// fma(-2^40, ta, 2^40 next(0.99f)) is exactly 2^40 (next(0.99f) - ta) for ta near 0.99f (both operands scaled by a
+// power of two), so it is >= 2^16 (one ulp of 0.99f, scaled) for ta <= 0.99f and <= 0 for ta > 0.99f; the clamp makes
+// it 1 or 0 (NaN -> 0).  2^40 next(0.99f) = 1088516587520 is exact in float32 (tests/test_gpu_parity.py::
+// test_alpha_clamp_threshold_exact checks prev(0.99f), 0.99f, next(0.99f) and next(next(0.99f))).
+__device__ __forceinline__ float below_clamp(float test_alpha)
+{
+    return __builtin_amdgcn_fmed3f(fmaf(-1099511627776.0f, test_alpha, 1088516587520.0f), 0.f, 1.f);
+}
+
+// 1/(1 - alpha) for alpha in [0, 0.99].  HLGS_BWD_RCP_NR > 0: that many Newton steps from the bit-pattern seed
+// instead of v_rcp_f32 (A/B of the transcendental's issue cost, tools/valu_probe.hip).
+#ifndef HLGS_BWD_HOIST
+#define HLGS_BWD_HOIST 1
+#endif
+#ifndef HLGS_BWD_RCP_NR
+#define HLGS_BWD_RCP_NR 0
+#endif
+__device__ __forceinline__ float rcp_one_minus(float alpha)
+{
+    const float d = 1.f - alpha;
+#if HLGS_BWD_RCP_NR > 0
+    float r = __int_as_float(0x7EF311C3 - __float_as_int(d));
+#pragma unroll
+    for (int i = 0; i < HLGS_BWD_RCP_NR; i++) r = r * fmaf(-d, r, 2.f);
+    return r;
+#else
+    return __builtin_amdgcn_rcpf(d);
+#endif
+}
+
+// One (pixel, splat) step of renderCUDA backward (backward.cu:601-718).  The splat's gradient terms
+// are linear in w = G * dL/dalpha and its moments over the pixels,
+//   dL/dmean2D = -o * (conic * [Sum w dx, Sum w dy]) * (W/2, H/2),
+//   dL/dconic  = -o/2 * [Sum w dx^2, Sum w dx dy, Sum w dy^2],   dL/dopacity = Sum w (x mult if lerped),
+// so each pixel adds ten moments to acc and finish_record() applies the per-splat factors once.
+//   acc = [Sum w dx, Sum w dy, Sum w dx^2, Sum w dx dy, Sum w dy^2, Sum w*mult, dcolor r g b, dinvdepth]
+// q = (-a/2, -b, -c/2) * log2(e) so that G = exp2(q0 dx^2 + q1 dx dy + q2 dy^2) = exp(power).
+// ALT: the alt rasterizer's backward (alt-rasterizer/cuda_rasterizer/backward.cu:596-624) has no
+// o * G > 0.99 => dL/dalpha = 0 rule; its doubled background term is folded into ARD by the caller.
+//
+// The pair step in two halves.  The front (falloff, alpha, 1/(1 - alpha), the threshold tests) depends on the pair
+// alone; the back (transmittance, ARD and the moments) on the pixel's replay state.
+struct BwdFront {
+    float G, alpha, r1m, my_alpha, dx, dy;
+    uint64_t ok;  // wave mask: alpha >= 1/255 (alpha_e2_threshold)
+};
+
+// clampable: wave-uniform, the splat's opacity exceeds 0.99f.  Otherwise o G <= o <= 0.99f for every kept pair
+// (G = exp2(e2) <= 1 for e2 <= 0), below_clamp is 1, and the two VALU it costs per pass are skipped (HLGS_BWD_OPQ).
+template <bool INTERP, bool ALT>
+__device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& q, float tt, float fr, float thr,
+                                              bool clampable = true)
+{
+    BwdFront f;
+    f.dx = dx;
+    f.dy = dy;
+    const float e2 = splat_e2(q, dx, dy);  // power * log2(e)
+    float G = __builtin_amdgcn_exp2f(e2);
+    const float test_alpha = q.w * G;
+#if HLGS_BWD_OPQ
+    // min(0.99f, o G) as one v_min_f32 (fminf across the clamp branch below otherwise gets a canonicalising v_max)
+    asm("v_min_f32 %0, 0x3f7d70a4, %1" : "=v"(f.my_alpha) : "v"(test_alpha));
+#else
+    f.my_alpha = fminf(0.99f, test_alpha);
+#endif
+    f.alpha = f.my_alpha;
+    if (INTERP) f.alpha = tt * f.my_alpha + (1.0f - tt) * (1.0f - powf(1.0f - f.my_alpha, fr));
+    f.r1m = rcp_one_minus(f.alpha);
+    if (!ALT && clampable) {
+        float b = below_clamp(test_alpha);
+        asm volatile("" : "+v"(b));  // not speculatable: a scalar branch around two VALU, not a select after them
+        G *= b;
+    }
+    f.G = G;
+    // as wave masks: one v_cmp per test, combined in SALU (the wave is full)
+    f.ok = ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < thr);
+    return f;
+}
+
+template <bool INTERP, bool DEPTH>
+__device__ __forceinline__ void bwd_back(PixB& p, uint32_t li, const BwdFront& f, const float4& col, float invz, float tt,
+                                         float fr, float (&acc)[10])
+{
+    const uint64_t valid = __builtin_amdgcn_ballot_w64(li < p.last) & f.ok;
+    if (__builtin_amdgcn_inverse_ballot_w64(valid)) {
+        const float alpha = f.alpha, dx = f.dx, dy = f.dy;
+        p.T = p.T * f.r1m;
+        const float weight = alpha * p.T;
+        // <colour, dL/dpixel> stays uncontracted: it feeds dL/dalpha and through it the ill-conditioned conic ->
+        // scale / rotation chain, where contracting it moved the GPU further from the oracle than the oracle's own
+        // contracted build is (tests/test_gpu_configs.py).  The colour / depth moments feed only dL/dcolour and
+        // dL/ddepth and are contracted (four VALU fewer per pass).
+        float cd = col.x * p.dr + col.y * p.dg + col.z * p.db;
+        if (DEPTH) cd += invz * p.dinv;
+        const float raw = cd - p.ARD;
+        p.ARD = fmaf(alpha, raw, p.ARD);
+#if HLGS_BWD_PK
+        if (!INTERP && DEPTH) {
+            typedef float v2f __attribute__((ext_vector_type(2)));
+            v2f a67 = {acc[6], acc[7]}, a89 = {acc[8], acc[9]};
+            a67 = __builtin_elementwise_fma(v2f{weight, weight}, v2f{p.dr, p.dg}, a67);
+            a89 = __builtin_elementwise_fma(v2f{weight, weight}, v2f{p.db, p.dinv}, a89);
+            acc[6] = a67.x; acc[7] = a67.y; acc[8] = a89.x; acc[9] = a89.y;
+        } else
+#endif
+        {
+            acc[6] = fmaf(weight, p.dr, acc[6]);
+            acc[7] = fmaf(weight, p.dg, acc[7]);
+            acc[8] = fmaf(weight, p.db, acc[8]);
+            if (DEPTH) acc[9] = fmaf(weight, p.dinv, acc[9]);
+        }
+        const float dL_dalpha = raw * p.T;
+        const float w = f.G * dL_dalpha;
+#if HLGS_BWD_PK
+        if (!INTERP) {  // the same IEEE products and sums, two per instruction
+            typedef float v2f __attribute__((ext_vector_type(2)));
+            const v2f dxy = {dx, dy};
+            const v2f wd = v2f{w, w} * dxy;
+            v2f a01 = {acc[0], acc[1]}, a23 = {acc[2], acc[3]};
+            a01 += wd;
+            a23 = __builtin_elementwise_fma(v2f{wd.x, wd.x}, dxy, a23);
+            acc[0] = a01.x; acc[1] = a01.y; acc[2] = a23.x; acc[3] = a23.y;
+            acc[4] = fmaf(wd.y, dy, acc[4]);
+            acc[5] += w;
+            return;
+        }
+#endif
+        const float wdx = w * dx, wdy = w * dy;
+        acc[0] += wdx;
+        acc[1] += wdy;
+        acc[2] = fmaf(wdx, dx, acc[2]);
+        acc[3] = fmaf(wdx, dy, acc[3]);
+        acc[4] = fmaf(wdy, dy, acc[4]);
+        if (INTERP) acc[5] += (tt - powf(1.0f - f.my_alpha, fr - 1.0f) * (tt - 1.0f) * fr) * w;
+        else acc[5] += w;
+    }
+}
+
+// One quadrant pass: the front is computed for every lane ahead of the validity branch (HLGS_BWD_HOIST), so its
+// transcendental latency overlaps the compare -> SALU -> exec chain that decides the branch instead of following it.
+template <bool INTERP, bool DEPTH, bool ALT, int K>
+__device__ __forceinline__ void bwd_pass(PixB (&ps)[4], uint32_t li, float lx, float ly, const float4& xy, const float4& q,
+                                         const float4& col, float2 tf, float (&acc)[10], bool clampable)
+{
+    BwdFront f = bwd_front<INTERP, ALT>(xy.x - (lx + 8.f * (K & 1)), xy.y - (ly + 8.f * (K >> 1)), q, tf.x, tf.y, col.w,
+                                        clampable);
+#if HLGS_BWD_HOIST
+    asm volatile("" : "+v"(f.G), "+v"(f.r1m), "+v"(f.alpha));  // keep them above the branch
+#endif
+    bwd_back<INTERP, DEPTH>(ps[K], li, f, col, xy.z, tf.x, tf.y, acc);
+}
+
+// Per-splat record from the reduced moments (see bwd_back); co = conic and opacity of the splat.
+__device__ __forceinline__ void finish_record(const float* m, float4 co, float ddelx_dx, float ddely_dy, float4& ra,
+                                              float4& rb, float2& rc)
+{
+    const float o = co.w;
+    ra.x = -o * (co.x * m[0] + co.y * m[1]) * ddelx_dx;
+    ra.y = -o * (co.z * m[1] + co.y * m[0]) * ddely_dy;
+    ra.z = -0.5f * o * m[2];
+    ra.w = -0.5f * o * m[3];
+    rb.x = -0.5f * o * m[4];
+    rb.y = m[5];
+    rb.z = m[6];
+    rb.w = m[7];
+    rc.x = m[8];
+    rc.y = m[9];
+}
+
+struct BwdArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    int W, H, gx, gy, T;
+    Geom g;
+    const float* final_Ts;
+    const uint32_t* n_contrib;
+    const float* split_state;
+    const float* bg;
+    const float* dL_dpixels;
+    const float* dL_dinvdepths;
+    BwdScratch rec;
+    const uint32_t* misc;  // Img::misc of the forward: [kMiscPack] says whether its point_list entries are packed
+};
+
+// One wave per (tile, chunk of the tile's list), back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8
+// quadrant.  Chunk c covers list entries [c clen, min(count, (c + 1) clen)) (bwd_chunk_len); blocks are ordered
+// chunk-major, so the front chunks, where most pixels are still live, start first.  A pixel whose last contributor
+// lies behind the chunk's end starts from the forward's sample there (transmittance, and what was blended behind
+// it), otherwise from its final state, as the reference's single back-to-front pass has it at that point.  Each
+// 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
+// whose n_contrib lies behind it) run bwd_pass, the ten moments are folded over the wave, and one record per
+// (tile, splat) is stored after the batch.
+// Traffic-attribution switches (tools/ab_fetch.sh, timing and counters only; each breaks parity): skip the
+// point_offsets gather, the per-pixel inputs, the split-state reads, or the record stores.
+#ifndef HLGS_BWD_NT_LOAD
+#define HLGS_BWD_NT_LOAD 0
+#endif
+#ifndef HLGS_BWD_NT_STORE
+#define HLGS_BWD_NT_STORE 0
+#endif
+#ifndef HLGS_DIAG_BWD_FAKE_SBASE
+#define HLGS_DIAG_BWD_FAKE_SBASE 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_GATHER
+#define HLGS_DIAG_BWD_NO_GATHER 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_PIXIN
+#define HLGS_DIAG_BWD_NO_PIXIN 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_SPLIT
+#define HLGS_DIAG_BWD_NO_SPLIT 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_STORE
+#define HLGS_DIAG_BWD_NO_STORE 0
+#endif
+#ifndef HLGS_DIAG_BWD_NO_ZERO
+#define HLGS_DIAG_BWD_NO_ZERO 0
+#endif
+#ifndef HLGS_BWD_PAIR
+#define HLGS_BWD_PAIR 0  // two visited splats per loop iteration, one twenty-moment reduction (wave_reduce20_rs)
+#endif
+#ifndef HLGS_BWD_TILE_MAJOR
+#define HLGS_BWD_TILE_MAJOR 0  // 0: chunk-major (the front chunks, where most pixels are live, start first)
+#endif
+#ifndef HLGS_BWD_MSTRIDE
+#define HLGS_BWD_MSTRIDE 65
+#endif
+#ifndef HLGS_BWD_WAVES
+#define HLGS_BWD_WAVES 5  // waves per SIMD: 96 VGPRs
+#endif
+template <bool INTERP, bool DEPTH, bool ALT>
+__global__ void __launch_bounds__(64, HLGS_BWD_WAVES) k_blend_bwd(BwdArgs A)
+{
+#if HLGS_BWD_TILE_MAJOR
+    // a tile's chunk waves next to each other in dispatch order and on one XCD, so the second and third read of the
+    // tile's per-pixel inputs hit that XCD's L2
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = L / (kBwdSplits + 1), part = L - tile * (kBwdSplits + 1);
+#else
+    const int part = blockIdx.x / A.T;
+    const int tile = xcd_remap(blockIdx.x - part * A.T, A.T);
+#endif
+    const uint2* __restrict__ ranges = A.ranges;
+    const uint32_t* __restrict__ point_list = A.point_list;
+    const int W = A.W, H = A.H, gx = A.gx;
+    const Geom& g = A.g;
+    const float* __restrict__ final_Ts = A.final_Ts;
+    const uint32_t* __restrict__ n_contrib = A.n_contrib;
+    const float* __restrict__ bg = A.bg;
+    const float* __restrict__ dL_dpixels = A.dL_dpixels;
+    const float* __restrict__ dL_dinvdepths = A.dL_dinvdepths;
+    const BwdScratch& rec = A.rec;
+    const uint32_t pack = __builtin_amdgcn_readfirstlane(A.misc[kMiscPack]);  // as the forward packed them
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, unused
+    __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
+    __shared__ float4 s_col[64];  // r, g, b, alpha threshold on e2
+    __shared__ float2 s_tf[64];   // interpolation t, 1/kids
+    // reduced moments per splat (+ a spare row the non-storing lanes write), rows padded to kMStride = 65 floats: the
+    // ten lanes holding totals store moment v of splat j at kMStride v + j, on ten different banks ((v + j) mod 32),
+    // where a 64-float stride put all ten (and the spare row) on bank j mod 32
+    constexpr int kMStride = HLGS_BWD_MSTRIDE;
+    __shared__ float s_m[kMStride * 11];
+#if HLGS_BWD_ZERO_LDS
+    __shared__ float4 s_zero[3];
+    if (threadIdx.x < 3) s_zero[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);  // ordered by the batch barrier
+#endif
+    const int lane = threadIdx.x;
+    const int tx = tile % gx, ty = tile / gx;
+    const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
+    const uint2 range = ranges[tile];
+    const uint32_t count = range.y - range.x;
+    const uint32_t clen = bwd_chunk_len(count);
+    const uint32_t c0 = (uint32_t)part * clen;  // chunk = local list positions [c0, cnt)
+    if (c0 >= count) return;
+    const uint32_t cnt = min(count, c0 + clen);
+    const float* __restrict__ st =
+        cnt < count ? A.split_state + (size_t)(tile * kBwdSplits + part) * kSplitFloats + lane : nullptr;
+    const size_t HW = (size_t)H * W;
+    const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+    const float lx = (float)(tx0 + (lane & 7)), ly = (float)(ty0 + (lane >> 3));
+    // the reduced moment this lane stores (wave_reduce10_rs layout) as an offset into s_m; lanes holding no total
+    // store into the spare row s_m[10 kMStride ..]
+    const int wm_i = (lane & 3) ? -1 : reduce10_index(lane >> 4, (lane >> 2) & 3);
+    const int wmd = wm_i < 0 ? 10 * kMStride : kMStride * wm_i;
+#if HLGS_BWD_PAIR
+    // wave_reduce20_rs layout: this lane's two totals, each a moment of the pair's first (A) or second (B) splat
+    int wmd0, wmd1;
+    bool w0b, w1b;
+    {
+        const int v0 = (lane & 3) ? -1 : reduce20_index(lane >> 4, (lane >> 2) & 3, 0);
+        const int v1 = (lane & 3) ? -1 : reduce20_index(lane >> 4, (lane >> 2) & 3, 1);
+        wmd0 = v0 < 0 ? 10 * kMStride : kMStride * (v0 % 10);
+        wmd1 = v1 < 0 ? 10 * kMStride : kMStride * (v1 % 10);
+        w0b = v0 >= 10;
+        w1b = v1 >= 10;
+    }
+#endif
+
+    // lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant k
+    PixB ps[4];
+    uint32_t qlast[4];  // wave-uniform per quadrant: furthest-back position any of its pixels needs
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int px = tx0 + 8 * (k & 1) + (lane & 7), py = ty0 + 8 * (k >> 1) + (lane >> 3);
+        const bool inside = px < W && py < H;
+        const size_t pid = (size_t)W * py + px;
+        PixB& p = ps[k];
+#if HLGS_DIAG_BWD_NO_PIXIN  // traffic attribution only (tools/ab_fetch.sh): no per-pixel input reads, parity broken
+        const float tf = inside ? 0.5f : 0.f;
+        p.T = tf;
+        p.last = inside ? count : 0u;
+        p.dr = p.dg = p.db = p.dinv = inside ? 0.1f : 0.f;
+#else
+        const float tf = inside ? final_Ts[pid] : 0.f;
+        p.T = tf;
+        p.last = inside ? n_contrib[pid] : 0u;
+        p.dr = inside ? dL_dpixels[pid] : 0.f;
+        p.dg = inside ? dL_dpixels[HW + pid] : 0.f;
+        p.db = inside ? dL_dpixels[2 * HW + pid] : 0.f;
+        p.dinv = (DEPTH && inside) ? dL_dinvdepths[pid] : 0.f;
+#endif
+        float bgd = 0.f;
+        bgd += bg[0] * p.dr;
+        bgd += bg[1] * p.dg;
+        bgd += bg[2] * p.db;
+        // the alt rasterizer's ar includes the final colour's T_final * bg and adds the bg term once more
+        // (alt-rasterizer backward.cu:608, 619): the background enters dL/dalpha twice
+        if (ALT) bgd *= 2.f;
+        p.ARD = bgd;  // T_final <bg, dL/dpixel> / T_final
+        if (p.last > cnt && !HLGS_DIAG_BWD_NO_SPLIT) {  // still blending at the chunk's end (so the forward sampled it there)
+            const float* sk = st + k * 5 * 64;
+            p.T = sk[0];
+            float behind = sk[64] * p.dr + sk[128] * p.dg + sk[192] * p.db;
+            if (DEPTH) behind += sk[256] * p.dinv;
+            p.ARD = fmaf(tf, bgd, behind) / p.T;  // <accum_rec, dL/dpixel> (+ depth, + bg term) at the chunk's end
+        }
+        uint32_t m = min(p.last, cnt);
+        for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        qlast[k] = __builtin_amdgcn_readfirstlane(m);
+    }
+    const uint32_t maxlast = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
+
+    for (uint32_t b0 = 0; b0 < cnt - c0; b0 += 64) {
+        // batch covers local positions cnt-1-b0 down to cnt-1-b0-(n-1), loaded back to front
+        const int n = (int)min(64u, cnt - c0 - b0);
+        const uint32_t li_top = cnt - 1 - b0;
+        const bool lane_valid = lane < n;
+        uint32_t slot = 0, qm = 0;
+        float4 my_co = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane_valid) {
+            const uint32_t pos = range.x + li_top - lane;
+            uint32_t id = point_list[pos], pm = 0;
+            if (pack) {  // packed entry (pack_entries): the quadrant mask comes with it
+                pm = id & ((1u << kEntryShift) - 1u);
+                id >>= kEntryShift;
+            }
+            const float4* sr = g.splat + 4 * (size_t)id;
+#if HLGS_DIAG_BWD_FAKE_SBASE  // traffic attribution: slots spread by id, no point_offsets gather (parity broken)
+            const uint32_t sbase = id;
+#else
+            const uint32_t sbase = (id && !HLGS_DIAG_BWD_NO_GATHER) ? g.point_offsets[id - 1] : 0u;
+#endif
+#if HLGS_BWD_NT_LOAD  // records streamed past L2 (no reuse across tile waves), so point_offsets stays resident
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            const v4f* srv = reinterpret_cast<const v4f*>(sr);
+            const v4f q0 = __builtin_nontemporal_load(srv), q1 = __builtin_nontemporal_load(srv + 1),
+                      q2 = __builtin_nontemporal_load(srv + 2), q3 = __builtin_nontemporal_load(srv + 3);
+            const float4 r0 = make_float4(q0.x, q0.y, q0.z, q0.w), r1 = make_float4(q1.x, q1.y, q1.z, q1.w),
+                         r2 = make_float4(q2.x, q2.y, q2.z, q2.w), r3 = make_float4(q3.x, q3.y, q3.z, q3.w);
+#else
+            const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
+#endif
+            const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
+            qm = pack ? pm : quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
+            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
+            s_q[lane] = conic_q(co);
+            my_co = co;
+            s_col[lane] = make_float4(r1.z, r1.w, r2.x, r3.w);
+            if (INTERP) s_tf[lane] = make_float2(r2.z, r2.w);
+            const int x0 = __float_as_int(r3.y) & 0xffff, y0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
+            const int w = __float_as_int(r3.z);
+            // the Gaussian's record slots start at the exclusive scan of the rect sizes (point_offsets is inclusive)
+            slot = sbase + (uint32_t)((ty - y0) * w + (tx - x0));
+        }
+#pragma unroll
+        for (int v = 0; v < 10; v++) s_m[kMStride * v + lane] = 0.f;
+        __syncthreads();
+        // a batch entirely behind every pixel's last contributor leaves its records zero
+        const uint32_t li_bot = li_top - (uint32_t)(n - 1);
+        if (li_bot < maxlast) {
+            // per quadrant, the wave-uniform set of the batch's splats to visit: footprint reaches the quadrant
+            // (quad_mask) and the splat lies in front of the quadrant's furthest contributor (li < qlast[k],
+            // i.e. j > li_top - qlast[k]); the loop then visits set bits only, with no LDS read to decide
+            uint64_t qv[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint64_t m = __ballot((qm >> k) & 1u);
+                if (li_top >= qlast[k]) {
+                    const uint32_t d = li_top - qlast[k];  // splats 0..d are behind every pixel of quadrant k
+                    m = d >= 63 ? 0ull : m & (~0ull << (d + 1));
+                }
+                qv[k] = m;
+            }
+            uint64_t todo = qv[0] | qv[1] | qv[2] | qv[3];
+            // the batch's splats whose opacity can reach the 0.99 clamp (bit j: splat j)
+            const uint64_t opq = __ballot(lane_valid && my_co.w > 0.99f);
+            // Splat loop with the least scalar bookkeeping: the visited bit is cleared (s_bitset0), the next visited
+            // splat found by s_ff1 (-1 once none is left; its LDS reads use index 0 then), and every visited splat
+            // is reduced (0.15% of them have no valid pair), so no per-pass wave-mask tracking.
+            if (todo) {
+                int j = __builtin_ctzll(todo);
+                float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
+                float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
+                // the quadrants splat jj visits, in quadrant order (uniform branches), into acc
+                auto passes = [&](int jj, const float4& pxy, const float4& pco, const float4& pcol, const float2& ptf,
+                                  float(&acc)[10]) {
+                    const uint32_t li = li_top - (uint32_t)jj;
+#if HLGS_BWD_ZERO_LDS
+                    // the ten accumulators zeroed by three LDS reads of a zero block (the LDS pipe, ~29% busy here)
+                    // instead of five v_mov_b64 on the VALU pipe, which this kernel saturates
+                    {
+                        typedef float v4f __attribute__((ext_vector_type(4)));
+                        typedef __attribute__((address_space(3))) const volatile v4f lds_v4f;  // stays a ds_read
+                        lds_v4f* vz = (lds_v4f*)(s_zero);
+                        const v4f z0 = vz[0], z1 = vz[1], z2 = vz[2];
+                        acc[0] = z0.x; acc[1] = z0.y; acc[2] = z0.z; acc[3] = z0.w;
+                        acc[4] = z1.x; acc[5] = z1.y; acc[6] = z1.z; acc[7] = z1.w;
+                        acc[8] = z2.x; acc[9] = z2.y;
+                    }
+#elif HLGS_DIAG_BWD_NO_ZERO  // timing only: accumulators not reset between splats (parity broken)
+#else
+#pragma unroll
+                    for (int v = 0; v < 10; v += 2) {  // five v_mov_b64 (the compiler otherwise copies zeros around)
+                        uint64_t z;
+                        asm volatile("v_mov_b64 %0, 0" : "=v"(z));
+                        acc[v] = __uint_as_float((uint32_t)z);
+                        acc[v + 1] = __uint_as_float((uint32_t)(z >> 32));
+                    }
+#endif
+                    // wave-uniform (scalar mask); the hierarchy-mode kernels keep the factor (no VGPRs for the branch)
+                    const bool clampable = !HLGS_BWD_OPQ || INTERP || ((opq >> jj) & 1u);
+                    if ((qv[0] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 0>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
+                    if ((qv[1] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 1>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
+                    if ((qv[2] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 2>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
+                    if ((qv[3] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 3>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc, clampable);
+                };
+#if HLGS_BWD_PAIR
+                // Two visited splats per iteration, their twenty moments folded by one reduce-scatter
+                // (wave_reduce20_rs): 34 DPP adds and 5 permlane swaps where two ten-moment reductions take 36 and 6
+                while (true) {
+                    int jn;  // s_ff1: -1 once todo is empty
+                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
+                    float accA[10];
+                    passes(j, xy, co, col, tf, accA);
+                    if (jn < 0) {
+                        s_m[wmd + j] = wave_reduce10_rs(accA);
+                        break;
+                    }
+                    float accB[10];
+                    {
+                        const float4 xyB = s_xy[jn], coB = s_q[jn], colB = s_col[jn];
+                        const float2 tfB = INTERP ? s_tf[jn] : make_float2(0.f, 0.f);
+                        int jn2;
+                        asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn2) : "s"(jn));
+                        passes(jn, xyB, coB, colB, tfB, accB);
+                        const int jl = jn2 < 0 ? 0 : jn2;  // the next pair's first splat, read ahead of the reduction
+                        xy = s_xy[jl];
+                        co = s_q[jl];
+                        col = s_col[jl];
+                        if (INTERP) tf = s_tf[jl];
+                        float w0, w1;
+                        wave_reduce20_rs(accA, accB, w0, w1);
+                        s_m[wmd0 + (w0b ? jn : j)] = w0;
+                        s_m[wmd1 + (w1b ? jn : j)] = w1;
+                        if (jn2 < 0) break;
+                        j = jn2;
+                    }
+                }
+#else
+                float acc[10];  // (reset by passes() for every splat)
+#if HLGS_DIAG_BWD_NO_ZERO
+                for (int v = 0; v < 10; v++) acc[v] = 0.f;
+#endif
+                while (true) {
+                    int jn;  // s_ff1: -1 once todo is empty
+                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
+                    passes(j, xy, co, col, tf, acc);
+                    const int jl = jn < 0 ? 0 : jn;  // the next visited splat's LDS reads ahead of the reduction
+                    xy = s_xy[jl];
+                    co = s_q[jl];
+                    col = s_col[jl];
+                    if (INTERP) tf = s_tf[jl];
+                    // every lane stores (the spare row takes the non-totals), so no exec-mask change
+                    s_m[wmd + j] = wave_reduce10_rs(acc);
+                    if (jn < 0) break;
+                    j = jn;
+                }
+#endif
+            }
+        }
+        __syncthreads();
+        if (lane_valid && !HLGS_DIAG_BWD_NO_STORE) {
+            float m[10];
+#pragma unroll
+            for (int v = 0; v < 10; v++) m[v] = s_m[kMStride * v + lane];
+            float4 ra, rb;
+            float2 rc;
+            finish_record(m, my_co, ddelx_dx, ddely_dy, ra, rb, rc);
+            float4* r = rec.rec + 3 * (size_t)slot;
+#if HLGS_BWD_NT_STORE
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            v4f* rv = reinterpret_cast<v4f*>(r);
+            __builtin_nontemporal_store(v4f{ra.x, ra.y, ra.z, ra.w}, rv);
+            __builtin_nontemporal_store(v4f{rb.x, rb.y, rb.z, rb.w}, rv + 1);
+            __builtin_nontemporal_store(v4f{rc.x, rc.y, 0.f, 0.f}, rv + 2);
+#else
+            r[0] = ra;
+            r[1] = rb;
+            r[2] = make_float4(rc.x, rc.y, 0.f, 0.f);
+#endif
+        }
+        __syncthreads();
+    }
+}
+
+
+
+void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, const BwdScratch& rs,
+                      int gx, int gy, const float* dL_dpix, const float* dL_dinv, hipStream_t s)
+{
+    const int T = gx * gy;
+    const bool interp = a.ts != nullptr && a.kids != nullptr;
+    BwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, gy, T, g, im.final_T, im.n_contrib, im.split_state, a.bg, dL_dpix,
+              dL_dinv, rs, im.misc};
+#define HLGS_BB(I, Dp, Al) hipLaunchKernelGGL((k_blend_bwd<I, Dp, Al>), dim3((kBwdSplits + 1) * T), dim3(64), 0, s, A)
+    if (a.variant == HLGS_VARIANT_ALT) { if (dL_dinv) HLGS_BB(false, true, true); else HLGS_BB(false, false, true); }
+    else if (interp) { if (dL_dinv) HLGS_BB(true, true, false); else HLGS_BB(true, false, false); }
+    else { if (dL_dinv) HLGS_BB(false, true, false); else HLGS_BB(false, false, false); }
+#undef HLGS_BB
+}
+
+
+}  // namespace hlgs

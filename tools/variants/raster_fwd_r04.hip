@@ -176,16 +176,17 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
         for (int y = y0; y < y1; y++)
             for (int x = x0; x < x1; x++, r++)
                 if ((!alt || alt_tile_keep(pix_x, pix_y, co, kthr, x, y)) &&
-                    !(g.drop && !rect_tile_mask(masks, r)))
+                    !(g.pack && HLGS_DROP_EMPTY && !rect_tile_mask(masks, r)))
                     atomicAdd(&tile_count[y * gx + x], 1u);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// Preprocess, common path (no hierarchy indices, SH coefficients given): k_preprocess_sh2 below.
-// The geometry is per thread as in k_preprocess; the block's SH rows are copied into LDS with all 64 lanes on
-// consecutive float4s, so the 192-byte SH rows (M = 16) stream from HBM in whole lines instead of 48 strided
-// 4-byte loads per thread.  Every per-Gaussian output is bit-identical to k_preprocess (same arithmetic, same order).
+// Preprocess, common path (no hierarchy indices, SH coefficients given): one wave per 64 Gaussians.
+// The geometry is per thread as in k_preprocess; then the rows of the Gaussians that survived culling
+// are compacted (ballot + mbcnt) and copied into LDS with all 64 lanes on consecutive float4s, so the
+// 192-byte SH rows (M = 16) stream from HBM in whole lines instead of 48 strided 4-byte loads per thread.
+// Every per-Gaussian output is bit-identical to k_preprocess (same arithmetic, same order).
 // ------------------------------------------------------------------------------------------------
 struct PreGeom {
     float pix_x, pix_y, depth, conic_x, conic_y, conic_z, h_scale, radius;
@@ -257,11 +258,74 @@ __device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const
     return (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0) != 0;
 }
 
-// Two waves per 64 Gaussians: wave 0 runs the geometry while wave 1 streams
+template <bool ALT, int M3T>
+__global__ void __launch_bounds__(64) k_preprocess_sh(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
+                                                      int gy, float fx, float fy, ZeroJob z)
+{
+    __shared__ float s_rows[64 * kShStride];
+    __shared__ int s_idx[64];
+    const int lane = threadIdx.x;
+    const int t_idx = blockIdx.x * 64 + lane;
+    zero_prelude(z, t_idx, gridDim.x * 64);
+    PreGeom o;
+    const bool need = t_idx < a.P && preprocess_geom<ALT>(a, g, radii, t_idx, gx, gy, fx, fy, o);
+    const uint64_t bal = __ballot(need);
+    if (bal == 0) return;  // wave-uniform: nothing of this block reaches the screen
+    const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    const int n = __popcll(bal);
+    if (need) s_idx[slot] = t_idx;
+    __syncthreads();
+    sh_rows_load<M3T>(a.shs, s_rows, s_idx, n, lane, 3 * a.M);
+    __syncthreads();
+    if (!need) return;
+    const float* row = s_rows + slot * kShStride;
+    const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+    const f3 mean_r = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
+    uint32_t cb = 0;
+    const float* d0 = ALT ? a.dc + 3 * (size_t)t_idx : nullptr;
+    auto shv = [&](int c) {
+        if (ALT) return c == 0 ? mk(d0[0], d0[1], d0[2]) : mk(row[3 * c - 3], row[3 * c - 2], row[3 * c - 1]);
+        return mk(row[3 * c], row[3 * c + 1], row[3 * c + 2]);
+    };
+    const f3 col = sh_to_rgb(a.D, shv, mean_r, campos, cb);
+    if (HLGS_SH_JAC) {  // d colour / d view direction for the SH backward (Geom::sh_jac), from the coefficients in LDS
+        const f3 d = sub(mean_r, campos);
+        const float len = sqrtf(dot(d, d));
+        f3 jx, jy, jz;
+        sh_dir_jacobian(a.D, shv, d.x / len, d.y / len, d.z / len, jx, jy, jz);
+        float* J = g.sh_jac + 9 * (size_t)t_idx;
+        J[0] = jx.x; J[1] = jx.y; J[2] = jx.z;
+        J[3] = jy.x; J[4] = jy.y; J[5] = jy.z;
+        J[6] = jz.x; J[7] = jz.y; J[8] = jz.z;
+    }
+    g.clamped[t_idx] = cb;
+    g.depths[t_idx] = o.depth;
+    radii[t_idx] = (int)o.radius;
+    g.means2D[t_idx] = make_float2(o.pix_x, o.pix_y);
+    const float opacity = a.opacities[t_idx];
+    g.tiles_touched[t_idx] = (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0);
+    const bool interp = a.ts && a.kids;
+    float4* rec = g.splat + 4 * (size_t)t_idx;
+    rec[0] = make_float4(o.pix_x, o.pix_y, o.conic_x, o.conic_y);
+    rec[1] = make_float4(o.conic_z, opacity * o.h_scale, col.x, col.y);
+    const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+    rec[2] = make_float4(col.z, 1.f / o.depth, tt, fr);
+    const float thr = alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr);
+    if (g.pack)
+        g.qmask[t_idx] = rect_quad_masks(o.pix_x, o.pix_y, make_float4(o.conic_x, o.conic_y, o.conic_z, opacity * o.h_scale),
+                                         thr, o.x0, o.y0, o.x1, o.y1);
+    rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
+}
+
+// The same preprocess with two waves per 64 Gaussians (HLGS_PRE_SPLIT): wave 0 runs the geometry while wave 1 streams
 // the block's 64 SH rows (contiguous in the AoS input, culled rows included) into LDS; after a barrier wave 1
 // evaluates the colour and the direction Jacobian from LDS while wave 0 classifies the footprint quadrants, and
 // after a second barrier wave 0 writes the records.  The SH rows' HBM latency overlaps the geometry instead of
 // following it, and one 12.5 KB LDS stage now keeps two waves busy.  Same arithmetic, same outputs.
+#ifndef HLGS_PRE_SPLIT
+#define HLGS_PRE_SPLIT 1
+#endif
 template <int M3T>
 __device__ __forceinline__ void sh_rows_load_contig(const float* gbase, float* lds, int n, int lane, int m3)
 {
@@ -291,8 +355,16 @@ __device__ __forceinline__ void sh_rows_load_contig(const float* gbase, float* l
     }
 }
 
+#ifndef HLGS_PRE_WAVES
+#define HLGS_PRE_WAVES 0  // > 0: ask for that many waves per SIMD (a VGPR cap; 102 VGPRs give 4; measured no gain)
+#endif
+#if HLGS_PRE_WAVES > 0
+#define HLGS_PRE_BOUNDS __launch_bounds__(128, HLGS_PRE_WAVES)
+#else
+#define HLGS_PRE_BOUNDS __launch_bounds__(128)
+#endif
 template <bool ALT, int M3T>
-__global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
+__global__ void HLGS_PRE_BOUNDS k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
                                                         int gy, float fx, float fy, ZeroJob z)
 {
     __shared__ float s_rows[64 * kShStride];
@@ -326,7 +398,7 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
             uint32_t cb = 0;
             const f3 col = sh_to_rgb(a.D, shv, mean_r, campos, cb);
             s_col[lane] = make_float4(col.x, col.y, col.z, __uint_as_float(cb));
-            {  // d colour / d view direction for the SH backward (Geom::sh_jac), from the coefficients in LDS
+            if (HLGS_SH_JAC) {
                 const f3 d = sub(mean_r, campos);
                 const float len = sqrtf(dot(d, d));
                 f3 jx, jy, jz;
@@ -513,30 +585,27 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
 
 // hist != nullptr (bin_histogram): the block's per-tile counts are stored as row blockIdx.x of hist (coalesced), and
 // k_tile_offsets turns the rows into per-(block, tile) offsets and tile totals; otherwise they are added to
-// tile_count with one device atomic per non-empty tile.  zero_words: k_tile_offsets_plan's look-back words and the
-// plan's failure / completion words (misc[kMiscFail], misc[kMiscDone]), cleared by block 0 for this frame.
-template <int BG, bool DROP>
+// tile_count with one device atomic per non-empty tile.  SUPER: the bins are super-tiles of kSuperTiles consecutive
+// tiles (the two-level binning, k_supertile_sort), not tiles.
+template <int BG, bool DROP, bool SUPER>
 __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
                                                              uint32_t* __restrict__ tile_count, int gx, int gy, int alt,
                                                              uint32_t* __restrict__ block_tot, uint32_t* __restrict__ hist,
-                                                             uint32_t* __restrict__ zero_words, int n_zero,
-                                                             uint32_t* __restrict__ misc)
+                                                             uint32_t* __restrict__ zero_words, int n_zero)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_pre[BG + 1];
     __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
-    const int T = gx * gy;
+    const int T = SUPER ? super_tiles(gx * gy) : gx * gy;  // bins
     for (int t = threadIdx.x; t < T; t += (BG / 4)) s_hist[t] = 0;
     if (threadIdx.x == 0) s_w[(BG / 4) / 64] = 0;
     __syncthreads();
     block_rect_prefix<BG>(P, g, s_pre, s_w);
     if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[BG];
-    if (zero_words && blockIdx.x == 0) {  // k_tile_offsets_plan's look-back words, failure and completion words
+    if (zero_words && blockIdx.x == 0)  // k_tile_offsets_plan's look-back words
         for (int i = threadIdx.x; i < n_zero; i += BG / 4) zero_words[i] = 0u;
-        if (threadIdx.x == 0) { misc[kMiscFail] = 0u; misc[kMiscDone] = 0u; }
-    }
     for_each_instance<BG, false, DROP>(g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t qm, uint32_t) {
-        if (!DROP || qm) atomicAdd(&s_hist[y * gx + x], 1u);
+        if (!DROP || qm) atomicAdd(&s_hist[SUPER ? (y * gx + x) / kSuperTiles : y * gx + x], 1u);
     });
     __syncthreads();
     if (hist) {
@@ -550,20 +619,25 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     }
 }
 
-// A tile segment holds the count blocks' runs in XCD-grouped block order (xcd_unmap), not in block order,
+// HLGS_XCD_RUNS: a tile segment holds the count blocks' runs in XCD-grouped block order (xcd_unmap), not in block order,
 // so that the runs next to each other in memory are written by scatter blocks of the same XCD (workgroups go to XCDs
 // round robin): their partial lines meet in that XCD's L2 and leave it whole, instead of as partial lines from eight
 // L2s.  The order inside a segment is free (k_tile_sort orders it).
+#ifndef HLGS_XCD_RUNS
+#define HLGS_XCD_RUNS 1
+#endif
 // The histogram rows of logical positions i, i + 1, ... in that order, stepped without a division per row.
 struct HistRows {
     int i, x, k, q, r;
     __device__ HistRows(int i0, int nb) : i(i0), x(0), k(0), q(nb / 8), r(nb % 8)
     {
-        const int b = xcd_unmap(i0, nb);
-        x = b % 8;
-        k = b / 8;
+        if (HLGS_XCD_RUNS) {
+            const int b = xcd_unmap(i0, nb);
+            x = b % 8;
+            k = b / 8;
+        }
     }
-    __device__ int row() const { return x + 8 * k; }
+    __device__ int row() const { return HLGS_XCD_RUNS ? x + 8 * k : i; }
     __device__ void next()
     {
         i++;
@@ -633,24 +707,31 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hi
     if (r == 0) tile_count[t] = tot;
 }
 
+#ifndef HLGS_SCATTER_BATCH
+#define HLGS_SCATTER_BATCH 1  // key scatter: four rank atomics in flight per thread (narrow rects)
+#endif
 // Same block -> Gaussian mapping as k_count_tiles: reserve the block's run inside every tile segment
 // with one returning atomic per bin, then hand out slots from LDS.  Slot order inside a tile is
 // irrelevant: k_tile_sort orders each segment by (depth, index) afterwards.
 // hist != nullptr: the block's base inside each tile segment is ranges[t].x + its k_tile_offsets offset, so the block
 // walks its instances once (no count walk, no returning device atomics).
-template <int BG, bool PACK>
+// SUPER (the two-level binning): the bins are super-tiles; ranges are the super-tiles' segments (k_tile_offsets_plan),
+// each key goes to its super-tile's segment and its tile's index inside the super-tile to tile_local at the same
+// position, for k_supertile_sort.
+template <int BG, bool PACK, bool SUPER>
 __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
                                                                   uint64_t* __restrict__ keys, int gx, int gy, int alt,
                                                                   Guard gd, const uint32_t* __restrict__ block_tot,
-                                                                  const uint32_t* __restrict__ hist)
+                                                                  const uint32_t* __restrict__ hist,
+                                                                  uint8_t* __restrict__ tile_local)
 {
     if (guard_fail(gd)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_base;
     __shared__ uint32_t s_pre[BG + 1];
     __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
-    const int T = gx * gy;
+    const int T = SUPER ? super_tiles(gx * gy) : gx * gy;  // bins
     uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
     uint32_t* s_rank = s_hist + T; // per-tile running rank
     for (int t = threadIdx.x; t < T; t += (BG / 4)) { s_cnt[t] = 0; s_rank[t] = 0; }
@@ -677,7 +758,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         for (int t = threadIdx.x; t < T; t += (BG / 4)) s_cnt[t] = ranges[t].x + row[t];
     } else {
         for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t qm, uint32_t) {
-            if (!(g.drop && !qm)) atomicAdd(&s_cnt[y * gx + x], 1u);
+            if (!(PACK && HLGS_DROP_EMPTY && !qm)) atomicAdd(&s_cnt[y * gx + x], 1u);
         });
         __syncthreads();
         for (int t = threadIdx.x; t < T; t += (BG / 4)) {
@@ -686,6 +767,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         }
     }
     __syncthreads();
+#if HLGS_SCATTER_BATCH
     if (!alt && s_w[(BG / 4) / 64] <= kNarrowRect) {
         // Narrow rects (for_each_instance's one-thread-per-Gaussian path): each thread's instances in groups of four,
         // the four rank atomics issued together and then the four key stores -- one at a time, every store waits for
@@ -716,31 +798,38 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
             const int w = x1 - x0, n = w * (y1 - y0);
             int tx = 0, ty = 0;
             for (int c = 0; c < n; c += 4) {
-                uint32_t pos[4], ent[4];
+                uint32_t pos[4], ent[4], loc[4];
                 bool use[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int r = c + u;
                     const uint32_t qm = PACK ? rect_tile_mask(gmask[j], (uint32_t)r) : 0u;
-                    use[u] = r < n && !(g.drop && !qm);
-                    const int tile = (y0 + ty) * gx + x0 + tx;
-                    if (use[u]) pos[u] = s_cnt[tile] + atomicAdd(&s_rank[tile], 1u);
+                    use[u] = r < n && !(PACK && HLGS_DROP_EMPTY && !qm);
+                    const int tile = (y0 + ty) * gx + x0 + tx, bin = SUPER ? tile / kSuperTiles : tile;
+                    if (use[u]) pos[u] = s_cnt[bin] + atomicAdd(&s_rank[bin], 1u);
                     ent[u] = PACK ? (idx << kEntryShift) | qm : idx;
+                    loc[u] = (uint32_t)(tile % kSuperTiles);
                     if (++tx == w) { tx = 0; ty++; }
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++)
-                    if (use[u]) keys[pos[u]] = ((uint64_t)gdb[j] << 32) | ent[u];
+                    if (use[u]) {
+                        keys[pos[u]] = ((uint64_t)gdb[j] << 32) | ent[u];
+                        if (SUPER) tile_local[pos[u]] = (uint8_t)loc[u];
+                    }
             }
         }
         return;
     }
+#endif
     for_each_instance<BG, true, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int x, int y, uint32_t qm, uint32_t dbits) {
-        if (g.drop && !qm) return;  // the footprint reaches none of the tile's quadrants
-        const int tile = y * gx + x;
-        const uint32_t r = atomicAdd(&s_rank[tile], 1u);
+        if (PACK && HLGS_DROP_EMPTY && !qm) return;  // the footprint reaches none of the tile's quadrants
+        const int tile = y * gx + x, bin = SUPER ? tile / kSuperTiles : tile;
+        const uint32_t r = atomicAdd(&s_rank[bin], 1u);
         const uint32_t entry = PACK ? ((uint32_t)idx << kEntryShift) | qm : (uint32_t)idx;
-        keys[s_cnt[tile] + r] = ((uint64_t)dbits << 32) | entry;
+        const uint32_t pos = s_cnt[bin] + r;
+        keys[pos] = ((uint64_t)dbits << 32) | entry;
+        if (SUPER) tile_local[pos] = (uint8_t)(tile % kSuperTiles);
     });
 }
 
@@ -826,16 +915,6 @@ __device__ __forceinline__ uint32_t plan_scan(const PlanRun& r, uint32_t* s_w, u
     return total;
 }
 
-// The plan's words for the host in its pinned read-back slot (capi.hip plan_words_ready).
-__device__ __forceinline__ void plan_host_words(uint32_t* host, uint32_t seq, uint32_t R, uint32_t mx, uint32_t slots)
-{
-    uint64_t* h = reinterpret_cast<uint64_t*>(host);
-    const uint64_t tag = (uint64_t)seq << 32;
-    h[0] = tag | R;
-    h[1] = tag | mx;
-    h[2] = tag | slots;
-}
-
 __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot, int nb,
                                                const uint32_t* __restrict__ count, uint32_t* __restrict__ cursor,
                                                uint2* __restrict__ ranges, int T, uint32_t* __restrict__ misc,
@@ -861,14 +940,25 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
         misc[1] = s_max;
         misc[2] = slots;
         misc[kMiscPack] = pack;
-        // the host polls these words instead of putting an event (a queue barrier) here: three 64-bit words, each
-        // carrying the frame's sequence number in its high half, written by single-copy-atomic stores, so the host
-        // waits until all three carry it and the kernel needs no system-scope release to order them
-        if (host) plan_host_words(host, seq, R, s_max, slots);
+        if (host) {  // the host polls these words instead of putting an event (a queue barrier) here
+#if HLGS_PLAN_TAGGED
+            uint64_t* h = reinterpret_cast<uint64_t*>(host);
+            const uint64_t tag = (uint64_t)seq << 32;
+            h[0] = tag | R;
+            h[1] = tag | s_max;
+            h[2] = tag | slots;
+#else
+            host[0] = R;
+            host[1] = s_max;
+            host[2] = slots;
+            __threadfence_system();
+            host[3] = seq;  // visible at the latest when the kernel completes
+#endif
+        }
     }
 }
 
-// k_tile_offsets and k_plan in one launch (the default plan): each block turns its 32 tiles' histogram columns into
+// k_tile_offsets and k_plan in one launch (HLGS_FUSED_PLAN): each block turns its 32 tiles' histogram columns into
 // block offsets as k_tile_offsets does, publishes its tiles' total and longest list in one 64-bit word (flags[b]:
 // high half 1 << 31 | max, low half total; zeroed by k_count_tiles), and sums its predecessors' published totals for
 // its ranges (a decoupled look-back: every block publishes before it waits, and blocks are dispatched in order, so a
@@ -876,19 +966,15 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
 // sums the count blocks' totals (record slots) and writes misc and the host words; the totals stay as they are (each
 // scatter block sums its predecessors' for its base), so no block reads what another rewrites.  One launch and one
 // dependent round trip instead of two launches, the second a single block.
-//
-// Every poll is bounded (`polls` sc1 loads per word, ~0.1 s by default), so a word that never arrives cannot hang the
-// queue.  A block whose look-back times out sets misc[kMiscFail] before it counts itself done (misc[kMiscDone], a
-// release increment after its ranges); the last block waits for every other block to be done, then reports R = ~0u if
-// any block failed (or the wait itself timed out).  The host then re-plans the frame with the two launches that need no
-// inter-block wait (k_tile_offsets + k_plan, capi.hip replan), and the render kernels queued behind the failed plan
-// exit at once (Guard: R exceeds every capacity).  hlgs_set_plan_polls lowers the bound for the tests that force it.
-constexpr uint32_t kPlanPolls = 1u << 20;
+constexpr uint32_t kPlanPolls = 1u << 20;  // ~0.1 s of polling per word
+// super != 0 (the two-level binning): the columns are super-tiles, ranges their segments, tile_count unused; misc[1]
+// is left 0 for k_supertile_sort to raise to the longest tile list, and the host's word is the longest super-tile
+// segment (a bound on it); the big-tile list count misc[kMiscBig] is reset.
 __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict__ hist, int nb, int T,
                                                             uint32_t* __restrict__ tile_count, uint2* __restrict__ ranges,
                                                             uint32_t* __restrict__ block_tot, uint64_t* flags,
-                                                            uint32_t* misc, uint32_t* host, uint32_t seq, uint32_t pack,
-                                                            uint32_t polls)
+                                                            uint32_t* __restrict__ misc, uint32_t* host, uint32_t seq,
+                                                            uint32_t pack, int super_)
 {
     __shared__ uint32_t s_part[32][33];
     __shared__ uint32_t s_ex[32];
@@ -897,7 +983,6 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
     const int c = threadIdx.x & 31, r = threadIdx.x >> 5;
     const int t = blockIdx.x * 32 + c;
     const int NB = (T + 31) / 32;
-    const bool last = (int)blockIdx.x == NB - 1;
     const int run = (nb + 31) / 32, b0 = r * run, b1 = min(nb, b0 + run);
     constexpr int K = 8;
     uint32_t v[K];
@@ -967,16 +1052,17 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
         if (r == 0 && tile_count) tile_count[t] = tot;
     }
     uint32_t slots = 0;
-    if (last) {  // the count blocks' totals summed (record slots), ahead of the look-back wait
+    if ((int)blockIdx.x == NB - 1) {  // the count blocks' totals summed (record slots), ahead of the look-back wait
         PlanRun rb;
         plan_load(block_tot, nb, rb);
         uint32_t unused = 0;
         slots = plan_scan(rb, s_w, unused, [&](int, uint32_t, uint32_t) {});
     }
-    // look-back: thread i < blockIdx.x polls block i's word (sc1 loads, bounded)
+    // look-back: thread i < blockIdx.x polls block i's word (sc1 loads, bounded: a word that never arrives marks the
+    // frame failed instead of hanging the queue)
     if ((int)threadIdx.x < (int)blockIdx.x) {
         uint64_t w = 0;
-        for (uint32_t n = 0; n < polls; n++) {
+        for (uint32_t n = 0; n < kPlanPolls; n++) {
             w = __hip_atomic_load(&flags[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (w >> 63) break;
             __builtin_amdgcn_s_sleep(2);
@@ -988,31 +1074,31 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
     __syncthreads();
     const uint32_t E = s_sum;
     if (r == 0 && t < T) ranges[t] = make_uint2(E + s_ex[c], E + s_ex[c] + tot);
-    if (!last) {
-        __syncthreads();  // the block's ranges are written
+    if ((int)blockIdx.x == NB - 1) {  // misc and the host words (the scatter sums its own base)
         if (threadIdx.x == 0) {
-            if (s_fail) __hip_atomic_fetch_or(&misc[kMiscFail], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&misc[kMiscDone], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            // a failed look-back reports R = ~0u, which the host turns into an error
+            const uint32_t R = s_fail ? ~0u : E + s_agg, mx = max(s_max, s_bmax);
+            misc[0] = R;
+            misc[1] = super_ ? 0u : mx;
+            misc[2] = slots;
+            misc[kMiscPack] = pack;
+            misc[kMiscBig] = 0u;
+            if (host) {
+#if HLGS_PLAN_TAGGED
+                uint64_t* h = reinterpret_cast<uint64_t*>(host);
+                const uint64_t tag = (uint64_t)seq << 32;
+                h[0] = tag | R;
+                h[1] = tag | mx;
+                h[2] = tag | slots;
+#else
+                host[0] = R;
+                host[1] = mx;
+                host[2] = slots;
+                __threadfence_system();
+                host[3] = seq;
+#endif
+            }
         }
-        return;
-    }
-    if (threadIdx.x == 0) {  // misc and the host words (the scatter sums its own base)
-        bool ok = !s_fail;
-        uint32_t done = 0;
-        for (uint32_t n = 0; ok && n < polls; n++) {  // every other block done (bounded)
-            done = __hip_atomic_load(&misc[kMiscDone], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (done == (uint32_t)(NB - 1)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        ok = ok && done == (uint32_t)(NB - 1) &&
-             __hip_atomic_load(&misc[kMiscFail], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-        // a failed look-back reports R = ~0u: the host re-plans the frame (k_tile_offsets + k_plan)
-        const uint32_t R = ok ? E + s_agg : ~0u, mx = max(s_max, s_bmax);
-        misc[0] = R;
-        misc[1] = mx;
-        misc[2] = slots;
-        misc[kMiscPack] = pack;
-        if (host) plan_host_words(host, seq, R, mx, slots);
     }
 }
 
@@ -1038,7 +1124,7 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
     for (int y = y0; y < y1; y++)
         for (int x = x0; x < x1; x++, r++) {
             if (alt && !alt_tile_keep(xy.x, xy.y, co, kthr, x, y)) continue;
-            if (g.drop && !rect_tile_mask(masks, r)) continue;
+            if (pack && HLGS_DROP_EMPTY && !rect_tile_mask(masks, r)) continue;
             const int tile = y * gx + x;
             const uint32_t slot = atomicAdd(&cursor[tile], 1u);
             keys[ranges[tile].x + slot] =
@@ -1149,11 +1235,14 @@ __device__ __forceinline__ void wave_sort_upto(LD&& ld, uint32_t n, ST&& st, int
     if constexpr (KMAX >= 8) if (n <= 512) { wave_sort_keys_st<8>(ld, n, st, lane); return; }
     if constexpr (KMAX >= 16) wave_sort_keys_st<16>(ld, n, st, lane);
 }
-// n in (64 KH, 128 KH]: the first 64 KH keys sorted with KH keys per lane and the other n - 64 KH
+// HLGS_SORT_SPLIT: n in (64 KH, 128 KH]: the first 64 KH keys sorted with KH keys per lane and the other n - 64 KH
 // with the fewest that hold them, both into LDS, then merged -- each lane finds the start of its run of ceil(n / 64)
 // outputs on the merge path (binary search) and merges the run.  A 300-key tile then costs a 256-key and a 64-key
 // register sort instead of a 512-key one (the mean configs[1] list is 258 keys).  Keys are unique, so the merge is
 // the same total order.
+#ifndef HLGS_SORT_SPLIT
+#define HLGS_SORT_SPLIT 1
+#endif
 template <int KH>
 __device__ __forceinline__ void wave_sort_split(const uint64_t* __restrict__ keys, uint32_t base, uint32_t n,
                                                 uint32_t* __restrict__ out, int lane, uint64_t* s)
@@ -1187,6 +1276,18 @@ __device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ keys, uint
 {
     wave_sort_keys<KPL>([&](uint32_t e) { return keys[base + e]; }, n, point_list + base, lane);
 }
+// n <= kWaveSortCap keys, the smallest register layout that holds them
+template <typename LD>
+__device__ __forceinline__ void wave_sort_any(LD&& ld, uint32_t n, uint32_t* __restrict__ out, int lane)
+{
+    if (n == 0) return;
+    if (n <= 64) wave_sort_keys<1>(ld, n, out, lane);
+    else if (n <= 128) wave_sort_keys<2>(ld, n, out, lane);
+    else if (n <= 256) wave_sort_keys<4>(ld, n, out, lane);
+    else if (n <= 512) wave_sort_keys<8>(ld, n, out, lane);
+    else wave_sort_keys<16>(ld, n, out, lane);
+}
+
 // Tiles of up to kWaveSortCap instances: one wave each (k_tile_sort handles the longer ones).
 __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__ ranges, uint64_t* keys,
                                                        uint32_t* __restrict__ point_list, int T, Guard gd)
@@ -1197,12 +1298,156 @@ __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__
     const uint32_t n = r.y - r.x;
     const int lane = threadIdx.x;
     if (n == 0 || n > (uint32_t)kWaveSortCap) return;
+#if HLGS_SORT_SPLIT
     __shared__ uint64_t s_sort[kWaveSortCap + 1];  // + 1: the merge may read one past the second run
     if (n <= 64) wave_sort_tile<1>(keys, point_list, r.x, n, lane);
     else if (n <= 128) wave_sort_split<1>(keys, r.x, n, point_list, lane, s_sort);
     else if (n <= 256) wave_sort_split<2>(keys, r.x, n, point_list, lane, s_sort);
     else if (n <= 512) wave_sort_split<4>(keys, r.x, n, point_list, lane, s_sort);
     else wave_sort_split<8>(keys, r.x, n, point_list, lane, s_sort);
+    return;
+#endif
+    if (n <= 64) wave_sort_tile<1>(keys, point_list, r.x, n, lane);
+    else if (n <= 128) wave_sort_tile<2>(keys, point_list, r.x, n, lane);
+    else if (n <= 256) wave_sort_tile<4>(keys, point_list, r.x, n, lane);
+    else if (n <= 512) wave_sort_tile<8>(keys, point_list, r.x, n, lane);
+    else wave_sort_tile<16>(keys, point_list, r.x, n, lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Two-level binning, second level (HLGS_TWO_LEVEL).  One 512-thread block per super-tile: the segment the key scatter
+// filled (keys2, with each key's tile index inside the super-tile in tile_local) is counted per tile, which gives the
+// tiles' ranges (the segment's start plus the tile's prefix: tile-major order, as a one-level binning has it), then
+// split into its tiles in LDS (a segment of up to kSuperCap keys; longer ones through keys in global memory), and each
+// tile of up to kWaveSortCap keys is sorted by one wave in registers and written to point_list.  Longer tiles are left
+// unsorted in keys at their range and listed for k_big_tile_sort.  Every tile list is (depth, entry)-ordered, the same
+// total order the one-level sort gives, so point_list is identical.
+// ------------------------------------------------------------------------------------------------
+constexpr int kSuperCap = 8192;  // 64 KiB of LDS
+__global__ void __launch_bounds__(512) k_supertile_sort(const uint2* __restrict__ st_ranges, int T,
+                                                        const uint64_t* __restrict__ src, const uint8_t* __restrict__ tl,
+                                                        uint64_t* __restrict__ dst, uint32_t* __restrict__ point_list,
+                                                        uint2* __restrict__ ranges, uint32_t* misc,
+                                                        uint32_t* __restrict__ big, Guard gd)
+{
+    if (guard_fail(gd)) return;
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
+    __shared__ uint32_t s_cnt[kSuperTiles], s_off[kSuperTiles], s_cur[kSuperTiles];
+    const int st = blockIdx.x;
+    const uint2 seg = st_ranges[st];
+    const uint32_t n = seg.y - seg.x;
+    const int t0 = st * kSuperTiles, nt = min(kSuperTiles, T - t0);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid < kSuperTiles) s_cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += 512) atomicAdd(&s_cnt[tl[seg.x + i]], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t a = 0;
+        for (int k = 0; k < kSuperTiles; k++) {
+            s_off[k] = a;
+            s_cur[k] = a;
+            a += s_cnt[k];
+        }
+    }
+    __syncthreads();
+    if (tid < nt) {
+        const uint32_t b = seg.x + s_off[tid];
+        ranges[t0 + tid] = make_uint2(b, b + s_cnt[tid]);
+        atomicMax(&misc[1], s_cnt[tid]);  // the longest tile list (k_tile_offsets_plan left it 0)
+    }
+    const bool staged = n <= (uint32_t)kSuperCap;
+    for (uint32_t i = tid; i < n; i += 512) {
+        const uint32_t p = atomicAdd(&s_cur[tl[seg.x + i]], 1u);  // order inside a tile is irrelevant: sorted below
+        const uint64_t key = src[seg.x + i];
+        if (staged) s_keys[p] = key;
+        else dst[seg.x + p] = key;
+    }
+    if (!staged) __threadfence_block();  // this block's own global stores, read back below
+    __syncthreads();
+    for (int k = w; k < nt; k += 512 / 64) {
+        const uint32_t c = s_cnt[k], o = s_off[k];
+        if (c <= (uint32_t)kWaveSortCap) {
+            if (staged) wave_sort_any([&](uint32_t e) { return s_keys[o + e]; }, c, point_list + seg.x + o, lane);
+            else wave_sort_any([&](uint32_t e) { return dst[seg.x + o + e]; }, c, point_list + seg.x + o, lane);
+        } else {
+            if (staged)
+                for (uint32_t e = lane; e < c; e += 64) dst[seg.x + o + e] = s_keys[o + e];
+            if (lane == 0) big[atomicAdd(&misc[kMiscBig], 1u)] = (uint32_t)(t0 + k);
+        }
+    }
+}
+
+// Tiles longer than kWaveSortCap that k_supertile_sort listed (misc[kMiscBig] of them, in big[]), keys unsorted at their
+// range in keys: a few persistent blocks take them in turn; runs of kSortCap are sorted in LDS (bitonic, as
+// k_tile_sort), then merged pairwise through keys2 (each key's rank in the partner run by binary search, as
+// k_merge_runs) until one run is left, written to point_list.
+__global__ void __launch_bounds__(256) k_big_tile_sort(const uint2* __restrict__ ranges, uint64_t* keys, uint64_t* keys2,
+                                                       uint32_t* __restrict__ point_list, const uint32_t* misc,
+                                                       const uint32_t* __restrict__ big, Guard gd)
+{
+    if (guard_fail(gd)) return;
+    __shared__ uint64_t s[kSortCap];
+    const uint32_t nbig = misc[kMiscBig];
+    const int tid = threadIdx.x;
+    for (uint32_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+        const uint2 r = ranges[big[bi]];
+        const uint32_t cnt = r.y - r.x;
+        const bool multi = cnt > (uint32_t)kSortCap;
+        for (uint32_t c0 = 0; c0 < cnt; c0 += kSortCap) {
+            const uint32_t n = min((uint32_t)kSortCap, cnt - c0);
+            uint32_t np = 2;
+            while (np < n) np <<= 1;
+            for (uint32_t i = tid; i < np; i += 256) s[i] = i < n ? keys[r.x + c0 + i] : ~0ull;
+            __syncthreads();
+            for (uint32_t kk = 2; kk <= np; kk <<= 1)
+                for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                    for (uint32_t i = tid; i < np / 2; i += 256) {
+                        const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                        const bool asc = (lo & kk) == 0;
+                        const uint64_t x = s[lo], y = s[hi];
+                        if ((x > y) == asc) { s[lo] = y; s[hi] = x; }
+                    }
+                    __syncthreads();
+                }
+            for (uint32_t i = tid; i < n; i += 256) {
+                if (multi) keys[r.x + c0 + i] = s[i];
+                else point_list[r.x + c0 + i] = (uint32_t)s[i];
+            }
+            __syncthreads();
+        }
+        if (!multi) continue;
+        uint64_t* from = keys;
+        uint64_t* to = keys2;
+        for (uint32_t L = kSortCap; L < cnt; L <<= 1) {
+            __threadfence_block();
+            __syncthreads();
+            const bool last = (L << 1) >= cnt;
+            for (uint32_t i = tid; i < cnt; i += 256) {
+                const uint64_t key = from[r.x + i];
+                const uint32_t run = i / L, a = i - run * L, prun = run ^ 1u;
+                uint32_t out = i;
+                const uint64_t pstart64 = (uint64_t)prun * L;
+                if (pstart64 < cnt) {
+                    const uint32_t ps = (uint32_t)pstart64, pe = min(cnt, ps + L);
+                    uint32_t lo = ps, hi = pe;  // partner keys < key (keys are unique)
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (from[r.x + mid] < key) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    out = min(run, prun) * L + a + (lo - ps);
+                }
+                to[r.x + out] = key;
+                if (last) point_list[r.x + out] = (uint32_t)key;
+            }
+            uint64_t* t = from;
+            from = to;
+            to = t;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
 }
 
 // Merge pass for long tiles: element of run r finds its rank in the partner run by binary search.
@@ -1256,6 +1501,21 @@ struct FwdArgs {
 // set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
 // visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
 // ------------------------------------------------------------------------------------------------
+#ifndef HLGS_FUSED_PLAN
+#define HLGS_FUSED_PLAN 1  // k_tile_offsets + k_plan as one launch (k_tile_offsets_plan)
+#endif
+#ifndef HLGS_BIN_HIST
+#define HLGS_BIN_HIST 1  // atomic-free binning through stored per-block histograms (0: device atomics)
+#endif
+#ifndef HLGS_FWD_PREFETCH_ID
+#define HLGS_FWD_PREFETCH_ID 1
+#endif
+#ifndef HLGS_FWD_PREFETCH_REC
+#define HLGS_FWD_PREFETCH_REC 1
+#endif
+#ifndef HLGS_FWD_BITSET
+#define HLGS_FWD_BITSET 1
+#endif
 template <bool INTERP, bool DEPTH, bool SEEN>  // SEEN: A.seen is set (the per-splat mask is only kept then)
 __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 {
@@ -1284,6 +1544,12 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
     // per-lane predicates are kept as wave masks (the wave is always full): compares are ballots of one v_cmp
     // each, their combinations scalar mask operations, and selects read them back with inverse_ballot
     uint64_t done = __builtin_amdgcn_ballot_w64(!(px < A.W && py < A.H));
+#if HLGS_FWD_PREFETCH_ID && !HLGS_FWD_PREFETCH_REC
+    // each batch's list entries are loaded one batch ahead, so a batch waits for one dependent load (its records),
+    // not two
+    uint32_t next_id = range.x + lane < range.y ? A.point_list[range.x + lane] : 0u;
+#endif
+#if HLGS_FWD_PREFETCH_REC
     // Software pipeline over batches: while batch b is blended, the records of batch b+1 and the list entries of
     // batch b+2 are in flight.  Every lane issues every load (a lane with nothing to stage reads record 0, a lane
     // past the list end re-reads the list's last entry), so the loads retire in a fixed order and the wait at the top
@@ -1307,6 +1573,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
         const float4* rec = A.splat + 4 * (size_t)(cur_stage ? cur_id : 0u);
         R0 = rec[0]; R1 = rec[1]; R2 = rec[2]; R3 = rec[3];
     }
+#endif
     for (uint32_t base = range.x; base < range.y; base += 64) {
         if (done == ~0ull) break;
         if (base == next_split && st) {  // wave-uniform; never past kBwdSplits boundaries (bwd_chunk_len)
@@ -1320,15 +1587,14 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
         const uint32_t pos = base + lane;
         uint32_t my_id = 0;
         bool hit = false;
+#if HLGS_FWD_PREFETCH_REC
         {
             my_id = cur_id;
             const float4 co = make_float4(R0.z, R0.w, R1.x, R1.y);
-            // packed entries (pack_entries) carry the quadrant mask: only the splats reaching this quadrant are staged
             hit = cur_stage && (A.pack || touches_quad(R0.x, R0.y, co, R3.w, fqx, fqy));
             // unconditional: lanes that stage nothing write slots no lane visits
             s_xy[lane] = make_float4(R0.x, R0.y, DEPTH ? R2.y : 0.f, R3.w);
             s_co[lane] = conic_q(co);
-            // .w: 1/kids in hierarchy mode, otherwise the splat's 1-based position in the tile list (n_contrib value)
             s_col[lane] = make_float4(R1.z, R1.w, R2.x, INTERP ? R2.w : __uint_as_float(base - range.x + lane + 1));
             if (INTERP) s_t[lane] = R2.z;
             cur_stage = decode(nxt_entry, pos + 64, cur_id);
@@ -1336,12 +1602,42 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             R0 = rec[0]; R1 = rec[1]; R2 = rec[2]; R3 = rec[3];
             nxt_entry = entry_at(pos + 128);
         }
+#else
+#if HLGS_FWD_PREFETCH_ID
+        my_id = next_id;
+        next_id = pos + 64 < range.y ? A.point_list[pos + 64] : 0u;
+#else
+        if (pos < range.y) my_id = A.point_list[pos];
+#endif
+        // packed entries (pack_entries) carry the quadrant mask: only the splats reaching this quadrant are loaded
+        bool stage = pos < range.y;
+        if (A.pack) {
+            stage = stage && ((my_id >> q) & 1u);
+            my_id >>= kEntryShift;
+        }
+        if (stage) {
+            const float4* rec = A.splat + 4 * (size_t)my_id;
+            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+            const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
+            hit = A.pack || touches_quad(r0.x, r0.y, co, r3.w, fqx, fqy);
+            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, r3.w);
+            s_co[lane] = conic_q(co);
+            // .w: 1/kids in hierarchy mode, otherwise the splat's 1-based position in the tile list (n_contrib value)
+            s_col[lane] = make_float4(r1.z, r1.w, r2.x, INTERP ? r2.w : __uint_as_float(base - range.x + lane + 1));
+            if (INTERP) s_t[lane] = r2.z;
+        }
+#endif
         uint64_t todo = __ballot(hit);
         __syncthreads();
         uint64_t seen_mask = 0;
         while (todo) {
+#if HLGS_FWD_BITSET
             int j;  // find-first-set and clear it: two SALU instead of four
             asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(j), "+s"(todo));
+#else
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+#endif
             const float4 xy = s_xy[j];
             const float4 co = s_co[j];
             const float4 c = s_col[j];
@@ -1430,7 +1726,10 @@ __global__ void __launch_bounds__(256) k_relocation(int P, const float* __restri
 // LDS-histogram binning with the one-block plan: tile grids up to kBinMaxTiles and up to kPlanRun * 1024 blocks of
 // bin_gauss(P) Gaussians (67M); anything larger takes the generic per-Gaussian path.
 // Gaussians per binning block: 4,096, or 2,048 when that would leave fewer than ~200 blocks for the 256 CUs
-int bin_gauss(int P) { return P >= 200 * 4096 ? 4096 : 2048; }
+#ifndef HLGS_BIN_GAUSS
+#define HLGS_BIN_GAUSS 0  // 0: by P as above; 2048 or 4096: that size always (A/B)
+#endif
+int bin_gauss(int P) { return HLGS_BIN_GAUSS ? HLGS_BIN_GAUSS : P >= 200 * 4096 ? 4096 : 2048; }
 
 bool lds_binning(int P, int gx, int gy)
 {
@@ -1446,11 +1745,16 @@ static void allow_big_lds()
     const int dyn = 2 * (int)sizeof(uint32_t) * kBinMaxTiles;
     const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
 #define HLGS_BIG(...) (void)hipFuncSetAttribute((const void*)__VA_ARGS__, A, dyn)
-    HLGS_BIG(k_count_tiles<4096, false>); HLGS_BIG(k_count_tiles<2048, false>);
-    HLGS_BIG(k_count_tiles<4096, true>); HLGS_BIG(k_count_tiles<2048, true>);
-    HLGS_BIG(k_scatter_keys_lds<4096, true>); HLGS_BIG(k_scatter_keys_lds<2048, true>);
-    HLGS_BIG(k_scatter_keys_lds<4096, false>); HLGS_BIG(k_scatter_keys_lds<2048, false>);
+    HLGS_BIG(k_count_tiles<4096, false, false>); HLGS_BIG(k_count_tiles<2048, false, false>);
+    HLGS_BIG(k_count_tiles<4096, true, false>); HLGS_BIG(k_count_tiles<2048, true, false>);
+    HLGS_BIG(k_count_tiles<4096, false, true>); HLGS_BIG(k_count_tiles<2048, false, true>);
+    HLGS_BIG(k_count_tiles<4096, true, true>); HLGS_BIG(k_count_tiles<2048, true, true>);
+    HLGS_BIG(k_scatter_keys_lds<4096, true, false>); HLGS_BIG(k_scatter_keys_lds<2048, true, false>);
+    HLGS_BIG(k_scatter_keys_lds<4096, false, false>); HLGS_BIG(k_scatter_keys_lds<2048, false, false>);
+    HLGS_BIG(k_scatter_keys_lds<4096, true, true>); HLGS_BIG(k_scatter_keys_lds<2048, true, true>);
+    HLGS_BIG(k_scatter_keys_lds<4096, false, true>); HLGS_BIG(k_scatter_keys_lds<2048, false, true>);
 #undef HLGS_BIG
+    (void)hipFuncSetAttribute((const void*)k_supertile_sort, A, (int)sizeof(uint64_t) * kSuperCap);
     hipGetLastError();
     done = true;
 }
@@ -1459,55 +1763,76 @@ static void allow_big_lds()
 // blend), when nb x T words fit in it; nullptr -> the device-atomic binning.
 uint32_t* bin_histogram(const Img& im, int P, int gx, int gy)
 {
+#if HLGS_BIN_HIST
     const size_t T = (size_t)gx * gy, nb = (size_t)(P + bin_gauss(P) - 1) / bin_gauss(P);
     if (lds_binning(P, gx, gy) && nb * T <= T * kBwdSplits * (size_t)kSplitFloats)
         return reinterpret_cast<uint32_t*>(im.split_state);
+#endif
     return nullptr;
 }
 
 // The fused plan's look-back words live in the tile cursors (unused by the histogram binning): ceil(T / 32) 64-bit
 // words, within the cursors' align_up(4 T) bytes for every T >= 1.
 static uint64_t* plan_flags(const Img& im) { return reinterpret_cast<uint64_t*>(im.tile_cursor); }
-// fused: the plan that follows is k_tile_offsets_plan (it needs its look-back words cleared); otherwise, with histogram
-// rows, k_tile_offsets runs here and k_plan after it (the re-plan of a frame whose fused plan failed, capi.hip).
-void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, int gx, int gy, bool alt,
-                        hipStream_t s, uint32_t* hist, bool fused)
+// The two-level binning applies (the LDS binning with histogram rows and the fused plan): the count, plan and scatter
+// work on super-tiles, and k_supertile_sort forms the tiles.  Its super-tile segments follow the look-back words in the
+// tile cursors: 8 ceil(NST / 32) + 8 NST bytes, NST = ceil(T / 16), within align_up(4 T) for every T >= 1.
+bool two_level(const Img& im, int P, int gx, int gy)
 {
-    const int T = gx * gy;
-    const size_t lds = sizeof(uint32_t) * (size_t)T;
+    return HLGS_TWO_LEVEL && HLGS_FUSED_PLAN && bin_histogram(im, P, gx, gy) != nullptr;
+}
+static uint2* super_ranges(const Img& im, int T)
+{
+    return reinterpret_cast<uint2*>(im.tile_cursor + 2 * ((super_tiles(T) + 31) / 32));
+}
+
+void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, int gx, int gy, bool alt,
+                        hipStream_t s, uint32_t* hist)
+{
+    uint32_t* tile_count = im.tile_count;
+    const bool sup = two_level(im, P, gx, gy);
+    const int bins = sup ? super_tiles(gx * gy) : gx * gy;
+    const size_t lds = sizeof(uint32_t) * (size_t)bins;
     allow_big_lds();
     const int bg = bin_gauss(P);
-    fused = fused && hist;
+    const bool fused = hist && HLGS_FUSED_PLAN;
     uint32_t* zw = fused ? im.tile_cursor : nullptr;
-    const int nz = fused ? 2 * ((T + 31) / 32) : 0;
-#define HLGS_CNT(BG, D) hipLaunchKernelGGL((k_count_tiles<BG, D>), dim3((P + BG - 1) / BG), dim3(BG / 4), lds, s, P, \
-                                          radii, g, im.tile_count, gx, gy, (int)alt, g.scan_tmp, hist, zw, nz, im.misc)
-    if (bg == 4096) { if (g.drop) HLGS_CNT(4096, true); else HLGS_CNT(4096, false); }
-    else { if (g.drop) HLGS_CNT(2048, true); else HLGS_CNT(2048, false); }
+    const int nz = fused ? 2 * ((bins + 31) / 32) : 0;
+    const bool drop = g.pack && HLGS_DROP_EMPTY;
+#define HLGS_CNT(BG, D, S) hipLaunchKernelGGL((k_count_tiles<BG, D, S>), dim3((P + BG - 1) / BG), dim3(BG / 4), lds, s, P, \
+                                             radii, g, tile_count, gx, gy, (int)alt, g.scan_tmp, hist, zw, nz)
+#define HLGS_CNT2(BG, S) do { if (drop) HLGS_CNT(BG, true, S); else HLGS_CNT(BG, false, S); } while (0)
+    if (sup) { if (bg == 4096) HLGS_CNT2(4096, true); else HLGS_CNT2(2048, true); }
+    else { if (bg == 4096) HLGS_CNT2(4096, false); else HLGS_CNT2(2048, false); }
+#undef HLGS_CNT2
 #undef HLGS_CNT
     if (hist && !fused) {
-        const int nb = (P + bg - 1) / bg;
-        hipLaunchKernelGGL(k_tile_offsets, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count);
+        const int T = gx * gy, nb = (P + bin_gauss(P) - 1) / bin_gauss(P);
+        hipLaunchKernelGGL(k_tile_offsets, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, tile_count);
     }
 }
 
-uint32_t g_plan_polls = kPlanPolls;  // hlgs_set_plan_polls (tests)
-
-void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s,
-                 bool fused)
+void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s)
 {
     const int T = gx * gy;
     static_assert(kPlanRun * 1024 >= kBinMaxTiles, "one k_plan block covers every LDS-binned tile grid");
+
     uint32_t* hist = bin_histogram(im, P, gx, gy);
     const int nb = (P + bin_gauss(P) - 1) / bin_gauss(P);
-    if (hist && fused) {
+    if (two_level(im, P, gx, gy)) {  // columns = super-tiles
+        const int C = super_tiles(T);
+        hipLaunchKernelGGL(k_tile_offsets_plan, dim3((C + 31) / 32), dim3(1024), 0, s, hist, nb, C, nullptr,
+                           super_ranges(im, T), g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, 1);
+        return;
+    }
+    if (hist && HLGS_FUSED_PLAN) {
         hipLaunchKernelGGL(k_tile_offsets_plan, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count,
-                           im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, g_plan_polls);
+                           im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, 0);
         return;
     }
     uint32_t* cursor = hist ? nullptr : im.tile_cursor;
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, nb, im.tile_count, cursor, im.ranges, T, im.misc,
-                       host, seq, (uint32_t)g.pack);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, (P + bin_gauss(P) - 1) / bin_gauss(P), im.tile_count,
+                       cursor, im.ranges, T, im.misc, host, seq, (uint32_t)g.pack);
 }
 
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
@@ -1519,8 +1844,13 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
     const bool alt = a.variant == HLGS_VARIANT_ALT;
     if (!a.indices && !a.colors_precomp && a.shs && a.M > 0 && !tile_count && a.M <= 16) {
         const dim3 g64((a.P + 63) / 64);
-#define HLGS_PSH(AL, M3) \
-    hipLaunchKernelGGL((k_preprocess_sh2<AL, M3>), g64, dim3(128), 0, s, a, g, radii, gx, gy, fx, fy, z)
+#define HLGS_PSH(AL, M3)                                                                                           \
+    do {                                                                                                           \
+        if (HLGS_PRE_SPLIT)                                                                                        \
+            hipLaunchKernelGGL((k_preprocess_sh2<AL, M3>), g64, dim3(128), 0, s, a, g, radii, gx, gy, fx, fy, z);  \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_preprocess_sh<AL, M3>), g64, dim3(64), 0, s, a, g, radii, gx, gy, fx, fy, z);    \
+    } while (0)
         if (alt) {
             switch (a.M) {
             case 3: HLGS_PSH(true, 9); break;
@@ -1560,12 +1890,33 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
     const int T = gx * gy;
     const int alt = a.variant == HLGS_VARIANT_ALT;
     if (timing) stage_mark(s, 3, true);
+    if (two_level(im, a.P, gx, gy)) {
+        // first level: keys into their super-tiles' segments (keys2) with their tile inside it (tile_local)
+        allow_big_lds();
+        const int C = super_tiles(T);
+#define HLGS_SCATTER(BG, PK)                                                                                       \
+    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK, true>), dim3((a.P + BG - 1) / BG), dim3(BG / 4),                     \
+                       2 * sizeof(uint32_t) * (size_t)C, s, a.P, radii, g, super_ranges(im, T), nullptr, b.keys2, gx, gy, \
+                       alt, gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy), b.tile_local)
+        const bool pk = pack_entries(a.P);
+        if (bin_gauss(a.P) == 4096) { if (pk) HLGS_SCATTER(4096, true); else HLGS_SCATTER(4096, false); }
+        else { if (pk) HLGS_SCATTER(2048, true); else HLGS_SCATTER(2048, false); }
+#undef HLGS_SCATTER
+        if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
+        // second level: tiles, their ranges and their sorted lists; tiles past kWaveSortCap through k_big_tile_sort
+        hipLaunchKernelGGL(k_supertile_sort, dim3(C), dim3(512), sizeof(uint64_t) * kSuperCap, s, super_ranges(im, T), T,
+                           b.keys2, b.tile_local, b.keys, b.point_list, im.ranges, im.misc, im.tile_count, gd);
+        hipLaunchKernelGGL(k_big_tile_sort, dim3(64), dim3(256), 0, s, im.ranges, b.keys, b.keys2, b.point_list, im.misc,
+                           im.tile_count, gd);
+        if (timing) stage_mark(s, 4, false);
+        return;
+    }
     if (lds_binning(a.P, gx, gy)) {
         allow_big_lds();
 #define HLGS_SCATTER(BG, PK)                                                                                       \
-    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK>), dim3((a.P + BG - 1) / BG), dim3(BG / 4),                           \
+    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK, false>), dim3((a.P + BG - 1) / BG), dim3(BG / 4),                    \
                        2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy, alt, \
-                       gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy))
+                       gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy), nullptr)
         const bool pk = pack_entries(a.P);
         if (bin_gauss(a.P) == 4096) { if (pk) HLGS_SCATTER(4096, true); else HLGS_SCATTER(4096, false); }
         else { if (pk) HLGS_SCATTER(2048, true); else HLGS_SCATTER(2048, false); }
