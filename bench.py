@@ -689,6 +689,7 @@ def main():
     # profiles/r04/timing.json), so the timed steps start from the clock a training run holds: untimed blocks of 10
     # steps, at least 50, until two blocks in a row are no faster than the best one by 0.5%, at most args.settle_max.
     settle = 0
+    settle_blocks = []  # ms per step of each untimed settle block: the clock ramp the settle phase waits out
     if args.settle_max > 0:
         best, flat = None, 0
         while settle < args.settle_max:
@@ -698,6 +699,7 @@ def main():
                 step()
             torch.cuda.synchronize()
             dt = time.perf_counter() - tb
+            settle_blocks.append(dt / 10 * 1e3)
             settle += 10
             flat = flat + 1 if best is not None and dt > best * 0.995 else 0
             best = dt if best is None else min(best, dt)
@@ -819,6 +821,12 @@ def main():
             "metric": "forward+backward Mpix/s at 1080p (1M Gaussians); grad max-abs-err vs ref",
             "value": round(value, 3), "unit": "Mpix/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            # every untimed step before the timed ones: warm-up, the stage-timing pass and the clock settle (launch_plan)
+            "untimed_steps": args.warmup + n_stage + settle,
+            "clock": ("sustained: the timed steps follow untimed ones until the step time stops falling (the core "
+                      "clock's ramp under load); settle_ms_per_step is each untimed settle block's time, so the first "
+                      "against the last shows what the settle phase changed"),
+            "settle_ms_per_step": [round(x, 4) for x in settle_blocks],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded PCG64 scene and upstream gradients; no dataset)",
             "config": {"workload": wl, "num_rendered": nr, "visible": V, "tiles": T,

@@ -395,6 +395,25 @@ __device__ __forceinline__ uint32_t sub_block_mask(const SplatBands& s, int tx0,
     }
     return m;
 }
+// The same for one 8x8 quadrant at (qx0, qy0): bit g = sub-block g (x half g & 1, y half g >> 1) is reached.
+__device__ __forceinline__ uint32_t quad_sub_mask(const SplatBands& s, int qx0, int qy0)
+{
+#pragma clang fp contract(off)
+    if (s.mode) return s.mode == 1 ? 0xFu : 0u;
+    const float u0 = (float)qx0 - s.x;
+    uint32_t m = 0;
+#pragma unroll
+    for (int band = 0; band < 2; band++) {
+        float lo, hi;
+        band_extent(s, (float)(qy0 + 4 * band) - s.y, lo, hi, 3.f);
+#pragma unroll
+        for (int col = 0; col < 2; col++) {
+            const float c0 = u0 + (float)(4 * col);
+            if (hi >= c0 && lo <= c0 + 3.f) m |= 1u << (col + 2 * band);
+        }
+    }
+    return m;
+}
 // The quadrant bits of a 4-bit mask spread over their four sub-block bits (bit k -> bits 4 k .. 4 k + 3).
 __device__ __forceinline__ uint32_t quad_to_sub(uint32_t qm)
 {

@@ -10,7 +10,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 OBJDIR = os.path.join(PKG, "build", "obj")
 LIB = os.path.join(LIBDIR, "libhlgs.so")
-SOURCES = ["scan.hip", "raster_fwd.hip", "raster_bwd.hip", "gauss_bwd.hip", "lod.hip", "optim.hip", "loss.hip", "stream.hip", "capi.hip", "hier_io.cpp", "spt_build.cpp"]
+SOURCES = ["scan.hip", "preprocess.hip", "raster_fwd.hip", "raster_bwd.hip", "gauss_bwd.hip", "lod.hip", "optim.hip", "loss.hip", "stream.hip", "capi.hip", "hier_io.cpp", "spt_build.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HLGS_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-Wall",
@@ -23,13 +23,13 @@ def _deps_mtime():
     return max(os.path.getmtime(f) for f in files if os.path.exists(f))
 
 
-# raster_fwd.hip: no a*b+c contraction, so the preprocess rounds every product and sum as the oracle
+# preprocess.hip, raster_fwd.hip: no a*b+c contraction, so the preprocess (and the key scatter's quadrant masks) round every product and sum as the oracle
 # does (-ffp-contract=off there) and its per-Gaussian outputs are bit-identical; the blend's hot
 # arithmetic is written with explicit fmaf and is unaffected.
 # lod.hip: the same for the LOD sizes (distance, max scale / distance) and interpolation weights, which the
 # oracle computes uncontracted: cut decisions and weights are then bit-identical, not only within rounding.
 # gauss_bwd.hip: the per-Gaussian backward, likewise (its conic -> cov3D chain is ill-conditioned for wide splats).
-PER_FILE = {"raster_fwd.hip": ["-ffp-contract=off"], "lod.hip": ["-ffp-contract=off"],
+PER_FILE = {"preprocess.hip": ["-ffp-contract=off"], "raster_fwd.hip": ["-ffp-contract=off"], "lod.hip": ["-ffp-contract=off"],
             "gauss_bwd.hip": ["-ffp-contract=off"]}
 
 

@@ -16,10 +16,21 @@ The reference keeps every Gaussian in host storage (GaussianModel.move_storage_t
                                       padded to whole 64-byte lines), so the host link carries whole lines
   optimizer step         :786-812  -> hlgs_adam_step (one launch over the six tensors, skybox gradients zeroed)
 
+  occlusion cull         :344-351  -> optional (occlusion_culling=True, train_post.py's Use_Occlusion_Culling, off by
+                                      default there, :83): the coarse cut's upper-tree Gaussians are read from host
+                                      storage and rendered, and the cut keeps the ones the render reports (below)
+
 Differences from the reference: when the Gaussian budget forces a second pass, each pass
 starts again from the step's initial state with the larger distance multiplier (the reference's second pass
-reads state its first pass already replaced and then fails on mismatched masks); occlusion culling (a render
-inside the cut) is not provided.
+reads state its first pass already replaced and then fails on mismatched masks).
+
+Occlusion culling as the reference runs it (gaussian_renderer/__init__.py:24-33, render_on_disk :163-232): the
+Gaussians of the coarse cut's nodes (upper_tree_nodes[:, 5]) are taken from storage with the activations applied
+(sigmoid opacity clamped to [0, 1], exp scale, normalised rotation, SH degree 3), rendered without depth on a black
+background, and the cut keeps the nodes whose `seen` is set -- where `seen` is the second value the reference's
+GaussianRasterizer returns, i.e. the radii (render_on_disk unpacks `rendered_image, seen, depth`): a node stays when
+its Gaussian has a non-zero screen radius (in front of the near plane, on screen).  With a batch of views a node
+stays when any view keeps it.
 """
 import ctypes as C
 import math
@@ -146,7 +157,7 @@ class SPTCache:
 
     def __init__(self, storage, spt, skybox_points, opt_storage=None, reuse_tolerance=0.9,
                  max_gaussian_budget=100_000_000, distance_multiplier_until_budget=1.5, use_frustum_culling=True,
-                 use_bounding_spheres=True, device="cuda"):
+                 use_bounding_spheres=True, device="cuda", occlusion_culling=False):
         # packed pinned host storage: one row per Gaussian holding its six parameter rows, then the six exp_avgs and
         # the six exp_avg_sqs rows, padded to whole 64-byte lines; self.storage / self.opt_storage are views of it
         G = int(storage[NAMES[0]].shape[0])
@@ -183,6 +194,8 @@ class SPTCache:
         self.budget = max_gaussian_budget
         self.dm_step = distance_multiplier_until_budget
         self.use_frustum = use_frustum_culling
+        self.occlusion = bool(occlusion_culling)
+        self.last_occlusion = None  # the last occlusion cull's inputs and mask (tests)
         # setup, train_post.py:208-231
         self.render_indices = torch.arange(0, self.sky, device=dev, dtype=torch.int32)
         head = torch.arange(0, self.sky, device=dev, dtype=torch.int32)
@@ -208,7 +221,44 @@ class SPTCache:
         return torch.empty((rows,) + tuple(self.storage[k].shape[1:]), dtype=torch.float32, device=self.device)
 
     # ------------------------------------------------------------ bookkeeping (:326-430)
-    def plan(self, full_proj_transform, camera_center, distance_multiplier=1.0):
+    def _occlusion_cull(self, views):
+        """Filter the device coarse cut (self._cut, length in self._cut_count[0]) as train_post.py:344-351 does."""
+        from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+        dev = self.device
+        n = int(self._cut_count[0].item())
+        cut = self._cut[:n]
+        gid = self.nodes[cut.long(), 5].contiguous()
+        if self.wb_done is not None:  # storage as the previous steps' write-backs left it
+            torch.cuda.current_stream(dev).wait_event(self.wb_done)
+        rows = {k: self._alloc(k, n) for k in NAMES}
+        load_rows_packed([rows[k] for k in NAMES], n, gid, self.host)
+        means = rows["xyz"]
+        opac = torch.clamp(torch.sigmoid(rows["opacity"]), 0, 1)
+        scales = torch.exp(rows["scaling"])
+        rots = torch.nn.functional.normalize(rows["rotation"])
+        shs = torch.cat((rows["f_dc"], rows["f_rest"]), dim=1).contiguous()
+        keep = torch.zeros(n, dtype=torch.bool, device=dev)
+        with torch.no_grad():
+            for v in views:
+                rs = GaussianRasterizationSettings(
+                    image_height=int(v["H"]), image_width=int(v["W"]), tanfovx=float(v["tanfovx"]),
+                    tanfovy=float(v["tanfovy"]), bg=torch.zeros(3, device=dev), scale_modifier=1.0,
+                    viewmatrix=v["viewmatrix"].to(dev), projmatrix=v["projmatrix"].to(dev), sh_degree=3,
+                    campos=v["campos"].to(dev), prefiltered=False, debug=True,
+                    render_indices=torch.empty(0, dtype=torch.int32, device=dev),
+                    parent_indices=torch.empty(0, dtype=torch.int32, device=dev),
+                    interpolation_weights=torch.empty(0, device=dev),
+                    num_node_kids=torch.empty(0, dtype=torch.int32, device=dev), do_depth=False)
+                _, radii, _ = GaussianRasterizer(rs)(means3D=means, means2D=torch.zeros_like(means), opacities=opac,
+                                                     shs=shs, scales=scales, rotations=rots)
+                keep |= radii > 0
+        kept = cut[keep]
+        self._cut[:kept.numel()] = kept
+        self._cut_count[0] = kept.numel()
+        self.last_occlusion = dict(indices=gid, means3D=means, opacities=opac, scales=scales, rotations=rots, shs=shs,
+                                   keep=keep, n_before=n, n_after=int(kept.numel()))
+
+    def plan(self, full_proj_transform, camera_center, distance_multiplier=1.0, views=None):
         """One bookkeeping pass for a view; no parameter moves.  Returns the reference's per-pass variables.
 
         A batch of G views (full_proj_transform G x 4 x 4, camera_center G x 3; one view per rank of a
@@ -234,6 +284,11 @@ class SPTCache:
                                                      float(distance_multiplier), int(bool(self.use_frustum)), 1,
                                                      _p(self._cut_scratch), _p(self._cut), _p(self._cut_count),
                                                      L.stream()))
+        if self.occlusion:
+            if views is None:
+                raise ValueError("occlusion culling renders the cut: pass the view(s) (W, H, tanfovx, tanfovy, "
+                                 "viewmatrix, projmatrix, campos) to step()")
+            self._occlusion_cull(views if isinstance(views, (list, tuple)) else [views])
         coarse = self._cut
         n_cut, m, R = N, self.prev_SPT_indices.numel(), self.render_indices.numel()
         # the ten output lists carved from one int32 allocation (the distances as float32 views of it)
@@ -274,10 +329,12 @@ class SPTCache:
             distance_multiplier=distance_multiplier)
 
     # ------------------------------------------------------------ one view (:326-483), or a batch of views
-    def step(self, full_proj_transform, camera_center):
+    def step(self, full_proj_transform, camera_center, views=None):
+        """views: the camera(s) of this step as dicts (W, H, tanfovx, tanfovy, viewmatrix, projmatrix, campos), needed
+        only with occlusion_culling (the cull renders the cut's upper-tree Gaussians)."""
         dm = 1.0
         while True:
-            pl = self.plan(full_proj_transform, camera_center, dm)
+            pl = self.plan(full_proj_transform, camera_center, dm, views)
             if pl["render_indices"].numel() <= self.budget:
                 break
             dm *= self.dm_step

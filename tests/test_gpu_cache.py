@@ -51,8 +51,9 @@ class _Oracle:
         self.render, self.n_loaded = np.arange(sky, dtype=np.int32), 0
         self.prev = (np.zeros(0, np.int32), np.zeros(0, np.float32), np.zeros(0, np.int32))
 
-    def step(self, cam):
-        """cam: one camera dict, or a list of them (a batch of views: the union cut)."""
+    def step(self, cam, keep=None):
+        """cam: one camera dict, or a list of them (a batch of views: the union cut).  keep: the occlusion
+        cull's mask over the coarse cut (train_post.py:344-351), applied before the bookkeeping."""
         from hlgs_core import spt
         b = self.b
         cams = cam if isinstance(cam, (list, tuple)) else [cam]
@@ -64,6 +65,8 @@ class _Oracle:
         while True:
             coarse = SR.upper_tree_cut(b["upper_tree_nodes"], b["upper_tree_xyz"], b["bounding_sphere_radii"],
                                        b["min_distance_squared"], planes, campos, dm, True, True)
+            if keep is not None:
+                coarse = np.asarray(coarse)[np.asarray(keep, bool)]
             r = SR.cache_pass(b["upper_tree_nodes"], b["upper_tree_xyz"], coarse, campos, dm, *self.prev,
                               self.render, self.n_loaded, self.sky, self.rtol, 0.05, cut_fn)
             if len(r["render_indices"]) <= self.budget:
@@ -286,3 +289,41 @@ def test_union_cut_semantics_and_cost(G):
         mse = float(((iu.clamp(0, 1) - io.clamp(0, 1)) ** 2).mean())
         psnr = 10 * np.log10(1.0 / max(mse, 1e-12))
         assert psnr >= 38.0, psnr
+
+
+def test_occlusion_culling_matches_restatement():
+    """SPTCache(occlusion_culling=True) = train_post.py:344-351 with Use_Occlusion_Culling: the coarse cut's upper-tree
+    Gaussians are read from storage (activated), rendered, and the cut keeps the nodes whose rasterizer `seen` -- the
+    radii the reference's wrapper returns second (gaussian_renderer/__init__.py:24-33, 213-221) -- is non-zero.  The
+    kept set is checked against the oracle's radii on the same activated inputs, the inputs against the restatement's
+    storage, and the rest of the step against the restatement run on the filtered cut."""
+    from hlgs_core.spt_cache import SPTCache
+    sky = 4
+    b, storage = _scene(sky)
+    cams = _cameras()
+    cache = SPTCache(storage, b, sky, reuse_tolerance=0.9, occlusion_culling=True)
+    orc = _Oracle(b, storage, sky, 0.9, 10 ** 9)
+    culled = 0
+    for step, cam in enumerate(cams):
+        got = cache.step(cam["projmatrix"], cam["campos"], views=cam)
+        occ = cache.last_occlusion
+        gid = occ["indices"].cpu().numpy()
+        # the inputs: storage rows of the cut's node Gaussians, activated as render_on_disk's caller does
+        host = {k: orc.host[i][gid] for i, k in enumerate(NAMES)}
+        np.testing.assert_array_equal(occ["means3D"].cpu().numpy(), host["xyz"])
+        np.testing.assert_allclose(occ["opacities"].cpu().numpy(), 1 / (1 + np.exp(-host["opacity"].astype(np.float64))),
+                                   rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(occ["scales"].cpu().numpy(), np.exp(host["scaling"].astype(np.float64)), rtol=1e-6)
+        # the kept set: the oracle's radii on the very same inputs
+        sc = dict(means3D=occ["means3D"].cpu().numpy(), opacities=occ["opacities"].cpu().numpy(),
+                  scales=occ["scales"].cpu().numpy(), rotations=occ["rotations"].cpu().numpy(),
+                  shs=occ["shs"].cpu().numpy(), sh_degree=3)
+        camn = S.cam_numpy(dict(cam, bg=np.zeros(3, np.float32)))
+        keep = O.forward(sc, camn, do_depth=False).radii > 0 if len(gid) else np.zeros(0, bool)
+        np.testing.assert_array_equal(occ["keep"].cpu().numpy(), keep, err_msg=f"view {step}")
+        culled += int((~keep).sum())
+        want = orc.step(cam, keep=keep)
+        np.testing.assert_array_equal(got.cpu().numpy(), want["render_indices"], err_msg=f"view {step}")
+        for t, (g, w) in enumerate(zip(_dev_list(cache), orc.dev)):
+            np.testing.assert_array_equal(g.detach().cpu().numpy(), w, err_msg=f"tensor {t} view {step}")
+    assert culled > 0  # the random storage positions put part of the upper tree off screen or behind the camera

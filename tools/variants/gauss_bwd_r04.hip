@@ -122,85 +122,8 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             }
         }
     }
-    // ---- per-Gaussian sum of the blend records in slot order (fixed => deterministic); wide ones were summed above.
-    // The wave's records are contiguous (consecutive Gaussians own consecutive slot ranges), so they are copied to
-    // LDS in chunks of kChunk records by LDS-DMA -- coalesced 1 KiB wave instructions instead of every lane reading
-    // its own 48-byte records at its own address -- and each lane then sums its records from LDS, in slot order as
-    // before (bitwise the same sums).  Done before any lane leaves: the copy is a wave instruction.
-    constexpr bool alt = ALT;
-    float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
-    float kx = 0.f, ky = 0.f, kthr = 0.f;
-    int kx0 = 0, ky0 = 0, kw = 1;
-    if (alt && vis) {  // slots of tiles the binning culled (alt_tile_keep) hold no record: skip them
-        const float4 r0 = g.splat[4 * (size_t)t_idx], r1 = g.splat[4 * (size_t)t_idx + 1];
-        const float4 r3 = g.splat[4 * (size_t)t_idx + 3];
-        kx = r0.x; ky = r0.y;
-        kco = make_float4(r0.z, r0.w, r1.x, r1.y);
-        kthr = alt_keep_threshold(kco.w);
-        kx0 = __float_as_int(r3.y) & 0xffff;
-        ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
-        kw = __float_as_int(r3.z);
-    }
-    const uint32_t start = r_start, end = vis && r_end - r_start > kWide ? r_start : r_end;  // narrow range
-    // per-Gaussian inputs of the covariance / projection backward, issued ahead of the record sums so their latency
-    // overlaps them
-    const int idx = t_idx < a.P ? (HIER ? a.indices[t_idx] : t_idx) : 0;
-    f3 mean = mk(0.f, 0.f, 0.f), scl3 = mk(0.f, 0.f, 0.f);
-    float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
-    float c3[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (vis) {
-        mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-        if (a.cov3D_precomp || HIER) {
-            const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
-            for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
-        } else {
-            scl3 = mk(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-            rq = reinterpret_cast<const float4*>(a.rotations)[idx];
-        }
-    }
-    {
-        constexpr int kChunk = 128;  // records per chunk: 6 KiB of LDS per wave
-        __shared__ float4 s_rec[4][3 * kChunk];
-        float4* buf = s_rec[threadIdx.x >> 6];
-        const int lane = threadIdx.x & 63;
-        const bool any = start < end;
-        uint32_t lo = any ? start : 0xFFFFFFFFu, hi = any ? end : 0u;
-        for (int off = 32; off > 0; off >>= 1) {
-            lo = min(lo, (uint32_t)__shfl_xor((int)lo, off, 64));
-            hi = max(hi, (uint32_t)__shfl_xor((int)hi, off, 64));
-        }
-        lo = __builtin_amdgcn_readfirstlane(lo);
-        hi = __builtin_amdgcn_readfirstlane(hi);
-        typedef __attribute__((address_space(3))) void lds_t;
-        for (uint32_t c0 = lo; c0 < hi; c0 += kChunk) {
-            const uint32_t c1 = min(hi, c0 + kChunk);
-            if (__ballot(start < c1 && end > c0) == 0) continue;  // inside a wide Gaussian's range: nobody needs it
-            const uint32_t nf = 3 * (c1 - c0);
-            const float4* src = rec.rec + 3 * (size_t)c0;
-#pragma unroll
-            for (int k = 0; k < 3 * kChunk / 64; k++) {
-                if ((uint32_t)(64 * k) >= nf) break;  // wave-uniform
-                const uint32_t f = min((uint32_t)(64 * k + lane), nf - 1);
-                __builtin_amdgcn_global_load_lds((const void*)(src + f), (lds_t*)(buf + 64 * k), 16, 0, 0);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA has landed (this wave's own LDS region)
-            const uint32_t r0 = max(start, c0), r1 = min(end, c1);
-            for (uint32_t r = r0; r < r1; r++) {
-                bool use = rect_tile_mask(qmasks, r - start);
-                if (alt && use) {
-                    const int kk = (int)(r - start);
-                    use = alt_tile_keep(kx, ky, kco, kthr, kx0 + kk % kw, ky0 + kk / kw);
-                }
-                if (!use) continue;
-                const float4 A = buf[3 * (r - c0)], B = buf[3 * (r - c0) + 1], Cc = buf[3 * (r - c0) + 2];
-                s0 += A.x; s1 += A.y; s2 += A.z; s3 += A.w;
-                s4 += B.x; s5 += B.y; s6 += B.z; s7 += B.w;
-                s8 += Cc.x; s9 += Cc.y;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the chunk done before the next DMA
-        }
-    }
     if (t_idx >= a.P) return;
+    const int idx = HIER ? a.indices[t_idx] : t_idx;
     const int M3 = a.M * 3;
     if (!vis) {
         if (!HIER) {
@@ -217,8 +140,59 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
         }
         return;
     }
-    // cov3D is not stored by the forward: recomputed from the scale and rotation the forward used
-    if (!(a.cov3D_precomp || HIER)) cov3d_exact(scl3, a.scale_modifier, rq, c3);
+    // ---- per-Gaussian sum of the blend records (fixed order => deterministic); wide ones were summed above
+    const uint32_t end = r_end - r_start > kWide ? r_start : r_end, start = r_start;
+    constexpr bool alt = ALT;
+    float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
+    float kx = 0.f, ky = 0.f, kthr = 0.f;
+    int kx0 = 0, ky0 = 0, kw = 1;
+    if (alt) {  // slots of tiles the binning culled (alt_tile_keep) hold no record: skip them
+        const float4 r0 = g.splat[4 * (size_t)t_idx], r1 = g.splat[4 * (size_t)t_idx + 1];
+        const float4 r3 = g.splat[4 * (size_t)t_idx + 3];
+        kx = r0.x; ky = r0.y;
+        kco = make_float4(r0.z, r0.w, r1.x, r1.y);
+        kthr = alt_keep_threshold(kco.w);
+        kx0 = __float_as_int(r3.y) & 0xffff;
+        ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
+        kw = __float_as_int(r3.z);
+    }
+    // per-Gaussian inputs of the covariance / projection backward, loaded before the record sum so their
+    // latency overlaps it
+    float c3[6];
+    if (a.cov3D_precomp || HIER) {
+        const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
+        for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
+    } else {  // not stored by the forward: recomputed from the scale and rotation the forward used
+        cov3d_exact(mk(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]), a.scale_modifier,
+                    reinterpret_cast<const float4*>(a.rotations)[idx], c3);
+    }
+    const f3 mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    // records four at a time: all loads of a group are in flight together, the sums stay in slot order
+    for (uint32_t r0 = start; r0 < end; r0 += 4) {
+        float4 A[4], B[4], Cc[4];
+        bool use[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r = r0 + k;
+            use[k] = r < end && rect_tile_mask(qmasks, r - start);
+            if (alt && use[k]) {
+                const int kk = (int)(r - start);
+                use[k] = alt_tile_keep(kx, ky, kco, kthr, kx0 + kk % kw, ky0 + kk / kw);
+            }
+            if (use[k]) {
+                A[k] = rec.rec[3 * (size_t)r];
+                B[k] = rec.rec[3 * (size_t)r + 1];
+                Cc[k] = rec.rec[3 * (size_t)r + 2];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!use[k]) continue;
+            s0 += A[k].x; s1 += A[k].y; s2 += A[k].z; s3 += A[k].w;
+            s4 += B[k].x; s5 += B[k].y; s6 += B[k].z; s7 += B[k].w;
+            s8 += Cc[k].x; s9 += Cc[k].y;
+        }
+    }
     o.dmean2D[3 * idx] = s0;
     o.dmean2D[3 * idx + 1] = s1;
     o.dmean2D[3 * idx + 2] = 0.f;

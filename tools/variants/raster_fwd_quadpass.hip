@@ -1,3 +1,5 @@
+// Round-4 forward blend (one splat per iteration for the whole 8x8 quadrant wave), for A/B against the sub-block
+// lists of the product k_blend_fwd: python tools/build_variant.py quadfwd tools/variants/raster_fwd_quadpass.hip raster_fwd.hip
 // raster_fwd.hip -- forward rasterizer kernels for gfx950.
 //
 // Reference semantics (submodules/hierarchy-rasterizer/cuda_rasterizer; the preprocess is in preprocess.hip):
@@ -905,50 +907,39 @@ struct FwdArgs {
 };
 
 // ------------------------------------------------------------------------------------------------
-// Front-to-back blend.  One wave64 per 8x8 quadrant of a 16x16 tile, one pixel per lane; the four quadrant waves of a
-// tile are independent blocks placed on one XCD (xcd_remap) so the tile's splat reads hit the same L2.  Each 64-splat
-// batch is staged in LDS.  Lanes form four 16-lane rows, row g being the quadrant's 4x4 sub-block g (x half g & 1, y
-// half g >> 1); per sub-block, the staged splats whose alpha >= 1/255 footprint reaches it (quad_sub_mask, within the
-// list entry's quadrant bit) are listed in LDS in list order, and every row walks its own list: one iteration blends
-// one splat into each row's 16 pixels.  Rows whose list is done idle until the longest ends.  Against one splat per
-// iteration for the whole quadrant (round 4: kept as tools/variants/raster_fwd_quadpass.hip), a third fewer iterations
-// on the configs[1] frame (tools/fold_stats.py), at the price of per-lane LDS addresses.  Skipped pairs are exactly
-// the ones the reference discards (the sub-block test is conservative; each pair's own test decides), so every
-// pixel's result is unchanged bit for bit.
+// Front-to-back blend.  One wave64 per 8x8 quadrant of a 16x16 tile, one pixel per lane; the four
+// quadrant waves of a tile are independent blocks placed on one XCD (xcd_remap) so the tile's splat
+// reads hit the same L2.  Each 64-splat batch is staged in LDS; a ballot builds the wave-uniform bit
+// set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
+// visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
 // ------------------------------------------------------------------------------------------------
-template <bool INTERP, bool DEPTH, bool SEEN>  // SEEN: A.seen is set
+template <bool INTERP, bool DEPTH, bool SEEN>  // SEEN: A.seen is set (the per-splat mask is only kept then)
 __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 {
     if (guard_fail(gd)) return;
-    __shared__ float4 s_sp[3 * 64];  // splat j: [j] x, y, 1/depth, alpha threshold on e2; [64 + j] conic_q, opacity;
-                                     // [128 + j] r, g, b, 1/kids (hierarchy mode) or 1-based list position
-    __shared__ float s_t[64];        // interpolation t
-    __shared__ uint8_t s_list[4 * 64];
-    __shared__ uint8_t s_seen[64];
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, alpha threshold on e2
+    __shared__ float4 s_co[64];   // conic_q, opacity
+    __shared__ float4 s_col[64];  // r, g, b, 1/kids (hierarchy mode) or 1-based list position
+    __shared__ float s_t[64];     // interpolation t
     const int L = xcd_remap(blockIdx.x, 4 * A.T);
     const int tile = L >> 2, q = L & 3;
-    const int lane = threadIdx.x, grp = lane >> 4;
+    const int lane = threadIdx.x;
     const int qx0 = (tile % A.gx) * HLGS_TILE + 8 * (q & 1), qy0 = (tile / A.gx) * HLGS_TILE + 8 * (q >> 1);
-    const int qxl = 4 * (grp & 1) + (lane & 3), qyl = 4 * (grp >> 1) + ((lane >> 2) & 3);  // pixel in the quadrant
-    const int px = qx0 + qxl, py = qy0 + qyl;
+    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const float pxf = (float)px, pyf = (float)py;
     const float fqx = (float)qx0, fqy = (float)qy0;
     const uint2 range = A.ranges[tile];
-    if (SEEN) s_seen[lane] = 0;
 
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     uint32_t last = 0;
     // Backward chunk boundaries (bwd_chunk_len): at each, the transmittance is stored at once and the colour /
-    // inverse depth blended so far is kept, so that the end can store what was blended behind the boundary.  The split
-    // state is indexed by pixel (x + 8 y in the quadrant), as the blend backward reads it.
+    // inverse depth blended so far is kept, so that the end can store what was blended behind the boundary.
     const uint32_t clen = bwd_chunk_len(range.y - range.x);
-    float* st = A.split_state
-                    ? A.split_state + (size_t)tile * kBwdSplits * kSplitFloats + q * 5 * 64 + qxl + 8 * qyl
-                    : nullptr;
+    float* st = A.split_state ? A.split_state + (size_t)tile * kBwdSplits * kSplitFloats + q * 5 * 64 + lane : nullptr;
     uint32_t next_split = range.x + clen, nsplit = 0;
     float S0[kBwdSplits][4];
-    // per-lane predicates are kept as wave masks: compares are ballots of one v_cmp each, their combinations scalar mask
-    // operations, and selects read them back with inverse_ballot (ballots of inactive lanes are 0)
+    // per-lane predicates are kept as wave masks (the wave is always full): compares are ballots of one v_cmp
+    // each, their combinations scalar mask operations, and selects read them back with inverse_ballot
     uint64_t done = __builtin_amdgcn_ballot_w64(!(px < A.W && py < A.H));
     // Software pipeline over batches: while batch b is blended, the records of batch b+1 and the list entries of
     // batch b+2 are in flight.  Every lane issues every load (a lane with nothing to stage reads record 0, a lane
@@ -984,74 +975,59 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             next_split += clen;
         }
         const uint32_t pos = base + lane;
-        const uint32_t my_id = cur_id;
-        uint32_t sbm = 0;  // the sub-blocks of this quadrant the staged splat reaches
+        uint32_t my_id = 0;
+        bool hit = false;
         {
+            my_id = cur_id;
             const float4 co = make_float4(R0.z, R0.w, R1.x, R1.y);
-            // packed entries (pack_entries) carry the quadrant mask: only the splats reaching this quadrant are listed
-            const bool hit = cur_stage && (A.pack || touches_quad(R0.x, R0.y, co, R3.w, fqx, fqy));
-            if (hit) sbm = quad_sub_mask(splat_bands(R0.x, R0.y, co, R3.w), qx0, qy0);
+            // packed entries (pack_entries) carry the quadrant mask: only the splats reaching this quadrant are staged
+            hit = cur_stage && (A.pack || touches_quad(R0.x, R0.y, co, R3.w, fqx, fqy));
             // unconditional: lanes that stage nothing write slots no lane visits
-            s_sp[lane] = make_float4(R0.x, R0.y, DEPTH ? R2.y : 0.f, R3.w);
-            s_sp[64 + lane] = conic_q(co);
+            s_xy[lane] = make_float4(R0.x, R0.y, DEPTH ? R2.y : 0.f, R3.w);
+            s_co[lane] = conic_q(co);
             // .w: 1/kids in hierarchy mode, otherwise the splat's 1-based position in the tile list (n_contrib value)
-            s_sp[128 + lane] = make_float4(R1.z, R1.w, R2.x, INTERP ? R2.w : __uint_as_float(base - range.x + lane + 1));
+            s_col[lane] = make_float4(R1.z, R1.w, R2.x, INTERP ? R2.w : __uint_as_float(base - range.x + lane + 1));
             if (INTERP) s_t[lane] = R2.z;
             cur_stage = decode(nxt_entry, pos + 64, cur_id);
             const float4* rec = A.splat + 4 * (size_t)(cur_stage ? cur_id : 0u);
             R0 = rec[0]; R1 = rec[1]; R2 = rec[2]; R3 = rec[3];
             nxt_entry = entry_at(pos + 128);
         }
-        uint32_t nl[4];
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const bool in = (sbm >> g) & 1u;
-            const uint64_t M = __builtin_amdgcn_ballot_w64(in);
-            nl[g] = (uint32_t)__popcll(M);
-            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
-            if (in) s_list[64 * g + rank] = (uint8_t)lane;
-        }
+        uint64_t todo = __ballot(hit);
         __syncthreads();
-        const uint32_t nmax = max(max(nl[0], nl[1]), max(nl[2], nl[3]));
-        const uint32_t myn = grp == 0 ? nl[0] : grp == 1 ? nl[1] : grp == 2 ? nl[2] : nl[3];
-        const uint8_t* lst = s_list + 64 * grp;
-        for (uint32_t it = 0; it < nmax; it++) {
-            if (it < myn) {
-                const int j = lst[it];
-                const float4 xy = s_sp[j];
-                const float4 co = s_sp[64 + j];
-                const float4 c = s_sp[128 + j];
-                // straight-line step: the reference's skip / stop tests become lane predicates
-                const float e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
-                const float my_alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(e2));
-                float alpha = my_alpha;
-                if (INTERP) {
-                    const float tt = s_t[j];
-                    alpha = tt * my_alpha + (1.0f - tt) * (1.0f - __powf(1.0f - my_alpha, c.w));
-                }
-                const float test_T = Tt * (1 - alpha);
-                // alpha >= 1/255 (alpha_e2_threshold); a NaN e2 passes both tests, as in the reference
-                const uint64_t valid =
-                    ~done & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < xy.w);
-                const uint64_t tlow = __builtin_amdgcn_ballot_w64(test_T < 0.0001f);
-                const uint64_t blended = valid & ~tlow;
-                done |= valid & tlow;  // the pixel stops; this splat is not blended into it
-                const bool bl = __builtin_amdgcn_inverse_ballot_w64(blended);
-                const float wgt = bl ? alpha * Tt : 0.f;
-                C0 = fmaf(c.x, wgt, C0);
-                C1 = fmaf(c.y, wgt, C1);
-                C2 = fmaf(c.z, wgt, C2);
-                if (DEPTH) D = fmaf(xy.z, wgt, D);
-                Tt = bl ? test_T : Tt;
-                last = bl ? (INTERP ? base - range.x + (uint32_t)j + 1 : __float_as_uint(c.w)) : last;
-                if (SEEN && bl) s_seen[j] = 1;
+        uint64_t seen_mask = 0;
+        while (todo) {
+            int j;  // find-first-set and clear it: two SALU instead of four
+            asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(j), "+s"(todo));
+            const float4 xy = s_xy[j];
+            const float4 co = s_co[j];
+            const float4 c = s_col[j];
+            // straight-line step: the reference's skip / stop tests become lane predicates
+            const float e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
+            const float my_alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(e2));
+            float alpha = my_alpha;
+            if (INTERP) {
+                const float tt = s_t[j];
+                alpha = tt * my_alpha + (1.0f - tt) * (1.0f - __powf(1.0f - my_alpha, c.w));
             }
+            const float test_T = Tt * (1 - alpha);
+            // alpha >= 1/255 (alpha_e2_threshold); a NaN e2 passes both tests, as in the reference
+            const uint64_t valid = ~done & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < xy.w);
+            const uint64_t tlow = __builtin_amdgcn_ballot_w64(test_T < 0.0001f);
+            const uint64_t blended = valid & ~tlow;
+            done |= valid & tlow;  // the pixel stops; this splat is not blended into it
+            const bool bl = __builtin_amdgcn_inverse_ballot_w64(blended);
+            const float wgt = bl ? alpha * Tt : 0.f;
+            C0 = fmaf(c.x, wgt, C0);
+            C1 = fmaf(c.y, wgt, C1);
+            C2 = fmaf(c.z, wgt, C2);
+            if (DEPTH) D = fmaf(xy.z, wgt, D);
+            Tt = bl ? test_T : Tt;
+            last = bl ? (INTERP ? base - range.x + (uint32_t)j + 1 : __float_as_uint(c.w)) : last;
+            if (SEEN && blended) seen_mask |= 1ull << j;
         }
+        if (SEEN && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
         __syncthreads();
-        if (SEEN && s_seen[lane]) {
-            A.seen[my_id] = 1;
-            s_seen[lane] = 0;
-        }
     }
     if (px < A.W && py < A.H) {
         const size_t HW = (size_t)A.H * A.W;
