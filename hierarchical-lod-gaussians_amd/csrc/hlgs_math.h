@@ -371,55 +371,6 @@ __device__ __forceinline__ uint32_t rect_quad_masks(float x, float y, float4 co,
     }
     return m;
 }
-// The blend backward's 4x4 sub-block masks of one tile (origin tx0, ty0 in pixels): bit 4 k + g is set iff the footprint
-// reaches sub-block g (x half g & 1, y half g >> 1) of 8x8 quadrant k -- per 4-row band the footprint's x-extent (the
-// band form above with 4-row bands: the same tolerances, so just as conservative; tools/cull_check.py checks both
-// block sizes against brute force), tested against the band's four 4-column blocks.  Only a culling superset: the
-// backward decides every pair with the exact e2 >= thr test.
-__device__ __forceinline__ uint32_t sub_block_mask(const SplatBands& s, int tx0, int ty0)
-{
-#pragma clang fp contract(off)
-    if (s.mode) return s.mode == 1 ? 0xFFFFu : 0u;
-    const float u0 = (float)tx0 - s.x;
-    uint32_t m = 0;
-#pragma unroll
-    for (int band = 0; band < 4; band++) {
-        float lo, hi;
-        band_extent(s, (float)(ty0 + 4 * band) - s.y, lo, hi, 3.f);
-#pragma unroll
-        for (int col = 0; col < 4; col++) {
-            const float c0 = u0 + (float)(4 * col);
-            const int k = (col >> 1) + 2 * (band >> 1), g = (col & 1) + 2 * (band & 1);
-            if (hi >= c0 && lo <= c0 + 3.f) m |= 1u << (4 * k + g);
-        }
-    }
-    return m;
-}
-// The same for one 8x8 quadrant at (qx0, qy0): bit g = sub-block g (x half g & 1, y half g >> 1) is reached.
-__device__ __forceinline__ uint32_t quad_sub_mask(const SplatBands& s, int qx0, int qy0)
-{
-#pragma clang fp contract(off)
-    if (s.mode) return s.mode == 1 ? 0xFu : 0u;
-    const float u0 = (float)qx0 - s.x;
-    uint32_t m = 0;
-#pragma unroll
-    for (int band = 0; band < 2; band++) {
-        float lo, hi;
-        band_extent(s, (float)(qy0 + 4 * band) - s.y, lo, hi, 3.f);
-#pragma unroll
-        for (int col = 0; col < 2; col++) {
-            const float c0 = u0 + (float)(4 * col);
-            if (hi >= c0 && lo <= c0 + 3.f) m |= 1u << (col + 2 * band);
-        }
-    }
-    return m;
-}
-// The quadrant bits of a 4-bit mask spread over their four sub-block bits (bit k -> bits 4 k .. 4 k + 3).
-__device__ __forceinline__ uint32_t quad_to_sub(uint32_t qm)
-{
-    return ((qm & 1u) ? 0xFu : 0u) | ((qm & 2u) ? 0xF0u : 0u) | ((qm & 4u) ? 0xF00u : 0u) | ((qm & 8u) ? 0xF000u : 0u);
-}
-
 // The quadrant mask of rect tile r from the record's masks; tiles past kRectMasks take every quadrant (conservative).
 __device__ __forceinline__ uint32_t rect_tile_mask(uint32_t masks, uint32_t r)
 {
@@ -633,43 +584,54 @@ __device__ __forceinline__ float dpp(float v)
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW, 0xF, BC));
 }
 
-// Ten per-lane values summed over each 16-lane row of the wave (rows independently: in the blend backward each row is one
-// 4x4 sub-block working on its own splat).  Bank-masked DPP adds fold lanes l and l^8 (values 2i into banks 0-1, 2i+1
-// into banks 2-3), then l and l^4 (FOLD4: five values into three), and two quad_perm adds finish each bank: 22 DPP
-// adds.  Every lane of bank beta then holds t0 = the row total of value {0, 2, 1, 3}[beta], t1 = of {4, 6, 5, 7}[beta]
-// and t2 = of {8, 8, 9, 9}[beta] (tools/diag/reduce_layout.py simulates the lane operations).  A row whose lanes are
-// inactive (exec) is left alone: DPP row operations read within the row only.
-__device__ __forceinline__ void row_reduce10(const float (&v)[10], float& t0, float& t1, float& t2)
+// Reduce-scatter of ten per-lane values over the wave, cheapest stages first (issue costs measured by
+// tools/issue_probe.hip: a DPP add 4.2 cycles per wave instruction, a permlane swap 8.3).  Each fold halves the number
+// of registers: within each 16-lane row, bank-masked DPP adds fold lanes l and l^8 (values 2i into lanes 0-7, 2i+1 into
+// lanes 8-15), then l and l^4 (per 4-lane bank); permlane32 / permlane16 swaps fold the halves and the row pairs; a
+// quad_perm full reduction finishes each bank.  18 DPP + 3 permlane swaps, where ten full-wave reductions take
+// 12 DPP + 8 permlane swaps.  (row_ror:n: lane l reads lane l - n of its row.)  The result w holds, in every lane of
+// row rho and bank beta (lane = 16 rho + 4 beta + i), the total of value reduce10_index(rho, beta), or nothing for
+// rho = 3.
+__device__ __forceinline__ int reduce10_index(int rho, int beta)
 {
-    float s0, s1, s2, s3, s4;
+    const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
+    return rho == 0 ? cb : rho == 2 ? 4 + cb : rho == 1 ? ((beta & 1) ? -1 : 8 + (beta >> 1)) : -1;
+}
+// One instruction stream, ordered so that every DPP / permlane-swap source was written at least two instructions
+// earlier where the sequence allows it (the gfx950 VALU-write -> DPP-read and -> permlane-swap-read hazards need two
+// wait states): 4 s_nop where the builtin-and-asm version took 7.
+__device__ __forceinline__ float wave_reduce10_rs(const float (&v)[10])
+{
+    float s0, s1, s2, s3, s4, t0, t1, t2, z, w;
 #define HLGS_FOLD8(d, a, b)                                                                                        \
     "v_add_f32_dpp " d ", " a ", " a " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
     "v_add_f32_dpp " d ", " b ", " b " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
 #define HLGS_FOLD4(d, a, b)                                                                                        \
     "v_add_f32_dpp " d ", " a ", " a " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
     "v_add_f32_dpp " d ", " b ", " b " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
-#define HLGS_QUAD(d, p) "v_add_f32_dpp " d ", " d ", " d " quad_perm:" p " row_mask:0xf bank_mask:0xf\n\t"
-    // every DPP source was written at least two instructions earlier (the VALU-write -> DPP-read hazard), except the
-    // inputs, hence the leading s_nop
-    asm volatile("s_nop 1\n\t"
-                 HLGS_FOLD8("%0", "%8", "%9") HLGS_FOLD8("%1", "%10", "%11") HLGS_FOLD8("%2", "%12", "%13")
-                 HLGS_FOLD8("%3", "%14", "%15") HLGS_FOLD8("%4", "%16", "%17")
-                 HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%7", "%4", "%4")
-                 HLGS_QUAD("%5", "[1,0,3,2]") HLGS_QUAD("%6", "[1,0,3,2]") HLGS_QUAD("%7", "[1,0,3,2]")
-                 HLGS_QUAD("%5", "[2,3,0,1]") HLGS_QUAD("%6", "[2,3,0,1]") HLGS_QUAD("%7", "[2,3,0,1]")
-                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2)
+    asm volatile("s_nop 0\n\t"
+                 "v_mov_b32 %8, 0\n\t"
+                 HLGS_FOLD8("%0", "%10", "%11") HLGS_FOLD8("%1", "%12", "%13") HLGS_FOLD8("%2", "%14", "%15")
+                 HLGS_FOLD8("%3", "%16", "%17") HLGS_FOLD8("%4", "%18", "%19")
+                 HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%7", "%4", "%4")
+                 "v_permlane32_swap_b32 %5, %6\n\t"   // t0 (written two instructions back), t1
+                 "v_add_f32 %5, %5, %6\n\t"           // rows 0-1: t0, rows 2-3: t1
+                 "v_permlane32_swap_b32 %7, %8\n\t"   // t2 (two back), 0
+                 "v_add_f32 %7, %7, %8\n\t"           // rows 0-1: t2, rows 2-3: 0
+                 "s_nop 1\n\t"
+                 "v_permlane16_swap_b32 %5, %7\n\t"
+                 "v_add_f32 %9, %5, %7\n\t"           // row 0: t0, row 1: t2, row 2: t1, row 3: 0
+                 "s_nop 1\n\t"
+                 "v_add_f32_dpp %9, %9, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\t"
+                 "v_add_f32_dpp %9, %9, %9 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(z),
+                   "=&v"(w)
                  : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]),
                    "v"(v[9]));
 #undef HLGS_FOLD8
 #undef HLGS_FOLD4
-#undef HLGS_QUAD
-}
-// The moment whose row total lane position (bank beta = (l >> 2) & 3, p = l & 3) stores after row_reduce10: p = 0 -> t0,
-// p = 1 -> t1, p = 2 -> t2 in banks 0 and 2; -1: none.
-__host__ __device__ inline int row_reduce10_index(int beta, int p)
-{
-    const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
-    return p == 0 ? cb : p == 1 ? 4 + cb : (p == 2 && !(beta & 1)) ? 8 + (beta >> 1) : -1;
+    return w;
 }
 
 }  // namespace hlgs

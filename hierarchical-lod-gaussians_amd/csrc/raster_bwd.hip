@@ -4,18 +4,19 @@
 //   k_blend_bwd  <- renderCUDA<3> backward      backward.cu:498-721
 //
 // The reference issues one global float atomic per (pixel, Gaussian, gradient component)
-// (backward.cu:669-718).  Here each wave owns one tile (one chunk of its list): every 16-lane row folds its pixels'
-// moments with DPP adds, the rows' totals meet in LDS, and the per-(tile, Gaussian) partial is stored once -- with a
-// plain store -- into a Gaussian-major record slot (the Gaussian's point_offsets range, indexed by the tile's position
-// inside its rect).  k_gauss_bwd then sums each Gaussian's contiguous records in a fixed order, so the backward has
-// no global float atomics and is bitwise reproducible.
+// (backward.cu:669-718).  Here each wave owns one tile: every lane folds its four pixels, a
+// permlane/DPP reduce-scatter folds the 64 lanes, and the per-(tile, Gaussian) partial is stored once -- with
+// a plain store -- into a Gaussian-major record slot (the Gaussian's point_offsets range, indexed by
+// the tile's position inside its rect).  k_gauss_bwd then sums each Gaussian's contiguous records
+// in a fixed order, so the backward has no float atomics and is bitwise reproducible.
 //
-// The measured variants of rounds 1-4 (wave-wide quadrant passes, two splats per reduction, opacity-uniform clamp
-// branches, packed moments, Newton reciprocals, tile-major chunk order, non-temporal loads and stores, and the
-// traffic-attribution builds) are kept outside the product source as tools/variants/raster_bwd_r04.hip, built for A/B
-// by tools/build_variant.py; DESIGN.md section 5 records each result.
+// The measured variants of rounds 1-5 (two splats per reduction, opacity-uniform clamp branches, packed moments,
+// Newton reciprocals, tile-major chunk order, non-temporal loads and stores, the traffic-attribution builds, and round
+// 5's 4x4 sub-block lists) live outside the product source in tools/variants/ (raster_bwd_r04.hip, raster_bwd_sub4.hip),
+// built for A/B by tools/build_variant.py; DESIGN.md section 5 records each result.
 #include "hlgs_internal.h"
 #include "hlgs_math.h"
+
 
 namespace hlgs {
 
@@ -45,6 +46,7 @@ __device__ __forceinline__ float below_clamp(float test_alpha)
 {
     return __builtin_amdgcn_fmed3f(fmaf(-1099511627776.0f, test_alpha, 1088516587520.0f), 0.f, 1.f);
 }
+
 
 // One (pixel, splat) step of renderCUDA backward (backward.cu:601-718).  The splat's gradient terms
 // are linear in w = G * dL/dalpha and its moments over the pixels,
@@ -82,7 +84,7 @@ __device__ __forceinline__ BwdFront bwd_front(float dx, float dy, const float4& 
         G *= b;
     }
     f.G = G;
-    // as wave masks: one v_cmp per test, combined in SALU
+    // as wave masks: one v_cmp per test, combined in SALU (the wave is full)
     f.ok = ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < thr);
     return f;
 }
@@ -121,6 +123,17 @@ __device__ __forceinline__ void bwd_back(PixB& p, uint32_t li, const BwdFront& f
     }
 }
 
+// One quadrant pass: the front is computed for every lane ahead of the validity branch, so its transcendental latency
+// overlaps the compare -> SALU -> exec chain that decides the branch instead of following it.
+template <bool INTERP, bool DEPTH, bool ALT, int K>
+__device__ __forceinline__ void bwd_pass(PixB (&ps)[4], uint32_t li, float lx, float ly, const float4& xy, const float4& q,
+                                         const float4& col, float2 tf, float (&acc)[10])
+{
+    BwdFront f = bwd_front<INTERP, ALT>(xy.x - (lx + 8.f * (K & 1)), xy.y - (ly + 8.f * (K >> 1)), q, tf.x, tf.y, col.w);
+    asm volatile("" : "+v"(f.G), "+v"(f.r1m), "+v"(f.alpha));  // keep them above the branch
+    bwd_back<INTERP, DEPTH>(ps[K], li, f, col, xy.z, tf.x, tf.y, acc);
+}
+
 // Per-splat record from the reduced moments (see bwd_back); co = conic and opacity of the splat.
 __device__ __forceinline__ void finish_record(const float* m, float4 co, float ddelx_dx, float ddely_dy, float4& ra,
                                               float4& rb, float2& rc)
@@ -153,25 +166,19 @@ struct BwdArgs {
     const uint32_t* misc;  // Img::misc of the forward: [kMiscPack] says whether its point_list entries are packed
 };
 
-// One wave per (tile, chunk of the tile's list), back to front.  Chunk c covers list entries [c clen, min(count,
-// (c + 1) clen)) (bwd_chunk_len); blocks are ordered chunk-major, so the front chunks, where most pixels are still live,
-// start first.  A pixel whose last contributor lies behind the chunk's end starts from the forward's sample there
-// (transmittance, and what was blended behind it), otherwise from its final state, as the reference's single
-// back-to-front pass has it at that point.
-//
-// Lanes and sub-blocks.  Lane l owns one pixel of each 8x8 quadrant k: 16-lane row g = l >> 4 is the 4x4 sub-block g of
-// the quadrant (x half g & 1, y half g >> 1) and l & 15 the pixel inside it.  Each 64-splat batch is staged in LDS with
-// a 16-bit sub-block mask per splat (sub_block_mask, intersected with the list entry's quadrant mask); per quadrant and
-// sub-block, the splats that reach it and lie in front of its furthest contributor are listed in LDS, back to front.
-// Then, per quadrant, every row walks its own sub-block's list: one iteration is one (splat, 4x4 sub-block) pair per row,
-// the ten moments are folded over the row (row_reduce10) and the totals added into the splat's moments in LDS.  Rows
-// whose list is done idle until the quadrant's longest list ends.  Against 8x8 passes with one wave-wide reduction
-// per splat (round 4), this keeps 61% of the pass lanes busy instead of 36% (configs[1] frame, tools/fold_stats.py),
-// and one row reduction costs 22 DPP adds where the wave reduction cost 24 instructions and 4 wait states.  After
-// the batch, lane j finishes splat j's record and stores it.
-// Moments of one splat meet by LDS float atomics (ds_add_f32).  Each is one instruction of one wave: the order in which
-// the rows' totals arrive is fixed by the lists, so the sums are the same on every run.
-constexpr int kMStride = 65;  // moment rows padded to 65 floats (moment v of splat j at v kMStride + j: distinct banks)
+// One wave per (tile, chunk of the tile's list), back to front; lane owns pixel (lane & 7, lane >> 3) of each 8x8
+// quadrant.  Chunk c covers list entries [c clen, min(count, (c + 1) clen)) (bwd_chunk_len); blocks are ordered
+// chunk-major, so the front chunks, where most pixels are still live, start first.  A pixel whose last contributor
+// lies behind the chunk's end starts from the forward's sample there (transmittance, and what was blended behind
+// it), otherwise from its final state, as the reference's single back-to-front pass has it at that point.  Each
+// 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
+// whose n_contrib lies behind it) run bwd_pass, the ten moments are folded over the wave, and one record per
+// (tile, splat) is stored after the batch.
+// Round 5 measured 4x4 sub-block lists per 16-lane row here instead of 8x8 quadrant passes (tools/variants/
+// raster_bwd_sub4.hip): 61% of the pass lanes busy instead of 36%, but 697 against 354 us -- the per-row splat
+// indices put six LDS round trips and an LDS float atomic on every iteration, and the LDS became the limit (SQ_LDS_IDX_ACTIVE
+// 5.7x, SQ_WAIT_INST_LDS 256x); DESIGN.md section 5.
+constexpr int kMStride = 65;  // moment rows padded to 65 floats (see s_m below)
 template <bool INTERP, bool DEPTH, bool ALT>
 __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
 {
@@ -188,13 +195,17 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
     const float* __restrict__ dL_dinvdepths = A.dL_dinvdepths;
     const BwdScratch& rec = A.rec;
     const uint32_t pack = __builtin_amdgcn_readfirstlane(A.misc[kMiscPack]);  // as the forward packed them
-    __shared__ float4 s_sp[3 * 64];   // splat j: [j] x, y, 1/depth, -; [64 + j] conic_q, opacity; [128 + j] r, g, b, thr
-    __shared__ float2 s_tf[64];       // interpolation t, 1/kids (hierarchy mode)
-    __shared__ float s_m[10 * kMStride];
-    __shared__ uint8_t s_list[16 * 64];  // per (quadrant k, sub-block g): the batch positions j, back to front
+    __shared__ float4 s_xy[64];   // x, y, 1/depth, unused
+    __shared__ float4 s_q[64];    // -a/2, -b, -c/2 (times log2 e), opacity
+    __shared__ float4 s_col[64];  // r, g, b, alpha threshold on e2
+    __shared__ float2 s_tf[64];   // interpolation t, 1/kids
+    // reduced moments per splat (+ a spare row the non-storing lanes write), rows padded to kMStride = 65 floats: the
+    // ten lanes holding totals store moment v of splat j at kMStride v + j, on ten different banks ((v + j) mod 32),
+    // where a 64-float stride put all ten (and the spare row) on bank j mod 32
+    __shared__ float s_m[kMStride * 11];
     __shared__ float4 s_zero[3];
     if (threadIdx.x < 3) s_zero[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);  // ordered by the batch barrier
-    const int lane = threadIdx.x, grp = lane >> 4;
+    const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
     const int tx0 = tx * HLGS_TILE, ty0 = ty * HLGS_TILE;
     const uint2 range = ranges[tile];
@@ -203,24 +214,21 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
     const uint32_t c0 = (uint32_t)part * clen;  // chunk = local list positions [c0, cnt)
     if (c0 >= count) return;
     const uint32_t cnt = min(count, c0 + clen);
-    // this lane's pixel inside each quadrant, and the forward's lane for it (its split-state column)
-    const int qxl = 4 * (grp & 1) + (lane & 3), qyl = 4 * (grp >> 1) + ((lane >> 2) & 3);
     const float* __restrict__ st =
-        cnt < count ? A.split_state + (size_t)(tile * kBwdSplits + part) * kSplitFloats + qxl + 8 * qyl : nullptr;
+        cnt < count ? A.split_state + (size_t)(tile * kBwdSplits + part) * kSplitFloats + lane : nullptr;
     const size_t HW = (size_t)H * W;
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
-    const float lx = (float)(tx0 + qxl), ly = (float)(ty0 + qyl);
-    // the row total this lane adds into s_m (row_reduce10 layout), or none
-    const int wm_i = row_reduce10_index((lane >> 2) & 3, lane & 3);
-    const bool has_total = wm_i >= 0;
-    const int wmd = has_total ? kMStride * wm_i : 0;
-    const int psel = lane & 3;  // which of t0, t1, t2 it adds
-
+    const float lx = (float)(tx0 + (lane & 7)), ly = (float)(ty0 + (lane >> 3));
+    // the reduced moment this lane stores (wave_reduce10_rs layout) as an offset into s_m; lanes holding no total
+    // store into the spare row s_m[10 kMStride ..]
+    const int wm_i = (lane & 3) ? -1 : reduce10_index(lane >> 4, (lane >> 2) & 3);
+    const int wmd = wm_i < 0 ? 10 * kMStride : kMStride * wm_i;
+    // lane owns pixel (lane & 7, lane >> 3) of each 8x8 quadrant k
     PixB ps[4];
-    uint32_t slast[4];  // per quadrant, row-uniform: the furthest-back position any pixel of the row's sub-block needs
+    uint32_t qlast[4];  // wave-uniform per quadrant: furthest-back position any of its pixels needs
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int px = tx0 + 8 * (k & 1) + qxl, py = ty0 + 8 * (k >> 1) + qyl;
+        const int px = tx0 + 8 * (k & 1) + (lane & 7), py = ty0 + 8 * (k >> 1) + (lane >> 3);
         const bool inside = px < W && py < H;
         const size_t pid = (size_t)W * py + px;
         PixB& p = ps[k];
@@ -247,43 +255,35 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
             p.ARD = fmaf(tf, bgd, behind) / p.T;  // <accum_rec, dL/dpixel> (+ depth, + bg term) at the chunk's end
         }
         uint32_t m = min(p.last, cnt);
-        for (int off = 8; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-        slast[k] = m;
+        for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        qlast[k] = __builtin_amdgcn_readfirstlane(m);
     }
-    // the same per (quadrant, sub-block) as scalars: sl[4 k + g]
-    uint32_t sl[16];
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) sl[4 * k + r] = __builtin_amdgcn_readlane(slast[k], 16 * r);
-    uint32_t maxlast = 0;
-#pragma unroll
-    for (int b = 0; b < 16; b++) maxlast = max(maxlast, sl[b]);
+    const uint32_t maxlast = max(max(qlast[0], qlast[1]), max(qlast[2], qlast[3]));
 
     for (uint32_t b0 = 0; b0 < cnt - c0; b0 += 64) {
         // batch covers local positions cnt-1-b0 down to cnt-1-b0-(n-1), loaded back to front
         const int n = (int)min(64u, cnt - c0 - b0);
         const uint32_t li_top = cnt - 1 - b0;
         const bool lane_valid = lane < n;
-        uint32_t slot = 0, sbm = 0;
+        uint32_t slot = 0, qm = 0;
         float4 my_co = make_float4(0.f, 0.f, 0.f, 0.f);
         if (lane_valid) {
             const uint32_t pos = range.x + li_top - lane;
-            uint32_t id = point_list[pos], qm = 0xFu;
+            uint32_t id = point_list[pos], pm = 0;
             if (pack) {  // packed entry (pack_entries): the quadrant mask comes with it
-                qm = id & ((1u << kEntryShift) - 1u);
+                pm = id & ((1u << kEntryShift) - 1u);
                 id >>= kEntryShift;
             }
             const float4* sr = g.splat + 4 * (size_t)id;
             const uint32_t sbase = id ? g.point_offsets[id - 1] : 0u;
             const float4 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
             const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-            s_sp[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
-            s_sp[64 + lane] = conic_q(co);
-            s_sp[128 + lane] = make_float4(r1.z, r1.w, r2.x, r3.w);
-            if (INTERP) s_tf[lane] = make_float2(r2.z, r2.w);
+            qm = pack ? pm : quad_mask(r0.x, r0.y, co, r3.w, tx0, ty0);
+            s_xy[lane] = make_float4(r0.x, r0.y, DEPTH ? r2.y : 0.f, 0.f);
+            s_q[lane] = conic_q(co);
             my_co = co;
-            sbm = sub_block_mask(splat_bands(r0.x, r0.y, co, r3.w), tx0, ty0) & quad_to_sub(qm);
+            s_col[lane] = make_float4(r1.z, r1.w, r2.x, r3.w);
+            if (INTERP) s_tf[lane] = make_float2(r2.z, r2.w);
             const int x0 = __float_as_int(r3.y) & 0xffff, y0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
             const int w = __float_as_int(r3.z);
             // the Gaussian's record slots start at the exclusive scan of the rect sizes (point_offsets is inclusive)
@@ -291,57 +291,65 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
         }
 #pragma unroll
         for (int v = 0; v < 10; v++) s_m[kMStride * v + lane] = 0.f;
+        __syncthreads();
         // a batch entirely behind every pixel's last contributor leaves its records zero
         const uint32_t li_bot = li_top - (uint32_t)(n - 1);
-        uint32_t nl[16];  // list lengths (scalars)
         if (li_bot < maxlast) {
-            // splat j (this lane) goes to the list of sub-block b if its footprint reaches b and it lies in front of
-            // b's furthest contributor (li < sl[b]); lists are in ascending j, i.e. back to front
-            const uint32_t li = li_top - (uint32_t)lane;
-#pragma unroll
-            for (int b = 0; b < 16; b++) {
-                const bool in = ((sbm >> b) & 1u) && li < sl[b];
-                const uint64_t M = __builtin_amdgcn_ballot_w64(in);
-                nl[b] = (uint32_t)__popcll(M);
-                const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
-                if (in) s_list[64 * b + rank] = (uint8_t)lane;
-            }
-        }
-        __syncthreads();
-        if (li_bot < maxlast) {
+            // per quadrant, the wave-uniform set of the batch's splats to visit: footprint reaches the quadrant
+            // (quad_mask) and the splat lies in front of the quadrant's furthest contributor (li < qlast[k],
+            // i.e. j > li_top - qlast[k]); the loop then visits set bits only, with no LDS read to decide
+            uint64_t qv[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint32_t n0 = nl[4 * k], n1 = nl[4 * k + 1], n2 = nl[4 * k + 2], n3 = nl[4 * k + 3];
-                const uint32_t nmax = max(max(n0, n1), max(n2, n3));
-                const uint32_t myn = grp == 0 ? n0 : grp == 1 ? n1 : grp == 2 ? n2 : n3;
-                const uint8_t* lst = s_list + 64 * (4 * k + grp);
-                for (uint32_t it = 0; it < nmax; it++) {
-                    if (it < myn) {
-                        const int j = lst[it];
-                        const float4 xy = s_sp[j], q = s_sp[64 + j], col = s_sp[128 + j];
-                        const float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
-                        float acc[10];
-                        {  // zeroed by three LDS reads of a zero block (the LDS pipe has room; the VALU pipe is the limit)
-                            typedef float v4f __attribute__((ext_vector_type(4)));
-                            typedef __attribute__((address_space(3))) const volatile v4f lds_v4f;  // stays a ds_read
-                            lds_v4f* vz = (lds_v4f*)(s_zero);
-                            const v4f z0 = vz[0], z1 = vz[1], z2 = vz[2];
-                            acc[0] = z0.x; acc[1] = z0.y; acc[2] = z0.z; acc[3] = z0.w;
-                            acc[4] = z1.x; acc[5] = z1.y; acc[6] = z1.z; acc[7] = z1.w;
-                            acc[8] = z2.x; acc[9] = z2.y;
-                        }
-                        BwdFront f = bwd_front<INTERP, ALT>(xy.x - (lx + 8.f * (k & 1)), xy.y - (ly + 8.f * (k >> 1)), q,
-                                                            tf.x, tf.y, col.w);
-                        // the front above the validity branch: its transcendental latency overlaps the compare -> SALU
-                        // -> exec chain that decides the branch instead of following it
-                        asm volatile("" : "+v"(f.G), "+v"(f.r1m), "+v"(f.alpha));
-                        bwd_back<INTERP, DEPTH>(ps[k], li_top - (uint32_t)j, f, col, xy.z, tf.x, tf.y, acc);
-                        float t0, t1, t2;
-                        row_reduce10(acc, t0, t1, t2);
-                        const float t = psel == 0 ? t0 : psel == 1 ? t1 : t2;
-                        if (has_total) atomicAdd(&s_m[wmd + j], t);
+                uint64_t m = __ballot((qm >> k) & 1u);
+                if (li_top >= qlast[k]) {
+                    const uint32_t d = li_top - qlast[k];  // splats 0..d are behind every pixel of quadrant k
+                    m = d >= 63 ? 0ull : m & (~0ull << (d + 1));
+                }
+                qv[k] = m;
+            }
+            uint64_t todo = qv[0] | qv[1] | qv[2] | qv[3];
+            // Splat loop with the least scalar bookkeeping: the visited bit is cleared (s_bitset0), the next visited
+            // splat found by s_ff1 (-1 once none is left; its LDS reads use index 0 then), and every visited splat
+            // is reduced (0.15% of them have no valid pair), so no per-pass wave-mask tracking.
+            if (todo) {
+                int j = __builtin_ctzll(todo);
+                float4 xy = s_xy[j], co = s_q[j], col = s_col[j];
+                float2 tf = INTERP ? s_tf[j] : make_float2(0.f, 0.f);
+                // the quadrants splat jj visits, in quadrant order (uniform branches), into acc
+                auto passes = [&](int jj, const float4& pxy, const float4& pco, const float4& pcol, const float2& ptf,
+                                  float(&acc)[10]) {
+                    const uint32_t li = li_top - (uint32_t)jj;
+                    // the ten accumulators zeroed by three LDS reads of a zero block (the LDS pipe, ~29% busy here)
+                    // instead of five v_mov_b64 on the VALU pipe, which this kernel saturates
+                    {
+                        typedef float v4f __attribute__((ext_vector_type(4)));
+                        typedef __attribute__((address_space(3))) const volatile v4f lds_v4f;  // stays a ds_read
+                        lds_v4f* vz = (lds_v4f*)(s_zero);
+                        const v4f z0 = vz[0], z1 = vz[1], z2 = vz[2];
+                        acc[0] = z0.x; acc[1] = z0.y; acc[2] = z0.z; acc[3] = z0.w;
+                        acc[4] = z1.x; acc[5] = z1.y; acc[6] = z1.z; acc[7] = z1.w;
+                        acc[8] = z2.x; acc[9] = z2.y;
                     }
+                    if ((qv[0] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 0>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+                    if ((qv[1] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 1>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+                    if ((qv[2] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 2>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+                    if ((qv[3] >> jj) & 1u) bwd_pass<INTERP, DEPTH, ALT, 3>(ps, li, lx, ly, pxy, pco, pcol, ptf, acc);
+                };
+                float acc[10];  // (reset by passes() for every splat)
+                while (true) {
+                    int jn;  // s_ff1: -1 once todo is empty
+                    asm("s_bitset0_b64 %0, %2\n\ts_ff1_i32_b64 %1, %0" : "+s"(todo), "=s"(jn) : "s"(j));
+                    passes(j, xy, co, col, tf, acc);
+                    const int jl = jn < 0 ? 0 : jn;  // the next visited splat's LDS reads ahead of the reduction
+                    xy = s_xy[jl];
+                    co = s_q[jl];
+                    col = s_col[jl];
+                    if (INTERP) tf = s_tf[jl];
+                    // every lane stores (the spare row takes the non-totals), so no exec-mask change
+                    s_m[wmd + j] = wave_reduce10_rs(acc);
+                    if (jn < 0) break;
+                    j = jn;
                 }
             }
         }
@@ -361,6 +369,7 @@ __global__ void __launch_bounds__(64, 5) k_blend_bwd(BwdArgs A)
         __syncthreads();
     }
 }
+
 
 
 void launch_blend_bwd(const hlgs_raster_args& a, const Geom& g, const Img& im, const Bin& b, const BwdScratch& rs,

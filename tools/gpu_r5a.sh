@@ -5,4 +5,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_r5a.log
 # a parity failure (rc 1) still gets its timing; anything else (a crash, a time limit) ends the call here
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-SKIP_TESTS=1 VARIANTS="${VARIANTS:-r04bwd quadfwd pre04 gbwd04 C}" bash tools/ab_prof.sh
+SKIP_TESTS=1 VARIANTS="${VARIANTS:-sub4bwd sub4fwd pre04 gbwd04 C}" bash tools/ab_prof.sh

@@ -1,3 +1,4 @@
+// Round-5 measured variant: SH rows by LDS-DMA into a chunk-major image (115 against 97 us; see preprocess.hip).
 // preprocess.hip -- the forward's per-Gaussian preprocess for gfx950.
 //
 // Reference semantics (submodules/hierarchy-rasterizer/cuda_rasterizer):
@@ -256,45 +257,37 @@ __device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const
 // Jacobian from LDS while wave 0 classifies the footprint quadrants, and after a second barrier wave 0 writes the
 // records.  The SH rows' HBM latency overlaps the geometry instead of following it, and one 12 KB LDS stage keeps two
 // waves busy.  Same arithmetic, same outputs.
-// The rows arrive through registers: every lane loads consecutive float4s of the block's contiguous rows (1 KiB per
-// wave instruction) and stores them into LDS rows of odd stride (kShStride), so that each lane's own row walk hits
-// distinct banks.  (Round 5 measured LDS-DMA into a chunk-major image instead -- conflict-free b128 reads, no staging
-// registers: 115 against 97 us, because the DMA's source side then reads 16 bytes per lane at the row stride, 64 lines
-// per wave instruction instead of 8; tools/variants/preprocess_dma.hip.)
+//
+// Rows of a multiple of 4 floats (SH degree 1 and 3; the alt rasterizer's degree 2) arrive by LDS-DMA
+// (global_load_lds_dwordx4, no VGPRs, no LDS store instructions) into a chunk-major image: chunk q of row r at float4
+// q * 64 + r, so that one DMA instruction (64 lanes x 16 bytes, lane-linear in LDS) moves chunk q of all 64 rows, and
+// lane r reads its row with conflict-free ds_read_b128 (16 consecutive lanes, 16 consecutive chunks).  Other row lengths
+// go through registers into rows of odd stride (kShStride).
 template <int M3T>
 __device__ __forceinline__ void sh_rows_load_contig(const float* gbase, float* lds, int n, int lane, int m3)
 {
-    if constexpr (M3T > 0 && M3T % 4 == 0) {
-        constexpr int Q = M3T / 4;
-        float4 v[Q];
-#pragma unroll
-        for (int k = 0; k < Q; k++) {
-            const int f = lane + 64 * k;
-            v[k] = f < n * Q ? reinterpret_cast<const float4*>(gbase)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int k = 0; k < Q; k++) {
-            const int f = lane + 64 * k;
-            if (f < n * Q) {
-                const int r = f / Q, q = f - r * Q;
-                float* lp = lds + r * kShStride + 4 * q;
-                lp[0] = v[k].x; lp[1] = v[k].y; lp[2] = v[k].z; lp[3] = v[k].w;
-            }
-        }
-    } else {
-        const int M3 = M3T ? M3T : m3;
-        for (int f = lane; f < n * M3; f += 64) {
-            const int r = f / M3, q = f - r * M3;
-            lds[r * kShStride + q] = gbase[f];
-        }
+    const int M3 = M3T ? M3T : m3;
+    for (int f = lane; f < n * M3; f += 64) {
+        const int r = f / M3, q = f - r * M3;
+        lds[r * kShStride + q] = gbase[f];
     }
+}
+template <int M3T>
+__device__ __forceinline__ void sh_rows_dma(const float* gbase, float4* lds, int n, int lane)
+{
+    typedef __attribute__((address_space(3))) void lds_t;
+    constexpr int Q = M3T / 4;
+    const float* src = gbase + (size_t)min(lane, n - 1) * M3T;  // rows past P re-read the block's last row (unused)
+#pragma unroll
+    for (int q = 0; q < Q; q++) __builtin_amdgcn_global_load_lds((const void*)(src + 4 * q), (lds_t*)(lds + q * 64), 16, 0, 0);
 }
 
 template <bool ALT, int M3T>
 __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
                                                         int gy, float fx, float fy, ZeroJob z)
 {
-    __shared__ float s_rows[64 * kShStride];
+    constexpr bool DMA = M3T > 0 && M3T % 4 == 0;
+    __shared__ float s_rows[DMA ? 4 * (M3T / 4) * 64 : 64 * kShStride];
     __shared__ float4 s_col[64];  // r, g, b, clamp bits
     __shared__ int s_need[64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -309,7 +302,8 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
         s_need[lane] = need;
     } else {
         const int n = min(64, a.P - t0);
-        sh_rows_load_contig<M3T>(a.shs + (size_t)t0 * M3, s_rows, n, lane, M3);
+        if (DMA) sh_rows_dma<M3T>(a.shs + (size_t)t0 * M3, reinterpret_cast<float4*>(s_rows), n, lane);
+        else sh_rows_load_contig<M3T>(a.shs + (size_t)t0 * M3, s_rows, n, lane, M3);
         // the colour's own inputs in the same round trip as the rows (not behind the barrier)
         if (t_idx < a.P) {
             mean_r = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
@@ -323,8 +317,14 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
     if (wave == 1) {
         if (s_need[lane]) {
             // coefficient c of this lane's row (the full index: the alt rasterizer's 0 is dc)
-            const float* row = s_rows + lane * kShStride;
-            auto rowf = [&](int f) -> float { return row[f]; };
+            auto rowf = [&](int f) -> float {
+                if constexpr (DMA) {
+                    const float4 v = reinterpret_cast<const float4*>(s_rows)[(f >> 2) * 64 + lane];
+                    return (f & 3) == 0 ? v.x : (f & 3) == 1 ? v.y : (f & 3) == 2 ? v.z : v.w;
+                } else {
+                    return s_rows[lane * kShStride + f];
+                }
+            };
             auto shv = [&](int c) {
                 if (ALT) return c == 0 ? dc0 : mk(rowf(3 * c - 3), rowf(3 * c - 2), rowf(3 * c - 1));
                 return mk(rowf(3 * c), rowf(3 * c + 1), rowf(3 * c + 2));

@@ -1,7 +1,7 @@
 // Round-4 blend backward (wave-wide 8x8 quadrant passes, one wave reduce-scatter per visited splat) with every
 // measured variant switch of rounds 1-4, kept outside the product source for A/B builds:
 //   python tools/build_variant.py r04 tools/variants/raster_bwd_r04.hip raster_bwd.hip
-// DESIGN.md section 5 records the result of each switch.  The wave reduce-scatters it uses are defined below.
+// DESIGN.md section 5 records the result of each switch.  The twenty-moment reduce-scatter of its HLGS_BWD_PAIR option is defined below.
 // raster_bwd.hip -- the blend backward for gfx950 (the per-Gaussian kernels are in gauss_bwd.hip).
 //
 // Reference semantics (submodules/hierarchy-rasterizer/cuda_rasterizer):
@@ -28,56 +28,6 @@
 #endif
 
 namespace hlgs {
-
-// Reduce-scatter of ten per-lane values over the wave, cheapest stages first (issue costs measured by
-// tools/issue_probe.hip: a DPP add 4.2 cycles per wave instruction, a permlane swap 8.3).  Each fold halves the number
-// of registers: within each 16-lane row, bank-masked DPP adds fold lanes l and l^8 (values 2i into lanes 0-7, 2i+1 into
-// lanes 8-15), then l and l^4 (per 4-lane bank); permlane32 / permlane16 swaps fold the halves and the row pairs; a
-// quad_perm full reduction finishes each bank.  18 DPP + 3 permlane swaps, where ten full-wave reductions take
-// 12 DPP + 8 permlane swaps.  (row_ror:n: lane l reads lane l - n of its row.)  The result w holds, in every lane of
-// row rho and bank beta (lane = 16 rho + 4 beta + i), the total of value reduce10_index(rho, beta), or nothing for
-// rho = 3.
-__device__ __forceinline__ int reduce10_index(int rho, int beta)
-{
-    const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
-    return rho == 0 ? cb : rho == 2 ? 4 + cb : rho == 1 ? ((beta & 1) ? -1 : 8 + (beta >> 1)) : -1;
-}
-// One instruction stream, ordered so that every DPP / permlane-swap source was written at least two instructions
-// earlier where the sequence allows it (the gfx950 VALU-write -> DPP-read and -> permlane-swap-read hazards need two
-// wait states): 4 s_nop where the builtin-and-asm version took 7.
-__device__ __forceinline__ float wave_reduce10_rs(const float (&v)[10])
-{
-    float s0, s1, s2, s3, s4, t0, t1, t2, z, w;
-#define HLGS_FOLD8(d, a, b)                                                                                        \
-    "v_add_f32_dpp " d ", " a ", " a " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
-    "v_add_f32_dpp " d ", " b ", " b " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
-#define HLGS_FOLD4(d, a, b)                                                                                        \
-    "v_add_f32_dpp " d ", " a ", " a " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
-    "v_add_f32_dpp " d ", " b ", " b " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
-    asm volatile("s_nop 0\n\t"
-                 "v_mov_b32 %8, 0\n\t"
-                 HLGS_FOLD8("%0", "%10", "%11") HLGS_FOLD8("%1", "%12", "%13") HLGS_FOLD8("%2", "%14", "%15")
-                 HLGS_FOLD8("%3", "%16", "%17") HLGS_FOLD8("%4", "%18", "%19")
-                 HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%7", "%4", "%4")
-                 "v_permlane32_swap_b32 %5, %6\n\t"   // t0 (written two instructions back), t1
-                 "v_add_f32 %5, %5, %6\n\t"           // rows 0-1: t0, rows 2-3: t1
-                 "v_permlane32_swap_b32 %7, %8\n\t"   // t2 (two back), 0
-                 "v_add_f32 %7, %7, %8\n\t"           // rows 0-1: t2, rows 2-3: 0
-                 "s_nop 1\n\t"
-                 "v_permlane16_swap_b32 %5, %7\n\t"
-                 "v_add_f32 %9, %5, %7\n\t"           // row 0: t0, row 1: t2, row 2: t1, row 3: 0
-                 "s_nop 1\n\t"
-                 "v_add_f32_dpp %9, %9, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 1\n\t"
-                 "v_add_f32_dpp %9, %9, %9 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
-                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(z),
-                   "=&v"(w)
-                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]),
-                   "v"(v[9]));
-#undef HLGS_FOLD8
-#undef HLGS_FOLD4
-    return w;
-}
 
 // Reduce-scatter of two splats' ten moments each (a = values 0-9, b = values 10-19) in one pass: FOLD8 of the ten
 // pairs, FOLD4 of five, permlane32 swaps fold 5 -> 3, permlane16 swaps 3 -> 2, quad_perm adds finish both.  34 DPP adds,

@@ -16,6 +16,95 @@
 
 namespace hlgs {
 
+// The blend backward's 4x4 sub-block masks of one tile (origin tx0, ty0 in pixels): bit 4 k + g is set iff the footprint
+// reaches sub-block g (x half g & 1, y half g >> 1) of 8x8 quadrant k -- per 4-row band the footprint's x-extent (the
+// band form above with 4-row bands: the same tolerances, so just as conservative; tools/cull_check.py checks both
+// block sizes against brute force), tested against the band's four 4-column blocks.  Only a culling superset: the
+// backward decides every pair with the exact e2 >= thr test.
+__device__ __forceinline__ uint32_t sub_block_mask(const SplatBands& s, int tx0, int ty0)
+{
+#pragma clang fp contract(off)
+    if (s.mode) return s.mode == 1 ? 0xFFFFu : 0u;
+    const float u0 = (float)tx0 - s.x;
+    uint32_t m = 0;
+#pragma unroll
+    for (int band = 0; band < 4; band++) {
+        float lo, hi;
+        band_extent(s, (float)(ty0 + 4 * band) - s.y, lo, hi, 3.f);
+#pragma unroll
+        for (int col = 0; col < 4; col++) {
+            const float c0 = u0 + (float)(4 * col);
+            const int k = (col >> 1) + 2 * (band >> 1), g = (col & 1) + 2 * (band & 1);
+            if (hi >= c0 && lo <= c0 + 3.f) m |= 1u << (4 * k + g);
+        }
+    }
+    return m;
+}
+// The same for one 8x8 quadrant at (qx0, qy0): bit g = sub-block g (x half g & 1, y half g >> 1) is reached.
+__device__ __forceinline__ uint32_t quad_sub_mask(const SplatBands& s, int qx0, int qy0)
+{
+#pragma clang fp contract(off)
+    if (s.mode) return s.mode == 1 ? 0xFu : 0u;
+    const float u0 = (float)qx0 - s.x;
+    uint32_t m = 0;
+#pragma unroll
+    for (int band = 0; band < 2; band++) {
+        float lo, hi;
+        band_extent(s, (float)(qy0 + 4 * band) - s.y, lo, hi, 3.f);
+#pragma unroll
+        for (int col = 0; col < 2; col++) {
+            const float c0 = u0 + (float)(4 * col);
+            if (hi >= c0 && lo <= c0 + 3.f) m |= 1u << (col + 2 * band);
+        }
+    }
+    return m;
+}
+// The quadrant bits of a 4-bit mask spread over their four sub-block bits (bit k -> bits 4 k .. 4 k + 3).
+__device__ __forceinline__ uint32_t quad_to_sub(uint32_t qm)
+{
+    return ((qm & 1u) ? 0xFu : 0u) | ((qm & 2u) ? 0xF0u : 0u) | ((qm & 4u) ? 0xF00u : 0u) | ((qm & 8u) ? 0xF000u : 0u);
+}
+
+// Ten per-lane values summed over each 16-lane row of the wave (rows independently: in the blend backward each row is one
+// 4x4 sub-block working on its own splat).  Bank-masked DPP adds fold lanes l and l^8 (values 2i into banks 0-1, 2i+1
+// into banks 2-3), then l and l^4 (FOLD4: five values into three), and two quad_perm adds finish each bank: 22 DPP
+// adds.  Every lane of bank beta then holds t0 = the row total of value {0, 2, 1, 3}[beta], t1 = of {4, 6, 5, 7}[beta]
+// and t2 = of {8, 8, 9, 9}[beta] (tools/diag/reduce_layout.py simulates the lane operations).  A row whose lanes are
+// inactive (exec) is left alone: DPP row operations read within the row only.
+__device__ __forceinline__ void row_reduce10(const float (&v)[10], float& t0, float& t1, float& t2)
+{
+    float s0, s1, s2, s3, s4;
+#define HLGS_FOLD8(d, a, b)                                                                                        \
+    "v_add_f32_dpp " d ", " a ", " a " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"                                  \
+    "v_add_f32_dpp " d ", " b ", " b " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+#define HLGS_FOLD4(d, a, b)                                                                                        \
+    "v_add_f32_dpp " d ", " a ", " a " row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                                 \
+    "v_add_f32_dpp " d ", " b ", " b " row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
+#define HLGS_QUAD(d, p) "v_add_f32_dpp " d ", " d ", " d " quad_perm:" p " row_mask:0xf bank_mask:0xf\n\t"
+    // every DPP source was written at least two instructions earlier (the VALU-write -> DPP-read hazard), except the
+    // inputs, hence the leading s_nop
+    asm volatile("s_nop 1\n\t"
+                 HLGS_FOLD8("%0", "%8", "%9") HLGS_FOLD8("%1", "%10", "%11") HLGS_FOLD8("%2", "%12", "%13")
+                 HLGS_FOLD8("%3", "%14", "%15") HLGS_FOLD8("%4", "%16", "%17")
+                 HLGS_FOLD4("%5", "%0", "%1") HLGS_FOLD4("%6", "%2", "%3") HLGS_FOLD4("%7", "%4", "%4")
+                 HLGS_QUAD("%5", "[1,0,3,2]") HLGS_QUAD("%6", "[1,0,3,2]") HLGS_QUAD("%7", "[1,0,3,2]")
+                 HLGS_QUAD("%5", "[2,3,0,1]") HLGS_QUAD("%6", "[2,3,0,1]") HLGS_QUAD("%7", "[2,3,0,1]")
+                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(t0), "=&v"(t1), "=&v"(t2)
+                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]),
+                   "v"(v[9]));
+#undef HLGS_FOLD8
+#undef HLGS_FOLD4
+#undef HLGS_QUAD
+}
+// The moment whose row total lane position (bank beta = (l >> 2) & 3, p = l & 3) stores after row_reduce10: p = 0 -> t0,
+// p = 1 -> t1, p = 2 -> t2 in banks 0 and 2; -1: none.
+__host__ __device__ inline int row_reduce10_index(int beta, int p)
+{
+    const int cb = ((beta & 1) << 1) | (beta >> 1);  // 0, 2, 1, 3
+    return p == 0 ? cb : p == 1 ? 4 + cb : (p == 2 && !(beta & 1)) ? 8 + (beta >> 1) : -1;
+}
+
+
 // ------------------------------------------------------------------------------------------------
 // Tile binning with block-level LDS histograms.  A block owns BG consecutive Gaussians (bin_gauss); its
 // instances are counted per tile in LDS and each non-empty bin costs one coalesced device atomic,
@@ -905,43 +994,51 @@ struct FwdArgs {
 };
 
 // ------------------------------------------------------------------------------------------------
-// Front-to-back blend.  One wave64 per 8x8 quadrant of a 16x16 tile, one pixel per lane; the four
-// quadrant waves of a tile are independent blocks placed on one XCD (xcd_remap) so the tile's splat
-// reads hit the same L2.  Each 64-splat batch is staged in LDS; a ballot builds the wave-uniform bit
-// set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
-// visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
-// Round 5 measured per-row 4x4 sub-block lists instead (tools/variants/raster_fwd_sub4.hip): a third fewer
-// iterations, but 209 against 151 us -- per-lane LDS addresses and the row bookkeeping cost more VALU than the
-// iterations saved.
+// Front-to-back blend.  One wave64 per 8x8 quadrant of a 16x16 tile, one pixel per lane; the four quadrant waves of a
+// tile are independent blocks placed on one XCD (xcd_remap) so the tile's splat reads hit the same L2.  Each 64-splat
+// batch is staged in LDS.  Lanes form four 16-lane rows, row g being the quadrant's 4x4 sub-block g (x half g & 1, y
+// half g >> 1); per sub-block, the staged splats whose alpha >= 1/255 footprint reaches it (quad_sub_mask, within the
+// list entry's quadrant bit) are listed in LDS in list order, and every row walks its own list: one iteration blends
+// one splat into each row's 16 pixels.  Rows whose list is done idle until the longest ends.  Against one splat per
+// iteration for the whole quadrant (round 4: kept as tools/variants/raster_fwd_quadpass.hip), a third fewer iterations
+// on the configs[1] frame (tools/fold_stats.py), at the price of per-lane LDS addresses.  Skipped pairs are exactly
+// the ones the reference discards (the sub-block test is conservative; each pair's own test decides), so every
+// pixel's result is unchanged bit for bit.
 // ------------------------------------------------------------------------------------------------
-template <bool INTERP, bool DEPTH, bool SEEN>  // SEEN: A.seen is set (the per-splat mask is only kept then)
+template <bool INTERP, bool DEPTH, bool SEEN>  // SEEN: A.seen is set
 __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
 {
     if (guard_fail(gd)) return;
-    __shared__ float4 s_xy[64];   // x, y, 1/depth, alpha threshold on e2
-    __shared__ float4 s_co[64];   // conic_q, opacity
-    __shared__ float4 s_col[64];  // r, g, b, 1/kids (hierarchy mode) or 1-based list position
-    __shared__ float s_t[64];     // interpolation t
+    __shared__ float4 s_sp[3 * 64];  // splat j: [j] x, y, 1/depth, alpha threshold on e2; [64 + j] conic_q, opacity;
+                                     // [128 + j] r, g, b, 1/kids (hierarchy mode) or 1-based list position
+    __shared__ float s_t[64];        // interpolation t
+    __shared__ uint8_t s_list[4 * 64];
+    __shared__ uint8_t s_seen[64];
     const int L = xcd_remap(blockIdx.x, 4 * A.T);
     const int tile = L >> 2, q = L & 3;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x, grp = lane >> 4;
     const int qx0 = (tile % A.gx) * HLGS_TILE + 8 * (q & 1), qy0 = (tile / A.gx) * HLGS_TILE + 8 * (q >> 1);
-    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+    const int qxl = 4 * (grp & 1) + (lane & 3), qyl = 4 * (grp >> 1) + ((lane >> 2) & 3);  // pixel in the quadrant
+    const int px = qx0 + qxl, py = qy0 + qyl;
     const float pxf = (float)px, pyf = (float)py;
     const float fqx = (float)qx0, fqy = (float)qy0;
     const uint2 range = A.ranges[tile];
+    if (SEEN) s_seen[lane] = 0;
 
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
     uint32_t last = 0;
     // Backward chunk boundaries (bwd_chunk_len): at each, the transmittance is stored at once and the colour /
-    // inverse depth blended so far is kept, so that the end can store what was blended behind the boundary.
+    // inverse depth blended so far is kept, so that the end can store what was blended behind the boundary.  The split
+    // state is indexed by pixel (x + 8 y in the quadrant), as the blend backward reads it.
     const uint32_t clen = bwd_chunk_len(range.y - range.x);
-    float* st = A.split_state ? A.split_state + (size_t)tile * kBwdSplits * kSplitFloats + q * 5 * 64 + lane : nullptr;
+    float* st = A.split_state
+                    ? A.split_state + (size_t)tile * kBwdSplits * kSplitFloats + q * 5 * 64 + qxl + 8 * qyl
+                    : nullptr;
     uint32_t next_split = range.x + clen, nsplit = 0;
     float S0[kBwdSplits][4];
-    // per-lane predicates are kept as wave masks (the wave is always full): compares are ballots of one v_cmp
-    // each, their combinations scalar mask operations, and selects read them back with inverse_ballot
-    uint64_t done = __builtin_amdgcn_ballot_w64(!(px < A.W && py < A.H));
+    // the pixel has stopped (T < 1e-4) or lies outside the image: a per-lane flag, since rows iterate independently (a
+    // wave mask carried through the divergent row loop would be a per-lane copy that goes stale for the other rows)
+    bool done = !(px < A.W && py < A.H);
     // Software pipeline over batches: while batch b is blended, the records of batch b+1 and the list entries of
     // batch b+2 are in flight.  Every lane issues every load (a lane with nothing to stage reads record 0, a lane
     // past the list end re-reads the list's last entry), so the loads retire in a fixed order and the wait at the top
@@ -966,7 +1063,7 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
         R0 = rec[0]; R1 = rec[1]; R2 = rec[2]; R3 = rec[3];
     }
     for (uint32_t base = range.x; base < range.y; base += 64) {
-        if (done == ~0ull) break;
+        if (__builtin_amdgcn_ballot_w64(!done) == 0) break;
         if (base == next_split && st) {  // wave-uniform; never past kBwdSplits boundaries (bwd_chunk_len)
             st[nsplit * kSplitFloats] = Tt;
 #pragma unroll
@@ -976,59 +1073,80 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             next_split += clen;
         }
         const uint32_t pos = base + lane;
-        uint32_t my_id = 0;
-        bool hit = false;
+        const uint32_t my_id = cur_id;
+        uint32_t sbm = 0;  // the sub-blocks of this quadrant the staged splat reaches
         {
-            my_id = cur_id;
             const float4 co = make_float4(R0.z, R0.w, R1.x, R1.y);
-            // packed entries (pack_entries) carry the quadrant mask: only the splats reaching this quadrant are staged
-            hit = cur_stage && (A.pack || touches_quad(R0.x, R0.y, co, R3.w, fqx, fqy));
+            // packed entries (pack_entries) carry the quadrant mask: only the splats reaching this quadrant are listed
+            const bool hit = cur_stage && (A.pack || touches_quad(R0.x, R0.y, co, R3.w, fqx, fqy));
+            if (hit) sbm = quad_sub_mask(splat_bands(R0.x, R0.y, co, R3.w), qx0, qy0);
             // unconditional: lanes that stage nothing write slots no lane visits
-            s_xy[lane] = make_float4(R0.x, R0.y, DEPTH ? R2.y : 0.f, R3.w);
-            s_co[lane] = conic_q(co);
+            s_sp[lane] = make_float4(R0.x, R0.y, DEPTH ? R2.y : 0.f, R3.w);
+            s_sp[64 + lane] = conic_q(co);
             // .w: 1/kids in hierarchy mode, otherwise the splat's 1-based position in the tile list (n_contrib value)
-            s_col[lane] = make_float4(R1.z, R1.w, R2.x, INTERP ? R2.w : __uint_as_float(base - range.x + lane + 1));
+            s_sp[128 + lane] = make_float4(R1.z, R1.w, R2.x, INTERP ? R2.w : __uint_as_float(base - range.x + lane + 1));
             if (INTERP) s_t[lane] = R2.z;
             cur_stage = decode(nxt_entry, pos + 64, cur_id);
             const float4* rec = A.splat + 4 * (size_t)(cur_stage ? cur_id : 0u);
             R0 = rec[0]; R1 = rec[1]; R2 = rec[2]; R3 = rec[3];
             nxt_entry = entry_at(pos + 128);
         }
-        uint64_t todo = __ballot(hit);
-        __syncthreads();
-        uint64_t seen_mask = 0;
-        while (todo) {
-            int j;  // find-first-set and clear it: two SALU instead of four
-            asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(j), "+s"(todo));
-            const float4 xy = s_xy[j];
-            const float4 co = s_co[j];
-            const float4 c = s_col[j];
-            // straight-line step: the reference's skip / stop tests become lane predicates
-            const float e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
-            const float my_alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(e2));
-            float alpha = my_alpha;
-            if (INTERP) {
-                const float tt = s_t[j];
-                alpha = tt * my_alpha + (1.0f - tt) * (1.0f - __powf(1.0f - my_alpha, c.w));
-            }
-            const float test_T = Tt * (1 - alpha);
-            // alpha >= 1/255 (alpha_e2_threshold); a NaN e2 passes both tests, as in the reference
-            const uint64_t valid = ~done & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < xy.w);
-            const uint64_t tlow = __builtin_amdgcn_ballot_w64(test_T < 0.0001f);
-            const uint64_t blended = valid & ~tlow;
-            done |= valid & tlow;  // the pixel stops; this splat is not blended into it
-            const bool bl = __builtin_amdgcn_inverse_ballot_w64(blended);
-            const float wgt = bl ? alpha * Tt : 0.f;
-            C0 = fmaf(c.x, wgt, C0);
-            C1 = fmaf(c.y, wgt, C1);
-            C2 = fmaf(c.z, wgt, C2);
-            if (DEPTH) D = fmaf(xy.z, wgt, D);
-            Tt = bl ? test_T : Tt;
-            last = bl ? (INTERP ? base - range.x + (uint32_t)j + 1 : __float_as_uint(c.w)) : last;
-            if (SEEN && blended) seen_mask |= 1ull << j;
+        uint32_t nl[4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const bool in = (sbm >> g) & 1u;
+            const uint64_t M = __builtin_amdgcn_ballot_w64(in);
+            nl[g] = (uint32_t)__popcll(M);
+            const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+            if (in) s_list[64 * g + rank] = (uint8_t)lane;
         }
-        if (SEEN && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
         __syncthreads();
+        const uint32_t nmax = max(max(nl[0], nl[1]), max(nl[2], nl[3]));
+        const uint32_t myn = grp == 0 ? nl[0] : grp == 1 ? nl[1] : grp == 2 ? nl[2] : nl[3];
+        const uint8_t* lst = s_list + 64 * grp;
+        // Software pipeline over the row's list: iteration it blends splat j(it) while the LDS reads of splat j(it + 1)
+        // and of list entry it + 2 are in flight (each iteration otherwise waits for two dependent LDS round trips).
+        // Reads past the list's end fetch unused entries (masked to a staged splat).
+        int jn = lst[0] & 63, jnn = lst[1] & 63;
+        float4 xy = s_sp[jn], co = s_sp[64 + jn], c = s_sp[128 + jn];
+        float tn = INTERP ? s_t[jn] : 0.f;
+        for (uint32_t it = 0; it < nmax; it++) {
+            if (it < myn) {
+                const int j = jn;
+                const float4 cxy = xy, cco = co, cc = c;
+                const float ct = tn;
+                jn = jnn;
+                jnn = lst[min(it + 2, 63u)] & 63;
+                xy = s_sp[jn];
+                co = s_sp[64 + jn];
+                c = s_sp[128 + jn];
+                if (INTERP) tn = s_t[jn];
+                // straight-line step: the reference's skip / stop tests become lane predicates
+                const float e2 = splat_e2(cco, cxy.x - pxf, cxy.y - pyf);  // power * log2(e)
+                const float my_alpha = fminf(0.99f, cco.w * __builtin_amdgcn_exp2f(e2));
+                float alpha = my_alpha;
+                if (INTERP) alpha = ct * my_alpha + (1.0f - ct) * (1.0f - __powf(1.0f - my_alpha, cc.w));
+                const float test_T = Tt * (1 - alpha);
+                // alpha >= 1/255 (alpha_e2_threshold); a NaN e2 passes both tests, as in the reference
+                const bool valid = !done && !(e2 > 0.0f) && !(e2 < cxy.w);
+                const bool tlow = test_T < 0.0001f;
+                const bool bl = valid && !tlow;
+                done = done || (valid && tlow);  // the pixel stops; this splat is not blended into it
+                const float wgt = bl ? alpha * Tt : 0.f;
+                C0 = fmaf(cc.x, wgt, C0);
+                C1 = fmaf(cc.y, wgt, C1);
+                C2 = fmaf(cc.z, wgt, C2);
+                if (DEPTH) D = fmaf(cxy.z, wgt, D);
+                Tt = bl ? test_T : Tt;
+                last = bl ? (INTERP ? base - range.x + (uint32_t)j + 1 : __float_as_uint(cc.w)) : last;
+                if (SEEN && bl) s_seen[j] = 1;
+            }
+        }
+        __syncthreads();
+        if (SEEN && s_seen[lane]) {
+            A.seen[my_id] = 1;
+            s_seen[lane] = 0;
+        }
     }
     if (px < A.W && py < A.H) {
         const size_t HW = (size_t)A.H * A.W;
