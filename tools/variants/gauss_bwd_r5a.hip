@@ -144,27 +144,16 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     const uint32_t start = r_start, end = vis && r_end - r_start > kWide ? r_start : r_end;  // narrow range
     // per-Gaussian inputs of the covariance / projection backward, issued ahead of the record sums so their latency
     // overlaps them
-    // (The camera matrices too, before the kernel's first global store: a load that follows a store waits for it
-    // (vmcnt counts both), and uniform loads only take the scalar path when no store can precede them.)
-    float view[16], proj[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        view[i] = a.viewmatrix[i];
-        proj[i] = a.projmatrix[i];
-    }
     const int idx = t_idx < a.P ? (HIER ? a.indices[t_idx] : t_idx) : 0;
     f3 mean = mk(0.f, 0.f, 0.f), scl3 = mk(0.f, 0.f, 0.f);
     float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
     float c3[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float opac = 0.f;
     if (vis) {
         mean = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-        opac = a.opacities[idx];
         if (a.cov3D_precomp || HIER) {
             const float* cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * t_idx : g.cov3D + 6 * (size_t)t_idx;
             for (int i = 0; i < 6; i++) c3[i] = cov3D[i];
-        }
-        if (a.scales) {  // the cov3D recomputation and the scale / rotation backward
+        } else {
             scl3 = mk(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
             rq = reinterpret_cast<const float4*>(a.rotations)[idx];
         }
@@ -230,10 +219,16 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     }
     // cov3D is not stored by the forward: recomputed from the scale and rotation the forward used
     if (!(a.cov3D_precomp || HIER)) cov3d_exact(scl3, a.scale_modifier, rq, c3);
+    o.dmean2D[3 * idx] = s0;
+    o.dmean2D[3 * idx + 1] = s1;
+    o.dmean2D[3 * idx + 2] = 0.f;
+    o.dcolor[3 * idx] = s6;
+    o.dcolor[3 * idx + 1] = s7;
+    o.dcolor[3 * idx + 2] = s8;
 
     // ---- computeCov2DCUDA (backward.cu:147-326)
     Cov2D k;
-    cov2d_eval(mean, fx, fy, a.tanfovx, a.tanfovy, c3, view, k);
+    cov2d_eval(mean, fx, fy, a.tanfovx, a.tanfovy, c3, a.viewmatrix, k);
     const float xg = k.txtz < -k.limx || k.txtz > k.limx ? 0.f : 1.f;
     const float yg = k.tytz < -k.limy || k.tytz > k.limy ? 0.f : 1.f;
     float c_xx = k.cov.m[0][0], c_xy = k.cov.m[0][1], c_yy = k.cov.m[1][1];
@@ -246,7 +241,7 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     float dxx = 0.f, dxy = 0.f, dyy = 0.f;
     if (!alt || a.antialiasing) {  // the alt rasterizer applies the AA term only with antialiasing (backward.cu:212-245)
         const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
-        const float d_hs = s5 * opac;
+        const float d_hs = s5 * a.opacities[idx];
         dop = s5 * hs;
         const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
         const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
@@ -294,11 +289,12 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     const float dty = yg * -fy * tz2 * dJ12;
     float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * t.x) * tz3 * dJ02 + (2 * fy * t.y) * tz3 * dJ12;
     if (has_depth) dtz -= alt ? s9 * tz2 : s9 / (t.z * t.z);  // alt-rasterizer backward.cu:312
-    const float* vm = view;
+    const float* vm = a.viewmatrix;
     f3 dmean = mk(vm[0] * dtx + vm[1] * dty + vm[2] * dtz, vm[4] * dtx + vm[5] * dty + vm[6] * dtz,
                   vm[8] * dtx + vm[9] * dty + vm[10] * dtz);
 
     // ---- preprocessCUDA backward (backward.cu:398-495): screen-space mean -> world mean
+    const float* proj = a.projmatrix;
     const f3 m = mean;
     const float m_w = 1.0f / (xform44w(m, proj) + 0.0000001f);
     const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
@@ -320,11 +316,12 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     // ---- cov3D backward (backward.cu:330-393)
     float dscale[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
     if (a.scales) {
-        const float qq[4] = {rq.x, rq.y, rq.z, rq.w};
+        const float4 q4 = reinterpret_cast<const float4*>(a.rotations)[idx];
+        const float qq[4] = {q4.x, q4.y, q4.z, q4.w};
         const float r = qq[0], x = qq[1], y = qq[2], z = qq[3];
         const m3 R = quat_rot(qq);
         m3 S = mcols(1, 0, 0, 0, 1, 0, 0, 0, 1);
-        const f3 s = scl(a.scale_modifier, scl3);
+        const f3 s = scl(a.scale_modifier, mk(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]));
         S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
         const m3 Mm = mmul(S, R);
         const m3 dS = mcols(dc[0], 0.5f * dc[1], 0.5f * dc[2], 0.5f * dc[1], dc[3], 0.5f * dc[4], 0.5f * dc[2],
@@ -359,12 +356,6 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             dmean = mk(0.f, 0.f, 0.f);
         }
     }
-    o.dmean2D[3 * idx] = s0;
-    o.dmean2D[3 * idx + 1] = s1;
-    o.dmean2D[3 * idx + 2] = 0.f;
-    o.dcolor[3 * idx] = s6;
-    o.dcolor[3 * idx + 1] = s7;
-    o.dcolor[3 * idx + 2] = s8;
     o.dopacity[idx] = dop_out;
     for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = dc[i];
     o.dmean3D[3 * idx] = dmean.x;
@@ -540,22 +531,7 @@ __global__ void __launch_bounds__(128) k_sh_bwd_jac2(hlgs_raster_args a, const i
     if (wave == 0) {
         const int t_idx = t0 + lane, idx = t_idx;
         const bool active = lane < n;
-        // every input in one round trip, ahead of the first store (an invisible Gaussian's loads are unused)
-        const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
-        bool vis = false;
-        f3 m = mk(0.f, 0.f, 0.f), dcol = m, jx = m, jy = m, jz = m, dm = m;
-        uint32_t cl = 0;
-        if (active) {
-            vis = radii[t_idx] > 0;
-            m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-            dcol = mk(o.dcolor[3 * idx], o.dcolor[3 * idx + 1], o.dcolor[3 * idx + 2]);
-            cl = g.clamped[t_idx];
-            const float* J = g.sh_jac + 9 * (size_t)t_idx;
-            jx = mk(J[0], J[1], J[2]);
-            jy = mk(J[3], J[4], J[5]);
-            jz = mk(J[6], J[7], J[8]);
-            dm = mk(o.dmean3D[3 * idx], o.dmean3D[3 * idx + 1], o.dmean3D[3 * idx + 2]);
-        }
+        const bool vis = active && radii[t_idx] > 0;
         float* row = s_rows + lane * kShStride;
         if (!vis) {
             for (int c = 0; c < M3; c++) row[c] = 0.f;  // invisible rows are zero
@@ -565,6 +541,12 @@ __global__ void __launch_bounds__(128) k_sh_bwd_jac2(hlgs_raster_args a, const i
                 o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f;
             }
         } else {
+            const f3 m = mk(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+            const f3 dcol = mk(o.dcolor[3 * idx], o.dcolor[3 * idx + 1], o.dcolor[3 * idx + 2]);
+            const uint32_t cl = g.clamped[t_idx];
+            const float* J = g.sh_jac + 9 * (size_t)t_idx;
+            const f3 jx = mk(J[0], J[1], J[2]), jy = mk(J[3], J[4], J[5]), jz = mk(J[6], J[7], J[8]);
+            const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
             const f3 dir_orig = sub(m, campos);
             const float len = sqrtf(dot(dir_orig, dir_orig));
             const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
@@ -596,9 +578,9 @@ __global__ void __launch_bounds__(128) k_sh_bwd_jac2(hlgs_raster_args a, const i
                 row[3 * (c - OFF) + 2] = basis[c] * dB;
             }
             const f3 d = dnormvdv(dir_orig, mk(vx, vy, vz));
-            o.dmean3D[3 * idx] = dm.x + d.x;
-            o.dmean3D[3 * idx + 1] = dm.y + d.y;
-            o.dmean3D[3 * idx + 2] = dm.z + d.z;
+            o.dmean3D[3 * idx] += d.x;
+            o.dmean3D[3 * idx + 1] += d.y;
+            o.dmean3D[3 * idx + 2] += d.z;
         }
     }
     if (factored) return;  // block-uniform

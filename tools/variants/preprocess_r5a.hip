@@ -1,0 +1,408 @@
+// preprocess.hip -- the forward's per-Gaussian preprocess for gfx950.
+//
+// Reference semantics (submodules/hierarchy-rasterizer/cuda_rasterizer):
+//   k_preprocess, k_preprocess_sh2  <- preprocessCUDA<3>   forward.cu:218-445
+//                                      (+ per-tile instance counting for the generic binning path)
+// Built with -ffp-contract=off (hlgs_core/build.py PER_FILE): every per-Gaussian value the blends read is computed in
+// the oracle's operation order without contraction, so the splat records are bitwise equal to the oracle's
+// (the shared arithmetic contract).
+#include "hlgs_internal.h"
+#include "hlgs_math.h"
+
+namespace hlgs {
+
+// ------------------------------------------------------------------------------------------------
+// Preprocess: one thread per rasterised Gaussian.
+// ------------------------------------------------------------------------------------------------
+template <bool HIER, bool ALT>
+__global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, int* __restrict__ radii,
+                                                    uint32_t* __restrict__ tile_count, int gx, int gy, float fx,
+                                                    float fy, ZeroJob z)
+{
+    const int t_idx = blockIdx.x * 256 + threadIdx.x;
+    zero_prelude(z, t_idx, gridDim.x * 256);
+    if (t_idx >= a.P) return;
+    const int r_idx = HIER ? a.indices[t_idx] : t_idx;
+    radii[t_idx] = 0;
+    g.tiles_touched[t_idx] = 0;
+    g.rects[t_idx] = make_int2(0, 0);
+    g.clamped[t_idx] = 0;
+
+    bool use_parent = false;
+    int p_idx = 0;
+    float t = 0.f;
+    f3 p_orig = mk(a.means3D[3 * r_idx], a.means3D[3 * r_idx + 1], a.means3D[3 * r_idx + 2]);
+    if (HIER) {
+        p_idx = a.parent_indices[t_idx];
+        if (p_idx != -1) { use_parent = true; t = a.ts[t_idx]; }
+        else p_idx = 0;
+        if (use_parent) {
+            f3 pa = mk(a.means3D[3 * p_idx], a.means3D[3 * p_idx + 1], a.means3D[3 * p_idx + 2]);
+            p_orig = mk(t * p_orig.x + (1.0f - t) * pa.x, t * p_orig.y + (1.0f - t) * pa.y,
+                        t * p_orig.z + (1.0f - t) * pa.z);
+        }
+    }
+    const float* proj = a.projmatrix;
+    const float* view = a.viewmatrix;
+    float hx = proj[0] * p_orig.x + proj[4] * p_orig.y + proj[8] * p_orig.z + proj[12];
+    float hy = proj[1] * p_orig.x + proj[5] * p_orig.y + proj[9] * p_orig.z + proj[13];
+    float hw = xform44w(p_orig, proj);
+    float p_w = 1.0f / (hw + 0.0000001f);
+    float ppx = hx * p_w, ppy = hy * p_w;
+    f3 p_view = xform43(p_orig, view);
+    if (p_view.z <= 0.2f) return;
+
+    float c3[6];
+    const float* cov3D;
+    if (a.cov3D_precomp == nullptr) {
+        f3 scale = mk(a.scales[3 * r_idx], a.scales[3 * r_idx + 1], a.scales[3 * r_idx + 2]);
+        float4 rq = reinterpret_cast<const float4*>(a.rotations)[r_idx];
+        float rot[4] = {rq.x, rq.y, rq.z, rq.w};
+        if (HIER && use_parent) {
+            f3 ps = mk(a.scales[3 * p_idx], a.scales[3 * p_idx + 1], a.scales[3 * p_idx + 2]);
+            scale = add(scl(t, scale), scl(1.0f - t, ps));
+            float4 oq = reinterpret_cast<const float4*>(a.rotations)[p_idx];
+            float orot[4] = {oq.x, oq.y, oq.z, oq.w};
+            float dp = rot[0] * orot[0] + rot[1] * orot[1] + rot[2] * orot[2] + rot[3] * orot[3];
+            if (dp < 0.0f)
+                for (int i = 0; i < 4; i++) orot[i] = -orot[i];
+            for (int i = 0; i < 4; i++) rot[i] = t * rot[i] + (1.0f - t) * orot[i];
+        }
+        cov3d_fwd(scale, a.scale_modifier, rot, c3);
+        cov3D = c3;
+    } else {
+        // the reference leaves cov3D unassigned here; we take the evident intent.
+        for (int i = 0; i < 6; i++) c3[i] = a.cov3D_precomp[6 * t_idx + i];
+        cov3D = c3;
+    }
+    if (HIER) {  // the hierarchy-mode backward reads the lerped covariance; otherwise k_gauss_bwd recomputes it
+        float2* c3o = reinterpret_cast<float2*>(g.cov3D + 6 * (size_t)t_idx);
+        c3o[0] = make_float2(c3[0], c3[1]);
+        c3o[1] = make_float2(c3[2], c3[3]);
+        c3o[2] = make_float2(c3[4], c3[5]);
+    }
+
+    Cov2D k;
+    cov2d_eval(p_orig, fx, fy, a.tanfovx, a.tanfovy, cov3D, view, k);
+    float cx = k.cov.m[0][0], cy = k.cov.m[0][1], cz = k.cov.m[1][1];
+    const float h_var = 0.3f;
+    const float det_cov = cx * cz - cy * cy;
+    cx += h_var;
+    cz += h_var;
+    const float det_h = cx * cz - cy * cy;
+    float h_scale = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    constexpr bool alt = ALT;
+    if (alt && !a.antialiasing) h_scale = 1.0f;  // alt-rasterizer forward.cu:226-229
+    const float det = det_h;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float conic_x = cz * det_inv, conic_y = -cy * det_inv, conic_z = cx * det_inv;
+    const float mid = 0.5f * (cx + cz);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    const float pix_x = ndc2pix(ppx, a.W), pix_y = ndc2pix(ppy, a.H);
+    // per-axis 3-sigma rect (forward.cu:398-403); the alt rasterizer bins the eigen-radius square (its
+    // forward.cu:249), whose tiles it then culls exactly (alt_tile_keep)
+    const int ex = alt ? (int)my_radius : (int)ceilf(3.f * sqrtf(cx));
+    const int ey = alt ? (int)my_radius : (int)ceilf(3.f * sqrtf(cz));
+    g.rects[t_idx] = make_int2(ex, ey);
+    int x0, y0, x1, y1;
+    tile_rect(pix_x, pix_y, ex, ey, gx, gy, x0, y0, x1, y1);
+    const uint32_t area = (uint32_t)(x1 - x0) * (uint32_t)(y1 - y0);
+    if (area == 0) return;
+
+    f3 col;
+    if (a.colors_precomp) {
+        col = mk(a.colors_precomp[3 * t_idx], a.colors_precomp[3 * t_idx + 1], a.colors_precomp[3 * t_idx + 2]);
+    } else {
+        const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+        const f3 mean_r = mk(a.means3D[3 * r_idx], a.means3D[3 * r_idx + 1], a.means3D[3 * r_idx + 2]);
+        const float* sc = a.shs + (size_t)r_idx * a.M * 3;
+        uint32_t cb = 0;
+        f3 rgb;
+        if (alt) {
+            // alt-rasterizer forward.cu:23-75: coefficient 0 from dc, coefficient c >= 1 from shs[c - 1]
+            const float* d0 = a.dc + 3 * (size_t)r_idx;
+            rgb = sh_to_rgb(a.D, [&](int c) {
+                return c == 0 ? mk(d0[0], d0[1], d0[2]) : mk(sc[3 * c - 3], sc[3 * c - 2], sc[3 * c - 1]);
+            }, mean_r, campos, cb);
+        } else if (!(HIER && use_parent)) {
+            rgb = sh_to_rgb(a.D, [&](int c) { return mk(sc[3 * c], sc[3 * c + 1], sc[3 * c + 2]); }, mean_r, campos, cb);
+        } else {
+            // forward.cu:86-138: every coefficient lerped child<->parent, view direction from the child
+            const float* sp = a.shs + (size_t)p_idx * a.M * 3;
+            const float tt = t;
+            rgb = sh_to_rgb(a.D, [&](int c) {
+                return mk(tt * sc[3 * c] + (1.0f - tt) * sp[3 * c], tt * sc[3 * c + 1] + (1.0f - tt) * sp[3 * c + 1],
+                          tt * sc[3 * c + 2] + (1.0f - tt) * sp[3 * c + 2]);
+            }, mean_r, campos, cb);
+        }
+        g.clamped[t_idx] = cb;
+        col = rgb;
+    }
+    g.depths[t_idx] = p_view.z;
+    radii[t_idx] = (int)my_radius;
+    g.means2D[t_idx] = make_float2(pix_x, pix_y);
+    float opacity = a.opacities[r_idx];
+    if (HIER && use_parent) opacity = t * opacity + (1.0f - t) * a.opacities[p_idx];
+    g.tiles_touched[t_idx] = area;
+    uint32_t masks = 0xFFFFFFFFu;
+    {
+        const float cr = col.x, cg = col.y, cbl = col.z;
+        const bool interp = a.ts && a.kids;
+        float4* rec = g.splat + 4 * (size_t)t_idx;
+        rec[0] = make_float4(pix_x, pix_y, conic_x, conic_y);
+        rec[1] = make_float4(conic_z, opacity * h_scale, cr, cg);
+        const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+        rec[2] = make_float4(cbl, 1.f / p_view.z, tt, fr);
+        const float thr = alpha_e2_threshold(opacity * h_scale, interp, tt, fr);
+        if (g.pack)
+            masks = rect_quad_masks(pix_x, pix_y, make_float4(conic_x, conic_y, conic_z, opacity * h_scale), thr, x0, y0,
+                                    x1, y1);
+        if (g.pack) g.qmask[t_idx] = masks;
+        rec[3] = make_float4(0.f, __int_as_float(x0 | (y0 << 16)), __int_as_float(x1 - x0), thr);
+    }
+    if (tile_count) {  // only when the tile grid is too large for the LDS-histogram binning
+        const float4 co = make_float4(conic_x, conic_y, conic_z, opacity * h_scale);
+        const float kthr = alt ? alt_keep_threshold(co.w) : 0.f;
+        uint32_t r = 0;
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++, r++)
+                if ((!alt || alt_tile_keep(pix_x, pix_y, co, kthr, x, y)) &&
+                    !(g.drop && !rect_tile_mask(masks, r)))
+                    atomicAdd(&tile_count[y * gx + x], 1u);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Preprocess, common path (no hierarchy indices, SH coefficients given): k_preprocess_sh2 below.
+// The geometry is per thread as in k_preprocess; the block's SH rows are copied into LDS with all 64 lanes on
+// consecutive float4s, so the 192-byte SH rows (M = 16) stream from HBM in whole lines instead of 48 strided
+// 4-byte loads per thread.  Every per-Gaussian output is bit-identical to k_preprocess (same arithmetic, same order).
+// ------------------------------------------------------------------------------------------------
+struct PreGeom {
+    float pix_x, pix_y, depth, conic_x, conic_y, conic_z, h_scale, radius;
+    int x0, y0, x1, y1;
+};
+
+// forward.cu:218-403 up to the colour: writes the zero defaults and rects; false = culled.
+template <bool ALT>
+__device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const Geom& g, int* radii, int t_idx,
+                                                int gx, int gy, float fx, float fy, PreGeom& o)
+{
+    radii[t_idx] = 0;
+    g.tiles_touched[t_idx] = 0;
+    g.rects[t_idx] = make_int2(0, 0);
+    g.clamped[t_idx] = 0;
+    const f3 p_orig = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
+    // scale and rotation issued with the mean (before the near-plane cull) so their latency overlaps
+    f3 scale = mk(0.f, 0.f, 0.f);
+    float4 rq = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.cov3D_precomp == nullptr) {
+        scale = mk(a.scales[3 * t_idx], a.scales[3 * t_idx + 1], a.scales[3 * t_idx + 2]);
+        rq = reinterpret_cast<const float4*>(a.rotations)[t_idx];
+    }
+    const float* proj = a.projmatrix;
+    const float* view = a.viewmatrix;
+    const float hx = proj[0] * p_orig.x + proj[4] * p_orig.y + proj[8] * p_orig.z + proj[12];
+    const float hy = proj[1] * p_orig.x + proj[5] * p_orig.y + proj[9] * p_orig.z + proj[13];
+    const float hw = xform44w(p_orig, proj);
+    const float p_w = 1.0f / (hw + 0.0000001f);
+    const float ppx = hx * p_w, ppy = hy * p_w;
+    const f3 p_view = xform43(p_orig, view);
+    if (p_view.z <= 0.2f) return false;
+    float c3[6];
+    if (a.cov3D_precomp == nullptr) {
+        const float rot[4] = {rq.x, rq.y, rq.z, rq.w};
+        cov3d_fwd(scale, a.scale_modifier, rot, c3);
+    } else {
+        for (int i = 0; i < 6; i++) c3[i] = a.cov3D_precomp[6 * t_idx + i];
+    }
+    // cov3D is not stored: k_gauss_bwd recomputes it bit-identically (cov3d_exact), 24 bytes per Gaussian saved
+    // on each side
+    Cov2D k;
+    cov2d_eval(p_orig, fx, fy, a.tanfovx, a.tanfovy, c3, view, k);
+    float cx = k.cov.m[0][0], cy = k.cov.m[0][1], cz = k.cov.m[1][1];
+    const float h_var = 0.3f;
+    const float det_cov = cx * cz - cy * cy;
+    cx += h_var;
+    cz += h_var;
+    const float det_h = cx * cz - cy * cy;
+    o.h_scale = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+    if (ALT && !a.antialiasing) o.h_scale = 1.0f;
+    const float det = det_h;
+    if (det == 0.0f) return false;
+    const float det_inv = 1.f / det;
+    o.conic_x = cz * det_inv;
+    o.conic_y = -cy * det_inv;
+    o.conic_z = cx * det_inv;
+    const float mid = 0.5f * (cx + cz);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    o.radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    o.pix_x = ndc2pix(ppx, a.W);
+    o.pix_y = ndc2pix(ppy, a.H);
+    const int ex = ALT ? (int)o.radius : (int)ceilf(3.f * sqrtf(cx));
+    const int ey = ALT ? (int)o.radius : (int)ceilf(3.f * sqrtf(cz));
+    g.rects[t_idx] = make_int2(ex, ey);
+    tile_rect(o.pix_x, o.pix_y, ex, ey, gx, gy, o.x0, o.y0, o.x1, o.y1);
+    o.depth = p_view.z;
+    return (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0) != 0;
+}
+
+// Two waves per 64 Gaussians: wave 0 runs the geometry while wave 1 streams the block's 64 SH rows (contiguous in
+// the AoS input, culled rows included) into LDS; after a barrier wave 1 evaluates the colour and the direction
+// Jacobian from LDS while wave 0 classifies the footprint quadrants, and after a second barrier wave 0 writes the
+// records.  The SH rows' HBM latency overlaps the geometry instead of following it, and one 12 KB LDS stage keeps two
+// waves busy.  Same arithmetic, same outputs.
+// The rows arrive through registers: every lane loads consecutive float4s of the block's contiguous rows (1 KiB per
+// wave instruction) and stores them into LDS rows of odd stride (kShStride), so that each lane's own row walk hits
+// distinct banks.  (Round 5 measured LDS-DMA into a chunk-major image instead -- conflict-free b128 reads, no staging
+// registers: 115 against 97 us, because the DMA's source side then reads 16 bytes per lane at the row stride, 64 lines
+// per wave instruction instead of 8; tools/variants/preprocess_dma.hip.)
+template <int M3T>
+__device__ __forceinline__ void sh_rows_load_contig(const float* gbase, float* lds, int n, int lane, int m3)
+{
+    if constexpr (M3T > 0 && M3T % 4 == 0) {
+        constexpr int Q = M3T / 4;
+        float4 v[Q];
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const int f = lane + 64 * k;
+            v[k] = f < n * Q ? reinterpret_cast<const float4*>(gbase)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const int f = lane + 64 * k;
+            if (f < n * Q) {
+                const int r = f / Q, q = f - r * Q;
+                float* lp = lds + r * kShStride + 4 * q;
+                lp[0] = v[k].x; lp[1] = v[k].y; lp[2] = v[k].z; lp[3] = v[k].w;
+            }
+        }
+    } else {
+        const int M3 = M3T ? M3T : m3;
+        for (int f = lane; f < n * M3; f += 64) {
+            const int r = f / M3, q = f - r * M3;
+            lds[r * kShStride + q] = gbase[f];
+        }
+    }
+}
+
+template <bool ALT, int M3T>
+__global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
+                                                        int gy, float fx, float fy, ZeroJob z)
+{
+    __shared__ float s_rows[64 * kShStride];
+    __shared__ float4 s_col[64];  // r, g, b, clamp bits
+    __shared__ int s_need[64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t0 = blockIdx.x * 64, t_idx = t0 + lane;
+    const int M3 = 3 * a.M;
+    PreGeom o;
+    bool need = false;
+    f3 mean_r = mk(0.f, 0.f, 0.f), dc0 = mk(0.f, 0.f, 0.f);
+    if (wave == 0) {
+        zero_prelude(z, t_idx, gridDim.x * 64);
+        need = t_idx < a.P && preprocess_geom<ALT>(a, g, radii, t_idx, gx, gy, fx, fy, o);
+        s_need[lane] = need;
+    } else {
+        const int n = min(64, a.P - t0);
+        sh_rows_load_contig<M3T>(a.shs + (size_t)t0 * M3, s_rows, n, lane, M3);
+        // the colour's own inputs in the same round trip as the rows (not behind the barrier)
+        if (t_idx < a.P) {
+            mean_r = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
+            if (ALT) dc0 = mk(a.dc[3 * (size_t)t_idx], a.dc[3 * (size_t)t_idx + 1], a.dc[3 * (size_t)t_idx + 2]);
+        }
+    }
+    __syncthreads();
+    const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+    const bool interp = a.ts && a.kids;
+    float thr = 0.f, opacity = 0.f;
+    if (wave == 1) {
+        if (s_need[lane]) {
+            // coefficient c of this lane's row (the full index: the alt rasterizer's 0 is dc)
+            const float* row = s_rows + lane * kShStride;
+            auto rowf = [&](int f) -> float { return row[f]; };
+            auto shv = [&](int c) {
+                if (ALT) return c == 0 ? dc0 : mk(rowf(3 * c - 3), rowf(3 * c - 2), rowf(3 * c - 1));
+                return mk(rowf(3 * c), rowf(3 * c + 1), rowf(3 * c + 2));
+            };
+            uint32_t cb = 0;
+            const f3 col = sh_to_rgb(a.D, shv, mean_r, campos, cb);
+            s_col[lane] = make_float4(col.x, col.y, col.z, __uint_as_float(cb));
+            {  // d colour / d view direction for the SH backward (Geom::sh_jac), from the coefficients in LDS
+                const f3 d = sub(mean_r, campos);
+                const float len = sqrtf(dot(d, d));
+                f3 jx, jy, jz;
+                sh_dir_jacobian(a.D, shv, d.x / len, d.y / len, d.z / len, jx, jy, jz);
+                float* J = g.sh_jac + 9 * (size_t)t_idx;
+                J[0] = jx.x; J[1] = jx.y; J[2] = jx.z;
+                J[3] = jy.x; J[4] = jy.y; J[5] = jy.z;
+                J[6] = jz.x; J[7] = jz.y; J[8] = jz.z;
+            }
+        }
+    } else if (need) {
+        opacity = a.opacities[t_idx];
+        const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+        thr = alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr);
+        if (g.pack)
+            g.qmask[t_idx] = rect_quad_masks(o.pix_x, o.pix_y, make_float4(o.conic_x, o.conic_y, o.conic_z,
+                                                                           opacity * o.h_scale), thr, o.x0, o.y0, o.x1, o.y1);
+    }
+    __syncthreads();
+    if (wave == 1 || !need) return;
+    const float4 c = s_col[lane];
+    g.clamped[t_idx] = __float_as_uint(c.w);
+    g.depths[t_idx] = o.depth;
+    radii[t_idx] = (int)o.radius;
+    g.means2D[t_idx] = make_float2(o.pix_x, o.pix_y);
+    g.tiles_touched[t_idx] = (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0);
+    const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+    float4* rec = g.splat + 4 * (size_t)t_idx;
+    rec[0] = make_float4(o.pix_x, o.pix_y, o.conic_x, o.conic_y);
+    rec[1] = make_float4(o.conic_z, opacity * o.h_scale, c.x, c.y);
+    rec[2] = make_float4(c.z, 1.f / o.depth, tt, fr);
+    rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
+}
+
+void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
+                       const ZeroJob& z, hipStream_t s)
+{
+    const float fy = a.H / (2.0f * a.tanfovy);
+    const float fx = a.W / (2.0f * a.tanfovx);
+    const dim3 grid((a.P + 255) / 256);
+    const bool alt = a.variant == HLGS_VARIANT_ALT;
+    if (!a.indices && !a.colors_precomp && a.shs && a.M > 0 && !tile_count && a.M <= 16) {
+        const dim3 g64((a.P + 63) / 64);
+#define HLGS_PSH(AL, M3) \
+    hipLaunchKernelGGL((k_preprocess_sh2<AL, M3>), g64, dim3(128), 0, s, a, g, radii, gx, gy, fx, fy, z)
+        if (alt) {
+            switch (a.M) {
+            case 3: HLGS_PSH(true, 9); break;
+            case 8: HLGS_PSH(true, 24); break;
+            case 15: HLGS_PSH(true, 45); break;
+            default: HLGS_PSH(true, 0); break;
+            }
+        } else {
+            switch (a.M) {
+            case 1: HLGS_PSH(false, 3); break;
+            case 4: HLGS_PSH(false, 12); break;
+            case 9: HLGS_PSH(false, 27); break;
+            case 16: HLGS_PSH(false, 48); break;
+            default: HLGS_PSH(false, 0); break;
+            }
+        }
+#undef HLGS_PSH
+        return;
+    }
+    if (a.indices)
+        hipLaunchKernelGGL((k_preprocess<true, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy, z);
+    else if (a.variant == HLGS_VARIANT_ALT)
+        hipLaunchKernelGGL((k_preprocess<false, true>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy, z);
+    else
+        hipLaunchKernelGGL((k_preprocess<false, false>), grid, dim3(256), 0, s, a, g, radii, tile_count, gx, gy, fx, fy, z);
+}
+
+}  // namespace hlgs
