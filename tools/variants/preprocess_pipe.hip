@@ -6,6 +6,8 @@
 // Built with -ffp-contract=off (hlgs_core/build.py PER_FILE): every per-Gaussian value the blends read is computed in
 // the oracle's operation order without contraction, so the splat records are bitwise equal to the oracle's
 // (the shared arithmetic contract).
+#include <algorithm>
+
 #include "hlgs_internal.h"
 #include "hlgs_math.h"
 
@@ -196,6 +198,21 @@ struct PreIn {
     float opacity;
 };
 
+// The loads alone, not waited for (the pipelined kernel consumes them one group later).
+__device__ __forceinline__ PreIn preprocess_load_issue(const hlgs_raster_args& a, int t_idx)
+{
+    PreIn in;
+    in.opacity = a.opacities[t_idx];
+    in.mean = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
+    in.scale = mk(0.f, 0.f, 0.f);
+    in.rq = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.cov3D_precomp == nullptr) {
+        in.scale = mk(a.scales[3 * t_idx], a.scales[3 * t_idx + 1], a.scales[3 * t_idx + 2]);
+        in.rq = reinterpret_cast<const float4*>(a.rotations)[t_idx];
+    }
+    return in;
+}
+
 __device__ __forceinline__ PreIn preprocess_load(const hlgs_raster_args& a, int t_idx)
 {
     PreIn in;
@@ -307,18 +324,15 @@ __device__ __forceinline__ void sh_rows_load_contig(const float* gbase, float* l
     }
 }
 
-template <bool ALT, int M3T, bool INTERP>  // INTERP = a.ts && a.kids, host-dispatched: its threshold bisection in
-                                          // double would otherwise set the register budget (90 VGPRs against 67)
+template <bool ALT, int M3T>
 __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
                                                         int gy, float fx, float fy, ZeroJob z)
 {
-    __shared__ float s_rows[64 * kShStride];  // the SH rows; after the second barrier the splat records' stage
-    __shared__ float4 s_col[64];              // r, g, b, clamp bits
+    __shared__ float s_rows[64 * kShStride];
+    __shared__ float4 s_col[64];  // r, g, b, clamp bits
     __shared__ int s_need[64];
-    __shared__ float s_jac[64 * 9];           // the direction Jacobians' stage
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int t0 = blockIdx.x * 64, t_idx = t0 + lane;
-    const int n_grp = min(64, a.P - t0);      // Gaussians of this block
     const int M3 = 3 * a.M;
     const bool live = t_idx < a.P;
     PreGeom o;
@@ -346,11 +360,10 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
     }
     __syncthreads();
     const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
-    constexpr bool interp = INTERP;
+    const bool interp = a.ts && a.kids;
     float thr = 0.f;
     const float opacity = in.opacity;
     if (wave == 1) {
-        float* sj = s_jac + 9 * lane;  // odd stride: the 64 lanes' 4-byte writes hit distinct banks
         if (s_need[lane]) {
             // coefficient c of this lane's row (the full index: the alt rasterizer's 0 is dc)
             const float* row = s_rows + lane * kShStride;
@@ -367,25 +380,10 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
                 const float len = sqrtf(dot(d, d));
                 f3 jx, jy, jz;
                 sh_dir_jacobian(a.D, shv, d.x / len, d.y / len, d.z / len, jx, jy, jz);
-                sj[0] = jx.x; sj[1] = jx.y; sj[2] = jx.z;
-                sj[3] = jy.x; sj[4] = jy.y; sj[5] = jy.z;
-                sj[6] = jz.x; sj[7] = jz.y; sj[8] = jz.z;
-            }
-        } else {
-            for (int k = 0; k < 9; k++) sj[k] = 0.f;
-        }
-        // the block's Jacobians are contiguous in Geom::sh_jac: stored from the stage as whole float4s (the rows are
-        // 36 bytes, so per-lane stores would write every line in pieces)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's own stage writes, before its reads
-        {
-            const int nf = 9 * n_grp;
-            float* jb = g.sh_jac + 9 * (size_t)t0;  // 16-byte aligned: t0 is a multiple of 64
-            for (int f4 = lane; 4 * f4 < nf; f4 += 64) {
-                if (4 * f4 + 3 < nf) {
-                    reinterpret_cast<float4*>(jb)[f4] = reinterpret_cast<const float4*>(s_jac)[f4];
-                } else {
-                    for (int e = 4 * f4; e < nf; e++) jb[e] = s_jac[e];
-                }
+                float* J = g.sh_jac + 9 * (size_t)t_idx;
+                J[0] = jx.x; J[1] = jx.y; J[2] = jx.z;
+                J[3] = jy.x; J[4] = jy.y; J[5] = jy.z;
+                J[6] = jz.x; J[7] = jz.y; J[8] = jz.z;
             }
         }
         // the zeroing the next stages need (after this wave's loads, so no load waits for these stores)
@@ -398,43 +396,202 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
                                                                            opacity * o.h_scale), thr, o.x0, o.y0, o.x1, o.y1);
     }
     __syncthreads();
-    if (wave == 1) return;
-    // the block's splat records through a stage (the row buffer, free now), stored as contiguous float4s: 4 KiB in
-    // four 1 KiB wave instructions instead of four 16-byte pieces of every lane's 64-byte record (a culled Gaussian's
-    // record is written as zeros; nothing reads it)
-    float4* st = reinterpret_cast<float4*>(s_rows);
-    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0, r3 = r0;
-    if (live) {
-        g.rects[t_idx] = make_int2(o.ex, o.ey);
-        if (!need) {  // culled: the zero outputs (rects as far as they were formed, forward.cu:398-403)
-            radii[t_idx] = 0;
-            g.tiles_touched[t_idx] = 0;
-            g.clamped[t_idx] = 0;
+    if (wave == 1 || !live) return;
+    g.rects[t_idx] = make_int2(o.ex, o.ey);
+    if (!need) {  // culled: the zero outputs (rects as far as they were formed, forward.cu:398-403)
+        radii[t_idx] = 0;
+        g.tiles_touched[t_idx] = 0;
+        g.clamped[t_idx] = 0;
+        return;
+    }
+    const float4 c = s_col[lane];
+    g.clamped[t_idx] = __float_as_uint(c.w);
+    g.depths[t_idx] = o.depth;
+    radii[t_idx] = (int)o.radius;
+    g.means2D[t_idx] = make_float2(o.pix_x, o.pix_y);
+    g.tiles_touched[t_idx] = (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0);
+    const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+    float4* rec = g.splat + 4 * (size_t)t_idx;
+    rec[0] = make_float4(o.pix_x, o.pix_y, o.conic_x, o.conic_y);
+    rec[1] = make_float4(o.conic_z, opacity * o.h_scale, c.x, c.y);
+    rec[2] = make_float4(c.z, 1.f / o.depth, tt, fr);
+    rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
+}
+
+// Persistent, software-pipelined form of k_preprocess_sh2 for rows of a multiple of four floats (SH degree 3 or 1,
+// alt degree 2): a grid of a few blocks per CU, each walking 64-Gaussian groups gi = blockIdx.x + i * gridDim.x.  While
+// a group is computed, the next group's inputs are already in flight: wave 0 holds the next geometry inputs in
+// registers, wave 1 has the next SH rows on their way into the second LDS buffer by LDS-DMA (lane-linear, so the
+// buffer is the rows' contiguous image; each lane then reads its own row as float4s, 4-way bank-conflicted, into
+// registers).  The one-group-per-block kernel above waits a full HBM round trip per group with nothing else to do;
+// here the memory system always has the next group's 12.7 KB per block outstanding.  Same arithmetic, same outputs.
+template <bool ALT, int M3T, bool INTERP>
+__global__ void __launch_bounds__(128) k_preprocess_pipe(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
+                                                         int gy, float fx, float fy, ZeroJob z, int ngroups)
+{
+    static_assert(M3T > 0 && M3T % 4 == 0, "rows of whole float4s");
+    constexpr int Q = M3T / 4;  // float4s per row
+    __shared__ float4 s_rows[2][64 * Q];
+    __shared__ float4 s_col[64];  // r, g, b, clamp bits
+    __shared__ int s_need[64];
+    typedef __attribute__((address_space(3))) void lds_t;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int G = gridDim.x;
+    constexpr bool interp = INTERP;  // a.ts && a.kids (host-dispatched: the bisection's double code is heavy)
+    // the rows of group gi into buffer b, 64 float4s per wave instruction (past the last row: the last float4 again)
+    auto rows_dma = [&](int gi, int b) {
+        const int t0 = gi * 64, nf = min(64, a.P - t0) * Q;
+        const float4* src = reinterpret_cast<const float4*>(a.shs) + (size_t)t0 * Q;
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+            const int f = min(64 * k + lane, nf - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(src + f), (lds_t*)(&s_rows[b][64 * k]), 16, 0, 0);
+        }
+    };
+    // prologue: the first group's inputs
+    int gi = blockIdx.x;
+    PreIn pre{};
+    f3 pmean = mk(0.f, 0.f, 0.f), pdc0 = pmean;
+    if (gi < ngroups) {
+        const int t = gi * 64 + lane;
+        if (wave == 0) {
+            if (t < a.P) pre = preprocess_load(a, t);
         } else {
-            const float4 c = s_col[lane];
-            g.clamped[t_idx] = __float_as_uint(c.w);
-            g.depths[t_idx] = o.depth;
-            radii[t_idx] = (int)o.radius;
-            g.means2D[t_idx] = make_float2(o.pix_x, o.pix_y);
-            g.tiles_touched[t_idx] = (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0);
-            const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
-            r0 = make_float4(o.pix_x, o.pix_y, o.conic_x, o.conic_y);
-            r1 = make_float4(o.conic_z, opacity * o.h_scale, c.x, c.y);
-            r2 = make_float4(c.z, 1.f / o.depth, tt, fr);
-            r3 = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
+            rows_dma(gi, 0);
+            if (t < a.P) {
+                pmean = mk(a.means3D[3 * t], a.means3D[3 * t + 1], a.means3D[3 * t + 2]);
+                if (ALT) pdc0 = mk(a.dc[3 * (size_t)t], a.dc[3 * (size_t)t + 1], a.dc[3 * (size_t)t + 2]);
+            }
         }
     }
-    st[4 * lane] = r0;
-    st[4 * lane + 1] = r1;
-    st[4 * lane + 2] = r2;
-    st[4 * lane + 3] = r3;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's own stage writes, before its reads
-    float4* rb = g.splat + 4 * (size_t)t0;
+    for (int it = 0; gi < ngroups; it++, gi += G) {
+        const int b = it & 1;
+        const int t_idx = gi * 64 + lane;
+        const bool live = t_idx < a.P;
+        const int gn = gi + G, tn = gn * 64 + lane;
+        const bool more = gn < ngroups;  // block-uniform
+        bool need = false;
+        float4 r1 = make_float4(0.f, 0.f, 0.f, 0.f), r2 = r1;  // record words 4-5 and 9-11 (no colour)
+        if (wave == 0) {
+            // everything but the colour before the first barrier, so little of this wave's state stays live across
+            // wave 1's SH evaluation
+            const PreIn in = pre;
+            if (more && tn < a.P) pre = preprocess_load_issue(a, tn);
+            float proj[16], view[16];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int f4 = 64 * k + lane;
-        if (f4 < 4 * n_grp) rb[f4] = st[f4];
+            for (int i = 0; i < 16; i++) {
+                proj[i] = a.projmatrix[i];
+                view[i] = a.viewmatrix[i];
+            }
+            PreGeom o;
+            need = live && preprocess_geom<ALT>(a, in, proj, view, t_idx, gx, gy, fx, fy, o);
+            s_need[lane] = need;
+            if (live) {
+                g.rects[t_idx] = make_int2(o.ex, o.ey);
+                if (!need) {  // culled: the zero outputs (rects as far as they were formed, forward.cu:398-403)
+                    radii[t_idx] = 0;
+                    g.tiles_touched[t_idx] = 0;
+                    g.clamped[t_idx] = 0;
+                } else {
+                    const float opacity = in.opacity;
+                    const float tt = interp ? a.ts[t_idx] : 0.f, fr = interp ? 1.0f / (float)a.kids[t_idx] : 0.f;
+                    const float thr = alpha_e2_threshold(opacity * o.h_scale, interp, tt, fr);
+                    if (g.pack)
+                        g.qmask[t_idx] = rect_quad_masks(o.pix_x, o.pix_y, make_float4(o.conic_x, o.conic_y, o.conic_z,
+                                                                                       opacity * o.h_scale),
+                                                         thr, o.x0, o.y0, o.x1, o.y1);
+                    g.depths[t_idx] = o.depth;
+                    radii[t_idx] = (int)o.radius;
+                    g.means2D[t_idx] = make_float2(o.pix_x, o.pix_y);
+                    g.tiles_touched[t_idx] = (uint32_t)(o.x1 - o.x0) * (uint32_t)(o.y1 - o.y0);
+                    float4* rec = g.splat + 4 * (size_t)t_idx;
+                    rec[0] = make_float4(o.pix_x, o.pix_y, o.conic_x, o.conic_y);
+                    rec[3] = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
+                    r1 = make_float4(o.conic_z, opacity * o.h_scale, 0.f, 0.f);
+                    r2 = make_float4(0.f, 1.f / o.depth, tt, fr);
+                }
+            }
+        } else {
+            const f3 mean_r = pmean, dc0 = pdc0;
+            // this group's rows have landed (with every earlier load and store of this wave); buffer b ^ 1 was last
+            // read in the previous group, before its second barrier
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (more) {
+                rows_dma(gn, b ^ 1);
+                if (tn < a.P) {
+                    pmean = mk(a.means3D[3 * tn], a.means3D[3 * tn + 1], a.means3D[3 * tn + 2]);
+                    if (ALT) pdc0 = mk(a.dc[3 * (size_t)tn], a.dc[3 * (size_t)tn + 1], a.dc[3 * (size_t)tn + 2]);
+                }
+            }
+            __syncthreads();  // s_need; this wave's view of its own DMA
+            if (s_need[lane]) {
+                const f3 campos = mk(a.campos[0], a.campos[1], a.campos[2]);
+                // the row as float4s (4-way bank-conflicted b128 reads; 4-byte reads of a 48-dword-stride row would be 16-way)
+                float4 rv[Q];
+                const float4* rp = &s_rows[b][lane * Q];
+#pragma unroll
+                for (int k = 0; k < Q; k++) rv[k] = rp[k];
+                auto rowf = [&](int f) -> float {
+                    const float4 v = rv[f >> 2];
+                    return (f & 3) == 0 ? v.x : (f & 3) == 1 ? v.y : (f & 3) == 2 ? v.z : v.w;
+                };
+                auto shv = [&](int c) {
+                    if (ALT) return c == 0 ? dc0 : mk(rowf(3 * c - 3), rowf(3 * c - 2), rowf(3 * c - 1));
+                    return mk(rowf(3 * c), rowf(3 * c + 1), rowf(3 * c + 2));
+                };
+                uint32_t cb = 0;
+                const f3 col = sh_to_rgb(a.D, shv, mean_r, campos, cb);
+                s_col[lane] = make_float4(col.x, col.y, col.z, __uint_as_float(cb));
+                const f3 d = sub(mean_r, campos);
+                const float len = sqrtf(dot(d, d));
+                f3 jx, jy, jz;
+                sh_dir_jacobian(a.D, shv, d.x / len, d.y / len, d.z / len, jx, jy, jz);
+                float* J = g.sh_jac + 9 * (size_t)t_idx;
+                J[0] = jx.x; J[1] = jx.y; J[2] = jx.z;
+                J[3] = jy.x; J[4] = jy.y; J[5] = jy.z;
+                J[6] = jz.x; J[7] = jz.y; J[8] = jz.z;
+            }
+            __syncthreads();  // s_col
+            continue;
+        }
+        __syncthreads();  // s_need
+        __syncthreads();  // s_col
+        if (need) {
+            const float4 c = s_col[lane];
+            g.clamped[t_idx] = __float_as_uint(c.w);
+            float4* rec = g.splat + 4 * (size_t)t_idx;
+            rec[1] = make_float4(r1.x, r1.y, c.x, c.y);
+            rec[2] = make_float4(c.z, r2.y, r2.z, r2.w);
+        }
     }
+    if (wave == 1) zero_prelude(z, blockIdx.x * 64 + lane, G * 64);
+}
+
+// Grid of the pipelined preprocess: as many blocks as fit on the device at once (occupancy query, once per
+// instantiation), at most one per group.
+template <bool ALT, int M3T, bool INTERP>
+static void launch_preprocess_pipe_i(const hlgs_raster_args& a, const Geom& g, int* radii, int gx, int gy, float fx,
+                                   float fy, const ZeroJob& z, hipStream_t s)
+{
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_preprocess_pipe<ALT, M3T, INTERP>, 128, 0);
+        resident = std::max(1, cus * std::max(1, per_cu));
+    }
+    const int ngroups = (a.P + 63) / 64;
+    const int blocks = std::min(ngroups, resident);
+    hipLaunchKernelGGL((k_preprocess_pipe<ALT, M3T, INTERP>), dim3(blocks), dim3(128), 0, s, a, g, radii, gx, gy, fx, fy,
+                       z, ngroups);
+}
+template <bool ALT, int M3T>
+static void launch_preprocess_pipe(const hlgs_raster_args& a, const Geom& g, int* radii, int gx, int gy, float fx,
+                                   float fy, const ZeroJob& z, hipStream_t s)
+{
+    if (a.ts && a.kids) launch_preprocess_pipe_i<ALT, M3T, true>(a, g, radii, gx, gy, fx, fy, z, s);
+    else launch_preprocess_pipe_i<ALT, M3T, false>(a, g, radii, gx, gy, fx, fy, z, s);
 }
 
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
@@ -446,27 +603,32 @@ void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uin
     const bool alt = a.variant == HLGS_VARIANT_ALT;
     if (!a.indices && !a.colors_precomp && a.shs && a.M > 0 && !tile_count && a.M <= 16) {
         const dim3 g64((a.P + 63) / 64);
-#define HLGS_PSH(AL, M3)                                                                                              \
-    do {                                                                                                              \
-        if (a.ts && a.kids)                                                                                           \
-            hipLaunchKernelGGL((k_preprocess_sh2<AL, M3, true>), g64, dim3(128), 0, s, a, g, radii, gx, gy, fx, fy, z); \
-        else                                                                                                          \
-            hipLaunchKernelGGL((k_preprocess_sh2<AL, M3, false>), g64, dim3(128), 0, s, a, g, radii, gx, gy, fx, fy,   \
-                               z);                                                                                    \
-    } while (0)
+#define HLGS_PSH(AL, M3) \
+    hipLaunchKernelGGL((k_preprocess_sh2<AL, M3>), g64, dim3(128), 0, s, a, g, radii, gx, gy, fx, fy, z)
+        // rows of whole float4s (16-byte aligned coefficients) take the pipelined kernel
+        const bool al16 = (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0;
         if (alt) {
             switch (a.M) {
             case 3: HLGS_PSH(true, 9); break;
-            case 8: HLGS_PSH(true, 24); break;
+            case 8:
+                if (al16) launch_preprocess_pipe<true, 24>(a, g, radii, gx, gy, fx, fy, z, s);
+                else HLGS_PSH(true, 24);
+                break;
             case 15: HLGS_PSH(true, 45); break;
             default: HLGS_PSH(true, 0); break;
             }
         } else {
             switch (a.M) {
             case 1: HLGS_PSH(false, 3); break;
-            case 4: HLGS_PSH(false, 12); break;
+            case 4:
+                if (al16) launch_preprocess_pipe<false, 12>(a, g, radii, gx, gy, fx, fy, z, s);
+                else HLGS_PSH(false, 12);
+                break;
             case 9: HLGS_PSH(false, 27); break;
-            case 16: HLGS_PSH(false, 48); break;
+            case 16:
+                if (al16) launch_preprocess_pipe<false, 48>(a, g, radii, gx, gy, fx, fy, z, s);
+                else HLGS_PSH(false, 48);
+                break;
             default: HLGS_PSH(false, 0); break;
             }
         }
