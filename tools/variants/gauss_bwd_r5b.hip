@@ -48,32 +48,6 @@ __device__ __forceinline__ void cov3d_exact(f3 scale, float mod, float4 q, float
     out[3] = Sig.m[1][1]; out[4] = Sig.m[1][2]; out[5] = Sig.m[2][2];
 }
 
-// Store a wave's rows of NF floats (row r = lane r; rows [0, nrows) of a contiguous row-major array starting at the
-// wave's first row) through an LDS stage of 64 * NF floats, as whole float4s where the destination is 16-byte aligned.
-template <int NF>
-__device__ __forceinline__ void wave_rows_store(float* gdst, const float (&v)[NF], float* lds, int lane, int nrows)
-{
-    if (reinterpret_cast<uintptr_t>(gdst) & 15) {  // (uniform) unaligned destination: per-lane stores
-        if (lane < nrows)
-            for (int k = 0; k < NF; k++) gdst[NF * lane + k] = v[k];
-        return;
-    }
-#pragma unroll
-    for (int k = 0; k < NF; k++) lds[NF * lane + k] = v[k];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's stage writes before its reads
-    const int nf = NF * nrows;
-    for (int f4 = lane; 4 * f4 < nf; f4 += 64) {
-        if (4 * f4 + 3 < nf) {
-            reinterpret_cast<float4*>(gdst)[f4] = reinterpret_cast<const float4*>(lds)[f4];
-        } else {
-            for (int e = 4 * f4; e < nf; e++) gdst[e] = lds[e];
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reads done before the stage is written again
-}
-
-constexpr int kGbwdChunk = 128;  // records per LDS chunk of k_gauss_bwd: 6 KiB per wave
-
 // One thread per rasterised Gaussian: sum its per-tile records, then covariance / SH / scale-rotation
 // backward.  Writes every output row it owns (zeros for invisible Gaussians), so no memset is needed.
 template <bool HIER, bool ALT>
@@ -84,8 +58,6 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     // the forward packed its entries (misc[kMiscPack]), so Geom::qmask holds this frame's quadrant masks: a slot whose
     // mask is 0 holds no record (drop_empty: never binned) or a zero one, and is skipped (rect_tile_mask)
     const bool masked = misc && misc[kMiscPack];
-    // per wave: the chunk of records being summed (LDS-DMA), then the stage of the output rows
-    __shared__ float4 s_rec[4][3 * kGbwdChunk];
     const int t_idx = blockIdx.x * 256 + threadIdx.x;
     // the slot range and the masks are loaded with the radius, not behind it (an invisible Gaussian's tiles_touched
     // is 0, so its range is empty; its qmask word is stale and never used)
@@ -198,7 +170,8 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
         }
     }
     {
-        constexpr int kChunk = kGbwdChunk;
+        constexpr int kChunk = 128;  // records per chunk: 6 KiB of LDS per wave
+        __shared__ float4 s_rec[4][3 * kChunk];
         float4* buf = s_rec[threadIdx.x >> 6];
         const int lane = threadIdx.x & 63;
         const bool any = start < end;
@@ -238,184 +211,169 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the chunk done before the next DMA
         }
     }
+    if (t_idx >= a.P) return;
     const int M3 = a.M * 3;
-    const bool live = t_idx < a.P;
-    // the outputs, zeros for an invisible Gaussian
-    float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dscale[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
-    f3 dmean = mk(0.f, 0.f, 0.f);
-    float dop_out = 0.f;
-    if (live && !vis && !HIER) {
-        if (o.dsh && !a.shs)
-            for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
-        if (o.ddc && !a.shs) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
-    }
-    if (vis) {
-        // cov3D is not stored by the forward: recomputed from the scale and rotation the forward used
-        if (!(a.cov3D_precomp || HIER)) cov3d_exact(scl3, a.scale_modifier, rq, c3);
-
-        // ---- computeCov2DCUDA (backward.cu:147-326)
-        Cov2D k;
-        cov2d_eval(mean, fx, fy, a.tanfovx, a.tanfovy, c3, view, k);
-        const float xg = k.txtz < -k.limx || k.txtz > k.limx ? 0.f : 1.f;
-        const float yg = k.tytz < -k.limy || k.tytz > k.limy ? 0.f : 1.f;
-        float c_xx = k.cov.m[0][0], c_xy = k.cov.m[0][1], c_yy = k.cov.m[1][1];
-        const float h_var = 0.3f;
-        const float det_cov = c_xx * c_yy - c_xy * c_xy;
-        c_xx += h_var;
-        c_yy += h_var;
-        const float det_h = c_xx * c_yy - c_xy * c_xy;
-        float dop = s5;
-        float dxx = 0.f, dxy = 0.f, dyy = 0.f;
-        if (!alt || a.antialiasing) {  // the alt rasterizer applies the AA term only with antialiasing (backward.cu:212-245)
-            const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
-            const float d_hs = s5 * opac;
-            dop = s5 * hs;
-            const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
-            const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
-            const float sqv = w * w + w * (x + y) + x * y - z * z;
-            const float denom_f = d_inside / (sqv * sqv);
-            dxx = w * (w * y + y * y + z * z) * denom_f;
-            dyy = w * (w * x + x * x + z * z) * denom_f;
-            dxy = -2.f * w * z * (w + x + y) * denom_f;
+    if (!vis) {
+        if (!HIER) {
+            o.dmean2D[3 * idx] = 0.f; o.dmean2D[3 * idx + 1] = 0.f; o.dmean2D[3 * idx + 2] = 0.f;
+            o.dcolor[3 * idx] = 0.f; o.dcolor[3 * idx + 1] = 0.f; o.dcolor[3 * idx + 2] = 0.f;
+            o.dopacity[idx] = 0.f;
+            o.dmean3D[3 * idx] = 0.f; o.dmean3D[3 * idx + 1] = 0.f; o.dmean3D[3 * idx + 2] = 0.f;
+            for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = 0.f;
+            if (o.dsh && !a.shs)
+                for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+            if (o.ddc && !a.shs) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
+            o.dscale[3 * idx] = 0.f; o.dscale[3 * idx + 1] = 0.f; o.dscale[3 * idx + 2] = 0.f;
+            reinterpret_cast<float4*>(o.drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        const float dcx = s2, dcy = s3, dcz = s4;
-        const float denom = c_xx * c_yy - c_xy * c_xy;
-        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-        const m3& Tm = k.T;
-        const m3& V = k.Vrk;
-    #define TT(c, r) Tm.m[c][r]
-    #define VK(c, r) V.m[c][r]
-        if (denom2inv != 0) {
-            dxx += denom2inv * (-c_yy * c_yy * dcx + 2 * c_xy * c_yy * dcy + (denom - c_xx * c_yy) * dcz);
-            dyy += denom2inv * (-c_xx * c_xx * dcz + 2 * c_xx * c_xy * dcy + (denom - c_xx * c_yy) * dcx);
-            dxy += denom2inv * 2 * (c_xy * c_yy * dcx - (denom + 2 * c_xy * c_xy) * dcy + c_xx * c_xy * dcz);
-            dc[0] = (TT(0, 0) * TT(0, 0) * dxx + TT(0, 0) * TT(1, 0) * dxy + TT(1, 0) * TT(1, 0) * dyy);
-            dc[3] = (TT(0, 1) * TT(0, 1) * dxx + TT(0, 1) * TT(1, 1) * dxy + TT(1, 1) * TT(1, 1) * dyy);
-            dc[5] = (TT(0, 2) * TT(0, 2) * dxx + TT(0, 2) * TT(1, 2) * dxy + TT(1, 2) * TT(1, 2) * dyy);
-            dc[1] = 2 * TT(0, 0) * TT(0, 1) * dxx + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dxy + 2 * TT(1, 0) * TT(1, 1) * dyy;
-            dc[2] = 2 * TT(0, 0) * TT(0, 2) * dxx + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dxy + 2 * TT(1, 0) * TT(1, 2) * dyy;
-            dc[4] = 2 * TT(0, 2) * TT(0, 1) * dxx + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dxy + 2 * TT(1, 1) * TT(1, 2) * dyy;
-        }
-        const float dT00 = 2 * (TT(0, 0) * VK(0, 0) + TT(0, 1) * VK(0, 1) + TT(0, 2) * VK(0, 2)) * dxx + (TT(1, 0) * VK(0, 0) + TT(1, 1) * VK(0, 1) + TT(1, 2) * VK(0, 2)) * dxy;
-        const float dT01 = 2 * (TT(0, 0) * VK(1, 0) + TT(0, 1) * VK(1, 1) + TT(0, 2) * VK(1, 2)) * dxx + (TT(1, 0) * VK(1, 0) + TT(1, 1) * VK(1, 1) + TT(1, 2) * VK(1, 2)) * dxy;
-        const float dT02 = 2 * (TT(0, 0) * VK(2, 0) + TT(0, 1) * VK(2, 1) + TT(0, 2) * VK(2, 2)) * dxx + (TT(1, 0) * VK(2, 0) + TT(1, 1) * VK(2, 1) + TT(1, 2) * VK(2, 2)) * dxy;
-        const float dT10 = 2 * (TT(1, 0) * VK(0, 0) + TT(1, 1) * VK(0, 1) + TT(1, 2) * VK(0, 2)) * dyy + (TT(0, 0) * VK(0, 0) + TT(0, 1) * VK(0, 1) + TT(0, 2) * VK(0, 2)) * dxy;
-        const float dT11 = 2 * (TT(1, 0) * VK(1, 0) + TT(1, 1) * VK(1, 1) + TT(1, 2) * VK(1, 2)) * dyy + (TT(0, 0) * VK(1, 0) + TT(0, 1) * VK(1, 1) + TT(0, 2) * VK(1, 2)) * dxy;
-        const float dT12 = 2 * (TT(1, 0) * VK(2, 0) + TT(1, 1) * VK(2, 1) + TT(1, 2) * VK(2, 2)) * dyy + (TT(0, 0) * VK(2, 0) + TT(0, 1) * VK(2, 1) + TT(0, 2) * VK(2, 2)) * dxy;
-    #undef VK
-    #undef TT
-        const m3& Wm = k.W;
-        const float dJ00 = Wm.m[0][0] * dT00 + Wm.m[0][1] * dT01 + Wm.m[0][2] * dT02;
-        const float dJ02 = Wm.m[2][0] * dT00 + Wm.m[2][1] * dT01 + Wm.m[2][2] * dT02;
-        const float dJ11 = Wm.m[1][0] * dT10 + Wm.m[1][1] * dT11 + Wm.m[1][2] * dT12;
-        const float dJ12 = Wm.m[2][0] * dT10 + Wm.m[2][1] * dT11 + Wm.m[2][2] * dT12;
-        const f3 t = k.t;
-        const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
-        const float dtx = xg * -fx * tz2 * dJ02;
-        const float dty = yg * -fy * tz2 * dJ12;
-        float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * t.x) * tz3 * dJ02 + (2 * fy * t.y) * tz3 * dJ12;
-        if (has_depth) dtz -= alt ? s9 * tz2 : s9 / (t.z * t.z);  // alt-rasterizer backward.cu:312
-        const float* vm = view;
-        dmean = mk(vm[0] * dtx + vm[1] * dty + vm[2] * dtz, vm[4] * dtx + vm[5] * dty + vm[6] * dtz,
-                      vm[8] * dtx + vm[9] * dty + vm[10] * dtz);
-
-        // ---- preprocessCUDA backward (backward.cu:398-495): screen-space mean -> world mean
-        const f3 m = mean;
-        const float m_w = 1.0f / (xform44w(m, proj) + 0.0000001f);
-        const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
-        const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
-        f3 d2;
-        d2.x = (proj[0] * m_w - proj[3] * mul1) * s0 + (proj[1] * m_w - proj[3] * mul2) * s1;
-        d2.y = (proj[4] * m_w - proj[7] * mul1) * s0 + (proj[5] * m_w - proj[7] * mul2) * s1;
-        d2.z = (proj[8] * m_w - proj[11] * mul1) * s0 + (proj[9] * m_w - proj[11] * mul2) * s1;
-        dmean = add(dmean, d2);
-
-        // ---- SH backward (backward.cu:23-142) runs in k_sh_bwd, which adds its view-direction term to
-        //      dmean3D (or to the parent-deferred share) after this kernel.
-        if (!a.shs && o.dsh)
-            for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
-        // alt without higher-order coefficients: the reference skips the whole SH backward (backward.cu:443),
-        // so even dc gets no gradient
-        if (!a.shs && o.ddc) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
-
-        // ---- cov3D backward (backward.cu:330-393)
-        if (a.scales) {
-            const float qq[4] = {rq.x, rq.y, rq.z, rq.w};
-            const float r = qq[0], x = qq[1], y = qq[2], z = qq[3];
-            const m3 R = quat_rot(qq);
-            m3 S = mcols(1, 0, 0, 0, 1, 0, 0, 0, 1);
-            const f3 s = scl(a.scale_modifier, scl3);
-            S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
-            const m3 Mm = mmul(S, R);
-            const m3 dS = mcols(dc[0], 0.5f * dc[1], 0.5f * dc[2], 0.5f * dc[1], dc[3], 0.5f * dc[4], 0.5f * dc[2],
-                                0.5f * dc[4], dc[5]);
-            m3 M2 = Mm;
-            for (int c = 0; c < 3; c++)
-                for (int rr = 0; rr < 3; rr++) M2.m[c][rr] = 2.0f * Mm.m[c][rr];
-            const m3 dM = mmul(M2, dS);
-            const m3 Rt = mtrans(R);
-            m3 dMt = mtrans(dM);
-            for (int i = 0; i < 3; i++)
-                dscale[i] = Rt.m[i][0] * dMt.m[i][0] + Rt.m[i][1] * dMt.m[i][1] + Rt.m[i][2] * dMt.m[i][2];
-            for (int rr = 0; rr < 3; rr++) { dMt.m[0][rr] *= s.x; dMt.m[1][rr] *= s.y; dMt.m[2][rr] *= s.z; }
-            dq[0] = 2 * z * (dMt.m[0][1] - dMt.m[1][0]) + 2 * y * (dMt.m[2][0] - dMt.m[0][2]) + 2 * x * (dMt.m[1][2] - dMt.m[2][1]);
-            dq[1] = 2 * y * (dMt.m[1][0] + dMt.m[0][1]) + 2 * z * (dMt.m[2][0] + dMt.m[0][2]) + 2 * r * (dMt.m[1][2] - dMt.m[2][1]) - 4 * x * (dMt.m[2][2] + dMt.m[1][1]);
-            dq[2] = 2 * x * (dMt.m[1][0] + dMt.m[0][1]) + 2 * r * (dMt.m[2][0] - dMt.m[0][2]) + 2 * z * (dMt.m[1][2] + dMt.m[2][1]) - 4 * y * (dMt.m[2][2] + dMt.m[0][0]);
-            dq[3] = 2 * r * (dMt.m[0][1] - dMt.m[1][0]) + 2 * x * (dMt.m[2][0] + dMt.m[0][2]) + 2 * y * (dMt.m[1][2] + dMt.m[2][1]) - 4 * z * (dMt.m[1][1] + dMt.m[0][0]);
-        }
-        dop_out = dop;
-        if (HIER) {
-            // backward.cu:458-494: the child's opacity/scale/rotation/SH gradients are dropped and
-            // (1 - t) of its mean gradient moves to the parent (added by k_parent_mean_add).
-            const int parent = a.parent_indices[t_idx];
-            if (parent != -1) {
-                const float tt = a.ts[t_idx];
-                dop_out = 0.f;
-                for (int i = 0; i < 3; i++) dscale[i] = 0.f;
-                for (int i = 0; i < 4; i++) dq[i] = 0.f;
-                rec.parent_dmean[3 * t_idx] = (1.0f - tt) * dmean.x;
-                rec.parent_dmean[3 * t_idx + 1] = (1.0f - tt) * dmean.y;
-                rec.parent_dmean[3 * t_idx + 2] = (1.0f - tt) * dmean.z;
-                dmean = mk(0.f, 0.f, 0.f);
-            }
-        }
-    }
-    if (HIER) {  // rows at the hierarchy's indices: per lane, visible Gaussians only
-        if (!vis) return;
-        o.dmean2D[3 * idx] = s0;
-        o.dmean2D[3 * idx + 1] = s1;
-        o.dmean2D[3 * idx + 2] = 0.f;
-        o.dcolor[3 * idx] = s6;
-        o.dcolor[3 * idx + 1] = s7;
-        o.dcolor[3 * idx + 2] = s8;
-        o.dopacity[idx] = dop_out;
-        for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = dc[i];
-        o.dmean3D[3 * idx] = dmean.x;
-        o.dmean3D[3 * idx + 1] = dmean.y;
-        o.dmean3D[3 * idx + 2] = dmean.z;
-        o.dscale[3 * idx] = dscale[0];
-        o.dscale[3 * idx + 1] = dscale[1];
-        o.dscale[3 * idx + 2] = dscale[2];
-        reinterpret_cast<float4*>(o.drot)[idx] = make_float4(dq[0], dq[1], dq[2], dq[3]);
         return;
     }
-    // Rows at t_idx: the wave's rows of each output are contiguous, so they go out through this wave's LDS stage (the
-    // record-sum buffer, free now) as whole float4s -- one or two 1 KiB wave stores per array instead of three or six
-    // 4-byte stores of every lane into pieces of the same lines.
-    {
-        float* stage = reinterpret_cast<float*>(s_rec[threadIdx.x >> 6]);
-        const int lane = threadIdx.x & 63, w0 = t_idx - lane, nrows = max(0, min(64, a.P - w0));
-        if (!vis) s0 = s1 = s6 = s7 = s8 = 0.f;
-        const float r_dm2[3] = {s0, s1, 0.f}, r_dcol[3] = {s6, s7, s8}, r_dop[1] = {dop_out};
-        const float r_dm3[3] = {dmean.x, dmean.y, dmean.z};
-        wave_rows_store<3>(o.dmean2D + 3 * (size_t)w0, r_dm2, stage, lane, nrows);
-        wave_rows_store<3>(o.dcolor + 3 * (size_t)w0, r_dcol, stage, lane, nrows);
-        wave_rows_store<1>(o.dopacity + (size_t)w0, r_dop, stage, lane, nrows);
-        wave_rows_store<6>(o.dcov3D + 6 * (size_t)w0, dc, stage, lane, nrows);
-        wave_rows_store<3>(o.dmean3D + 3 * (size_t)w0, r_dm3, stage, lane, nrows);
-        wave_rows_store<3>(o.dscale + 3 * (size_t)w0, dscale, stage, lane, nrows);
-        if (live) reinterpret_cast<float4*>(o.drot)[idx] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+    // cov3D is not stored by the forward: recomputed from the scale and rotation the forward used
+    if (!(a.cov3D_precomp || HIER)) cov3d_exact(scl3, a.scale_modifier, rq, c3);
+
+    // ---- computeCov2DCUDA (backward.cu:147-326)
+    Cov2D k;
+    cov2d_eval(mean, fx, fy, a.tanfovx, a.tanfovy, c3, view, k);
+    const float xg = k.txtz < -k.limx || k.txtz > k.limx ? 0.f : 1.f;
+    const float yg = k.tytz < -k.limy || k.tytz > k.limy ? 0.f : 1.f;
+    float c_xx = k.cov.m[0][0], c_xy = k.cov.m[0][1], c_yy = k.cov.m[1][1];
+    const float h_var = 0.3f;
+    const float det_cov = c_xx * c_yy - c_xy * c_xy;
+    c_xx += h_var;
+    c_yy += h_var;
+    const float det_h = c_xx * c_yy - c_xy * c_xy;
+    float dop = s5;
+    float dxx = 0.f, dxy = 0.f, dyy = 0.f;
+    if (!alt || a.antialiasing) {  // the alt rasterizer applies the AA term only with antialiasing (backward.cu:212-245)
+        const float hs = sqrtf(fmaxf(0.000025f, det_cov / det_h));
+        const float d_hs = s5 * opac;
+        dop = s5 * hs;
+        const float d_inside = (det_cov / det_h) <= 0.000025f ? 0.f : d_hs / (2 * hs);
+        const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
+        const float sqv = w * w + w * (x + y) + x * y - z * z;
+        const float denom_f = d_inside / (sqv * sqv);
+        dxx = w * (w * y + y * y + z * z) * denom_f;
+        dyy = w * (w * x + x * x + z * z) * denom_f;
+        dxy = -2.f * w * z * (w + x + y) * denom_f;
     }
+    const float dcx = s2, dcy = s3, dcz = s4;
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const m3& Tm = k.T;
+    const m3& V = k.Vrk;
+    float dc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#define TT(c, r) Tm.m[c][r]
+#define VK(c, r) V.m[c][r]
+    if (denom2inv != 0) {
+        dxx += denom2inv * (-c_yy * c_yy * dcx + 2 * c_xy * c_yy * dcy + (denom - c_xx * c_yy) * dcz);
+        dyy += denom2inv * (-c_xx * c_xx * dcz + 2 * c_xx * c_xy * dcy + (denom - c_xx * c_yy) * dcx);
+        dxy += denom2inv * 2 * (c_xy * c_yy * dcx - (denom + 2 * c_xy * c_xy) * dcy + c_xx * c_xy * dcz);
+        dc[0] = (TT(0, 0) * TT(0, 0) * dxx + TT(0, 0) * TT(1, 0) * dxy + TT(1, 0) * TT(1, 0) * dyy);
+        dc[3] = (TT(0, 1) * TT(0, 1) * dxx + TT(0, 1) * TT(1, 1) * dxy + TT(1, 1) * TT(1, 1) * dyy);
+        dc[5] = (TT(0, 2) * TT(0, 2) * dxx + TT(0, 2) * TT(1, 2) * dxy + TT(1, 2) * TT(1, 2) * dyy);
+        dc[1] = 2 * TT(0, 0) * TT(0, 1) * dxx + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dxy + 2 * TT(1, 0) * TT(1, 1) * dyy;
+        dc[2] = 2 * TT(0, 0) * TT(0, 2) * dxx + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dxy + 2 * TT(1, 0) * TT(1, 2) * dyy;
+        dc[4] = 2 * TT(0, 2) * TT(0, 1) * dxx + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dxy + 2 * TT(1, 1) * TT(1, 2) * dyy;
+    }
+    const float dT00 = 2 * (TT(0, 0) * VK(0, 0) + TT(0, 1) * VK(0, 1) + TT(0, 2) * VK(0, 2)) * dxx + (TT(1, 0) * VK(0, 0) + TT(1, 1) * VK(0, 1) + TT(1, 2) * VK(0, 2)) * dxy;
+    const float dT01 = 2 * (TT(0, 0) * VK(1, 0) + TT(0, 1) * VK(1, 1) + TT(0, 2) * VK(1, 2)) * dxx + (TT(1, 0) * VK(1, 0) + TT(1, 1) * VK(1, 1) + TT(1, 2) * VK(1, 2)) * dxy;
+    const float dT02 = 2 * (TT(0, 0) * VK(2, 0) + TT(0, 1) * VK(2, 1) + TT(0, 2) * VK(2, 2)) * dxx + (TT(1, 0) * VK(2, 0) + TT(1, 1) * VK(2, 1) + TT(1, 2) * VK(2, 2)) * dxy;
+    const float dT10 = 2 * (TT(1, 0) * VK(0, 0) + TT(1, 1) * VK(0, 1) + TT(1, 2) * VK(0, 2)) * dyy + (TT(0, 0) * VK(0, 0) + TT(0, 1) * VK(0, 1) + TT(0, 2) * VK(0, 2)) * dxy;
+    const float dT11 = 2 * (TT(1, 0) * VK(1, 0) + TT(1, 1) * VK(1, 1) + TT(1, 2) * VK(1, 2)) * dyy + (TT(0, 0) * VK(1, 0) + TT(0, 1) * VK(1, 1) + TT(0, 2) * VK(1, 2)) * dxy;
+    const float dT12 = 2 * (TT(1, 0) * VK(2, 0) + TT(1, 1) * VK(2, 1) + TT(1, 2) * VK(2, 2)) * dyy + (TT(0, 0) * VK(2, 0) + TT(0, 1) * VK(2, 1) + TT(0, 2) * VK(2, 2)) * dxy;
+#undef VK
+#undef TT
+    const m3& Wm = k.W;
+    const float dJ00 = Wm.m[0][0] * dT00 + Wm.m[0][1] * dT01 + Wm.m[0][2] * dT02;
+    const float dJ02 = Wm.m[2][0] * dT00 + Wm.m[2][1] * dT01 + Wm.m[2][2] * dT02;
+    const float dJ11 = Wm.m[1][0] * dT10 + Wm.m[1][1] * dT11 + Wm.m[1][2] * dT12;
+    const float dJ12 = Wm.m[2][0] * dT10 + Wm.m[2][1] * dT11 + Wm.m[2][2] * dT12;
+    const f3 t = k.t;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = xg * -fx * tz2 * dJ02;
+    const float dty = yg * -fy * tz2 * dJ12;
+    float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2 * fx * t.x) * tz3 * dJ02 + (2 * fy * t.y) * tz3 * dJ12;
+    if (has_depth) dtz -= alt ? s9 * tz2 : s9 / (t.z * t.z);  // alt-rasterizer backward.cu:312
+    const float* vm = view;
+    f3 dmean = mk(vm[0] * dtx + vm[1] * dty + vm[2] * dtz, vm[4] * dtx + vm[5] * dty + vm[6] * dtz,
+                  vm[8] * dtx + vm[9] * dty + vm[10] * dtz);
+
+    // ---- preprocessCUDA backward (backward.cu:398-495): screen-space mean -> world mean
+    const f3 m = mean;
+    const float m_w = 1.0f / (xform44w(m, proj) + 0.0000001f);
+    const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+    const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+    f3 d2;
+    d2.x = (proj[0] * m_w - proj[3] * mul1) * s0 + (proj[1] * m_w - proj[3] * mul2) * s1;
+    d2.y = (proj[4] * m_w - proj[7] * mul1) * s0 + (proj[5] * m_w - proj[7] * mul2) * s1;
+    d2.z = (proj[8] * m_w - proj[11] * mul1) * s0 + (proj[9] * m_w - proj[11] * mul2) * s1;
+    dmean = add(dmean, d2);
+
+    // ---- SH backward (backward.cu:23-142) runs in k_sh_bwd, which adds its view-direction term to
+    //      dmean3D (or to the parent-deferred share) after this kernel.
+    if (!a.shs && o.dsh)
+        for (int i = 0; i < M3; i++) o.dsh[(size_t)idx * M3 + i] = 0.f;
+    // alt without higher-order coefficients: the reference skips the whole SH backward (backward.cu:443),
+    // so even dc gets no gradient
+    if (!a.shs && o.ddc) { o.ddc[3 * idx] = 0.f; o.ddc[3 * idx + 1] = 0.f; o.ddc[3 * idx + 2] = 0.f; }
+
+    // ---- cov3D backward (backward.cu:330-393)
+    float dscale[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.scales) {
+        const float qq[4] = {rq.x, rq.y, rq.z, rq.w};
+        const float r = qq[0], x = qq[1], y = qq[2], z = qq[3];
+        const m3 R = quat_rot(qq);
+        m3 S = mcols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        const f3 s = scl(a.scale_modifier, scl3);
+        S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
+        const m3 Mm = mmul(S, R);
+        const m3 dS = mcols(dc[0], 0.5f * dc[1], 0.5f * dc[2], 0.5f * dc[1], dc[3], 0.5f * dc[4], 0.5f * dc[2],
+                            0.5f * dc[4], dc[5]);
+        m3 M2 = Mm;
+        for (int c = 0; c < 3; c++)
+            for (int rr = 0; rr < 3; rr++) M2.m[c][rr] = 2.0f * Mm.m[c][rr];
+        const m3 dM = mmul(M2, dS);
+        const m3 Rt = mtrans(R);
+        m3 dMt = mtrans(dM);
+        for (int i = 0; i < 3; i++)
+            dscale[i] = Rt.m[i][0] * dMt.m[i][0] + Rt.m[i][1] * dMt.m[i][1] + Rt.m[i][2] * dMt.m[i][2];
+        for (int rr = 0; rr < 3; rr++) { dMt.m[0][rr] *= s.x; dMt.m[1][rr] *= s.y; dMt.m[2][rr] *= s.z; }
+        dq[0] = 2 * z * (dMt.m[0][1] - dMt.m[1][0]) + 2 * y * (dMt.m[2][0] - dMt.m[0][2]) + 2 * x * (dMt.m[1][2] - dMt.m[2][1]);
+        dq[1] = 2 * y * (dMt.m[1][0] + dMt.m[0][1]) + 2 * z * (dMt.m[2][0] + dMt.m[0][2]) + 2 * r * (dMt.m[1][2] - dMt.m[2][1]) - 4 * x * (dMt.m[2][2] + dMt.m[1][1]);
+        dq[2] = 2 * x * (dMt.m[1][0] + dMt.m[0][1]) + 2 * r * (dMt.m[2][0] - dMt.m[0][2]) + 2 * z * (dMt.m[1][2] + dMt.m[2][1]) - 4 * y * (dMt.m[2][2] + dMt.m[0][0]);
+        dq[3] = 2 * r * (dMt.m[0][1] - dMt.m[1][0]) + 2 * x * (dMt.m[2][0] + dMt.m[0][2]) + 2 * y * (dMt.m[1][2] + dMt.m[2][1]) - 4 * z * (dMt.m[1][1] + dMt.m[0][0]);
+    }
+    float dop_out = dop;
+    if (HIER) {
+        // backward.cu:458-494: the child's opacity/scale/rotation/SH gradients are dropped and
+        // (1 - t) of its mean gradient moves to the parent (added by k_parent_mean_add).
+        const int parent = a.parent_indices[t_idx];
+        if (parent != -1) {
+            const float tt = a.ts[t_idx];
+            dop_out = 0.f;
+            for (int i = 0; i < 3; i++) dscale[i] = 0.f;
+            for (int i = 0; i < 4; i++) dq[i] = 0.f;
+            rec.parent_dmean[3 * t_idx] = (1.0f - tt) * dmean.x;
+            rec.parent_dmean[3 * t_idx + 1] = (1.0f - tt) * dmean.y;
+            rec.parent_dmean[3 * t_idx + 2] = (1.0f - tt) * dmean.z;
+            dmean = mk(0.f, 0.f, 0.f);
+        }
+    }
+    o.dmean2D[3 * idx] = s0;
+    o.dmean2D[3 * idx + 1] = s1;
+    o.dmean2D[3 * idx + 2] = 0.f;
+    o.dcolor[3 * idx] = s6;
+    o.dcolor[3 * idx + 1] = s7;
+    o.dcolor[3 * idx + 2] = s8;
+    o.dopacity[idx] = dop_out;
+    for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = dc[i];
+    o.dmean3D[3 * idx] = dmean.x;
+    o.dmean3D[3 * idx + 1] = dmean.y;
+    o.dmean3D[3 * idx + 2] = dmean.z;
+    o.dscale[3 * idx] = dscale[0];
+    o.dscale[3 * idx + 1] = dscale[1];
+    o.dscale[3 * idx + 2] = dscale[2];
+    reinterpret_cast<float4*>(o.drot)[idx] = make_float4(dq[0], dq[1], dq[2], dq[3]);
 }
 
 // Basis function c of the reference's SH colour (forward.cu:20-67) and its gradient with respect to the
