@@ -997,23 +997,20 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
         uint64_t todo = __ballot(hit);
         __syncthreads();
         uint64_t seen_mask = 0;
-        // Two visited splats per iteration: their falloffs, exponentials and alphas are independent of the pixel
-        // state, so both chains are in flight together; only the short transmittance / colour updates run in list
-        // order (the second sees the first's Tt and done).
-        auto front = [&](int j, float& e2, float& alpha) {
+        while (todo) {
+            int j;  // find-first-set and clear it: two SALU instead of four
+            asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(j), "+s"(todo));
             const float4 xy = s_xy[j];
             const float4 co = s_co[j];
-            e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
+            const float4 c = s_col[j];
+            // straight-line step: the reference's skip / stop tests become lane predicates
+            const float e2 = splat_e2(co, xy.x - pxf, xy.y - pyf);  // power * log2(e)
             const float my_alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(e2));
-            alpha = my_alpha;
+            float alpha = my_alpha;
             if (INTERP) {
                 const float tt = s_t[j];
-                alpha = tt * my_alpha + (1.0f - tt) * (1.0f - __powf(1.0f - my_alpha, s_col[j].w));
+                alpha = tt * my_alpha + (1.0f - tt) * (1.0f - __powf(1.0f - my_alpha, c.w));
             }
-        };
-        auto back = [&](int j, float e2, float alpha) {
-            const float4 xy = s_xy[j];
-            const float4 c = s_col[j];
             const float test_T = Tt * (1 - alpha);
             // alpha >= 1/255 (alpha_e2_threshold); a NaN e2 passes both tests, as in the reference
             const uint64_t valid = ~done & ~__builtin_amdgcn_ballot_w64(e2 > 0.0f) & ~__builtin_amdgcn_ballot_w64(e2 < xy.w);
@@ -1029,23 +1026,6 @@ __global__ void __launch_bounds__(64) k_blend_fwd(FwdArgs A, Guard gd)
             Tt = bl ? test_T : Tt;
             last = bl ? (INTERP ? base - range.x + (uint32_t)j + 1 : __float_as_uint(c.w)) : last;
             if (SEEN && blended) seen_mask |= 1ull << j;
-        };
-        if (__builtin_popcountll(todo) & 1) {  // an odd count: the first splat alone, then pairs in list order
-            int j;  // find-first-set and clear it: two SALU instead of four
-            asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(j), "+s"(todo));
-            float e2a, aa;
-            front(j, e2a, aa);
-            back(j, e2a, aa);
-        }
-        while (todo) {
-            int j, k;
-            asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(j), "+s"(todo));
-            asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(k), "+s"(todo));
-            float e2a, aa, e2b, ab;
-            front(j, e2a, aa);
-            front(k, e2b, ab);
-            back(j, e2a, aa);
-            back(k, e2b, ab);
         }
         if (SEEN && ((seen_mask >> lane) & 1ull)) A.seen[my_id] = 1;
         __syncthreads();
