@@ -207,6 +207,6 @@ def inspect_ranges(imageBuffer, W, H):
 def inspect_splats(geomBuffer, P):
     """(P, 16) float32 per-Gaussian blend records held in a forward's geometry buffer:
     [0:4] x, y, conic a, b | [4:8] conic c, opacity, r, g | [8:12] b, 1/depth, t, 1/kids |
-    [12:16] record base (uint32 bits), x0 | y0 << 16 (int bits), rect width (int bits), alpha threshold on e2
-    (csrc/hlgs_internal.h, Geom::splat)."""
+    [12:16] 0 (unused), x0 | y0 << 16 (int bits), rect width (int bits), alpha threshold on e2
+    (csrc/hlgs_internal.h, Geom::splat; a culled Gaussian's record is unspecified)."""
     return _field(geomBuffer, L.load().hlgs_geom_splat_offset(int(P)), 16 * int(P), torch.float32).view(int(P), 16)

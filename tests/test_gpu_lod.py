@@ -274,6 +274,36 @@ def test_in_kernel_hierarchy_mode_matches_oracle():
         assert_grad(name, leaf_t.grad.cpu().numpy(), gr[name])
 
 
+@pytest.mark.parametrize("deg", [3, 1])
+def test_interpolation_weights_without_render_indices(deg):
+    """interpolation_weights / num_node_kids given with an empty render_indices: the preprocess's common kernel takes
+    its separately instantiated interpolation path (the alpha threshold's bisection, the lerped alpha and the kids
+    exponent in both blends), against the oracle with the same ts / kids."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    cam = S.make_camera(160, 112)
+    sc = S.make_gaussians(3000, deg, cam, seed=5)
+    rng = np.random.default_rng(11)
+    P = sc["means3D"].shape[0]
+    ts = rng.uniform(0.05, 1.0, P).astype(np.float32)
+    kids = rng.integers(1, 9, P).astype(np.int32)
+    scene = dict(sc, ts=ts, kids=kids)
+    fr = O.forward(scene, S.cam_numpy(cam))
+    g, gd = S.upstream_grads(160, 112)
+    gr = O.backward(fr, scene, g, gd)
+    t = lambda a, rg=False: torch.tensor(a, device=DEV, requires_grad=rg)  # noqa: E731
+    hier = dict(interpolation_weights=t(ts), num_node_kids=t(kids))
+    rast = GaussianRasterizer(settings_for(cam, deg, DEV, hierarchy=hier))
+    m, o, sh, s, r = (t(sc[k], True) for k in ("means3D", "opacities", "shs", "scales", "rotations"))
+    m2 = torch.zeros_like(m, requires_grad=True)
+    color, radii, invd = rast(means3D=m, means2D=m2, opacities=o, shs=sh, scales=s, rotations=r)
+    np.testing.assert_array_equal(radii.cpu().numpy(), fr.radii)
+    mx, nbad, ok = image_check(color.detach().cpu().numpy(), fr.color)
+    assert ok, (mx, nbad)
+    ((color * t(g)).sum() + (invd * t(gd)).sum()).backward()
+    for name, leaf_t in (("dmean3D", m), ("dopacity", o), ("dscale", s), ("drot", r), ("dsh", sh), ("dmean2D", m2)):
+        assert_grad(name, leaf_t.grad.cpu().numpy(), gr[name])
+
+
 def test_morton_codes_bit_exact():
     """get_morton_indices (morton.cu:9-42) against the float32 numpy restatement, plus sort_morton's
     permutation (gaussian_model.py:570-589) keeping the root first."""

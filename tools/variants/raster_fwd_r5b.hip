@@ -303,9 +303,6 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
                                                                   const uint32_t* __restrict__ hist)
 {
     if (guard_fail(gd)) return;
-    // 4-byte entries only (the low words of the sort keys): the tile sort gathers each entry's depth itself, so the
-    // scattered stores -- about one per block and tile, each into its own line -- carry half the bytes
-    uint32_t* __restrict__ ents = reinterpret_cast<uint32_t*>(keys);
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_base;
     __shared__ uint32_t s_pre[BG + 1];
@@ -354,7 +351,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         constexpr int J = 4;
         float2 gxy[J];
         int2 gext[J];
-        uint32_t gmask[J];
+        uint32_t gmask[J], gdb[J];
         bool live[J];
 #pragma unroll
         for (int j = 0; j < J; j++) {
@@ -364,6 +361,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
                 gxy[j] = g.means2D[g0 + k];
                 gext[j] = g.rects[g0 + k];
                 gmask[j] = PACK ? g.qmask[g0 + k] : 0u;
+                gdb[j] = __float_as_uint(g.depths[g0 + k]);
             }
         }
 #pragma unroll
@@ -389,16 +387,17 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++)
-                    if (use[u]) ents[pos[u]] = ent[u];
+                    if (use[u]) keys[pos[u]] = ((uint64_t)gdb[j] << 32) | ent[u];
             }
         }
         return;
     }
-    for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int x, int y, uint32_t qm, uint32_t) {
+    for_each_instance<BG, true, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int x, int y, uint32_t qm, uint32_t dbits) {
         if (g.drop && !qm) return;  // the footprint reaches none of the tile's quadrants
         const int tile = y * gx + x;
         const uint32_t r = atomicAdd(&s_rank[tile], 1u);
-        ents[s_cnt[tile] + r] = PACK ? ((uint32_t)idx << kEntryShift) | qm : (uint32_t)idx;
+        const uint32_t entry = PACK ? ((uint32_t)idx << kEntryShift) | qm : (uint32_t)idx;
+        keys[s_cnt[tile] + r] = ((uint64_t)dbits << 32) | entry;
     });
 }
 
@@ -687,7 +686,7 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
     const int2 ext = g.rects[idx];
     int x0, y0, x1, y1;
     tile_rect(xy.x, xy.y, ext.x, ext.y, gx, gy, x0, y0, x1, y1);
-    uint32_t* __restrict__ ents = reinterpret_cast<uint32_t*>(keys);  // entries only, as k_scatter_keys_lds
+    const uint64_t dkey = (uint64_t)__float_as_uint(g.depths[idx]) << 32;
     const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
     const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
     const float kthr = alt ? alt_keep_threshold(co.w) : 0.f;
@@ -699,27 +698,14 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
             if (g.drop && !rect_tile_mask(masks, r)) continue;
             const int tile = y * gx + x;
             const uint32_t slot = atomicAdd(&cursor[tile], 1u);
-            ents[ranges[tile].x + slot] = pack ? ((uint32_t)idx << kEntryShift) | rect_tile_mask(masks, r) : (uint32_t)idx;
+            keys[ranges[tile].x + slot] =
+                dkey | (pack ? ((uint32_t)idx << kEntryShift) | rect_tile_mask(masks, r) : (uint32_t)idx);
         }
 }
 
-// The sort key of a binned entry: the Gaussian's depth bits above the entry (depths are positive, so their bits order
-// as the floats do; the entry orders equal depths by Gaussian index, CUB's stable order, App. A-4).
-struct KeySrc {
-    const uint32_t* ents;  // the scatter's entries (the keys buffer's first 4 R bytes)
-    const float* depths;   // Geom::depths
-    int pack;              // entries carry quadrant masks (pack_entries): index = entry >> kEntryShift
-    __device__ __forceinline__ uint64_t operator()(uint32_t p) const
-    {
-        const uint32_t e = ents[p];
-        const uint32_t id = pack ? e >> kEntryShift : e;
-        return ((uint64_t)__float_as_uint(depths[id]) << 32) | e;
-    }
-};
-
 // One 256-thread block per tile: bitonic sort of the tile's keys in LDS.  Tiles longer than kSortCap
 // are sorted in kSortCap runs here and merged by k_merge_runs.
-__global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ranges, KeySrc ks, uint64_t* runs,
+__global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ranges, uint64_t* keys,
                                                    uint32_t* __restrict__ point_list, int T, Guard gd)
 {
     if (guard_fail(gd)) return;
@@ -734,7 +720,7 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
         const uint32_t n = min((uint32_t)kSortCap, cnt - c0);
         uint32_t np = 2;
         while (np < n) np <<= 1;
-        for (uint32_t i = tid; i < np; i += 256) s[i] = i < n ? ks(r.x + c0 + i) : ~0ull;
+        for (uint32_t i = tid; i < np; i += 256) s[i] = i < n ? keys[r.x + c0 + i] : ~0ull;
         __syncthreads();
         for (uint32_t kk = 2; kk <= np; kk <<= 1)
             for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
@@ -746,8 +732,8 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
                 }
                 __syncthreads();
             }
-        if (big)  // sorted runs into the second key buffer (the entries of other tiles still occupy the first)
-            for (uint32_t i = tid; i < n; i += 256) runs[r.x + c0 + i] = s[i];
+        if (big)
+            for (uint32_t i = tid; i < n; i += 256) keys[r.x + c0 + i] = s[i];
         else
             for (uint32_t i = tid; i < n; i += 256) point_list[r.x + c0 + i] = (uint32_t)s[i];
         __syncthreads();
@@ -826,13 +812,14 @@ __device__ __forceinline__ void wave_sort_upto(LD&& ld, uint32_t n, ST&& st, int
 // register sort instead of a 512-key one (the mean configs[1] list is 258 keys).  Keys are unique, so the merge is
 // the same total order.
 template <int KH>
-__device__ __forceinline__ void wave_sort_split(const KeySrc& ks, uint32_t base, uint32_t n,
+__device__ __forceinline__ void wave_sort_split(const uint64_t* __restrict__ keys, uint32_t base, uint32_t n,
                                                 uint32_t* __restrict__ out, int lane, uint64_t* s)
 {
     constexpr uint32_t A = 64u * KH;
     const uint32_t m = n - A;  // 1 .. A
-    wave_sort_keys_st<KH>([&](uint32_t e) { return ks(base + e); }, A, [&](uint32_t e, uint64_t v) { s[e] = v; }, lane);
-    wave_sort_upto<KH>([&](uint32_t e) { return ks(base + A + e); }, m, [&](uint32_t e, uint64_t v) { s[A + e] = v; },
+    wave_sort_keys_st<KH>([&](uint32_t e) { return keys[base + e]; }, A, [&](uint32_t e, uint64_t v) { s[e] = v; },
+                          lane);
+    wave_sort_upto<KH>([&](uint32_t e) { return keys[base + A + e]; }, m, [&](uint32_t e, uint64_t v) { s[A + e] = v; },
                        lane);
     __syncthreads();  // one wave: the LDS stores before the loads
     const uint32_t per = (n + 63u) / 64u, k0 = min(n, (uint32_t)lane * per), k1 = min(n, k0 + per);
@@ -852,13 +839,13 @@ __device__ __forceinline__ void wave_sort_split(const KeySrc& ks, uint32_t base,
     }
 }
 template <int KPL>
-__device__ __forceinline__ void wave_sort_tile(const KeySrc& ks, uint32_t* __restrict__ point_list, uint32_t base,
-                                               uint32_t n, int lane)
+__device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list,
+                                               uint32_t base, uint32_t n, int lane)
 {
-    wave_sort_keys<KPL>([&](uint32_t e) { return ks(base + e); }, n, point_list + base, lane);
+    wave_sort_keys<KPL>([&](uint32_t e) { return keys[base + e]; }, n, point_list + base, lane);
 }
 // Tiles of up to kWaveSortCap instances: one wave each (k_tile_sort handles the longer ones).
-__global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__ ranges, KeySrc ks,
+__global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__ ranges, uint64_t* keys,
                                                        uint32_t* __restrict__ point_list, int T, Guard gd)
 {
     if (guard_fail(gd)) return;
@@ -868,11 +855,11 @@ __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__
     const int lane = threadIdx.x;
     if (n == 0 || n > (uint32_t)kWaveSortCap) return;
     __shared__ uint64_t s_sort[kWaveSortCap + 1];  // + 1: the merge may read one past the second run
-    if (n <= 64) wave_sort_tile<1>(ks, point_list, r.x, n, lane);
-    else if (n <= 128) wave_sort_split<1>(ks, r.x, n, point_list, lane, s_sort);
-    else if (n <= 256) wave_sort_split<2>(ks, r.x, n, point_list, lane, s_sort);
-    else if (n <= 512) wave_sort_split<4>(ks, r.x, n, point_list, lane, s_sort);
-    else wave_sort_split<8>(ks, r.x, n, point_list, lane, s_sort);
+    if (n <= 64) wave_sort_tile<1>(keys, point_list, r.x, n, lane);
+    else if (n <= 128) wave_sort_split<1>(keys, r.x, n, point_list, lane, s_sort);
+    else if (n <= 256) wave_sort_split<2>(keys, r.x, n, point_list, lane, s_sort);
+    else if (n <= 512) wave_sort_split<4>(keys, r.x, n, point_list, lane, s_sort);
+    else wave_sort_split<8>(keys, r.x, n, point_list, lane, s_sort);
 }
 
 // Merge pass for long tiles: element of run r finds its rank in the partner run by binary search.
@@ -1229,13 +1216,12 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
                            im.tile_cursor, b.keys, gx, gy, alt, gd, (int)pack_entries(a.P));
     if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
-    const KeySrc ks{reinterpret_cast<const uint32_t*>(b.keys), g.depths, (int)pack_entries(a.P)};
-    hipLaunchKernelGGL(k_tile_sort_wave, dim3(T), dim3(64), 0, s, im.ranges, ks, b.point_list, T, gd);
+    hipLaunchKernelGGL(k_tile_sort_wave, dim3(T), dim3(64), 0, s, im.ranges, b.keys, b.point_list, T, gd);
     if (max_count > (uint32_t)kWaveSortCap)
-        hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, ks, b.keys2, b.point_list, T, gd);
-    if (max_count > (uint32_t)kSortCap) {  // the runs are in keys2; every entry has been read by now
-        uint64_t* src = b.keys2;
-        uint64_t* dst = b.keys;
+        hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, b.keys, b.point_list, T, gd);
+    if (max_count > (uint32_t)kSortCap) {
+        uint64_t* src = b.keys;
+        uint64_t* dst = b.keys2;
         for (uint32_t L = kSortCap; L < max_count; L <<= 1) {
             const int last = (L << 1) >= max_count;
             hipLaunchKernelGGL(k_merge_runs, dim3((max_count + 255) / 256, T), dim3(256), 0, s, im.ranges, src, dst,
