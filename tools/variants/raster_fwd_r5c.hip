@@ -25,25 +25,16 @@ namespace hlgs {
 // ------------------------------------------------------------------------------------------------
 // s_pre[k] = exclusive prefix of tiles_touched over the block's BG Gaussians (0 past P), s_pre[BG] =
 // the block's total: thread t scans its four consecutive entries, then the 1024 thread totals are scanned.
-// The rect sizes thread t scans (Gaussians 4t .. 4t + 3 of the block), loaded apart from the scan so that a kernel
-// can issue them together with its other first-round loads.
 template <int BG>
-__device__ __forceinline__ void block_rect_sizes(int P, const Geom& g, uint32_t (&a)[4])
+__device__ __forceinline__ void block_rect_prefix(int P, const Geom& g, uint32_t* s_pre, uint32_t* s_w)
 {
-    const int g0 = blockIdx.x * BG, t = threadIdx.x;
+    constexpr int BT = BG / 4;  // threads: four Gaussians each
+    const int g0 = blockIdx.x * BG, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t a[4], sum = 0, mx = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int idx = g0 + 4 * t + k;
         a[k] = idx < P ? g.tiles_touched[idx] : 0u;
-    }
-}
-template <int BG>
-__device__ __forceinline__ void block_rect_prefix(const uint32_t (&a)[4], uint32_t* s_pre, uint32_t* s_w)
-{
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    uint32_t sum = 0, mx = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
         sum += a[k];
         mx = max(mx, a[k]);
     }
@@ -85,44 +76,28 @@ constexpr uint32_t kNarrowRect = 64;
 // rect the block's instances are numbered Gaussian by Gaussian (s_pre) and each thread takes one contiguous run of
 // them, so a Gaussian whose rect spans thousands of tiles is spread over the whole block instead of serialising one
 // thread.
-struct GIn {
-    float2 xy;
-    int2 ext;
-    float4 co;
-    uint32_t masks, dbits;
-};
-template <bool KEYS, bool MASKS>
-__device__ __forceinline__ void gauss_in(const Geom& g, bool alt, int idx, GIn& v)
-{
-    v.xy = g.means2D[idx];
-    v.ext = g.rects[idx];
-    v.co = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (alt) {
-        const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
-        v.co = make_float4(r0.z, r0.w, r1.x, r1.y);
-    }
-    v.masks = MASKS ? g.qmask[idx] : 0u;
-    v.dbits = KEYS ? __float_as_uint(g.depths[idx]) : 0u;
-}
-// The narrow path's inputs (Gaussians threadIdx.x + j BG / 4 of the block, every one below P, culled or not), issued at
-// the top of a kernel with its other first-round loads; for_each_instance then reads no Gaussian input itself.
-template <int BG, bool MASKS>
-__device__ __forceinline__ void prefetch_instances(const Geom& g, bool alt, int P, GIn (&in)[4])
-{
-    const int g0 = blockIdx.x * BG;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {  // past P: Gaussian P - 1 again (not used), so the loads need no branch
-        const int idx = min(g0 + (int)threadIdx.x + j * (BG / 4), P - 1);
-        gauss_in<false, MASKS>(g, alt, idx, in[j]);
-    }
-}
-
 template <int BG, bool KEYS, bool MASKS, typename F>
 __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy, bool alt, const uint32_t* s_pre,
-                                                  const uint32_t* s_w, const GIn (&pre)[4], F&& f)
+                                                  const uint32_t* s_w, F&& f)
 {
     const int g0 = blockIdx.x * BG;
-    auto gauss = [&](int idx, GIn& v) { gauss_in<KEYS, MASKS>(g, alt, idx, v); };
+    struct GIn {
+        float2 xy;
+        int2 ext;
+        float4 co;
+        uint32_t masks, dbits;
+    };
+    auto gauss = [&](int idx, GIn& v) {
+        v.xy = g.means2D[idx];
+        v.ext = g.rects[idx];
+        v.co = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (alt) {
+            const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
+            v.co = make_float4(r0.z, r0.w, r1.x, r1.y);
+        }
+        v.masks = MASKS ? g.qmask[idx] : 0u;
+        v.dbits = KEYS ? __float_as_uint(g.depths[idx]) : 0u;
+    };
     auto qmask = [&](uint32_t masks, uint32_t r) { return MASKS ? rect_tile_mask(masks, r) : 0u; };
     if (s_w[(BG / 4) / 64] <= kNarrowRect) {  // no wide rect in this block: one thread per Gaussian
         constexpr int J = 4;  // Gaussians per thread
@@ -132,7 +107,7 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
         for (int j = 0; j < J; j++) {
             const int k = threadIdx.x + j * (BG / 4);
             live[j] = s_pre[k + 1] != s_pre[k];
-            in[j] = pre[j];
+            if (live[j]) gauss(g0 + k, in[j]);
         }
 #pragma unroll
         for (int j = 0; j < J; j++) {
@@ -208,21 +183,16 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     __shared__ uint32_t s_pre[BG + 1];
     __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
     const int T = gx * gy;
-    // every input in the first round trip (the rect sizes for the scan and the narrow walk's Gaussians)
-    uint32_t sizes[4];
-    block_rect_sizes<BG>(P, g, sizes);
-    GIn pre[4];
-    prefetch_instances<BG, DROP>(g, alt, P, pre);
     for (int t = threadIdx.x; t < T; t += (BG / 4)) s_hist[t] = 0;
     if (threadIdx.x == 0) s_w[(BG / 4) / 64] = 0;
     __syncthreads();
-    block_rect_prefix<BG>(sizes, s_pre, s_w);
+    block_rect_prefix<BG>(P, g, s_pre, s_w);
     if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[BG];
     if (zero_words && blockIdx.x == 0) {  // k_tile_offsets_plan's look-back words, failure and completion words
         for (int i = threadIdx.x; i < n_zero; i += BG / 4) zero_words[i] = 0u;
         if (threadIdx.x == 0) { misc[kMiscFail] = 0u; misc[kMiscDone] = 0u; }
     }
-    for_each_instance<BG, false, DROP>(g, gx, gy, alt, s_pre, s_w, pre, [&](int, int x, int y, uint32_t qm, uint32_t) {
+    for_each_instance<BG, false, DROP>(g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t qm, uint32_t) {
         if (!DROP || qm) atomicAdd(&s_hist[y * gx + x], 1u);
     });
     __syncthreads();
@@ -343,38 +313,16 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
     const int T = gx * gy;
     uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
     uint32_t* s_rank = s_hist + T; // per-tile running rank
-    // The first round trip carries every input the block needs: the rect sizes for the scan, the preceding blocks'
-    // totals, the first kPreTiles of this thread's tile bases (the tile's range start + this block's histogram offset)
-    // and the narrow walk's Gaussians.  (Issued one after another, the five rounds of loads had been the kernel's time.)
-    constexpr int kPreTiles = 8;
-    uint32_t sizes[4];
-    block_rect_sizes<BG>(P, g, sizes);
-    // (every load unconditional, clamped into range, so that the compiler issues them back to back)
-    uint32_t part = block_tot[min((int)threadIdx.x, max((int)blockIdx.x - 1, 0))];  // preceding block threadIdx.x
-    uint32_t trange[kPreTiles], trow[kPreTiles];
-    const uint32_t* row = hist ? hist + (size_t)blockIdx.x * T : nullptr;
-    if (hist) {
-#pragma unroll
-        for (int k = 0; k < kPreTiles; k++) {
-            const int t = min((int)threadIdx.x + k * (BG / 4), T - 1);
-            trange[k] = ranges[t].x;
-            trow[k] = row[t];
-        }
-    }
-    GIn pre[4];
-    prefetch_instances<BG, PACK>(g, alt, P, pre);
-    if (threadIdx.x == 0) { s_w[(BG / 4) / 64] = 0; s_base = 0; }
-    if (hist) {
-        for (int t = threadIdx.x; t < T; t += (BG / 4)) s_rank[t] = 0;
-    } else {
-        for (int t = threadIdx.x; t < T; t += (BG / 4)) { s_cnt[t] = 0; s_rank[t] = 0; }
-    }
+    for (int t = threadIdx.x; t < T; t += (BG / 4)) { s_cnt[t] = 0; s_rank[t] = 0; }
+    if (threadIdx.x == 0) s_w[(BG / 4) / 64] = 0;
     __syncthreads();
-    block_rect_prefix<BG>(sizes, s_pre, s_w);
+    block_rect_prefix<BG>(P, g, s_pre, s_w);
     {  // point_offsets (the inclusive scan of tiles_touched) = the block's base + the block-local prefix; the base is
-       // the sum of the preceding count blocks' totals (k_count_tiles): thread i adds block i's, and i + BG / 4 ... too
-        if ((int)threadIdx.x >= (int)blockIdx.x) part = 0;
-        for (int i = threadIdx.x + BG / 4; i < (int)blockIdx.x; i += BG / 4) part += block_tot[i];
+       // the sum of the preceding count blocks' totals (k_count_tiles), at most 16 per thread
+        if (threadIdx.x == 0) s_base = 0;
+        __syncthreads();
+        uint32_t part = 0;
+        for (int i = threadIdx.x; i < (int)blockIdx.x; i += BG / 4) part += block_tot[i];
         if (part) atomicAdd(&s_base, part);
         __syncthreads();
         const int g0 = blockIdx.x * BG, g1 = min(P, g0 + BG);
@@ -385,14 +333,10 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         }
     }
     if (hist) {
-#pragma unroll
-        for (int k = 0; k < kPreTiles; k++) {
-            const int t = (int)threadIdx.x + k * (BG / 4);
-            if (t < T) s_cnt[t] = trange[k] + trow[k];
-        }
-        for (int t = threadIdx.x + kPreTiles * (BG / 4); t < T; t += (BG / 4)) s_cnt[t] = ranges[t].x + row[t];
+        const uint32_t* row = hist + (size_t)blockIdx.x * T;
+        for (int t = threadIdx.x; t < T; t += (BG / 4)) s_cnt[t] = ranges[t].x + row[t];
     } else {
-        for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, pre, [&](int, int x, int y, uint32_t qm, uint32_t) {
+        for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int, int x, int y, uint32_t qm, uint32_t) {
             if (!(g.drop && !qm)) atomicAdd(&s_cnt[y * gx + x], 1u);
         });
         __syncthreads();
@@ -408,19 +352,26 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         // its atomic's return.
         const int g0 = blockIdx.x * BG;
         constexpr int J = 4;
+        float2 gxy[J];
+        int2 gext[J];
+        uint32_t gmask[J];
         bool live[J];
 #pragma unroll
         for (int j = 0; j < J; j++) {
             const int k = threadIdx.x + j * (BG / 4);
             live[j] = s_pre[k + 1] != s_pre[k];
+            if (live[j]) {
+                gxy[j] = g.means2D[g0 + k];
+                gext[j] = g.rects[g0 + k];
+                gmask[j] = PACK ? g.qmask[g0 + k] : 0u;
+            }
         }
 #pragma unroll
         for (int j = 0; j < J; j++) {
             if (!live[j]) continue;
             const uint32_t idx = (uint32_t)(g0 + threadIdx.x + j * (BG / 4));
-            const uint32_t gmask = pre[j].masks;
             int x0, y0, x1, y1;
-            tile_rect(pre[j].xy.x, pre[j].xy.y, pre[j].ext.x, pre[j].ext.y, gx, gy, x0, y0, x1, y1);
+            tile_rect(gxy[j].x, gxy[j].y, gext[j].x, gext[j].y, gx, gy, x0, y0, x1, y1);
             const int w = x1 - x0, n = w * (y1 - y0);
             int tx = 0, ty = 0;
             for (int c = 0; c < n; c += 4) {
@@ -429,7 +380,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int r = c + u;
-                    const uint32_t qm = PACK ? rect_tile_mask(gmask, (uint32_t)r) : 0u;
+                    const uint32_t qm = PACK ? rect_tile_mask(gmask[j], (uint32_t)r) : 0u;
                     use[u] = r < n && !(g.drop && !qm);
                     const int tile = (y0 + ty) * gx + x0 + tx;
                     if (use[u]) pos[u] = s_cnt[tile] + atomicAdd(&s_rank[tile], 1u);
@@ -443,7 +394,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         }
         return;
     }
-    for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, pre, [&](int idx, int x, int y, uint32_t qm, uint32_t) {
+    for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, [&](int idx, int x, int y, uint32_t qm, uint32_t) {
         if (g.drop && !qm) return;  // the footprint reaches none of the tile's quadrants
         const int tile = y * gx + x;
         const uint32_t r = atomicAdd(&s_rank[tile], 1u);
@@ -761,20 +712,9 @@ struct KeySrc {
     __device__ __forceinline__ uint64_t operator()(uint32_t p) const
     {
         const uint32_t e = ents[p];
-        return ((uint64_t)depth_bits(e) << 32) | e;
+        const uint32_t id = pack ? e >> kEntryShift : e;
+        return ((uint64_t)__float_as_uint(depths[id]) << 32) | e;
     }
-    __device__ __forceinline__ uint32_t depth_bits(uint32_t e) const
-    {
-        return __float_as_uint(depths[pack ? e >> kEntryShift : e]);
-    }
-};
-// A tile's keys from position base on: the register sorts read all of a lane's entries first and then gather all of
-// their depths, two rounds of independent loads (a per-key entry -> depth chain would wait once per key).
-struct KeyView {
-    KeySrc ks;
-    uint32_t base;
-    __device__ __forceinline__ uint32_t entry(uint32_t e) const { return ks.ents[base + e]; }
-    __device__ __forceinline__ uint32_t depth_bits(uint32_t ent) const { return ks.depth_bits(ent); }
 };
 
 // One 256-thread block per tile: bitonic sort of the tile's keys in LDS.  Tiles longer than kSortCap
@@ -794,19 +734,7 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
         const uint32_t n = min((uint32_t)kSortCap, cnt - c0);
         uint32_t np = 2;
         while (np < n) np <<= 1;
-        {  // all of a thread's entries, then all of their depths: two rounds of loads, not one chain per key
-            constexpr int EPT = kSortCap / 256;
-            uint32_t en[EPT], dp[EPT];
-#pragma unroll
-            for (int k = 0; k < EPT; k++) en[k] = ks.ents[r.x + c0 + min(tid + 256u * k, n - 1)];
-#pragma unroll
-            for (int k = 0; k < EPT; k++) dp[k] = ks.depth_bits(en[k]);
-#pragma unroll
-            for (int k = 0; k < EPT; k++) {
-                const uint32_t i = tid + 256u * k;
-                if (i < np) s[i] = i < n ? ((uint64_t)dp[k] << 32) | en[k] : ~0ull;
-            }
-        }
+        for (uint32_t i = tid; i < np; i += 256) s[i] = i < n ? ks(r.x + c0 + i) : ~0ull;
         __syncthreads();
         for (uint32_t kk = 2; kk <= np; kk <<= 1)
             for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
@@ -829,24 +757,16 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
 // Per-tile sort of up to 64 * KPL keys by one wave, entirely in registers: lane l holds elements
 // l * KPL .. l * KPL + KPL - 1; bitonic stages with partner distance < KPL are compare-exchanges inside
 // a lane, longer ones exchange with lane l ^ (j / KPL).  No LDS, no barriers.
-// The keys are read through ld (a KeyView: ld.entry(e), e < n, then ld.depth_bits(entry)), and each sorted key handed to
-// st(e, key).
+// The keys are read through ld(e), e < n, and each sorted key handed to st(e, key).
 template <int KPL, typename LD, typename ST>
 __device__ __forceinline__ void wave_sort_keys_st(LD&& ld, uint32_t n, ST&& st, int lane)
 {
     constexpr uint32_t NP = 64u * KPL;
     uint64_t v[KPL];
-    {
-        uint32_t en[KPL], dp[KPL];
 #pragma unroll
-        for (int i = 0; i < KPL; i++) en[i] = ld.entry(min((uint32_t)lane * KPL + i, n - 1));  // n >= 1
-#pragma unroll
-        for (int i = 0; i < KPL; i++) dp[i] = ld.depth_bits(en[i]);
-#pragma unroll
-        for (int i = 0; i < KPL; i++) {
-            const uint32_t e = (uint32_t)lane * KPL + i;
-            v[i] = e < n ? ((uint64_t)dp[i] << 32) | en[i] : ~0ull;
-        }
+    for (int i = 0; i < KPL; i++) {
+        const uint32_t e = (uint32_t)lane * KPL + i;
+        v[i] = e < n ? ld(e) : ~0ull;
     }
 #pragma unroll
     for (uint32_t kk = 2; kk <= NP; kk <<= 1) {
@@ -911,8 +831,9 @@ __device__ __forceinline__ void wave_sort_split(const KeySrc& ks, uint32_t base,
 {
     constexpr uint32_t A = 64u * KH;
     const uint32_t m = n - A;  // 1 .. A
-    wave_sort_keys_st<KH>(KeyView{ks, base}, A, [&](uint32_t e, uint64_t v) { s[e] = v; }, lane);
-    wave_sort_upto<KH>(KeyView{ks, base + A}, m, [&](uint32_t e, uint64_t v) { s[A + e] = v; }, lane);
+    wave_sort_keys_st<KH>([&](uint32_t e) { return ks(base + e); }, A, [&](uint32_t e, uint64_t v) { s[e] = v; }, lane);
+    wave_sort_upto<KH>([&](uint32_t e) { return ks(base + A + e); }, m, [&](uint32_t e, uint64_t v) { s[A + e] = v; },
+                       lane);
     __syncthreads();  // one wave: the LDS stores before the loads
     const uint32_t per = (n + 63u) / 64u, k0 = min(n, (uint32_t)lane * per), k1 = min(n, k0 + per);
     uint32_t lo = k0 > m ? k0 - m : 0u, hi = min(k0, A);  // A keys among the first k0 outputs
@@ -934,7 +855,7 @@ template <int KPL>
 __device__ __forceinline__ void wave_sort_tile(const KeySrc& ks, uint32_t* __restrict__ point_list, uint32_t base,
                                                uint32_t n, int lane)
 {
-    wave_sort_keys<KPL>(KeyView{ks, base}, n, point_list + base, lane);
+    wave_sort_keys<KPL>([&](uint32_t e) { return ks(base + e); }, n, point_list + base, lane);
 }
 // Tiles of up to kWaveSortCap instances: one wave each (k_tile_sort handles the longer ones).
 __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__ ranges, KeySrc ks,
