@@ -171,6 +171,47 @@ __device__ __forceinline__ void cut_write(const CutArgs& a, const int* front, in
     }
 }
 
+// A thread's run of at most kCutRun frontier entries, classified once (with the expanding nodes' siblings): pass 1
+// counts from it and pass 2 writes from it, so pass 2 makes no global round trip (it re-read the entries, their rows
+// and the siblings: three of a level's five dependent round trips).
+constexpr int kCutRun = 2;  // entries per thread of a cached run (a level of up to 2,048 entries per workgroup)
+struct CutRun {
+    int v[kCutRun];
+    CutNode c[kCutRun];
+};
+__device__ __forceinline__ int3 cut_eval(const CutArgs& a, const int* front, int i0, int i1, CutRun& run)
+{
+    int3 n = make_int3(0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < kCutRun; j++) run.v[j] = i0 + j < i1 ? front[i0 + j] : -1;
+#pragma unroll
+    for (int j = 0; j < kCutRun; j++) {
+        run.c[j] = CutNode{0, 0, 0};
+        if (run.v[j] < 0) continue;
+        run.c[j] = cut_node(a, run.v[j]);
+        n.x += run.c[j].st == 1;
+        n.y += run.c[j].st == 2;
+        n.z += run.c[j].st == 3;
+    }
+    return n;
+}
+__device__ __forceinline__ void cut_write_run(const CutArgs& a, const CutRun& run, int* next, int o1, int o2, int o3,
+                                              int n3)
+{
+#pragma unroll
+    for (int j = 0; j < kCutRun; j++) {
+        if (run.v[j] < 0) continue;
+        const CutNode& c = run.c[j];
+        if (c.st == 1) a.cut[o1++] = run.v[j];
+        else if (c.st == 2) a.cut[o2++] = run.v[j];
+        else if (c.st == 3) {
+            next[o3] = c.fc;
+            next[n3 + o3] = c.ns;
+            o3++;
+        }
+    }
+}
+
 // resume = 0: start at the root and hand off at the first level wider than kCutNarrow;  resume = 1: continue from
 // the state the level launches left, to the end, and write the count.
 __global__ void __launch_bounds__(1024) k_upper_cut(CutArgs a, int resume)
@@ -199,9 +240,16 @@ __global__ void __launch_bounds__(1024) k_upper_cut(CutArgs a, int resume)
         const int K = (size + 1023) / 1024;
         const int i0 = min(size, (int)threadIdx.x * K), i1 = min(size, i0 + K);
         int3 tot;
-        const int3 o = block_excl3(cut_count(a, front, i0, i1), s_w, &tot);
-        if (total + tot.x + tot.y > a.capacity || 2 * tot.z > a.capacity) { overflow = 1; break; }
-        cut_write(a, front, next, i0, i1, total + o.x, total + tot.x + o.y, o.z, tot.z);
+        if (K <= kCutRun) {  // (uniform) one classification for both passes
+            CutRun run;
+            const int3 o = block_excl3(cut_eval(a, front, i0, i1, run), s_w, &tot);
+            if (total + tot.x + tot.y > a.capacity || 2 * tot.z > a.capacity) { overflow = 1; break; }
+            cut_write_run(a, run, next, total + o.x, total + tot.x + o.y, o.z, tot.z);
+        } else {
+            const int3 o = block_excl3(cut_count(a, front, i0, i1), s_w, &tot);
+            if (total + tot.x + tot.y > a.capacity || 2 * tot.z > a.capacity) { overflow = 1; break; }
+            cut_write(a, front, next, i0, i1, total + o.x, total + tot.x + o.y, o.z, tot.z);
+        }
         total += tot.x + tot.y;
         size = 2 * tot.z;
         parity ^= 1;
@@ -239,8 +287,11 @@ __global__ void __launch_bounds__(1024) k_cut_level(CutArgs a, int launch)
     const int K = per / 1024;
     const int e0 = b * per, e1 = min(size, e0 + per);
     const int i0 = min(e1, e0 + (int)threadIdx.x * K), i1 = min(e1, i0 + K);
-    int3 bt;
-    const int3 o = block_excl3(cut_count(a, front, i0, i1), s_w, &bt);
+    int3 bt, o;
+    CutRun run;
+    const bool cached = K <= kCutRun;  // uniform: one classification for both passes
+    if (cached) o = block_excl3(cut_eval(a, front, i0, i1, run), s_w, &bt);
+    else o = block_excl3(cut_count(a, front, i0, i1), s_w, &bt);
     if (threadIdx.x == 0) {
         int* pb = a.level_counts + 3 * b;
         __hip_atomic_store(pb, bt.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -268,7 +319,8 @@ __global__ void __launch_bounds__(1024) k_cut_level(CutArgs a, int launch)
         if (b == 0 && threadIdx.x == 0) cs->overflow = 1;
         return;
     }
-    cut_write(a, front, next, i0, i1, total + bp.x + o.x, total + tot.x + bp.y + o.y, bp.z + o.z, tot.z);
+    if (cached) cut_write_run(a, run, next, total + bp.x + o.x, total + tot.x + bp.y + o.y, bp.z + o.z, tot.z);
+    else cut_write(a, front, next, i0, i1, total + bp.x + o.x, total + tot.x + bp.y + o.y, bp.z + o.z, tot.z);
     if (b == 0 && threadIdx.x == 0) {  // every workgroup read the state before it arrived
         cs->size = 2 * tot.z;
         cs->total = total + tot.x + tot.y;
