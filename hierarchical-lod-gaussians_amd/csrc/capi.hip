@@ -56,6 +56,7 @@ void launch_depth_l1_forward(long n, const float* inv, const float* mono, const 
 void launch_depth_l1_backward(long n, const float* inv, const float* mono, const float* mask, const float* coef,
                               float* grad, hipStream_t s);
 void launch_upper_cut(const CutArgs& a, hipStream_t s);
+void launch_upper_cut_flat(const CutArgs& a, const int* order, hipStream_t s);
 void launch_rows(bool gather, long n, int row_bytes, const int64_t* idx, const void* src, void* dst, hipStream_t s);
 void launch_morton(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, hipStream_t s);
 void launch_adam(float* param, const float* grad, float* m, float* v, const uint8_t* vis, float lr, float b1, float b2,
@@ -687,7 +688,7 @@ size_t hlgs_upper_cut_scratch_size(int N)
 static int upper_cut_launch(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,
                             int nviews, const float* planes, const float* campos, float distance_multiplier,
                             int use_frustum, int use_lod, void* scratch, int* cut, int* count_out, hipStream_t s,
-                            int** count_dev)
+                            int** count_dev, const void* order = nullptr)
 {
     if (nviews < 1) return fail(HLGS_ERR_ARG, "n_views < 1");
     if (!nodes || !xyz || !cut || !scratch || (use_frustum && (!bounds || !planes)) ||
@@ -704,7 +705,8 @@ static int upper_cut_launch(int N, const int* nodes, const float* xyz, const flo
     a.state = reinterpret_cast<CutState*>(q);
     a.arrive = reinterpret_cast<unsigned*>(q + sizeof(CutState));
     a.level_counts = reinterpret_cast<int*>(a.arrive + kCutLevelLaunches);
-    launch_upper_cut(a, s);
+    if (order) launch_upper_cut_flat(a, static_cast<const int*>(order), s);
+    else launch_upper_cut(a, s);
     *count_dev = a.count;
     return check_stage(s, false, "upper_tree_cut");
 }
@@ -744,6 +746,24 @@ int hlgs_upper_tree_cut_views_device(int N, const int* nodes, const float* xyz, 
     int* dev = nullptr;
     return upper_cut_launch(N, nodes, xyz, bounds, min_dist2, n_views, planes, campos, distance_multiplier,
                             use_frustum, use_lod, scratch, cut, count_device, s, &dev);
+}
+
+int hlgs_upper_tree_cut_views_ordered_device(int N, const int* nodes, const void* order, const float* xyz,
+                                             const float* bounds, const float* min_dist2, int n_views,
+                                             const float* planes, const float* campos, float distance_multiplier,
+                                             int use_frustum, int use_lod, void* scratch, int* cut, int* count_device,
+                                             void* stream)
+{
+    if (N < 0) return fail(HLGS_ERR_ARG, "N < 0");
+    if (!count_device) return fail(HLGS_ERR_ARG, "missing count");
+    hipStream_t s = (hipStream_t)stream;
+    if (N == 0) {
+        HLGS_TRY_HIP(hipMemsetAsync(count_device, 0, 2 * sizeof(int), s));
+        return HLGS_OK;
+    }
+    int* dev = nullptr;
+    return upper_cut_launch(N, nodes, xyz, bounds, min_dist2, n_views, planes, campos, distance_multiplier,
+                            use_frustum, use_lod, scratch, cut, count_device, s, &dev, order);
 }
 
 int hlgs_upper_tree_cut_device(int N, const int* nodes, const float* xyz, const float* bounds, const float* min_dist2,

@@ -7,110 +7,205 @@
 // interior [5, H-5) x [5, W-5)), and the depth term of train_single.py:111-118
 // (mean |(invdepth - mono) * mask|).
 //
-// Design: one plane (channel) per grid.z, a 64 x 8 output tile per 512-thread block.  The tile plus a 5-pixel
-// halo of both images is staged in LDS; a horizontal 11-tap pass produces the five window sums
-// (x, y, x^2, y^2, x y) per row, a vertical pass finishes them per output pixel.  The forward writes the
-// partial derivatives of the SSIM map with respect to the window means
+// Design (round 5): one plane (channel) per grid.z, a 116 x 16 output tile per 256-thread workgroup, the two
+// separable passes in the order that keeps the first one in registers:
+//   vertical:   thread t owns input column t & 127 of the tile (its 116 output columns plus the 5-pixel halo on
+//               each side) and output rows [8 q, 8 q + 8), q = t >> 7: it loads the 18 input rows of that column
+//               (zero outside the image: zero padding), forms the five moments (x, y, x^2, y^2, x y) per row and
+//               writes the 11-tap column sums of its 8 rows to LDS (one row of 128 columns per (moment, row));
+//   horizontal: thread t owns output row j and the 8 output columns [8 s, 8 s + 8): 18 consecutive column sums
+//               per moment (four 16-byte LDS reads and one 8-byte read; row stride 132 floats puts the two rows of a
+//               16-lane group on opposite halves of the 64 banks) give the 8 window sums per moment.
+// Round 4 staged both images with the halo in LDS and ran the horizontal pass first over all 18 rows of an 8-row
+// tile (2.25 horizontal passes per output and 11 x 5 LDS reads per output in the vertical pass): 103 us forward and
+// 85 us backward at 3 x 1080 x 1920 (tools/variants/loss_r04.hip).
+// The forward writes the partial derivatives of the SSIM map with respect to the window means
 //   A = df/dmu1 (total), B = df/d E[x^2], C = df/d E[x y]
 // so that dSSIM/dx(p) = sum_q g(q) w(q - p) (A(q) + 2 x(p) B(q) + y(p) C(q)), which the backward evaluates with
-// the same separable stencil over the three maps.  Per-block sums go to a partial array that one block reduces
-// in double, in a fixed order: the losses are deterministic.
+// the same two passes over the three maps.  Per-workgroup sums go to a partial array that one block reduces in
+// double, in a fixed order: the losses are deterministic.
 #include <algorithm>
 
 #include "hlgs_internal.h"
 
 namespace hlgs {
 
-constexpr int kLW = 64, kLH = 8, kHalo = 5, kSW = kLW + 2 * kHalo, kSH = kLH + 2 * kHalo;
+constexpr int kHalo = 5;
+constexpr int kQW = 128;                // input columns per tile (one per vertical-pass thread of each half)
+constexpr int kQO = 116;                // output columns per tile (a multiple of 4: 16-byte map stores)
+constexpr int kQR = 8;                  // output rows per vertical-pass thread
+constexpr int kQH = 2 * kQR;            // output rows per tile
+constexpr int kQIn = kQR + 2 * kHalo;   // input rows per vertical-pass thread
+constexpr int kQS = 132;                // LDS row stride (floats)
+constexpr int kQThreads = 256;
 constexpr float kC1 = 0.01f * 0.01f, kC2 = 0.03f * 0.03f;
+static_assert(kQO + 2 * kHalo <= kQW && kQW * 2 == kQThreads && kQH * 16 == kQThreads, "tile shape");
 
 struct Win11 {
     float w[11];
 };
 
-// Load a (kSH x kSW) tile of one plane at (x0 - 5, y0 - 5) into LDS; zero outside the image (zero padding).
-__device__ __forceinline__ void load_halo(float (*dst)[kSW], const float* __restrict__ plane, int H, int W, int x0,
-                                          int y0)
+// Vertical pass: NI input planes -> NM moments per input row (mom) -> 11-tap column sums of the thread's kQR rows,
+// written to vs[(m kQH + row) kQS + column].
+template <int NI, int NM, class Mom>
+__device__ __forceinline__ void ssim_vertical(const float* const (&pl)[NI], int H, int W, int x0, int y0,
+                                              const Win11& win, float* vs, Mom mom)
 {
-    for (int i = threadIdx.x; i < kSH * kSW; i += 512) {
-        const int r = i / kSW, c = i - r * kSW;
-        const int gy = y0 + r - kHalo, gx = x0 + c - kHalo;
-        dst[r][c] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? plane[(size_t)gy * W + gx] : 0.f;
+    const int c = threadIdx.x & (kQW - 1), q = threadIdx.x / kQW;
+    const int gx = x0 - kHalo + c;
+    const bool colin = gx >= 0 && gx < W && c < kQO + 2 * kHalo;
+    const int gxc = min(max(gx, 0), W - 1);
+    const int gy0 = y0 - kHalo + kQR * q;
+    float in[NI][kQIn];
+#pragma unroll
+    for (int r = 0; r < kQIn; r++) {  // every load issued before the first use
+        const int gyc = min(max(gy0 + r, 0), H - 1);
+#pragma unroll
+        for (int i = 0; i < NI; i++) in[i][r] = pl[i][(size_t)gyc * W + gxc];
+    }
+#pragma unroll
+    for (int r = 0; r < kQIn; r++) {
+        const bool ok = colin && gy0 + r >= 0 && gy0 + r < H;
+#pragma unroll
+        for (int i = 0; i < NI; i++) in[i][r] = ok ? in[i][r] : 0.f;
+    }
+    float mv[NM][kQIn];
+#pragma unroll
+    for (int r = 0; r < kQIn; r++) mom(in, r, mv);
+#pragma unroll
+    for (int jj = 0; jj < kQR; jj++) {
+#pragma unroll
+        for (int m = 0; m < NM; m++) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < 11; k++) acc = fmaf(win.w[k], mv[m][jj + k], acc);
+            vs[(m * kQH + kQR * q + jj) * kQS + c] = acc;
+        }
+    }
+}
+
+// Horizontal pass: the 8 window sums per moment of output row j, tile columns [o0, o0 + 8).  Lanes 0-7 of each
+// 16-lane group take eight consecutive column groups of one row, lanes 8-15 the same groups of the next row.
+__device__ __forceinline__ void ssim_lane(int& j, int& o0)
+{
+    const int t = threadIdx.x;
+    j = 2 * (t >> 5) + ((t >> 3) & 1);
+    o0 = 8 * (8 * ((t >> 4) & 1) + (t & 7));
+}
+template <int NM>
+__device__ __forceinline__ void ssim_horizontal(const float* vs, const Win11& win, int j, int o0, float (&out)[NM][8])
+{
+#pragma unroll
+    for (int m = 0; m < NM; m++) {
+        const float* row = vs + (m * kQH + j) * kQS + o0;
+        float v[kQR + 2 * kHalo];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float4 f = *reinterpret_cast<const float4*>(row + 4 * u);
+            v[4 * u] = f.x; v[4 * u + 1] = f.y; v[4 * u + 2] = f.z; v[4 * u + 3] = f.w;
+        }
+        const float2 f = *reinterpret_cast<const float2*>(row + 16);
+        v[16] = f.x;
+        v[17] = f.y;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < 11; k++) acc = fmaf(win.w[k], v[i + k], acc);
+            out[m][i] = acc;
+        }
+    }
+}
+
+// 8 consecutive floats of one row (16-byte aligned when `vec`), zero beyond n
+__device__ __forceinline__ void load8(const float* p, bool vec, int n, float (&v)[8])
+{
+    if (vec) {
+        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = i < n ? p[i] : 0.f;
+    }
+}
+__device__ __forceinline__ void store8(float* p, bool vec, int n, const float (&v)[8])
+{
+    if (vec) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            if (i < n) p[i] = v[i];
     }
 }
 
 // SSIM forward.  partial[2 * block] = (sum of the SSIM map over counted pixels, sum |x - y|).
 template <bool TRAIN>
-__global__ void __launch_bounds__(512) k_ssim_fwd(int H, int W, const float* __restrict__ img1,
-                                                  const float* __restrict__ img2, int valid, Win11 win,
-                                                  float* __restrict__ abc, float* __restrict__ partial)
+__global__ void __launch_bounds__(kQThreads) k_ssim_fwd(int H, int W, const float* __restrict__ img1,
+                                                        const float* __restrict__ img2, int valid, Win11 win,
+                                                        float* __restrict__ abc, float* __restrict__ partial)
 {
-    __shared__ float sx[kSH][kSW], sy[kSH][kSW];
-    __shared__ float hs[5][kSH][kLW];
-    __shared__ float red[2][8];
+    __shared__ __attribute__((aligned(16))) float vs[5 * kQH * kQS + 8];
+    __shared__ float red[2][kQThreads / 64];
     const int ch = blockIdx.z;
     const size_t HW = (size_t)H * W;
     const float* x = img1 + ch * HW;
     const float* y = img2 + ch * HW;
-    const int x0 = blockIdx.x * kLW, y0 = blockIdx.y * kLH;
-    load_halo(sx, x, H, W, x0, y0);
-    load_halo(sy, y, H, W, x0, y0);
+    const int x0 = blockIdx.x * kQO, y0 = blockIdx.y * kQH;
+    const float* const pl[2] = {x, y};
+    ssim_vertical<2, 5>(pl, H, W, x0, y0, win, vs, [](const float (&in)[2][kQIn], int r, float (&mv)[5][kQIn]) {
+        const float u = in[0][r], v = in[1][r];
+        mv[0][r] = u;
+        mv[1][r] = v;
+        mv[2][r] = u * u;
+        mv[3][r] = v * v;
+        mv[4][r] = u * v;
+    });
     __syncthreads();
-    for (int i = threadIdx.x; i < kSH * kLW; i += 512) {
-        const int r = i / kLW, c = i - r * kLW;
-        float a = 0.f, b = 0.f, aa = 0.f, bb = 0.f, ab = 0.f;
-#pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float u = sx[r][c + k], v = sy[r][c + k], wk = win.w[k];
-            a = fmaf(wk, u, a);
-            b = fmaf(wk, v, b);
-            aa = fmaf(wk, u * u, aa);
-            bb = fmaf(wk, v * v, bb);
-            ab = fmaf(wk, u * v, ab);
-        }
-        hs[0][r][c] = a; hs[1][r][c] = b; hs[2][r][c] = aa; hs[3][r][c] = bb; hs[4][r][c] = ab;
+    int j, o0;
+    ssim_lane(j, o0);
+    float mo[5][8];
+    ssim_horizontal<5>(vs, win, j, o0, mo);
+    const int py = y0 + j, px0 = x0 + o0;
+    const int n = (py < H && o0 < kQO) ? max(0, min(8, W - px0)) : 0;
+    const bool vec = n == 8 && (W & 3) == 0;
+    const size_t pid = (size_t)py * W + px0;
+    float xv[8], yv[8];
+    if (n > 0) {
+        load8(x + pid, vec, n, xv);
+        load8(y + pid, vec, n, yv);
     }
-    __syncthreads();
-    const int tx = threadIdx.x & (kLW - 1), ty = threadIdx.x / kLW;
-    const int px = x0 + tx, py = y0 + ty;
-    float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 11; k++) {
-        const float wk = win.w[k];
-        m1 = fmaf(wk, hs[0][ty + k][tx], m1);
-        m2 = fmaf(wk, hs[1][ty + k][tx], m2);
-        e11 = fmaf(wk, hs[2][ty + k][tx], e11);
-        e22 = fmaf(wk, hs[3][ty + k][tx], e22);
-        e12 = fmaf(wk, hs[4][ty + k][tx], e12);
-    }
-    const bool inside = px < W && py < H;
-    const bool counted = inside && (!valid || (px >= kHalo && px < W - kHalo && py >= kHalo && py < H - kHalo));
     float s_map = 0.f, s_l1 = 0.f;
-    if (inside) {
+    float A[8], B[8], C[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const float m1 = mo[0][i], m2 = mo[1][i], e11 = mo[2][i], e22 = mo[3][i], e12 = mo[4][i];
+        const int px = px0 + i;
+        const bool counted = i < n && (!valid || (px >= kHalo && px < W - kHalo && py >= kHalo && py < H - kHalo));
         const float mu1_sq = m1 * m1, mu2_sq = m2 * m2, mu12 = m1 * m2;
         const float s11 = e11 - mu1_sq, s22 = e22 - mu2_sq, s12 = e12 - mu12;
         const float a = 2.f * mu12 + kC1, b = 2.f * s12 + kC2;
         const float c = mu1_sq + mu2_sq + kC1, d = s11 + s22 + kC2;
         const float f = (a * b) / (c * d);
-        if (counted) s_map = f;
-        s_l1 = fabsf(sx[ty + kHalo][tx + kHalo] - sy[ty + kHalo][tx + kHalo]);
-        if (TRAIN) {
-            float A = 0.f, B = 0.f, C = 0.f;
-            if (counted) {
-                const float cd = c * d;
-                const float dmu1 = (2.f * m2 * b) / cd - f * (2.f * m1) / c;  // df/dmu1 at fixed sigmas
-                B = -f / d;                                                  // df/dsigma1^2
-                C = (2.f * a) / cd;                                          // df/dsigma12
-                A = dmu1 - 2.f * m1 * B - m2 * C;                            // through sigma = E[.] - mu mu
-            }
-            const size_t pid = (size_t)py * W + px;
-            float* o = abc + (size_t)ch * 3 * HW;
-            o[pid] = A;
-            o[HW + pid] = B;
-            o[2 * HW + pid] = C;
+        if (counted) s_map += f;
+        if (i < n) s_l1 += fabsf(xv[i] - yv[i]);
+        A[i] = B[i] = C[i] = 0.f;
+        if (TRAIN && counted) {
+            const float cd = c * d;
+            const float dmu1 = (2.f * m2 * b) / cd - f * (2.f * m1) / c;  // df/dmu1 at fixed sigmas
+            B[i] = -f / d;                                                // df/dsigma1^2
+            C[i] = (2.f * a) / cd;                                        // df/dsigma12
+            A[i] = dmu1 - 2.f * m1 * B[i] - m2 * C[i];                    // through sigma = E[.] - mu mu
         }
     }
-    // block sums (fixed order: DPP-free shuffles then one lane per wave)
+    if (TRAIN && n > 0) {
+        float* o = abc + (size_t)ch * 3 * HW + pid;
+        store8(o, vec, n, A);
+        store8(o + HW, vec, n, B);
+        store8(o + 2 * HW, vec, n, C);
+    }
+    // workgroup sums (fixed order: shuffles, then one lane per wave)
     for (int off = 32; off > 0; off >>= 1) {
         s_map += __shfl_xor(s_map, off, 64);
         s_l1 += __shfl_xor(s_l1, off, 64);
@@ -120,7 +215,7 @@ __global__ void __launch_bounds__(512) k_ssim_fwd(int H, int W, const float* __r
     __syncthreads();
     if (threadIdx.x == 0) {
         float a = 0.f, b = 0.f;
-        for (int i = 0; i < 8; i++) { a += red[0][i]; b += red[1][i]; }
+        for (int i = 0; i < kQThreads / 64; i++) { a += red[0][i]; b += red[1][i]; }
         const size_t blk = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
         partial[2 * blk] = a;
         partial[2 * blk + 1] = b;
@@ -128,51 +223,44 @@ __global__ void __launch_bounds__(512) k_ssim_fwd(int H, int W, const float* __r
 }
 
 // grad1 = coef[0] * dSSIM-map-sum/dx + coef[1] * sign(x - y)  (coefficients on the device: no host sync).
-__global__ void __launch_bounds__(512) k_ssim_bwd(int H, int W, const float* __restrict__ img1,
-                                                  const float* __restrict__ img2, const float* __restrict__ abc,
-                                                  Win11 win, const float* __restrict__ coef,
-                                                  float* __restrict__ grad1)
+__global__ void __launch_bounds__(kQThreads) k_ssim_bwd(int H, int W, const float* __restrict__ img1,
+                                                        const float* __restrict__ img2, const float* __restrict__ abc,
+                                                        Win11 win, const float* __restrict__ coef,
+                                                        float* __restrict__ grad1)
 {
-    __shared__ float sm[3][kSH][kSW];
-    __shared__ float hs[3][kSH][kLW];
+    __shared__ __attribute__((aligned(16))) float vs[3 * kQH * kQS + 8];
     const int ch = blockIdx.z;
     const size_t HW = (size_t)H * W;
-    const int x0 = blockIdx.x * kLW, y0 = blockIdx.y * kLH;
+    const int x0 = blockIdx.x * kQO, y0 = blockIdx.y * kQH;
     const float* maps = abc + (size_t)ch * 3 * HW;
-    load_halo(sm[0], maps, H, W, x0, y0);
-    load_halo(sm[1], maps + HW, H, W, x0, y0);
-    load_halo(sm[2], maps + 2 * HW, H, W, x0, y0);
+    const float* const pl[3] = {maps, maps + HW, maps + 2 * HW};
+    ssim_vertical<3, 3>(pl, H, W, x0, y0, win, vs, [](const float (&in)[3][kQIn], int r, float (&mv)[3][kQIn]) {
+        mv[0][r] = in[0][r];
+        mv[1][r] = in[1][r];
+        mv[2][r] = in[2][r];
+    });
     __syncthreads();
-    for (int i = threadIdx.x; i < kSH * kLW; i += 512) {
-        const int r = i / kLW, c = i - r * kLW;
-        float a = 0.f, b = 0.f, cc = 0.f;
+    int j, o0;
+    ssim_lane(j, o0);
+    float g[3][8];
+    ssim_horizontal<3>(vs, win, j, o0, g);
+    const int py = y0 + j, px0 = x0 + o0;
+    const int n = (py < H && o0 < kQO) ? max(0, min(8, W - px0)) : 0;
+    if (n == 0) return;
+    const bool vec = n == 8 && (W & 3) == 0;
+    const size_t pid = (size_t)ch * HW + (size_t)py * W + px0;
+    float xv[8], yv[8], out[8];
+    load8(img1 + pid, vec, n, xv);
+    load8(img2 + pid, vec, n, yv);
+    const float c0 = coef[0], c1 = coef[1];
 #pragma unroll
-        for (int k = 0; k < 11; k++) {
-            const float wk = win.w[k];
-            a = fmaf(wk, sm[0][r][c + k], a);
-            b = fmaf(wk, sm[1][r][c + k], b);
-            cc = fmaf(wk, sm[2][r][c + k], cc);
-        }
-        hs[0][r][c] = a; hs[1][r][c] = b; hs[2][r][c] = cc;
+    for (int i = 0; i < 8; i++) {
+        const float dssim = g[0][i] + 2.f * xv[i] * g[1][i] + yv[i] * g[2][i];
+        const float diff = xv[i] - yv[i];
+        const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);  // torch.abs backward: sign, 0 at 0
+        out[i] = c0 * dssim + c1 * sgn;
     }
-    __syncthreads();
-    const int tx = threadIdx.x & (kLW - 1), ty = threadIdx.x / kLW;
-    const int px = x0 + tx, py = y0 + ty;
-    if (px >= W || py >= H) return;
-    float ga = 0.f, gb = 0.f, gc = 0.f;
-#pragma unroll
-    for (int k = 0; k < 11; k++) {
-        const float wk = win.w[k];
-        ga = fmaf(wk, hs[0][ty + k][tx], ga);
-        gb = fmaf(wk, hs[1][ty + k][tx], gb);
-        gc = fmaf(wk, hs[2][ty + k][tx], gc);
-    }
-    const size_t pid = (size_t)ch * HW + (size_t)py * W + px;
-    const float xv = img1[pid], yv = img2[pid];
-    const float dssim = ga + 2.f * xv * gb + yv * gc;
-    const float diff = xv - yv;
-    const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);  // torch.abs backward: sign, 0 at 0
-    grad1[pid] = coef[0] * dssim + coef[1] * sgn;
+    store8(grad1 + pid, vec, n, out);
 }
 
 // mean |(inv - mono) * mask| partial sums; mask may be NULL (= 1).
@@ -241,7 +329,7 @@ static Win11 gauss_window()
     return w;
 }
 
-static dim3 ssim_grid(int C, int H, int W) { return dim3((W + kLW - 1) / kLW, (H + kLH - 1) / kLH, C); }
+static dim3 ssim_grid(int C, int H, int W) { return dim3((W + kQO - 1) / kQO, (H + kQH - 1) / kQH, C); }
 
 size_t ssim_partials(int C, int H, int W)
 {
@@ -255,9 +343,9 @@ void launch_ssim_forward(int C, int H, int W, const float* img1, const float* im
     const dim3 g = ssim_grid(C, H, W);
     const Win11 w = gauss_window();
     if (abc)
-        hipLaunchKernelGGL(k_ssim_fwd<true>, g, dim3(512), 0, s, H, W, img1, img2, valid, w, abc, partial);
+        hipLaunchKernelGGL(k_ssim_fwd<true>, g, dim3(kQThreads), 0, s, H, W, img1, img2, valid, w, abc, partial);
     else
-        hipLaunchKernelGGL(k_ssim_fwd<false>, g, dim3(512), 0, s, H, W, img1, img2, valid, w, abc, partial);
+        hipLaunchKernelGGL(k_ssim_fwd<false>, g, dim3(kQThreads), 0, s, H, W, img1, img2, valid, w, abc, partial);
     const double n_map = valid ? (double)C * (H - 2 * kHalo) * (W - 2 * kHalo) : (double)C * H * W;
     const double n_all = (double)C * H * W;
     hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(1024), 0, s, (int)(g.x * g.y * g.z), 2, partial, 1.0 / n_map,
@@ -267,7 +355,7 @@ void launch_ssim_forward(int C, int H, int W, const float* img1, const float* im
 void launch_ssim_backward(int C, int H, int W, const float* img1, const float* img2, const float* abc,
                           const float* coef, float* grad1, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_ssim_bwd, ssim_grid(C, H, W), dim3(512), 0, s, H, W, img1, img2, abc, gauss_window(), coef,
+    hipLaunchKernelGGL(k_ssim_bwd, ssim_grid(C, H, W), dim3(kQThreads), 0, s, H, W, img1, img2, abc, gauss_window(), coef,
                        grad1);
 }
 

@@ -284,4 +284,89 @@ int hlgs_spt_result_copy(const hlgs_spt_result* r, int* starts, float* smax, flo
 
 void hlgs_spt_result_free(hlgs_spt_result* r) { delete r; }
 
+// Walk order of the upper tree for the flat coarse cut (hlgs_upper_tree_cut_views_ordered_device).  The reference's
+// walk (cut_hierarchy_on_condition, gaussian_model.py:364-404) keeps a frontier per level: the expanding nodes'
+// first children in order, then those children's next siblings in order.  Whatever the view, a level's frontier is a
+// subsequence of the frontier of the walk in which every node with children expands (F*, by induction: both halves
+// of the next frontier keep the order of their parents).  So the cut is, level by level, the leaves of F*'s level
+// that are alive (no ancestor culled or stopped), then its alive condition-false nodes, each in F* order.  Aliveness
+// is a subtree test: with the walk's binary tree numbered in preorder, a node is dead iff it lies strictly inside
+// the preorder interval of a non-expanding node.
+// Blob (int32): [0] M = entries of F*, [1] levels, [2] usable, [3] 0, [4 .. 4 + levels] the levels' first entries
+// (the last = M), then from HLGS_CUT_ORDER_HEADER: node[M], preorder position[M], preorder end[M] (position + subtree
+// size), all in F* order.
+size_t hlgs_upper_tree_order_size(int N)  // (64 words of room past the last array: whole 64-entry runs are read)
+{
+    return sizeof(int) * (HLGS_CUT_ORDER_HEADER + 3 * (size_t)(N > 0 ? N : 0) + 68);
+}
+
+int hlgs_upper_tree_order(int N, const int* nodes, void* order)
+{
+    if (N < 0 || !order || (N > 0 && !nodes)) return hlgs::fail_msg(HLGS_ERR_ARG, "bad upper-tree order arguments");
+    int* o = static_cast<int*>(order);
+    memset(o, 0, sizeof(int) * HLGS_CUT_ORDER_HEADER);
+    if (N == 0) return HLGS_OK;
+    auto nd = [&](int v) { return nodes + 6 * (size_t)v; };
+    // F*: the breadth-first frontiers with every node that has children expanding
+    std::vector<int> fs{0}, lev{0};
+    std::vector<char> seen(N, 0);
+    seen[0] = 1;
+    std::vector<int> first, second;
+    for (size_t b = 0; b < fs.size();) {
+        const size_t e = fs.size();
+        first.clear();
+        second.clear();
+        for (size_t i = b; i < e; i++) {
+            const int v = fs[i];
+            if (nd(v)[kChildCount] == 0) continue;
+            const int fc = nd(v)[kFirstChild];
+            if (fc < 0 || fc >= N) return HLGS_OK;  // not walkable as the reference walks it: usable stays 0
+            const int ns = nd(fc)[kNextSibling];
+            if (ns >= N) return HLGS_OK;
+            first.push_back(fc);
+            if (ns >= 0) second.push_back(ns);
+        }
+        for (const std::vector<int>* part : {&first, &second})
+            for (int c : *part) {
+                if (seen[c]) return HLGS_OK;  // reached twice: not a tree
+                seen[c] = 1;
+                fs.push_back(c);
+            }
+        b = e;
+        if (fs.size() > e) lev.push_back((int)e);  // the next level starts where this one ended
+    }
+    const int M = (int)fs.size(), levels = (int)lev.size();
+    lev.push_back(M);
+    if (M > HLGS_CUT_FLAT_MAX_ENTRIES || levels > HLGS_CUT_FLAT_MAX_LEVELS) return HLGS_OK;
+    // preorder positions and subtree sizes of the walk's binary tree (children: first child, then its next sibling)
+    std::vector<int> pos(N, -1), size(N, 1);
+    for (int i = M - 1; i >= 0; i--) {  // children come after their parent in F*
+        const int v = fs[i];
+        if (nd(v)[kChildCount] == 0) continue;
+        const int fc = nd(v)[kFirstChild], ns = nd(fc)[kNextSibling];
+        size[v] += size[fc] + (ns >= 0 ? size[ns] : 0);
+    }
+    pos[0] = 0;
+    for (int i = 0; i < M; i++) {
+        const int v = fs[i];
+        if (nd(v)[kChildCount] == 0) continue;
+        const int fc = nd(v)[kFirstChild], ns = nd(fc)[kNextSibling];
+        pos[fc] = pos[v] + 1;
+        if (ns >= 0) pos[ns] = pos[v] + 1 + size[fc];
+    }
+    o[0] = M;
+    o[1] = levels;
+    o[2] = 1;
+    for (int l = 0; l <= levels; l++) o[4 + l] = lev[l];
+    int* fn = o + HLGS_CUT_ORDER_HEADER;
+    uint16_t* pre16 = reinterpret_cast<uint16_t*>(fn + ((2 * M + 3) & ~3));  // 16-byte aligned
+    for (int i = 0; i < M; i++) {
+        const int v = fs[i];
+        fn[i] = v;
+        fn[M + i] = pos[v] | (pos[v] + size[v]) << 16;  // both < 2^16 (M < 2^16)
+        pre16[i] = (uint16_t)pos[v];
+    }
+    return HLGS_OK;
+}
+
 }  // extern "C"

@@ -335,6 +335,175 @@ void launch_upper_cut(const CutArgs& a, hipStream_t s)
     for (int l = 0; l < kCutLevelLaunches; l++) hipLaunchKernelGGL(k_cut_level, dim3(blocks), dim3(1024), 0, s, a, l);
     hipLaunchKernelGGL(k_upper_cut, dim3(1), dim3(1024), 0, s, a, 1);
 }
+// ---------------------------------------------------------------- flat coarse cut (round 5)
+// The same cut from the walk order hlgs_upper_tree_order precomputes (see there for why the order is static): the
+// level walk above costs a dependent chain per level (~3 us a narrow level, ~13 us a wide one, 180 us for the 21
+// levels of config #5's upper tree); here every node's state is one parallel pass and a single workgroup places the
+// survivors.
+//   k_cut_flat_eval:  per F* entry i: its state (cut_node) and, in preorder, the end of its subtree interval if it
+//                     does not expand (culled, leaf, condition false), else 0.
+//   k_cut_flat_place: covered(p) = (max of those ends over preorder positions < p) > p -- a max scan over preorder
+//                     into an LDS bit mask; then per F* entry alive = !covered(its position); the leaves and
+//                     condition-false nodes that are alive are counted per thread run and scanned, and placed:
+//                     a leaf at (stops before its level) + (leaves before it), a condition-false node at
+//                     (leaves up to the end of its level) + (stops before it).
+constexpr int kFlatRun = 64;  // entries per thread of k_cut_flat_place (1024 x 64 > HLGS_CUT_FLAT_MAX_ENTRIES)
+static_assert(1024 * kFlatRun > HLGS_CUT_FLAT_MAX_ENTRIES, "one 64-bit mask per thread run");
+
+__global__ void __launch_bounds__(256) k_cut_flat_eval(CutArgs a, const int* __restrict__ order,
+                                                       uint8_t* __restrict__ st8, uint16_t* __restrict__ endv)
+{
+    const int M = order[0];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (!order[2] || i >= M) return;  // an unusable blob: k_cut_flat_place reports it
+    const int* fn = order + HLGS_CUT_ORDER_HEADER;
+    const int v = fn[i], pe = fn[M + i];
+    const int st = cut_node<false>(a, v).st;
+    st8[i] = (uint8_t)st;
+    endv[pe & 0xffff] = (uint16_t)(st == 3 ? 0 : (unsigned)pe >> 16);
+}
+
+// exclusive max over the 1024-thread block (values >= 0)
+__device__ __forceinline__ int block_excl_max(int v, int* s_w)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int inc = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int x = __shfl_up(inc, d, 64);
+        if (lane >= d) inc = max(inc, x);
+    }
+    int ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = 0;
+    __syncthreads();
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    for (int k = 0; k < w; k++) ex = max(ex, s_w[k]);
+    return ex;
+}
+
+// A thread's run of 64 16-bit (or 8-bit) entries from p0 as 32-bit words, in 16-byte loads.  Entries at or beyond M
+// are read (the scratch regions and the order blob leave room for a whole run past M) but never used.
+template <int BYTES, int W>
+__device__ __forceinline__ void load_run(const void* base, int p0, uint32_t (&wd)[W])
+{
+    const uint4* q = reinterpret_cast<const uint4*>(static_cast<const char*>(base) + (size_t)p0 * BYTES);
+#pragma unroll
+    for (int u = 0; u < W / 4; u++) {
+        const uint4 x = q[u];
+        wd[4 * u] = x.x; wd[4 * u + 1] = x.y; wd[4 * u + 2] = x.z; wd[4 * u + 3] = x.w;
+    }
+}
+template <int BYTES>
+__device__ __forceinline__ uint32_t run_at(const uint32_t (&wd)[kFlatRun * BYTES / 4], int k)
+{
+    constexpr int kPer = 4 / BYTES;
+    return (wd[k / kPer] >> (8 * BYTES * (k % kPer))) & (BYTES == 2 ? 0xffffu : 0xffu);
+}
+static_assert(HLGS_CUT_ORDER_HEADER % 4 == 0, "16-byte aligned runs in the order blob");
+
+__global__ void __launch_bounds__(1024) k_cut_flat_place(CutArgs a, const int* __restrict__ order,
+                                                         const uint8_t* __restrict__ st8,
+                                                         const uint16_t* __restrict__ endv)
+{
+    __shared__ uint32_t s_bits[1024 * kFlatRun / 32];
+    __shared__ int s_w[16 * 3];
+    __shared__ int s_ls[HLGS_CUT_FLAT_MAX_LEVELS + 1];
+    __shared__ int2 s_lev[HLGS_CUT_FLAT_MAX_LEVELS + 1];
+    const int M = order[0], nlev = order[1];
+    const int t = threadIdx.x;
+    if (!order[2] || M <= 0 || M > HLGS_CUT_FLAT_MAX_ENTRIES || nlev < 1 || nlev > HLGS_CUT_FLAT_MAX_LEVELS) {
+        if (t == 0) { a.count[0] = 0; a.count[1] = 1; }  // (uniform) not a blob the flat cut can use
+        return;
+    }
+    if (t <= nlev) s_ls[t] = order[4 + t];
+    // thread t owns entries [t R, t R + R) of both orders (preorder here, F* below); R = 32 or 64
+    const int R = ((M + 1023) / 1024 + 31) & ~31;
+    const int p0 = t * R;
+    {  // covered bits over preorder positions
+        uint32_t e[kFlatRun / 2];
+        load_run<2>(endv, min(p0, M & ~31), e);
+        const int n = max(0, min(R, M - p0));
+        int mx = 0;
+#pragma unroll
+        for (int k = 0; k < kFlatRun; k++)
+            if (k < n) mx = max(mx, (int)run_at<2>(e, k));
+        int run = block_excl_max(mx, s_w);
+        uint32_t wd[2] = {0u, 0u};
+#pragma unroll
+        for (int k = 0; k < kFlatRun; k++) {
+            if (k < n) {
+                if (run > p0 + k) wd[k >> 5] |= 1u << (k & 31);
+                run = max(run, (int)run_at<2>(e, k));
+            }
+        }
+        if (p0 < M) {
+            s_bits[p0 >> 5] = wd[0];
+            if (R == 64) s_bits[(p0 >> 5) + 1] = wd[1];
+        }
+    }
+    __syncthreads();
+    // alive leaves and condition-false nodes of the thread's run of F* entries
+    const int* fn = order + HLGS_CUT_ORDER_HEADER;
+    const int n = max(0, min(R, M - p0));
+    uint64_t leaf = 0, stop = 0;
+    {
+        uint32_t pr[kFlatRun / 2], sw[kFlatRun / 4];
+        load_run<2>(fn + ((2 * M + 3) & ~3), min(p0, M & ~31), pr);
+        load_run<1>(st8, min(p0, M & ~31), sw);
+#pragma unroll
+        for (int k = 0; k < kFlatRun; k++) {
+            const int st = run_at<1>(sw, k), pre = run_at<2>(pr, k);
+            const bool alive = k < n && !((s_bits[pre >> 5] >> (pre & 31)) & 1u);
+            if (alive && st == 1) leaf |= 1ull << k;
+            if (alive && st == 2) stop |= 1ull << k;
+        }
+    }
+    int3 tot;
+    const int3 o = block_excl3(make_int3(__popcll(leaf), __popcll(stop), 0), s_w, &tot);
+    // (leaves, stops) before each level's first entry
+    for (int l = 0; l < nlev; l++) {
+        const int sl = s_ls[l];
+        if (sl >= p0 && sl < p0 + n) {
+            const uint64_t below = (1ull << (sl - p0)) - 1ull;
+            s_lev[l] = make_int2(o.x + __popcll(leaf & below), o.y + __popcll(stop & below));
+        }
+    }
+    if (t == 0) s_lev[nlev] = make_int2(tot.x, tot.y);
+    __syncthreads();
+    if (tot.x + tot.y > a.capacity) {
+        if (t == 0) { a.count[0] = 0; a.count[1] = 1; }
+        return;
+    }
+    if (n > 0) {
+        int l = 0;
+        while (l + 1 < nlev && s_ls[l + 1] <= p0) l++;
+        int nl = 0, ns = 0;
+        for (int h = 0; h < kFlatRun; h += 32) {  // two halves: 32 node ids in registers at a time
+            if (h >= n) break;
+            uint32_t nd[32];
+            load_run<4>(fn + h, p0, nd);
+#pragma unroll
+            for (int k = 0; k < 32; k++) {
+                if (h + k < n) {
+                    if (l + 1 < nlev && s_ls[l + 1] <= p0 + h + k) l++;  // levels hold at least one entry each
+                    if ((leaf >> (h + k)) & 1ull) a.cut[s_lev[l].y + o.x + nl++] = (int)nd[k];
+                    if ((stop >> (h + k)) & 1ull) a.cut[s_lev[l + 1].x + o.y + ns++] = (int)nd[k];
+                }
+            }
+        }
+    }
+    if (t == 0) { a.count[0] = tot.x + tot.y; a.count[1] = 0; }
+}
+
+void launch_upper_cut_flat(const CutArgs& a, const int* order, hipStream_t s)
+{
+    // the frontier buffers of the level walk hold the per-entry words and the preorder ends
+    uint8_t* st8 = reinterpret_cast<uint8_t*>(a.front_a);
+    uint16_t* endv = reinterpret_cast<uint16_t*>(a.front_b);
+    hipLaunchKernelGGL(k_cut_flat_eval, dim3((a.N + 255) / 256), dim3(256), 0, s, a, order, st8, endv);
+    hipLaunchKernelGGL(k_cut_flat_place, dim3(1), dim3(1024), 0, s, a, order, st8, endv);
+}
+
 size_t upper_cut_state_bytes() { return sizeof(CutState) + sizeof(unsigned) * kCutLevelLaunches + sizeof(int) * 3 * kCutMaxBlocks; }
 
 // ---------------------------------------------------------------- row gather / scatter
@@ -513,7 +682,8 @@ void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, 
     }
     constexpr int64_t kWriteBackBlocks = 128;
     // 4 waves (rows) per block, grid-stride above.  The write-back is bound by the host link, not by waves: a
-    // small grid moves it as fast and leaves the CUs to the compaction and load running beside it (SPTCache)
+    // small grid moves it as fast and leaves the CUs to the compaction and load running beside it (SPTCache).
+    // The load keeps the large grid: with 256 workgroups (fewer host reads in flight) it took 513 against 392 us
     const int64_t blocks = std::min<int64_t>((n + 3) / 4, to_host ? kWriteBackBlocks : 2048);
     if (blocks <= 0) return;
     if (to_host) hipLaunchKernelGGL(k_rows_packed<true>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw, (const int*)nullptr);
@@ -535,21 +705,54 @@ __global__ void __launch_bounds__(256) k_rows_compact(RowTabs tabs, int64_t n, c
     const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4, S = (int64_t)gridDim.x * 256 * 4;
     int64_t r = w0 / words, k = w0 - r * words;
     const int64_t dr = S / words, dk = S - dr * words;
-    for (int64_t w = w0; w < total; w += S) {
-        const int64_t r_end = r + (k + 3) / words;
-        const int64_t s0 = src_rows[r];
-        if (w + 4 <= total && src_rows[r_end] - s0 == r_end - r) {
-            *reinterpret_cast<uint4*>(dst + w) = *reinterpret_cast<const uint4_a4*>(src + s0 * words + k);
-        } else {
-            int64_t rr = r, kk = k;
-            for (int u = 0; u < 4 && w + u < total; u++) {
-                dst[w + u] = src[(int64_t)src_rows[rr] * words + kk];
-                if (++kk == words) { kk = 0; rr++; }
+    // kU chunks per round: their row indices are loaded together, then their sources, then the stores -- two load
+    // rounds per kU chunks instead of two per chunk
+    constexpr int kU = 4;
+    for (int64_t w = w0; w < total; w += kU * S) {
+        int64_t rr[kU], kk[kU], re[kU];
+        int s0[kU], s1[kU];
+        {
+            int64_t r1 = r, k1 = k;
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                rr[u] = r1;
+                kk[u] = k1;
+                re[u] = r1 + (k1 + 3) / words;
+                r1 += dr;
+                k1 += dk;
+                while (k1 >= words) { k1 -= words; r1++; }
+            }
+            r = r1;
+            k = k1;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const bool in = w + u * S < total;
+            s0[u] = in ? src_rows[rr[u]] : 0;
+            s1[u] = in ? src_rows[min(re[u], n - 1)] : 0;
+        }
+        uint4 v[kU];
+        bool fast[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int64_t wu = w + u * S;
+            fast[u] = wu + 4 <= total && s1[u] - s0[u] == re[u] - rr[u];
+            if (fast[u]) v[u] = *reinterpret_cast<const uint4_a4*>(src + (int64_t)s0[u] * words + kk[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int64_t wu = w + u * S;
+            if (wu >= total) continue;
+            if (fast[u]) {
+                *reinterpret_cast<uint4*>(dst + wu) = v[u];
+            } else {
+                int64_t r2 = rr[u], k2 = kk[u];
+                for (int q = 0; q < 4 && wu + q < total; q++) {
+                    dst[wu + q] = src[(int64_t)src_rows[r2] * words + k2];
+                    if (++k2 == words) { k2 = 0; r2++; }
+                }
             }
         }
-        r += dr;
-        k += dk;
-        while (k >= words) { k -= words; r++; }
     }
 }
 

@@ -95,6 +95,10 @@ _SIGS = {
     "hlgs_upper_tree_cut_device": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "hlgs_upper_tree_cut_views_device": (_i, [_i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _i, _i, _vp, _vp, _vp,
                                               _vp]),
+    "hlgs_upper_tree_cut_views_ordered_device": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _f, _i, _i, _vp, _vp,
+                                                      _vp, _vp]),
+    "hlgs_upper_tree_order_size": (_sz, [_i]),
+    "hlgs_upper_tree_order": (_i, [_i, _vp, _vp]),
     "hlgs_gather_rows": (_i, [C.c_int64, _i, _vp, _vp, _vp, _vp]),
     "hlgs_spt_cache_scratch_size": (_sz, [_i, _i, _i, _i]),
     "hlgs_spt_cache_plan": (_i, [C.POINTER(CacheArgs), C.POINTER(CachePlan), _vp, _vp]),

@@ -31,9 +31,24 @@ def extract_frustum_planes(view_proj_matrix):
     return planes
 
 
+def upper_tree_order(nodes, device=None):
+    """The walk order of an upper tree for the flat coarse cut (hlgs_upper_tree_order, host code): a device int32
+    blob, or None when the tree exceeds the flat cut's limits (65,535 nodes on the walk, 64 levels) or is not a tree
+    as the reference walks it -- then the cut walks level by level."""
+    lib = L.load()
+    nd = nodes.detach().to("cpu", torch.int32).contiguous()
+    N = int(nd.shape[0])
+    blob = torch.zeros(((lib.hlgs_upper_tree_order_size(N) + 3) // 4,), dtype=torch.int32)
+    L.check(lib.hlgs_upper_tree_order(N, L.ptr(nd) if N else None, L.ptr(blob)))
+    if not int(blob[2]):
+        return None
+    return blob.to(device if device is not None else nodes.device)
+
+
 def upper_tree_cut(nodes, xyz, bounds, min_distance_squared, planes, camera_position, distance_multiplier=1.0,
-                   use_frustum=True, use_lod=True):
-    """Coarse cut of the upper tree from root 0 (int32 device tensor, the reference's order)."""
+                   use_frustum=True, use_lod=True, order=None):
+    """Coarse cut of the upper tree from root 0 (int32 device tensor, the reference's order).  order: the blob of
+    upper_tree_order(nodes) for the flat cut (two launches), or None for the level walk; same result."""
     lib = L.load()
     nd = nodes.contiguous().to(torch.int32)
     p = xyz.contiguous().float()
@@ -46,6 +61,16 @@ def upper_tree_cut(nodes, xyz, bounds, min_distance_squared, planes, camera_posi
     N = nd.size(0)
     cut = torch.empty((max(N, 1),), dtype=torch.int32, device=dev)
     scratch = torch.empty(lib.hlgs_upper_cut_scratch_size(N), dtype=torch.uint8, device=dev)
+    if order is not None:
+        cnt = torch.zeros((2,), dtype=torch.int32, device=dev)
+        L.check(lib.hlgs_upper_tree_cut_views_ordered_device(
+            N, L.ptr(nd), L.ptr(order), L.ptr(p), L.ptr(b), L.ptr(md), 1, L.ptr(pl), L.ptr(cam),
+            float(distance_multiplier), int(bool(use_frustum)), int(bool(use_lod)), L.ptr(scratch), L.ptr(cut),
+            L.ptr(cnt), L.stream()))
+        n, overflow = (int(v) for v in cnt.cpu())
+        if overflow:
+            raise RuntimeError("hlgs: upper-tree cut: the order blob does not fit these nodes")
+        return cut[:n]
     count = C.c_int(0)
     L.check(lib.hlgs_upper_tree_cut(N, L.ptr(nd), L.ptr(p), L.ptr(b), L.ptr(md), L.ptr(pl), L.ptr(cam),
                                     float(distance_multiplier), int(bool(use_frustum)), int(bool(use_lod)),

@@ -157,7 +157,7 @@ class SPTCache:
 
     def __init__(self, storage, spt, skybox_points, opt_storage=None, reuse_tolerance=0.9,
                  max_gaussian_budget=100_000_000, distance_multiplier_until_budget=1.5, use_frustum_culling=True,
-                 use_bounding_spheres=True, device="cuda", occlusion_culling=False):
+                 use_bounding_spheres=True, device="cuda", occlusion_culling=False, flat_cut=True):
         # packed pinned host storage: one row per Gaussian holding its six parameter rows, then the six exp_avgs and
         # the six exp_avg_sqs rows, padded to whole 64-byte lines; self.storage / self.opt_storage are views of it
         G = int(storage[NAMES[0]].shape[0])
@@ -178,6 +178,8 @@ class SPTCache:
         self.device = torch.device(device)
         dev = self.device
         self.nodes = spt["upper_tree_nodes"].to(dev, torch.int32).contiguous()
+        # the upper tree's walk order for the flat coarse cut (hlgs_upper_tree_order), or None for the level walk
+        self.cut_order = _spt.upper_tree_order(spt["upper_tree_nodes"], dev) if flat_cut else None
         self.xyz = spt["upper_tree_xyz"].to(dev, torch.float32).contiguous()
         self.min_distance_squared = spt["min_distance_squared"].to(dev, torch.float32).contiguous()
         if use_bounding_spheres:
@@ -279,11 +281,10 @@ class SPTCache:
             self._cut = torch.empty((max(N, 1),), dtype=torch.int32, device=dev)
             self._cut_scratch = torch.empty(lib.hlgs_upper_cut_scratch_size(N), dtype=torch.uint8, device=dev)
             self._cut_count = torch.zeros((2,), dtype=torch.int32, device=dev)
-        L.check(lib.hlgs_upper_tree_cut_views_device(N, _p(self.nodes), _p(self.xyz), _p(self.bounds),
-                                                     _p(self.min_distance_squared), G, _p(planes), _p(cam),
-                                                     float(distance_multiplier), int(bool(self.use_frustum)), 1,
-                                                     _p(self._cut_scratch), _p(self._cut), _p(self._cut_count),
-                                                     L.stream()))
+        L.check(lib.hlgs_upper_tree_cut_views_ordered_device(
+            N, _p(self.nodes), _p(self.cut_order), _p(self.xyz), _p(self.bounds), _p(self.min_distance_squared), G,
+            _p(planes), _p(cam), float(distance_multiplier), int(bool(self.use_frustum)), 1, _p(self._cut_scratch),
+            _p(self._cut), _p(self._cut_count), L.stream()))
         if self.occlusion:
             if views is None:
                 raise ValueError("occlusion culling renders the cut: pass the view(s) (W, H, tanfovx, tanfovy, "

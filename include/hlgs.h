@@ -271,6 +271,24 @@ int hlgs_upper_tree_cut_views_device(int N, const int* nodes, const float* xyz, 
                                      const float* min_dist2, int n_views, const float* planes, const float* campos,
                                      float distance_multiplier, int use_frustum, int use_lod, void* scratch, int* cut,
                                      int* count_device, void* stream);
+/* The same cut from a precomputed walk order (round 5): two launches (every node's state in parallel, then one
+ * workgroup that places the surviving nodes) instead of one per level, with the result of
+ * hlgs_upper_tree_cut_views_device bit for bit.  order (device): the blob hlgs_upper_tree_order wrote for these
+ * nodes, or NULL for the level walk.  Same scratch. */
+int hlgs_upper_tree_cut_views_ordered_device(int N, const int* nodes, const void* order, const float* xyz,
+                                             const float* bounds, const float* min_dist2, int n_views,
+                                             const float* planes, const float* campos, float distance_multiplier,
+                                             int use_frustum, int use_lod, void* scratch, int* cut, int* count_device,
+                                             void* stream);
+/* Host: the walk order of an upper tree (nodes: N x 6 HierarchyNode rows, host memory) into order_host
+ * (hlgs_upper_tree_order_size(N) bytes).  Word 2 of the blob is 1 when the flat cut can use it: the nodes form a
+ * tree as the reference walks it (root 0; first child, then that child's next sibling) with at most 65,535 nodes
+ * on it over at most 64 levels; otherwise use the level walk (order = NULL above). */
+#define HLGS_CUT_ORDER_HEADER 80       /* words before the per-entry arrays of the order blob */
+#define HLGS_CUT_FLAT_MAX_ENTRIES 65535
+#define HLGS_CUT_FLAT_MAX_LEVELS 64
+size_t hlgs_upper_tree_order_size(int N);
+int hlgs_upper_tree_order(int N, const int* nodes_host, void* order_host);
 /* SPT construction (GaussianModel.build_hierarchical_SPT + get_min_distance, scene/gaussian_model.py:184-352), host
  * code over host arrays: nodes G x 6 (HierarchyNode), xyz G x 3, log_scales G x 3 (unactivated, as _scaling);
  * root = the hierarchy root (the reference's default root_node 100000 is its skybox size).  The result is an

@@ -42,7 +42,8 @@ def test_losses_match_reference_golden(i):
 
 
 @pytest.mark.parametrize("shape,padding", [((1, 3, 1080, 1920), "same"), ((1, 3, 1080, 1920), "valid"),
-                                           ((2, 3, 77, 131), "same"), ((3, 45, 29), "valid")])
+                                           ((2, 3, 77, 131), "same"), ((3, 45, 29), "valid"),
+                                           ((1, 2, 7, 9), "same"), ((1, 1, 33, 233), "valid")])
 def test_fused_ssim_matches_restatement(shape, padding):
     from fused_ssim import fused_ssim
     rng = np.random.default_rng(sum(shape))

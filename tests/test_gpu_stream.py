@@ -39,12 +39,20 @@ def test_upper_tree_cut_matches_reference_walk(seed, dmul, frustum, lod):
     want = SR.upper_tree_cut(nodes, xyz, bounds, md2, planes.numpy(), cam["campos"].numpy(), dmul, frustum, lod)
     assert 0 < len(want) < len(nodes)
     np.testing.assert_array_equal(got.cpu().numpy(), want)
+    # the flat cut (k_cut_flat_eval + k_cut_flat_place) from the precomputed walk order: the same nodes in the same order
+    order = spt.upper_tree_order(t(nodes))
+    assert order is not None
+    flat = spt.upper_tree_cut(t(nodes), t(xyz), t(bounds), t(md2), planes, cam["campos"], dmul, frustum, lod,
+                              order=order)
+    np.testing.assert_array_equal(flat.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("n,frustum,lod", [(40000, False, False), (40000, True, True), (300000, False, False)])
+@pytest.mark.parametrize("n,frustum,lod", [(40000, False, False), (40000, True, True), (300000, False, False),
+                                           (30000, False, False), (30000, True, True)])
 def test_upper_tree_cut_wide_levels(n, frustum, lod):
     """Levels wider than the single-workgroup walk's 1,024 entries run as multi-workgroup launches (k_cut_level);
-    300k leaves give nine such levels, one more than are queued, so the resume walk finishes the last one."""
+    300k leaves give nine such levels, one more than are queued, so the resume walk finishes the last one.  The
+    30k-leaf trees (59,999 nodes) are within the flat cut's 65,535 entries: its thread runs span several levels."""
     from hlgs_core import spt
     nodes, xyz, bounds, md2 = _upper_tree(n, 7)
     cam = S.make_camera(320, 240, T=np.array([0.05, 0.0, 0.3]))
@@ -54,6 +62,13 @@ def test_upper_tree_cut_wide_levels(n, frustum, lod):
     want = SR.upper_tree_cut(nodes, xyz, bounds, md2, planes.numpy(), cam["campos"].numpy(), 1.0, frustum, lod)
     assert len(want) > 2048
     np.testing.assert_array_equal(got.cpu().numpy(), want)
+    order = spt.upper_tree_order(t(nodes))
+    if len(nodes) > 65535:  # beyond the flat cut's entries: the level walk serves it
+        assert order is None
+        return
+    flat = spt.upper_tree_cut(t(nodes), t(xyz), t(bounds), t(md2), planes, cam["campos"], 1.0, frustum, lod,
+                              order=order)
+    np.testing.assert_array_equal(flat.cpu().numpy(), want)
 
 
 @pytest.mark.parametrize("width,dtype", [(3, torch.float32), (45, torch.float32), (4, torch.float32),
