@@ -118,7 +118,7 @@ __device__ __forceinline__ void prefetch_instances(const Geom& g, bool alt, int 
 }
 
 template <int BG, bool KEYS, bool MASKS, typename F>
-__device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy, bool alt, const uint32_t* s_pre,
+__device__ __forceinline__ void for_each_instance(const Geom& g, int P, int gx, int gy, bool alt, const uint32_t* s_pre,
                                                   const uint32_t* s_w, const GIn (&pre)[4], F&& f)
 {
     const int g0 = blockIdx.x * BG;
@@ -165,12 +165,10 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
         if (s_pre[mid] <= i) lo = mid;
         else hi = mid - 1;
     }
-    for (int k = lo; i < iend; k++) {
+    // the instances of Gaussian k from i on, up to the run's end
+    auto walk = [&](int k, const GIn& v) {
         const uint32_t b = s_pre[k], e = s_pre[k + 1];
-        if (e == b) continue;
         const int idx = g0 + k;
-        GIn v;
-        gauss(idx, v);
         int x0, y0, x1, y1;
         tile_rect(v.xy.x, v.xy.y, v.ext.x, v.ext.y, gx, gy, x0, y0, x1, y1);
         const int w = x1 - x0;
@@ -190,6 +188,23 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int gx, int gy,
                 if (++tx == w) { tx = 0; ty++; }
             }
         }
+    };
+    // the run's first kWidePre Gaussians are loaded together (a run crosses several small Gaussians when one wide
+    // rect puts its whole block on this path), the rest one by one
+    constexpr int kWidePre = 4;
+    GIn pv[kWidePre];
+#pragma unroll
+    for (int u = 0; u < kWidePre; u++) gauss(min(g0 + lo + u, P - 1), pv[u]);  // clamped: no branch before the loads
+#pragma unroll
+    for (int u = 0; u < kWidePre; u++) {
+        if (i >= iend) return;
+        if (s_pre[lo + u + 1] != s_pre[lo + u]) walk(lo + u, pv[u]);
+    }
+    for (int k = lo + kWidePre; i < iend; k++) {
+        if (s_pre[k + 1] == s_pre[k]) continue;
+        GIn v;
+        gauss(g0 + k, v);
+        walk(k, v);
     }
 }
 
@@ -222,7 +237,7 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
         for (int i = threadIdx.x; i < n_zero; i += BG / 4) zero_words[i] = 0u;
         if (threadIdx.x == 0) { misc[kMiscFail] = 0u; misc[kMiscDone] = 0u; }
     }
-    for_each_instance<BG, false, DROP>(g, gx, gy, alt, s_pre, s_w, pre, [&](int, int x, int y, uint32_t qm, uint32_t) {
+    for_each_instance<BG, false, DROP>(g, P, gx, gy, alt, s_pre, s_w, pre, [&](int, int x, int y, uint32_t qm, uint32_t) {
         if (!DROP || qm) atomicAdd(&s_hist[y * gx + x], 1u);
     });
     __syncthreads();
@@ -392,7 +407,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         }
         for (int t = threadIdx.x + kPreTiles * (BG / 4); t < T; t += (BG / 4)) s_cnt[t] = ranges[t].x + row[t];
     } else {
-        for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, pre, [&](int, int x, int y, uint32_t qm, uint32_t) {
+        for_each_instance<BG, false, PACK>(g, P, gx, gy, alt, s_pre, s_w, pre, [&](int, int x, int y, uint32_t qm, uint32_t) {
             if (!(g.drop && !qm)) atomicAdd(&s_cnt[y * gx + x], 1u);
         });
         __syncthreads();
@@ -443,7 +458,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
         }
         return;
     }
-    for_each_instance<BG, false, PACK>(g, gx, gy, alt, s_pre, s_w, pre, [&](int idx, int x, int y, uint32_t qm, uint32_t) {
+    for_each_instance<BG, false, PACK>(g, P, gx, gy, alt, s_pre, s_w, pre, [&](int idx, int x, int y, uint32_t qm, uint32_t) {
         if (g.drop && !qm) return;  // the footprint reaches none of the tile's quadrants
         const int tile = y * gx + x;
         const uint32_t r = atomicAdd(&s_rank[tile], 1u);

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=${1:-gpurun_out/stall}
 shift || true
 mkdir -p $O
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --no-stage-timing $*"
+B=${PMC_CMD:-"python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --no-stage-timing $*"}
 run() { name=$1; shift
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d $O/$name -o run --output-format csv -- $B > $O/$name.log 2>&1
   echo "pass $name ok"; }
