@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(kQThreads) k_ssim_fwd(int H, int W, const floa
     float mo[5][8];
     ssim_horizontal<5>(vs, win, j, o0, mo);
     const int py = y0 + j, px0 = x0 + o0;
-    const int n = (py < H && o0 < kQO) ? max(0, min(8, W - px0)) : 0;
+    const int n = (py < H && o0 < kQO) ? max(0, min(min(8, kQO - o0), W - px0)) : 0;
     const bool vec = n == 8 && (W & 3) == 0;
     const size_t pid = (size_t)py * W + px0;
     float xv[8], yv[8];
@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(kQThreads) k_ssim_bwd(int H, int W, const floa
     float g[3][8];
     ssim_horizontal<3>(vs, win, j, o0, g);
     const int py = y0 + j, px0 = x0 + o0;
-    const int n = (py < H && o0 < kQO) ? max(0, min(8, W - px0)) : 0;
+    const int n = (py < H && o0 < kQO) ? max(0, min(min(8, kQO - o0), W - px0)) : 0;
     if (n == 0) return;
     const bool vec = n == 8 && (W & 3) == 0;
     const size_t pid = (size_t)ch * HW + (size_t)py * W + px0;
