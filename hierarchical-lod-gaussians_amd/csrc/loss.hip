@@ -7,18 +7,20 @@
 // interior [5, H-5) x [5, W-5)), and the depth term of train_single.py:111-118
 // (mean |(invdepth - mono) * mask|).
 //
-// Design (round 5): one plane (channel) per grid.z, a 116 x 16 output tile per 256-thread workgroup, the two
-// separable passes in the order that keeps the first one in registers:
-//   vertical:   thread t owns input column t & 127 of the tile (its 116 output columns plus the 5-pixel halo on
-//               each side) and output rows [8 q, 8 q + 8), q = t >> 7: it loads the 18 input rows of that column
-//               (zero outside the image: zero padding), forms the five moments (x, y, x^2, y^2, x y) per row and
-//               writes the 11-tap column sums of its 8 rows to LDS (one row of 128 columns per (moment, row));
-//   horizontal: thread t owns output row j and the 8 output columns [8 s, 8 s + 8): 18 consecutive column sums
-//               per moment (four 16-byte LDS reads and one 8-byte read; row stride 132 floats puts the two rows of a
-//               16-lane group on opposite halves of the 64 banks) give the 8 window sums per moment.
-// Round 4 staged both images with the halo in LDS and ran the horizontal pass first over all 18 rows of an 8-row
-// tile (2.25 horizontal passes per output and 11 x 5 LDS reads per output in the vertical pass): 103 us forward and
-// 85 us backward at 3 x 1080 x 1920 (tools/variants/loss_r04.hip).
+// Design (round 5): one plane (channel) per grid.z, a 128 x 16 output tile per 256-thread workgroup, the two
+// separable passes with the first one in registers:
+//   horizontal: thread t < 208 owns input row t >> 3 of the tile's 26 (its 16 output rows and the 5-row halo above
+//               and below) and the 16 output columns [16 s, 16 s + 16), s = t & 7: it loads the 26 input pixels of
+//               that run (eight aligned 16-byte loads per image when W is a multiple of 4; zero outside the image:
+//               zero padding), forms each moment (x, y, x^2, y^2, x y) and writes its 16 11-tap row sums to LDS;
+//   vertical:   thread t owns output column t & 127 and output rows [8 q, 8 q + 8), q = t >> 7: 18 row sums per
+//               moment down its column (conflict-free: a wave reads 64 consecutive columns) give the window sums,
+//               and the per-pixel outputs go out as 256-byte rows.
+// The sums are the round-4 kernel's fmaf chains in the same order (horizontal first, tap 0 to 10, then vertical), so
+// every per-pixel value -- the SSIM map, the A, B, C maps, the gradient -- is bit-identical to it; only the
+// workgroup partial sums of the loss are added in another grouping.  Round 4 staged both images with the halo in LDS
+// and ran the horizontal pass over all 18 rows of each 64 x 8 tile (2.25 horizontal passes per output) and the
+// vertical pass from LDS: 103 us forward and 85 us backward at 3 x 1080 x 1920 (tools/variants/loss_r04.hip).
 // The forward writes the partial derivatives of the SSIM map with respect to the window means
 //   A = df/dmu1 (total), B = df/d E[x^2], C = df/d E[x y]
 // so that dSSIM/dx(p) = sum_q g(q) w(q - p) (A(q) + 2 x(p) B(q) + y(p) C(q)), which the backward evaluates with
@@ -31,112 +33,80 @@
 namespace hlgs {
 
 constexpr int kHalo = 5;
-constexpr int kQW = 128;                // input columns per tile (one per vertical-pass thread of each half)
-constexpr int kQO = 116;                // output columns per tile (a multiple of 4: 16-byte map stores)
-constexpr int kQR = 8;                  // output rows per vertical-pass thread
-constexpr int kQH = 2 * kQR;            // output rows per tile
-constexpr int kQIn = kQR + 2 * kHalo;   // input rows per vertical-pass thread
-constexpr int kQS = 132;                // LDS row stride (floats)
+constexpr int kQW = 128;                 // output columns per tile
+constexpr int kQH = 16;                  // output rows per tile
+constexpr int kQRows = kQH + 2 * kHalo;  // input rows per tile (26)
+constexpr int kQSeg = 16;                // output columns per horizontal-pass thread
+constexpr int kQIn = kQSeg + 2 * kHalo;  // input pixels per horizontal-pass thread (26)
+constexpr int kQR = 8;                   // output rows per vertical-pass thread
+constexpr int kQS = 132;                 // LDS row stride (floats)
 constexpr int kQThreads = 256;
 constexpr float kC1 = 0.01f * 0.01f, kC2 = 0.03f * 0.03f;
-static_assert(kQO + 2 * kHalo <= kQW && kQW * 2 == kQThreads && kQH * 16 == kQThreads, "tile shape");
+static_assert(kQRows * (kQW / kQSeg) <= kQThreads && kQW * 2 == kQThreads && 2 * kQR == kQH, "tile shape");
 
 struct Win11 {
     float w[11];
 };
 
-// Vertical pass: NI input planes -> NM moments per input row (mom) -> 11-tap column sums of the thread's kQR rows,
-// written to vs[(m kQH + row) kQS + column].
-template <int NI, int NM, class Mom>
-__device__ __forceinline__ void ssim_vertical(const float* const (&pl)[NI], int H, int W, int x0, int y0,
-                                              const Win11& win, float* vs, Mom mom)
+// The 26 input pixels of a horizontal-pass thread, columns x0 - 5 + c0 + [0, 26) of row gy (zero outside the image).
+__device__ __forceinline__ void load_run26(const float* __restrict__ plane, int H, int W, int gy, int xs,
+                                           float (&v)[kQIn])
 {
-    const int c = threadIdx.x & (kQW - 1), q = threadIdx.x / kQW;
-    const int gx = x0 - kHalo + c;
-    const bool colin = gx >= 0 && gx < W && c < kQO + 2 * kHalo;
-    const int gxc = min(max(gx, 0), W - 1);
-    const int gy0 = y0 - kHalo + kQR * q;
-    float in[NI][kQIn];
+    const bool rowin = gy >= 0 && gy < H;
+    const float* rowp = plane + (size_t)min(max(gy, 0), H - 1) * W;
+    if ((W & 3) == 0) {  // eight aligned float4 groups [xs - 3, xs + 29), each wholly inside or outside the image
+        const int a0 = xs - 3;
+        float f[32];
 #pragma unroll
-    for (int r = 0; r < kQIn; r++) {  // every load issued before the first use
-        const int gyc = min(max(gy0 + r, 0), H - 1);
+        for (int g4 = 0; g4 < 8; g4++) {
+            const int c = a0 + 4 * g4;
+            const bool in = rowin && c >= 0 && c < W;
+            const float4 q = *reinterpret_cast<const float4*>(rowp + min(max(c, 0), W - 4));
+            f[4 * g4] = in ? q.x : 0.f;
+            f[4 * g4 + 1] = in ? q.y : 0.f;
+            f[4 * g4 + 2] = in ? q.z : 0.f;
+            f[4 * g4 + 3] = in ? q.w : 0.f;
+        }
 #pragma unroll
-        for (int i = 0; i < NI; i++) in[i][r] = pl[i][(size_t)gyc * W + gxc];
+        for (int i = 0; i < kQIn; i++) v[i] = f[i + 3];
+    } else {
+#pragma unroll
+        for (int i = 0; i < kQIn; i++) {
+            const int c = xs + i;
+            const float q = rowp[min(max(c, 0), W - 1)];
+            v[i] = rowin && c >= 0 && c < W ? q : 0.f;
+        }
+    }
+}
+
+// 16 row sums of one moment (fmaf over taps 0..10, the round-4 order) into LDS row `dst`
+__device__ __forceinline__ void row_sums16(const float (&f)[kQIn], const Win11& win, float* dst)
+{
+    float o[kQSeg];
+#pragma unroll
+    for (int i = 0; i < kQSeg; i++) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; k++) acc = fmaf(win.w[k], f[i + k], acc);
+        o[i] = acc;
     }
 #pragma unroll
-    for (int r = 0; r < kQIn; r++) {
-        const bool ok = colin && gy0 + r >= 0 && gy0 + r < H;
+    for (int u = 0; u < kQSeg / 4; u++)
+        *reinterpret_cast<float4*>(dst + 4 * u) = make_float4(o[4 * u], o[4 * u + 1], o[4 * u + 2], o[4 * u + 3]);
+}
+
+// Vertical pass of one moment: the window sums of output rows [8 q, 8 q + 8) of column c
+__device__ __forceinline__ void col_sums8(const float* hs_m, const Win11& win, int c, int q, float (&out)[kQR])
+{
+    float v[kQR + 2 * kHalo];
 #pragma unroll
-        for (int i = 0; i < NI; i++) in[i][r] = ok ? in[i][r] : 0.f;
-    }
-    float mv[NM][kQIn];
-#pragma unroll
-    for (int r = 0; r < kQIn; r++) mom(in, r, mv);
+    for (int r = 0; r < kQR + 2 * kHalo; r++) v[r] = hs_m[(kQR * q + r) * kQS + c];
 #pragma unroll
     for (int jj = 0; jj < kQR; jj++) {
+        float acc = 0.f;
 #pragma unroll
-        for (int m = 0; m < NM; m++) {
-            float acc = 0.f;
-#pragma unroll
-            for (int k = 0; k < 11; k++) acc = fmaf(win.w[k], mv[m][jj + k], acc);
-            vs[(m * kQH + kQR * q + jj) * kQS + c] = acc;
-        }
-    }
-}
-
-// Horizontal pass: the 8 window sums per moment of output row j, tile columns [o0, o0 + 8).  Lanes 0-7 of each
-// 16-lane group take eight consecutive column groups of one row, lanes 8-15 the same groups of the next row.
-__device__ __forceinline__ void ssim_lane(int& j, int& o0)
-{
-    const int t = threadIdx.x;
-    j = 2 * (t >> 5) + ((t >> 3) & 1);
-    o0 = 8 * (8 * ((t >> 4) & 1) + (t & 7));
-}
-template <int NM>
-__device__ __forceinline__ void ssim_horizontal(const float* vs, const Win11& win, int j, int o0, float (&out)[NM][8])
-{
-#pragma unroll
-    for (int m = 0; m < NM; m++) {
-        const float* row = vs + (m * kQH + j) * kQS + o0;
-        float v[kQR + 2 * kHalo];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const float4 f = *reinterpret_cast<const float4*>(row + 4 * u);
-            v[4 * u] = f.x; v[4 * u + 1] = f.y; v[4 * u + 2] = f.z; v[4 * u + 3] = f.w;
-        }
-        const float2 f = *reinterpret_cast<const float2*>(row + 16);
-        v[16] = f.x;
-        v[17] = f.y;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            float acc = 0.f;
-#pragma unroll
-            for (int k = 0; k < 11; k++) acc = fmaf(win.w[k], v[i + k], acc);
-            out[m][i] = acc;
-        }
-    }
-}
-
-// 8 consecutive floats of one row (16-byte aligned when `vec`), zero beyond n
-__device__ __forceinline__ void load8(const float* p, bool vec, int n, float (&v)[8])
-{
-    if (vec) {
-        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 8; i++) v[i] = i < n ? p[i] : 0.f;
-    }
-}
-__device__ __forceinline__ void store8(float* p, bool vec, int n, const float (&v)[8])
-{
-    if (vec) {
-        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-            if (i < n) p[i] = v[i];
+        for (int k = 0; k < 11; k++) acc = fmaf(win.w[k], v[jj + k], acc);
+        out[jj] = acc;
     }
 }
 
@@ -146,79 +116,85 @@ __global__ void __launch_bounds__(kQThreads) k_ssim_fwd(int H, int W, const floa
                                                         const float* __restrict__ img2, int valid, Win11 win,
                                                         float* __restrict__ abc, float* __restrict__ partial)
 {
-    __shared__ __attribute__((aligned(16))) float vs[5 * kQH * kQS + 8];
+    __shared__ __attribute__((aligned(16))) float hs[5][kQRows * kQS];
     __shared__ float red[2][kQThreads / 64];
     const int ch = blockIdx.z;
     const size_t HW = (size_t)H * W;
     const float* x = img1 + ch * HW;
     const float* y = img2 + ch * HW;
-    const int x0 = blockIdx.x * kQO, y0 = blockIdx.y * kQH;
-    const float* const pl[2] = {x, y};
-    ssim_vertical<2, 5>(pl, H, W, x0, y0, win, vs, [](const float (&in)[2][kQIn], int r, float (&mv)[5][kQIn]) {
-        const float u = in[0][r], v = in[1][r];
-        mv[0][r] = u;
-        mv[1][r] = v;
-        mv[2][r] = u * u;
-        mv[3][r] = v * v;
-        mv[4][r] = u * v;
-    });
-    __syncthreads();
-    int j, o0;
-    ssim_lane(j, o0);
-    float mo[5][8];
-    ssim_horizontal<5>(vs, win, j, o0, mo);
-    const int py = y0 + j, px0 = x0 + o0;
-    const int n = (py < H && o0 < kQO) ? max(0, min(min(8, kQO - o0), W - px0)) : 0;
-    const bool vec = n == 8 && (W & 3) == 0;
-    const size_t pid = (size_t)py * W + px0;
-    float xv[8], yv[8];
-    if (n > 0) {
-        load8(x + pid, vec, n, xv);
-        load8(y + pid, vec, n, yv);
-    }
-    float s_map = 0.f, s_l1 = 0.f;
-    float A[8], B[8], C[8];
+    const int x0 = blockIdx.x * kQW, y0 = blockIdx.y * kQH;
+    const int t = threadIdx.x;
+    if (t < kQRows * (kQW / kQSeg)) {
+        const int r = t >> 3, c0 = kQSeg * (t & 7);
+        const int gy = y0 - kHalo + r, xs = x0 - kHalo + c0;
+        float u[kQIn], v[kQIn], f[kQIn];
+        load_run26(x, H, W, gy, xs, u);
+        load_run26(y, H, W, gy, xs, v);
+        float* row = &hs[0][r * kQS + c0];
+        row_sums16(u, win, row);
+        row_sums16(v, win, row + kQRows * kQS);
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const float m1 = mo[0][i], m2 = mo[1][i], e11 = mo[2][i], e22 = mo[3][i], e12 = mo[4][i];
-        const int px = px0 + i;
-        const bool counted = i < n && (!valid || (px >= kHalo && px < W - kHalo && py >= kHalo && py < H - kHalo));
-        const float mu1_sq = m1 * m1, mu2_sq = m2 * m2, mu12 = m1 * m2;
-        const float s11 = e11 - mu1_sq, s22 = e22 - mu2_sq, s12 = e12 - mu12;
-        const float a = 2.f * mu12 + kC1, b = 2.f * s12 + kC2;
-        const float c = mu1_sq + mu2_sq + kC1, d = s11 + s22 + kC2;
-        const float f = (a * b) / (c * d);
-        if (counted) s_map += f;
-        if (i < n) s_l1 += fabsf(xv[i] - yv[i]);
-        A[i] = B[i] = C[i] = 0.f;
-        if (TRAIN && counted) {
-            const float cd = c * d;
-            const float dmu1 = (2.f * m2 * b) / cd - f * (2.f * m1) / c;  // df/dmu1 at fixed sigmas
-            B[i] = -f / d;                                                // df/dsigma1^2
-            C[i] = (2.f * a) / cd;                                        // df/dsigma12
-            A[i] = dmu1 - 2.f * m1 * B[i] - m2 * C[i];                    // through sigma = E[.] - mu mu
-        }
+        for (int i = 0; i < kQIn; i++) f[i] = u[i] * u[i];
+        row_sums16(f, win, row + 2 * kQRows * kQS);
+#pragma unroll
+        for (int i = 0; i < kQIn; i++) f[i] = v[i] * v[i];
+        row_sums16(f, win, row + 3 * kQRows * kQS);
+#pragma unroll
+        for (int i = 0; i < kQIn; i++) f[i] = u[i] * v[i];
+        row_sums16(f, win, row + 4 * kQRows * kQS);
     }
-    if (TRAIN && n > 0) {
-        float* o = abc + (size_t)ch * 3 * HW + pid;
-        store8(o, vec, n, A);
-        store8(o + HW, vec, n, B);
-        store8(o + 2 * HW, vec, n, C);
+    __syncthreads();
+    const int c = t & (kQW - 1), q = t / kQW;
+    float mo[5][kQR];
+#pragma unroll
+    for (int m = 0; m < 5; m++) col_sums8(hs[m], win, c, q, mo[m]);
+    const int px = x0 + c;
+    float s_map = 0.f, s_l1 = 0.f;
+    if (px < W) {
+#pragma unroll
+        for (int jj = 0; jj < kQR; jj++) {
+            const int py = y0 + kQR * q + jj;
+            if (py >= H) break;
+            const size_t pid = (size_t)py * W + px;
+            const float m1 = mo[0][jj], m2 = mo[1][jj], e11 = mo[2][jj], e22 = mo[3][jj], e12 = mo[4][jj];
+            const bool counted = !valid || (px >= kHalo && px < W - kHalo && py >= kHalo && py < H - kHalo);
+            const float mu1_sq = m1 * m1, mu2_sq = m2 * m2, mu12 = m1 * m2;
+            const float s11 = e11 - mu1_sq, s22 = e22 - mu2_sq, s12 = e12 - mu12;
+            const float a = 2.f * mu12 + kC1, b = 2.f * s12 + kC2;
+            const float cc = mu1_sq + mu2_sq + kC1, d = s11 + s22 + kC2;
+            const float fm = (a * b) / (cc * d);
+            if (counted) s_map += fm;
+            s_l1 += fabsf(x[pid] - y[pid]);
+            if (TRAIN) {
+                float A = 0.f, B = 0.f, C = 0.f;
+                if (counted) {
+                    const float cd = cc * d;
+                    const float dmu1 = (2.f * m2 * b) / cd - fm * (2.f * m1) / cc;  // df/dmu1 at fixed sigmas
+                    B = -fm / d;                                                  // df/dsigma1^2
+                    C = (2.f * a) / cd;                                           // df/dsigma12
+                    A = dmu1 - 2.f * m1 * B - m2 * C;                             // through sigma = E[.] - mu mu
+                }
+                float* o = abc + (size_t)ch * 3 * HW + pid;
+                o[0] = A;
+                o[HW] = B;
+                o[2 * HW] = C;
+            }
+        }
     }
     // workgroup sums (fixed order: shuffles, then one lane per wave)
     for (int off = 32; off > 0; off >>= 1) {
         s_map += __shfl_xor(s_map, off, 64);
         s_l1 += __shfl_xor(s_l1, off, 64);
     }
-    const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[0][wave] = s_map; red[1][wave] = s_l1; }
+    const int wave = t >> 6;
+    if ((t & 63) == 0) { red[0][wave] = s_map; red[1][wave] = s_l1; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float a = 0.f, b = 0.f;
-        for (int i = 0; i < kQThreads / 64; i++) { a += red[0][i]; b += red[1][i]; }
+    if (t == 0) {
+        float sa = 0.f, sb = 0.f;
+        for (int i = 0; i < kQThreads / 64; i++) { sa += red[0][i]; sb += red[1][i]; }
         const size_t blk = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-        partial[2 * blk] = a;
-        partial[2 * blk + 1] = b;
+        partial[2 * blk] = sa;
+        partial[2 * blk + 1] = sb;
     }
 }
 
@@ -228,39 +204,41 @@ __global__ void __launch_bounds__(kQThreads) k_ssim_bwd(int H, int W, const floa
                                                         Win11 win, const float* __restrict__ coef,
                                                         float* __restrict__ grad1)
 {
-    __shared__ __attribute__((aligned(16))) float vs[3 * kQH * kQS + 8];
+    __shared__ __attribute__((aligned(16))) float hs[3][kQRows * kQS];
     const int ch = blockIdx.z;
     const size_t HW = (size_t)H * W;
-    const int x0 = blockIdx.x * kQO, y0 = blockIdx.y * kQH;
+    const int x0 = blockIdx.x * kQW, y0 = blockIdx.y * kQH;
     const float* maps = abc + (size_t)ch * 3 * HW;
-    const float* const pl[3] = {maps, maps + HW, maps + 2 * HW};
-    ssim_vertical<3, 3>(pl, H, W, x0, y0, win, vs, [](const float (&in)[3][kQIn], int r, float (&mv)[3][kQIn]) {
-        mv[0][r] = in[0][r];
-        mv[1][r] = in[1][r];
-        mv[2][r] = in[2][r];
-    });
+    const int t = threadIdx.x;
+    if (t < kQRows * (kQW / kQSeg)) {
+        const int r = t >> 3, c0 = kQSeg * (t & 7);
+        const int gy = y0 - kHalo + r, xs = x0 - kHalo + c0;
+        float f[kQIn];
+#pragma unroll
+        for (int m = 0; m < 3; m++) {
+            load_run26(maps + m * HW, H, W, gy, xs, f);
+            row_sums16(f, win, &hs[m][r * kQS + c0]);
+        }
+    }
     __syncthreads();
-    int j, o0;
-    ssim_lane(j, o0);
-    float g[3][8];
-    ssim_horizontal<3>(vs, win, j, o0, g);
-    const int py = y0 + j, px0 = x0 + o0;
-    const int n = (py < H && o0 < kQO) ? max(0, min(min(8, kQO - o0), W - px0)) : 0;
-    if (n == 0) return;
-    const bool vec = n == 8 && (W & 3) == 0;
-    const size_t pid = (size_t)ch * HW + (size_t)py * W + px0;
-    float xv[8], yv[8], out[8];
-    load8(img1 + pid, vec, n, xv);
-    load8(img2 + pid, vec, n, yv);
+    const int c = t & (kQW - 1), q = t / kQW;
+    const int px = x0 + c;
+    if (px >= W) return;
+    float g[3][kQR];
+#pragma unroll
+    for (int m = 0; m < 3; m++) col_sums8(hs[m], win, c, q, g[m]);
     const float c0 = coef[0], c1 = coef[1];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const float dssim = g[0][i] + 2.f * xv[i] * g[1][i] + yv[i] * g[2][i];
-        const float diff = xv[i] - yv[i];
+    for (int jj = 0; jj < kQR; jj++) {
+        const int py = y0 + kQR * q + jj;
+        if (py >= H) break;
+        const size_t pid = (size_t)ch * HW + (size_t)py * W + px;
+        const float xv = img1[pid], yv = img2[pid];
+        const float dssim = g[0][jj] + 2.f * xv * g[1][jj] + yv * g[2][jj];
+        const float diff = xv - yv;
         const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);  // torch.abs backward: sign, 0 at 0
-        out[i] = c0 * dssim + c1 * sgn;
+        grad1[pid] = c0 * dssim + c1 * sgn;
     }
-    store8(grad1 + pid, vec, n, out);
 }
 
 // mean |(inv - mono) * mask| partial sums; mask may be NULL (= 1).
@@ -329,7 +307,7 @@ static Win11 gauss_window()
     return w;
 }
 
-static dim3 ssim_grid(int C, int H, int W) { return dim3((W + kQO - 1) / kQO, (H + kQH - 1) / kQH, C); }
+static dim3 ssim_grid(int C, int H, int W) { return dim3((W + kQW - 1) / kQW, (H + kQH - 1) / kQH, C); }
 
 size_t ssim_partials(int C, int H, int W)
 {
