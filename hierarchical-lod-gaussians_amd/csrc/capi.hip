@@ -705,6 +705,8 @@ static int upper_cut_launch(int N, const int* nodes, const float* xyz, const flo
     a.state = reinterpret_cast<CutState*>(q);
     a.arrive = reinterpret_cast<unsigned*>(q + sizeof(CutState));
     a.level_counts = reinterpret_cast<int*>(a.arrive + kCutLevelLaunches);
+    a.flat = reinterpret_cast<CutFlat*>(q + align_up(sizeof(CutState) + sizeof(unsigned) * kCutLevelLaunches +
+                                                     sizeof(int) * 3 * kCutMaxBlocks));
     if (order) launch_upper_cut_flat(a, static_cast<const int*>(order), s);
     else launch_upper_cut(a, s);
     *count_dev = a.count;

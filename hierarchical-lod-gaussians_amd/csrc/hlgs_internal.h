@@ -167,6 +167,11 @@ constexpr int kCutMaxBlocks = 64;      // workgroups of one wide level (all resi
 struct CutState {          // the walk's state between k_upper_cut and the k_cut_level launches
     int size, total, parity, overflow;
 };
+struct CutFlat {           // the flat cut's placement state between k_cut_flat_place and k_cut_flat_write
+    uint64_t leaf[1024], stop[1024];            // per thread run: the alive leaves / condition-false nodes
+    int2 off[1024];                             // per run: leaves and condition-false nodes before it
+    int2 lev[HLGS_CUT_FLAT_MAX_LEVELS + 1];     // per level: (leaves, condition-false nodes) before its first entry
+};
 struct CutArgs {
     int N;
     const int* nodes;      // N x 6 HierarchyNode rows: 2 child_count, 3 first_child, 4 next_sibling
@@ -186,6 +191,7 @@ struct CutArgs {
     CutState* state;
     unsigned* arrive;      // kCutLevelLaunches arrival counters
     int* level_counts;     // 3 x kCutMaxBlocks
+    CutFlat* flat;
 };
 size_t upper_cut_state_bytes();
 

@@ -24,31 +24,33 @@ namespace hlgs {
 // instead of one lane-scattered atomic per (Gaussian, tile) instance.
 // ------------------------------------------------------------------------------------------------
 // s_pre[k] = exclusive prefix of tiles_touched over the block's BG Gaussians (0 past P), s_pre[BG] =
-// the block's total: thread t scans its four consecutive entries, then the 1024 thread totals are scanned.
-// The rect sizes thread t scans (Gaussians 4t .. 4t + 3 of the block), loaded apart from the scan so that a kernel
-// can issue them together with its other first-round loads.
+// the block's total: thread t scans its BG / 1024 consecutive entries, then the 1024 thread totals are scanned.
+// Every binning block has 1024 threads, so a thread takes four Gaussians at 4,096 per block and two at 2,048 (round 5:
+// 512-thread blocks of 2,048 took 78 / 87 us for config #5's count / scatter, 1024-thread blocks 61 / 71 us).
+// The rect sizes thread t scans (Gaussians J t .. J t + J - 1 of the block, J = BG / 1024), loaded apart from the
+// scan so that a kernel can issue them together with its other first-round loads.
 template <int BG>
-__device__ __forceinline__ void block_rect_sizes(int P, const Geom& g, uint32_t (&a)[4])
+__device__ __forceinline__ void block_rect_sizes(int P, const Geom& g, uint32_t (&a)[BG / 1024])
 {
     const int g0 = blockIdx.x * BG, t = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int idx = g0 + 4 * t + k;
+    for (int k = 0; k < BG / 1024; k++) {
+        const int idx = g0 + (BG / 1024) * t + k;
         a[k] = idx < P ? g.tiles_touched[idx] : 0u;
     }
 }
 template <int BG>
-__device__ __forceinline__ void block_rect_prefix(const uint32_t (&a)[4], uint32_t* s_pre, uint32_t* s_w)
+__device__ __forceinline__ void block_rect_prefix(const uint32_t (&a)[BG / 1024], uint32_t* s_pre, uint32_t* s_w)
 {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t sum = 0, mx = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < BG / 1024; k++) {
         sum += a[k];
         mx = max(mx, a[k]);
     }
     for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
-    if (lane == 0) atomicMax(&s_w[(BG / 4) / 64], mx);
+    if (lane == 0) atomicMax(&s_w[(1024) / 64], mx);
     uint32_t x = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -58,29 +60,29 @@ __device__ __forceinline__ void block_rect_prefix(const uint32_t (&a)[4], uint32
     if (lane == 63) s_w[w] = x;
     __syncthreads();
     uint32_t base = 0, total = 0;
-    for (int i = 0; i < (BG / 4) / 64; i++) {
+    for (int i = 0; i < (1024) / 64; i++) {
         const uint32_t c = s_w[i];
         if (i < w) base += c;
         total += c;
     }
     uint32_t run = base + x - sum;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        s_pre[4 * t + k] = run;
+    for (int k = 0; k < BG / 1024; k++) {
+        s_pre[(BG / 1024) * t + k] = run;
         run += a[k];
     }
     if (t == 0) s_pre[BG] = total;
     __syncthreads();
 }
 
-// the block's longest rect (s_w[(BG / 4) / 64], zeroed before block_rect_prefix)
+// the block's longest rect (s_w[(1024) / 64], zeroed before block_rect_prefix)
 constexpr uint32_t kNarrowRect = 64;
 
 // Calls f(idx, x, y, qm, dbits) for every binned instance (Gaussian idx, tile (x, y)) of the block's Gaussians: every
 // tile of the rect, or for the alt rasterizer the tiles alt_tile_keep leaves (rasterizer_impl.cu:147-179 of
 // alt-rasterizer).  KEYS: dbits = the Gaussian's depth bits (the sort key's high word); MASKS: qm = the instance's
 // footprint quadrant mask, from the masks the preprocess left in Geom::qmask (rect_tile_mask); otherwise 0.
-// Without wide rects each thread takes four Gaussians and loads everything they need before its first call, so the
+// Without wide rects each thread takes BG / 1024 Gaussians and loads everything they need before its first call, so the
 // key stores issued by f never have to drain for a later load (vmcnt counts loads and stores alike).  With a wide
 // rect the block's instances are numbered Gaussian by Gaussian (s_pre) and each thread takes one contiguous run of
 // them, so a Gaussian whose rect spans thousands of tiles is spread over the whole block instead of serialising one
@@ -104,40 +106,40 @@ __device__ __forceinline__ void gauss_in(const Geom& g, bool alt, int idx, GIn& 
     v.masks = MASKS ? g.qmask[idx] : 0u;
     v.dbits = KEYS ? __float_as_uint(g.depths[idx]) : 0u;
 }
-// The narrow path's inputs (Gaussians threadIdx.x + j BG / 4 of the block, every one below P, culled or not), issued at
+// The narrow path's inputs (Gaussians threadIdx.x + j 1024 of the block, every one below P, culled or not), issued at
 // the top of a kernel with its other first-round loads; for_each_instance then reads no Gaussian input itself.
 template <int BG, bool MASKS>
-__device__ __forceinline__ void prefetch_instances(const Geom& g, bool alt, int P, GIn (&in)[4])
+__device__ __forceinline__ void prefetch_instances(const Geom& g, bool alt, int P, GIn (&in)[BG / 1024])
 {
     const int g0 = blockIdx.x * BG;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {  // past P: Gaussian P - 1 again (not used), so the loads need no branch
-        const int idx = min(g0 + (int)threadIdx.x + j * (BG / 4), P - 1);
+    for (int j = 0; j < BG / 1024; j++) {  // past P: Gaussian P - 1 again (not used), so the loads need no branch
+        const int idx = min(g0 + (int)threadIdx.x + j * (1024), P - 1);
         gauss_in<false, MASKS>(g, alt, idx, in[j]);
     }
 }
 
 template <int BG, bool KEYS, bool MASKS, typename F>
 __device__ __forceinline__ void for_each_instance(const Geom& g, int P, int gx, int gy, bool alt, const uint32_t* s_pre,
-                                                  const uint32_t* s_w, const GIn (&pre)[4], F&& f)
+                                                  const uint32_t* s_w, const GIn (&pre)[BG / 1024], F&& f)
 {
     const int g0 = blockIdx.x * BG;
     auto gauss = [&](int idx, GIn& v) { gauss_in<KEYS, MASKS>(g, alt, idx, v); };
     auto qmask = [&](uint32_t masks, uint32_t r) { return MASKS ? rect_tile_mask(masks, r) : 0u; };
-    if (s_w[(BG / 4) / 64] <= kNarrowRect) {  // no wide rect in this block: one thread per Gaussian
-        constexpr int J = 4;  // Gaussians per thread
+    if (s_w[(1024) / 64] <= kNarrowRect) {  // no wide rect in this block: one thread per Gaussian
+        constexpr int J = BG / 1024;  // Gaussians per thread
         GIn in[J];
         bool live[J];
 #pragma unroll
         for (int j = 0; j < J; j++) {
-            const int k = threadIdx.x + j * (BG / 4);
+            const int k = threadIdx.x + j * (1024);
             live[j] = s_pre[k + 1] != s_pre[k];
             in[j] = pre[j];
         }
 #pragma unroll
         for (int j = 0; j < J; j++) {
             if (!live[j]) continue;
-            const int idx = g0 + threadIdx.x + j * (BG / 4);
+            const int idx = g0 + threadIdx.x + j * (1024);
             const GIn& v = in[j];
             int x0, y0, x1, y1;
             tile_rect(v.xy.x, v.xy.y, v.ext.x, v.ext.y, gx, gy, x0, y0, x1, y1);
@@ -155,7 +157,7 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int P, int gx, 
         return;
     }
     const uint32_t total = s_pre[BG];
-    const uint32_t chunk = (total + (BG / 4) - 1) / (BG / 4);
+    const uint32_t chunk = (total + (1024) - 1) / (1024);
     uint32_t i = threadIdx.x * chunk;
     const uint32_t iend = min(total, i + chunk);
     if (i >= iend) return;
@@ -213,7 +215,7 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int P, int gx, 
 // tile_count with one device atomic per non-empty tile.  zero_words: k_tile_offsets_plan's look-back words and the
 // plan's failure / completion words (misc[kMiscFail], misc[kMiscDone]), cleared by block 0 for this frame.
 template <int BG, bool DROP>
-__global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
+__global__ void __launch_bounds__(1024) k_count_tiles(int P, const int* __restrict__ radii, Geom g,
                                                              uint32_t* __restrict__ tile_count, int gx, int gy, int alt,
                                                              uint32_t* __restrict__ block_tot, uint32_t* __restrict__ hist,
                                                              uint32_t* __restrict__ zero_words, int n_zero,
@@ -221,20 +223,20 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_pre[BG + 1];
-    __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
+    __shared__ uint32_t s_w[(1024) / 64 + 1];
     const int T = gx * gy;
     // every input in the first round trip (the rect sizes for the scan and the narrow walk's Gaussians)
-    uint32_t sizes[4];
+    uint32_t sizes[BG / 1024];
     block_rect_sizes<BG>(P, g, sizes);
-    GIn pre[4];
+    GIn pre[BG / 1024];
     prefetch_instances<BG, DROP>(g, alt, P, pre);
-    for (int t = threadIdx.x; t < T; t += (BG / 4)) s_hist[t] = 0;
-    if (threadIdx.x == 0) s_w[(BG / 4) / 64] = 0;
+    for (int t = threadIdx.x; t < T; t += (1024)) s_hist[t] = 0;
+    if (threadIdx.x == 0) s_w[(1024) / 64] = 0;
     __syncthreads();
     block_rect_prefix<BG>(sizes, s_pre, s_w);
     if (threadIdx.x == 0) block_tot[blockIdx.x] = s_pre[BG];
     if (zero_words && blockIdx.x == 0) {  // k_tile_offsets_plan's look-back words, failure and completion words
-        for (int i = threadIdx.x; i < n_zero; i += BG / 4) zero_words[i] = 0u;
+        for (int i = threadIdx.x; i < n_zero; i += 1024) zero_words[i] = 0u;
         if (threadIdx.x == 0) { misc[kMiscFail] = 0u; misc[kMiscDone] = 0u; }
     }
     for_each_instance<BG, false, DROP>(g, P, gx, gy, alt, s_pre, s_w, pre, [&](int, int x, int y, uint32_t qm, uint32_t) {
@@ -243,10 +245,10 @@ __global__ void __launch_bounds__(BG / 4) k_count_tiles(int P, const int* __rest
     __syncthreads();
     if (hist) {
         uint32_t* row = hist + (size_t)blockIdx.x * T;
-        for (int t = threadIdx.x; t < T; t += (BG / 4)) row[t] = s_hist[t];
+        for (int t = threadIdx.x; t < T; t += (1024)) row[t] = s_hist[t];
         return;
     }
-    for (int t = threadIdx.x; t < T; t += (BG / 4)) {
+    for (int t = threadIdx.x; t < T; t += (1024)) {
         const uint32_t c = s_hist[t];
         if (c) atomicAdd(&tile_count[t], c);
     }
@@ -341,7 +343,7 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hi
 // hist != nullptr: the block's base inside each tile segment is ranges[t].x + its k_tile_offsets offset, so the block
 // walks its instances once (no count walk, no returning device atomics).
 template <int BG, bool PACK>
-__global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
+__global__ void __launch_bounds__(1024) k_scatter_keys_lds(int P, const int* __restrict__ radii, Geom g,
                                                                   const uint2* __restrict__ ranges, uint32_t* cursor,
                                                                   uint64_t* __restrict__ keys, int gx, int gy, int alt,
                                                                   Guard gd, const uint32_t* __restrict__ block_tot,
@@ -354,7 +356,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_base;
     __shared__ uint32_t s_pre[BG + 1];
-    __shared__ uint32_t s_w[(BG / 4) / 64 + 1];
+    __shared__ uint32_t s_w[(1024) / 64 + 1];
     const int T = gx * gy;
     uint32_t* s_cnt = s_hist;      // per-tile count, then the block's base inside the tile segment
     uint32_t* s_rank = s_hist + T; // per-tile running rank
@@ -362,7 +364,7 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
     // totals, the first kPreTiles of this thread's tile bases (the tile's range start + this block's histogram offset)
     // and the narrow walk's Gaussians.  (Issued one after another, the five rounds of loads had been the kernel's time.)
     constexpr int kPreTiles = 8;
-    uint32_t sizes[4];
+    uint32_t sizes[BG / 1024];
     block_rect_sizes<BG>(P, g, sizes);
     // (every load unconditional, clamped into range, so that the compiler issues them back to back)
     uint32_t part = block_tot[min((int)threadIdx.x, max((int)blockIdx.x - 1, 0))];  // preceding block threadIdx.x
@@ -371,30 +373,30 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
     if (hist) {
 #pragma unroll
         for (int k = 0; k < kPreTiles; k++) {
-            const int t = min((int)threadIdx.x + k * (BG / 4), T - 1);
+            const int t = min((int)threadIdx.x + k * (1024), T - 1);
             trange[k] = ranges[t].x;
             trow[k] = row[t];
         }
     }
-    GIn pre[4];
+    GIn pre[BG / 1024];
     prefetch_instances<BG, PACK>(g, alt, P, pre);
-    if (threadIdx.x == 0) { s_w[(BG / 4) / 64] = 0; s_base = 0; }
+    if (threadIdx.x == 0) { s_w[(1024) / 64] = 0; s_base = 0; }
     if (hist) {
-        for (int t = threadIdx.x; t < T; t += (BG / 4)) s_rank[t] = 0;
+        for (int t = threadIdx.x; t < T; t += (1024)) s_rank[t] = 0;
     } else {
-        for (int t = threadIdx.x; t < T; t += (BG / 4)) { s_cnt[t] = 0; s_rank[t] = 0; }
+        for (int t = threadIdx.x; t < T; t += (1024)) { s_cnt[t] = 0; s_rank[t] = 0; }
     }
     __syncthreads();
     block_rect_prefix<BG>(sizes, s_pre, s_w);
     {  // point_offsets (the inclusive scan of tiles_touched) = the block's base + the block-local prefix; the base is
-       // the sum of the preceding count blocks' totals (k_count_tiles): thread i adds block i's, and i + BG / 4 ... too
+       // the sum of the preceding count blocks' totals (k_count_tiles): thread i adds block i's, and i + 1024 ... too
         if ((int)threadIdx.x >= (int)blockIdx.x) part = 0;
-        for (int i = threadIdx.x + BG / 4; i < (int)blockIdx.x; i += BG / 4) part += block_tot[i];
+        for (int i = threadIdx.x + 1024; i < (int)blockIdx.x; i += 1024) part += block_tot[i];
         if (part) atomicAdd(&s_base, part);
         __syncthreads();
         const int g0 = blockIdx.x * BG, g1 = min(P, g0 + BG);
         const uint32_t base = s_base;
-        for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += (BG / 4)) {
+        for (int idx = g0 + (int)threadIdx.x; idx < g1; idx += (1024)) {
             const int k = idx - g0;
             g.point_offsets[idx] = base + s_pre[k + 1];
         }
@@ -402,37 +404,37 @@ __global__ void __launch_bounds__(BG / 4) k_scatter_keys_lds(int P, const int* _
     if (hist) {
 #pragma unroll
         for (int k = 0; k < kPreTiles; k++) {
-            const int t = (int)threadIdx.x + k * (BG / 4);
+            const int t = (int)threadIdx.x + k * (1024);
             if (t < T) s_cnt[t] = trange[k] + trow[k];
         }
-        for (int t = threadIdx.x + kPreTiles * (BG / 4); t < T; t += (BG / 4)) s_cnt[t] = ranges[t].x + row[t];
+        for (int t = threadIdx.x + kPreTiles * (1024); t < T; t += (1024)) s_cnt[t] = ranges[t].x + row[t];
     } else {
         for_each_instance<BG, false, PACK>(g, P, gx, gy, alt, s_pre, s_w, pre, [&](int, int x, int y, uint32_t qm, uint32_t) {
             if (!(g.drop && !qm)) atomicAdd(&s_cnt[y * gx + x], 1u);
         });
         __syncthreads();
-        for (int t = threadIdx.x; t < T; t += (BG / 4)) {
+        for (int t = threadIdx.x; t < T; t += (1024)) {
             const uint32_t c = s_cnt[t];
             s_cnt[t] = c ? ranges[t].x + atomicAdd(&cursor[t], c) : 0u;
         }
     }
     __syncthreads();
-    if (!alt && s_w[(BG / 4) / 64] <= kNarrowRect) {
+    if (!alt && s_w[(1024) / 64] <= kNarrowRect) {
         // Narrow rects (for_each_instance's one-thread-per-Gaussian path): each thread's instances in groups of four,
         // the four rank atomics issued together and then the four key stores -- one at a time, every store waits for
         // its atomic's return.
         const int g0 = blockIdx.x * BG;
-        constexpr int J = 4;
+        constexpr int J = BG / 1024;
         bool live[J];
 #pragma unroll
         for (int j = 0; j < J; j++) {
-            const int k = threadIdx.x + j * (BG / 4);
+            const int k = threadIdx.x + j * (1024);
             live[j] = s_pre[k + 1] != s_pre[k];
         }
 #pragma unroll
         for (int j = 0; j < J; j++) {
             if (!live[j]) continue;
-            const uint32_t idx = (uint32_t)(g0 + threadIdx.x + j * (BG / 4));
+            const uint32_t idx = (uint32_t)(g0 + threadIdx.x + j * (1024));
             const uint32_t gmask = pre[j].masks;
             int x0, y0, x1, y1;
             tile_rect(pre[j].xy.x, pre[j].xy.y, pre[j].ext.x, pre[j].ext.y, gx, gy, x0, y0, x1, y1);
@@ -1267,7 +1269,7 @@ void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, i
     fused = fused && hist;
     uint32_t* zw = fused ? im.tile_cursor : nullptr;
     const int nz = fused ? 2 * ((T + 31) / 32) : 0;
-#define HLGS_CNT(BG, D) hipLaunchKernelGGL((k_count_tiles<BG, D>), dim3((P + BG - 1) / BG), dim3(BG / 4), lds, s, P, \
+#define HLGS_CNT(BG, D) hipLaunchKernelGGL((k_count_tiles<BG, D>), dim3((P + BG - 1) / BG), dim3(1024), lds, s, P, \
                                           radii, g, im.tile_count, gx, gy, (int)alt, g.scan_tmp, hist, zw, nz, im.misc)
     if (bg == 4096) { if (g.drop) HLGS_CNT(4096, true); else HLGS_CNT(4096, false); }
     else { if (g.drop) HLGS_CNT(2048, true); else HLGS_CNT(2048, false); }
@@ -1312,7 +1314,7 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
     if (lds_binning(a.P, gx, gy)) {
         allow_big_lds();
 #define HLGS_SCATTER(BG, PK)                                                                                       \
-    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK>), dim3((a.P + BG - 1) / BG), dim3(BG / 4),                           \
+    hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK>), dim3((a.P + BG - 1) / BG), dim3(1024),                           \
                        2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy, alt, \
                        gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy))
         const bool pk = pack_entries(a.P);

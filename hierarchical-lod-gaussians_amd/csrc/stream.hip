@@ -344,9 +344,9 @@ void launch_upper_cut(const CutArgs& a, hipStream_t s)
 //                     does not expand (culled, leaf, condition false), else 0.
 //   k_cut_flat_place: covered(p) = (max of those ends over preorder positions < p) > p -- a max scan over preorder
 //                     into an LDS bit mask; then per F* entry alive = !covered(its position); the leaves and
-//                     condition-false nodes that are alive are counted per thread run and scanned, and placed:
-//                     a leaf at (stops before its level) + (leaves before it), a condition-false node at
-//                     (leaves up to the end of its level) + (stops before it).
+//                     condition-false nodes that are alive are counted per thread run and scanned (one workgroup);
+//   k_cut_flat_write: places them, one thread per entry: a leaf at (stops before its level) + (leaves before it), a
+//                     condition-false node at (leaves up to the end of its level) + (stops before it).
 constexpr int kFlatRun = 64;  // entries per thread of k_cut_flat_place (1024 x 64 > HLGS_CUT_FLAT_MAX_ENTRIES)
 static_assert(1024 * kFlatRun > HLGS_CUT_FLAT_MAX_ENTRIES, "one 64-bit mask per thread run");
 
@@ -470,29 +470,51 @@ __global__ void __launch_bounds__(1024) k_cut_flat_place(CutArgs a, const int* _
     }
     if (t == 0) s_lev[nlev] = make_int2(tot.x, tot.y);
     __syncthreads();
-    if (tot.x + tot.y > a.capacity) {
-        if (t == 0) { a.count[0] = 0; a.count[1] = 1; }
-        return;
+    a.flat->leaf[t] = leaf;
+    a.flat->stop[t] = stop;
+    a.flat->off[t] = make_int2(o.x, o.y);
+    if (t <= nlev) a.flat->lev[t] = s_lev[t];
+    if (t == 0) {
+        const bool over = tot.x + tot.y > a.capacity;
+        a.count[0] = over ? 0 : tot.x + tot.y;
+        a.count[1] = over ? 1 : 0;
     }
-    if (n > 0) {
-        int l = 0;
-        while (l + 1 < nlev && s_ls[l + 1] <= p0) l++;
-        int nl = 0, ns = 0;
-        for (int h = 0; h < kFlatRun; h += 32) {  // two halves: 32 node ids in registers at a time
-            if (h >= n) break;
-            uint32_t nd[32];
-            load_run<4>(fn + h, p0, nd);
-#pragma unroll
-            for (int k = 0; k < 32; k++) {
-                if (h + k < n) {
-                    if (l + 1 < nlev && s_ls[l + 1] <= p0 + h + k) l++;  // levels hold at least one entry each
-                    if ((leaf >> (h + k)) & 1ull) a.cut[s_lev[l].y + o.x + nl++] = (int)nd[k];
-                    if ((stop >> (h + k)) & 1ull) a.cut[s_lev[l + 1].x + o.y + ns++] = (int)nd[k];
-                }
-            }
-        }
+}
+
+// Placement, one thread per F* entry (consecutive lanes, consecutive entries: the stores of a wave land in one or two
+// runs of consecutive cut positions).  In k_cut_flat_place each thread stored its own run's nodes, 64 scattered
+// store instructions per wave from a single workgroup: 45 us of its time.
+__global__ void __launch_bounds__(256) k_cut_flat_write(CutArgs a, const int* __restrict__ order)
+{
+    __shared__ int s_ls[HLGS_CUT_FLAT_MAX_LEVELS + 1];
+    __shared__ int2 s_lev[HLGS_CUT_FLAT_MAX_LEVELS + 1];
+    const int M = order[0], nlev = order[1];
+    if (!order[2] || M <= 0 || M > HLGS_CUT_FLAT_MAX_ENTRIES || nlev < 1 || nlev > HLGS_CUT_FLAT_MAX_LEVELS ||
+        a.count[1])
+        return;  // (uniform) reported by k_cut_flat_place
+    const int t = threadIdx.x;
+    if (t <= nlev) {
+        s_ls[t] = order[4 + t];
+        s_lev[t] = a.flat->lev[t];
     }
-    if (t == 0) { a.count[0] = tot.x + tot.y; a.count[1] = 0; }
+    __syncthreads();
+    const int i = blockIdx.x * 256 + t;
+    if (i >= M) return;
+    const int R = ((M + 1023) / 1024 + 31) & ~31;
+    const int run = i / R, k = i - run * R;
+    const uint64_t leaf = a.flat->leaf[run], stop = a.flat->stop[run];
+    const bool isl = (leaf >> k) & 1ull, iss = (stop >> k) & 1ull;
+    if (!isl && !iss) return;
+    int lo = 0, hi = nlev - 1;  // the level holding entry i: last l with s_ls[l] <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_ls[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    const int2 off = a.flat->off[run];
+    const uint64_t below = (1ull << k) - 1ull;
+    const int pos = isl ? s_lev[lo].y + off.x + __popcll(leaf & below) : s_lev[lo + 1].x + off.y + __popcll(stop & below);
+    a.cut[pos] = order[HLGS_CUT_ORDER_HEADER + i];
 }
 
 void launch_upper_cut_flat(const CutArgs& a, const int* order, hipStream_t s)
@@ -502,9 +524,14 @@ void launch_upper_cut_flat(const CutArgs& a, const int* order, hipStream_t s)
     uint16_t* endv = reinterpret_cast<uint16_t*>(a.front_b);
     hipLaunchKernelGGL(k_cut_flat_eval, dim3((a.N + 255) / 256), dim3(256), 0, s, a, order, st8, endv);
     hipLaunchKernelGGL(k_cut_flat_place, dim3(1), dim3(1024), 0, s, a, order, st8, endv);
+    hipLaunchKernelGGL(k_cut_flat_write, dim3((a.N + 255) / 256), dim3(256), 0, s, a, order);
 }
 
-size_t upper_cut_state_bytes() { return sizeof(CutState) + sizeof(unsigned) * kCutLevelLaunches + sizeof(int) * 3 * kCutMaxBlocks; }
+size_t upper_cut_state_bytes()
+{
+    const size_t walk = sizeof(CutState) + sizeof(unsigned) * kCutLevelLaunches + sizeof(int) * 3 * kCutMaxBlocks;
+    return (walk + 255) / 256 * 256 + sizeof(CutFlat);  // capi.hip places CutFlat at align_up(walk)
+}
 
 // ---------------------------------------------------------------- row gather / scatter
 // 16 lanes per row (four rows per wave); each lane moves 16-byte words when the row size and both bases allow,
