@@ -113,14 +113,15 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             const uint32_t ws = (uint32_t)__shfl((int)r_start, src, 64), we = (uint32_t)__shfl((int)r_end, src, 64);
             const int sidx = t_idx - lane + src;  // the wide Gaussian's rasterised index
             float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
-            float kx = 0.f, ky = 0.f, kthr = 0.f;
+            float kx = 0.f, ky = 0.f;
+            AltKeep kthr{0.f, 0.f, 0.f};
             int kx0 = 0, ky0 = 0, kw = 1;
             if (ALT) {
                 const float4 r0 = g.splat[4 * (size_t)sidx], r1 = g.splat[4 * (size_t)sidx + 1];
                 const float4 r3 = g.splat[4 * (size_t)sidx + 3];
                 kx = r0.x; ky = r0.y;
                 kco = make_float4(r0.z, r0.w, r1.x, r1.y);
-                kthr = alt_keep_threshold(kco.w);
+                kthr = alt_keep_prep(kco);
                 kx0 = __float_as_int(r3.y) & 0xffff;
                 ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
                 kw = __float_as_int(r3.z);
@@ -157,14 +158,15 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     // before (bitwise the same sums).  Done before any lane leaves: the copy is a wave instruction.
     constexpr bool alt = ALT;
     float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
-    float kx = 0.f, ky = 0.f, kthr = 0.f;
+    float kx = 0.f, ky = 0.f;
+    AltKeep kthr{0.f, 0.f, 0.f};
     int kx0 = 0, ky0 = 0, kw = 1;
     if (alt && vis) {  // slots of tiles the binning culled (alt_tile_keep) hold no record: skip them
         const float4 r0 = g.splat[4 * (size_t)t_idx], r1 = g.splat[4 * (size_t)t_idx + 1];
         const float4 r3 = g.splat[4 * (size_t)t_idx + 3];
         kx = r0.x; ky = r0.y;
         kco = make_float4(r0.z, r0.w, r1.x, r1.y);
-        kthr = alt_keep_threshold(kco.w);
+        kthr = alt_keep_prep(kco);
         kx0 = __float_as_int(r3.y) & 0xffff;
         ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
         kw = __float_as_int(r3.z);

@@ -432,7 +432,21 @@ __device__ __forceinline__ float alt_keep_threshold(float o)
 {
     return (float)log((double)(o / (1.0f / 255.0f)));
 }
-__device__ __forceinline__ bool alt_tile_keep(float mx, float my, float4 co, float thr, int tx, int ty)
+// The per-Gaussian constants of the test, computed once per Gaussian instead of once per tile (round 5: the two IEEE
+// divisions were half of each tile's instructions): the threshold and the reciprocals 1 / (225 a), 1 / (225 c).
+struct AltKeep {
+    float thr, rcx, rcz;
+};
+__device__ __forceinline__ AltKeep alt_keep_prep(float4 co)
+{
+#pragma clang fp contract(off)
+    AltKeep k;
+    k.thr = alt_keep_threshold(co.w);
+    k.rcx = 1.0f / (225.0f * co.x);  // __frcp_rn: IEEE reciprocal
+    k.rcz = 1.0f / (225.0f * co.z);
+    return k;
+}
+__device__ __forceinline__ bool alt_tile_keep(float mx, float my, float4 co, const AltKeep& kp, int tx, int ty)
 {
 #pragma clang fp contract(off)
     const float rminx = (float)(tx * HLGS_TILE), rminy = (float)(ty * HLGS_TILE);
@@ -449,16 +463,15 @@ __device__ __forceinline__ bool alt_tile_keep(float mx, float my, float4 co, flo
         const float py = y_above * rminy + (1.0f - y_above) * rmaxy;
         const float dx = copysignf(15.0f, x_min_diff), dy = copysignf(15.0f, y_min_diff);
         const float diffx = mx - px, diffy = my - py;
-        const float rcx = 1.0f / (225.0f * co.x), rcz = 1.0f / (225.0f * co.z);  // __frcp_rn: IEEE reciprocal
-        float sx = (dx * co.x * diffx + dx * co.y * diffy) * rcx;
-        float sy = (dy * co.y * diffx + dy * co.z * diffy) * rcz;
+        float sx = (dx * co.x * diffx + dx * co.y * diffy) * kp.rcx;
+        float sy = (dy * co.y * diffx + dy * co.z * diffy) * kp.rcz;
         sx = sx != sx ? 0.0f : fminf(fmaxf(sx, 0.0f), 1.0f);  // __saturatef (NaN -> 0)
         sy = sy != sy ? 0.0f : fminf(fmaxf(sy, 0.0f), 1.0f);
         const float qx = px + not_in_y * sx * dx, qy = py + not_in_x * sy * dy;
         const float ddx = mx - qx, ddy = my - qy;
         power = 0.5f * (co.x * ddx * ddx + co.z * ddy * ddy) + co.y * ddx * ddy;
     }
-    return power <= thr;
+    return power <= kp.thr;
 }
 
 // Does the alpha >= 1/255 footprint of a splat (see quad_mask) reach the 8x8 pixel block at (qx, qy)?

@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) k_preprocess(hlgs_raster_args a, Geom g, 
     }
     if (tile_count) {  // only when the tile grid is too large for the LDS-histogram binning
         const float4 co = make_float4(conic_x, conic_y, conic_z, opacity * h_scale);
-        const float kthr = alt ? alt_keep_threshold(co.w) : 0.f;
+        const AltKeep kthr = alt ? alt_keep_prep(co) : AltKeep{0.f, 0.f, 0.f};
         uint32_t r = 0;
         for (int y = y0; y < y1; y++)
             for (int x = x0; x < x1; x++, r++)

@@ -145,7 +145,7 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int P, int gx, 
             tile_rect(v.xy.x, v.xy.y, v.ext.x, v.ext.y, gx, gy, x0, y0, x1, y1);
             uint32_t r = 0;
             if (alt) {
-                const AltKeep thr = alt_keep_prep(v.co);
+                const float thr = alt_keep_threshold(v.co.w);
                 for (int y = y0; y < y1; y++)
                     for (int x = x0; x < x1; x++, r++)
                         if (alt_tile_keep(v.xy.x, v.xy.y, v.co, thr, x, y)) f(idx, x, y, qmask(v.masks, r), v.dbits);
@@ -178,7 +178,7 @@ __device__ __forceinline__ void for_each_instance(const Geom& g, int P, int gx, 
         int ty = (int)(local / (uint32_t)w), tx = (int)local - ty * w;
         const uint32_t stop = min(iend, e);
         if (alt) {
-            const AltKeep thr = alt_keep_prep(v.co);
+            const float thr = alt_keep_threshold(v.co.w);
             for (; i < stop; i++) {
                 if (alt_tile_keep(v.xy.x, v.xy.y, v.co, thr, x0 + tx, y0 + ty))
                     f(idx, x0 + tx, y0 + ty, qmask(v.masks, i - b), v.dbits);
@@ -756,7 +756,7 @@ __global__ void __launch_bounds__(256) k_scatter_keys(int P, const int* __restri
     uint32_t* __restrict__ ents = reinterpret_cast<uint32_t*>(keys);  // entries only, as k_scatter_keys_lds
     const float4 r0 = g.splat[4 * (size_t)idx], r1 = g.splat[4 * (size_t)idx + 1];
     const float4 co = make_float4(r0.z, r0.w, r1.x, r1.y);
-    const AltKeep kthr = alt ? alt_keep_prep(co) : AltKeep{0.f, 0.f, 0.f};
+    const float kthr = alt ? alt_keep_threshold(co.w) : 0.f;
     const uint32_t masks = pack ? g.qmask[idx] : 0u;
     uint32_t r = 0;
     for (int y = y0; y < y1; y++)
@@ -1219,7 +1219,7 @@ __global__ void __launch_bounds__(256) k_relocation(int P, const float* __restri
 // LDS-histogram binning with the one-block plan: tile grids up to kBinMaxTiles and up to kPlanRun * 1024 blocks of
 // bin_gauss(P) Gaussians (67M); anything larger takes the generic per-Gaussian path.
 // Gaussians per binning block: 4,096, or 2,048 when that would leave fewer than ~200 blocks for the 256 CUs
-int bin_gauss(int P) { return P >= 200 * 4096 ? 4096 : 2048; }
+int bin_gauss(int P) { return 2048; }
 
 bool lds_binning(int P, int gx, int gy)
 {
