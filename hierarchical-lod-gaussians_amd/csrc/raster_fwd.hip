@@ -25,8 +25,9 @@ namespace hlgs {
 // ------------------------------------------------------------------------------------------------
 // s_pre[k] = exclusive prefix of tiles_touched over the block's BG Gaussians (0 past P), s_pre[BG] =
 // the block's total: thread t scans its BG / 1024 consecutive entries, then the 1024 thread totals are scanned.
-// Every binning block has 1024 threads, so a thread takes four Gaussians at 4,096 per block and two at 2,048 (round 5:
-// 512-thread blocks of 2,048 took 78 / 87 us for config #5's count / scatter, 1024-thread blocks 61 / 71 us).
+// Every binning block has 1024 threads, so a thread takes four Gaussians at 4,096 per block and one at 1,024 (round 5,
+// config #5's count / scatter: 512-thread blocks of 2,048 78 / 87 us, 1024-thread blocks of 2,048 61 / 70 us, of
+// 1,024 51 / 57 us, the plan 16 -> 22 us for the doubled histogram rows).
 // The rect sizes thread t scans (Gaussians J t .. J t + J - 1 of the block, J = BG / 1024), loaded apart from the
 // scan so that a kernel can issue them together with its other first-round loads.
 template <int BG>
@@ -1218,8 +1219,8 @@ __global__ void __launch_bounds__(256) k_relocation(int P, const float* __restri
 // ------------------------------------------------------------------------------------------------
 // LDS-histogram binning with the one-block plan: tile grids up to kBinMaxTiles and up to kPlanRun * 1024 blocks of
 // bin_gauss(P) Gaussians (67M); anything larger takes the generic per-Gaussian path.
-// Gaussians per binning block: 4,096, or 2,048 when that would leave fewer than ~200 blocks for the 256 CUs
-int bin_gauss(int P) { return P >= 200 * 4096 ? 4096 : 2048; }
+// Gaussians per binning block: 4,096, or 1,024 when 4,096 would leave fewer than ~200 blocks for the 256 CUs
+int bin_gauss(int P) { return P >= 200 * 4096 ? 4096 : 1024; }
 
 bool lds_binning(int P, int gx, int gy)
 {
@@ -1235,10 +1236,10 @@ static void allow_big_lds()
     const int dyn = 2 * (int)sizeof(uint32_t) * kBinMaxTiles;
     const hipFuncAttribute A = hipFuncAttributeMaxDynamicSharedMemorySize;
 #define HLGS_BIG(...) (void)hipFuncSetAttribute((const void*)__VA_ARGS__, A, dyn)
-    HLGS_BIG(k_count_tiles<4096, false>); HLGS_BIG(k_count_tiles<2048, false>);
-    HLGS_BIG(k_count_tiles<4096, true>); HLGS_BIG(k_count_tiles<2048, true>);
-    HLGS_BIG(k_scatter_keys_lds<4096, true>); HLGS_BIG(k_scatter_keys_lds<2048, true>);
-    HLGS_BIG(k_scatter_keys_lds<4096, false>); HLGS_BIG(k_scatter_keys_lds<2048, false>);
+    HLGS_BIG(k_count_tiles<4096, false>); HLGS_BIG(k_count_tiles<1024, false>);
+    HLGS_BIG(k_count_tiles<4096, true>); HLGS_BIG(k_count_tiles<1024, true>);
+    HLGS_BIG(k_scatter_keys_lds<4096, true>); HLGS_BIG(k_scatter_keys_lds<1024, true>);
+    HLGS_BIG(k_scatter_keys_lds<4096, false>); HLGS_BIG(k_scatter_keys_lds<1024, false>);
 #undef HLGS_BIG
     hipGetLastError();
     done = true;
@@ -1272,7 +1273,7 @@ void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, i
 #define HLGS_CNT(BG, D) hipLaunchKernelGGL((k_count_tiles<BG, D>), dim3((P + BG - 1) / BG), dim3(1024), lds, s, P, \
                                           radii, g, im.tile_count, gx, gy, (int)alt, g.scan_tmp, hist, zw, nz, im.misc)
     if (bg == 4096) { if (g.drop) HLGS_CNT(4096, true); else HLGS_CNT(4096, false); }
-    else { if (g.drop) HLGS_CNT(2048, true); else HLGS_CNT(2048, false); }
+    else { if (g.drop) HLGS_CNT(1024, true); else HLGS_CNT(1024, false); }
 #undef HLGS_CNT
     if (hist && !fused) {
         const int nb = (P + bg - 1) / bg;
@@ -1319,7 +1320,7 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
                        gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy))
         const bool pk = pack_entries(a.P);
         if (bin_gauss(a.P) == 4096) { if (pk) HLGS_SCATTER(4096, true); else HLGS_SCATTER(4096, false); }
-        else { if (pk) HLGS_SCATTER(2048, true); else HLGS_SCATTER(2048, false); }
+        else { if (pk) HLGS_SCATTER(1024, true); else HLGS_SCATTER(1024, false); }
 #undef HLGS_SCATTER
     } else
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
