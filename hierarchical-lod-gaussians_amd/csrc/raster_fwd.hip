@@ -281,6 +281,7 @@ struct HistRows {
 // loads before adding (up to 8 held in registers, so the offsets are written without a second read), and the 32 run
 // totals of a tile are scanned in LDS.  With it the binning has no device atomics and a tile's segment holds the
 // blocks' runs in block order.
+template <int K>  // histogram rows per thread held in registers: 8, or 24 for the 1,024-Gaussian blocks' longer columns
 __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hist, int nb, int T,
                                                        uint32_t* __restrict__ tile_count)
 {
@@ -288,7 +289,6 @@ __global__ void __launch_bounds__(1024) k_tile_offsets(uint32_t* __restrict__ hi
     const int c = threadIdx.x & 31, r = threadIdx.x >> 5;
     const int t = blockIdx.x * 32 + c;
     const int run = (nb + 31) / 32, b0 = r * run, b1 = min(nb, b0 + run);
-    constexpr int K = 8;
     uint32_t v[K];
     int rows[K];
     uint32_t sum = 0;
@@ -609,6 +609,7 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
 // inter-block wait (k_tile_offsets + k_plan, capi.hip replan), and the render kernels queued behind the failed plan
 // exit at once (Guard: R exceeds every capacity).  hlgs_set_plan_polls lowers the bound for the tests that force it.
 constexpr uint32_t kPlanPolls = 1u << 20;
+template <int K>  // as k_tile_offsets
 __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict__ hist, int nb, int T,
                                                             uint32_t* __restrict__ tile_count, uint2* __restrict__ ranges,
                                                             uint32_t* __restrict__ block_tot, uint64_t* flags,
@@ -624,7 +625,6 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
     const int NB = (T + 31) / 32;
     const bool last = (int)blockIdx.x == NB - 1;
     const int run = (nb + 31) / 32, b0 = r * run, b1 = min(nb, b0 + run);
-    constexpr int K = 8;
     uint32_t v[K];
     int rows[K];
     uint32_t sum = 0;
@@ -1277,7 +1277,8 @@ void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, i
 #undef HLGS_CNT
     if (hist && !fused) {
         const int nb = (P + bg - 1) / bg;
-        hipLaunchKernelGGL(k_tile_offsets, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count);
+        if (nb <= 32 * 8) hipLaunchKernelGGL(k_tile_offsets<8>, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count);
+        else hipLaunchKernelGGL(k_tile_offsets<24>, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count);
     }
 }
 
@@ -1291,8 +1292,12 @@ void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* 
     uint32_t* hist = bin_histogram(im, P, gx, gy);
     const int nb = (P + bin_gauss(P) - 1) / bin_gauss(P);
     if (hist && fused) {
-        hipLaunchKernelGGL(k_tile_offsets_plan, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count,
-                           im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, g_plan_polls);
+        if (nb <= 32 * 8)
+            hipLaunchKernelGGL(k_tile_offsets_plan<8>, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count,
+                               im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, g_plan_polls);
+        else
+            hipLaunchKernelGGL(k_tile_offsets_plan<24>, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count,
+                               im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, g_plan_polls);
         return;
     }
     uint32_t* cursor = hist ? nullptr : im.tile_cursor;
