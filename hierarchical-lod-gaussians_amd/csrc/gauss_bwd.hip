@@ -128,12 +128,18 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             }
             const uint32_t wq = (uint32_t)__shfl((int)qmasks, src, 64);
             float p[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            // the lane's tile, stepped by 64 slots at a time (divisions once per wide Gaussian, not per slot)
+            const int sy = ALT ? 64 / kw : 0, sx = ALT ? 64 - sy * kw : 0;
+            int ty = ALT ? lane / kw : 0, tx = ALT ? lane - ty * kw : 0;
             for (uint32_t r = ws + lane; r < we; r += 64) {
-                if (!rect_tile_mask(wq, r - ws)) continue;
+                const int cx = tx, cy = ty;
                 if (ALT) {
-                    const int k = (int)(r - ws);
-                    if (!alt_tile_keep(kx, ky, kco, kthr, kx0 + k % kw, ky0 + k / kw)) continue;
+                    tx += sx;
+                    ty += sy;
+                    if (tx >= kw) { tx -= kw; ty++; }
                 }
+                if (!rect_tile_mask(wq, r - ws)) continue;
+                if (ALT && !alt_tile_keep(kx, ky, kco, kthr, kx0 + cx, ky0 + cy)) continue;
                 const float4 A = rec.rec[3 * (size_t)r];
                 const float4 B = rec.rec[3 * (size_t)r + 1];
                 const float4 Cc = rec.rec[3 * (size_t)r + 2];
@@ -225,11 +231,17 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA has landed (this wave's own LDS region)
             const uint32_t r0 = max(start, c0), r1 = min(end, c1);
+            // the slot's tile, stepped along the rect's rows (one division per chunk, not two per slot)
+            int ty = 0, tx = 0;
+            if (alt && r0 < r1) {
+                ty = (int)(r0 - start) / kw;
+                tx = (int)(r0 - start) - ty * kw;
+            }
             for (uint32_t r = r0; r < r1; r++) {
                 bool use = rect_tile_mask(qmasks, r - start);
-                if (alt && use) {
-                    const int kk = (int)(r - start);
-                    use = alt_tile_keep(kx, ky, kco, kthr, kx0 + kk % kw, ky0 + kk / kw);
+                if (alt) {
+                    if (use) use = alt_tile_keep(kx, ky, kco, kthr, kx0 + tx, ky0 + ty);
+                    if (++tx == kw) { tx = 0; ty++; }
                 }
                 if (!use) continue;
                 const float4 A = buf[3 * (r - c0)], B = buf[3 * (r - c0) + 1], Cc = buf[3 * (r - c0) + 2];
