@@ -101,6 +101,22 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     // Gaussians with more than kWide record slots (rects over many tiles) are summed by their whole wave, lane-
     // strided, with a fixed butterfly at the end -- deterministic, and one wide splat no longer serialises a lane
     // over thousands of slots.  Done before any lane leaves, so every lane of the wave takes part.
+    constexpr bool alt = ALT;
+    // (loaded ahead of the wide sums: a wide Gaussian's constants come from its own lane, not from a second load)
+    float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
+    float kx = 0.f, ky = 0.f;
+    AltKeep kthr{0.f, 0.f, 0.f};
+    int kx0 = 0, ky0 = 0, kw = 1;
+    if (alt && vis) {  // slots of tiles the binning culled (alt_tile_keep) hold no record: skip them
+        const float4 r0 = g.splat[4 * (size_t)t_idx], r1 = g.splat[4 * (size_t)t_idx + 1];
+        const float4 r3 = g.splat[4 * (size_t)t_idx + 3];
+        kx = r0.x; ky = r0.y;
+        kco = make_float4(r0.z, r0.w, r1.x, r1.y);
+        kthr = alt_keep_prep(kco);
+        kx0 = __float_as_int(r3.y) & 0xffff;
+        ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
+        kw = __float_as_int(r3.z);
+    }
     constexpr uint32_t kWide = 32;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f, s8 = 0.f, s9 = 0.f;
     const uint32_t qmasks = (vis && masked) ? qraw : 0xFFFFFFFFu;
@@ -111,35 +127,33 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
             const int src = __ffsll((long long)wide) - 1;
             wide &= wide - 1;
             const uint32_t ws = (uint32_t)__shfl((int)r_start, src, 64), we = (uint32_t)__shfl((int)r_end, src, 64);
-            const int sidx = t_idx - lane + src;  // the wide Gaussian's rasterised index
-            float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
-            float kx = 0.f, ky = 0.f;
-            AltKeep kthr{0.f, 0.f, 0.f};
-            int kx0 = 0, ky0 = 0, kw = 1;
-            if (ALT) {
-                const float4 r0 = g.splat[4 * (size_t)sidx], r1 = g.splat[4 * (size_t)sidx + 1];
-                const float4 r3 = g.splat[4 * (size_t)sidx + 3];
-                kx = r0.x; ky = r0.y;
-                kco = make_float4(r0.z, r0.w, r1.x, r1.y);
-                kthr = alt_keep_prep(kco);
-                kx0 = __float_as_int(r3.y) & 0xffff;
-                ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
-                kw = __float_as_int(r3.z);
+            auto rl = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src)); };
+            float4 wco = make_float4(0.f, 0.f, 0.f, 0.f);
+            float wx = 0.f, wy = 0.f;
+            AltKeep wthr{0.f, 0.f, 0.f};
+            int wx0 = 0, wy0 = 0, ww = 1;
+            if (ALT) {  // the wide Gaussian's constants, from its lane
+                wx = rl(kx); wy = rl(ky);
+                wco = make_float4(rl(kco.x), rl(kco.y), rl(kco.z), rl(kco.w));
+                wthr = AltKeep{rl(kthr.thr), rl(kthr.rcx), rl(kthr.rcz)};
+                wx0 = __builtin_amdgcn_readlane(kx0, src);
+                wy0 = __builtin_amdgcn_readlane(ky0, src);
+                ww = __builtin_amdgcn_readlane(kw, src);
             }
             const uint32_t wq = (uint32_t)__shfl((int)qmasks, src, 64);
             float p[10] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             // the lane's tile, stepped by 64 slots at a time (divisions once per wide Gaussian, not per slot)
-            const int sy = ALT ? 64 / kw : 0, sx = ALT ? 64 - sy * kw : 0;
-            int ty = ALT ? lane / kw : 0, tx = ALT ? lane - ty * kw : 0;
+            const int sy = ALT ? 64 / ww : 0, sx = ALT ? 64 - sy * ww : 0;
+            int ty = ALT ? lane / ww : 0, tx = ALT ? lane - ty * ww : 0;
             for (uint32_t r = ws + lane; r < we; r += 64) {
                 const int cx = tx, cy = ty;
                 if (ALT) {
                     tx += sx;
                     ty += sy;
-                    if (tx >= kw) { tx -= kw; ty++; }
+                    if (tx >= ww) { tx -= ww; ty++; }
                 }
                 if (!rect_tile_mask(wq, r - ws)) continue;
-                if (ALT && !alt_tile_keep(kx, ky, kco, kthr, kx0 + cx, ky0 + cy)) continue;
+                if (ALT && !alt_tile_keep(wx, wy, wco, wthr, wx0 + cx, wy0 + cy)) continue;
                 const float4 A = rec.rec[3 * (size_t)r];
                 const float4 B = rec.rec[3 * (size_t)r + 1];
                 const float4 Cc = rec.rec[3 * (size_t)r + 2];
@@ -162,21 +176,6 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
     // LDS in chunks of kChunk records by LDS-DMA -- coalesced 1 KiB wave instructions instead of every lane reading
     // its own 48-byte records at its own address -- and each lane then sums its records from LDS, in slot order as
     // before (bitwise the same sums).  Done before any lane leaves: the copy is a wave instruction.
-    constexpr bool alt = ALT;
-    float4 kco = make_float4(0.f, 0.f, 0.f, 0.f);
-    float kx = 0.f, ky = 0.f;
-    AltKeep kthr{0.f, 0.f, 0.f};
-    int kx0 = 0, ky0 = 0, kw = 1;
-    if (alt && vis) {  // slots of tiles the binning culled (alt_tile_keep) hold no record: skip them
-        const float4 r0 = g.splat[4 * (size_t)t_idx], r1 = g.splat[4 * (size_t)t_idx + 1];
-        const float4 r3 = g.splat[4 * (size_t)t_idx + 3];
-        kx = r0.x; ky = r0.y;
-        kco = make_float4(r0.z, r0.w, r1.x, r1.y);
-        kthr = alt_keep_prep(kco);
-        kx0 = __float_as_int(r3.y) & 0xffff;
-        ky0 = (int)((uint32_t)__float_as_int(r3.y) >> 16);
-        kw = __float_as_int(r3.z);
-    }
     const uint32_t start = r_start, end = vis && r_end - r_start > kWide ? r_start : r_end;  // narrow range
     // per-Gaussian inputs of the covariance / projection backward, issued ahead of the record sums so their latency
     // overlaps them
