@@ -623,6 +623,36 @@ def bench_config4_dp(P, deg, W, H, dev, rank, world, steps, warmup, backend):
     return out
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` run without a launcher: the same command under torch.distributed.run with N ranks on this
+    node (rendezvous on 127.0.0.1, a free port), as a child process -- never an exec, and before any GPU call in this
+    process.  Returns the child's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] --gpus {n} without WORLD_SIZE: launching {n} ranks", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def dry_run(world, rank, backend, args):
+    """--dry-run: join the process group (when world > 1), agree on the world size with one collective, and have
+    rank 0 print the line's rank fields; no GPU work (the CPU test of the launch path, tests/test_bench_cpu.py)."""
+    seen = world
+    if world > 1:
+        dist.init_process_group(backend)
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": seen, "gpus_arg": args.gpus,
+                          "backend": backend if world > 1 else None}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -638,16 +668,29 @@ def main():
     ap.add_argument("--settle-max", type=int, default=200,
                     help="at most this many untimed steps before the timed ones, until the step time stops falling "
                          "(the core clock's ramp under load); 0: none")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and join the ranks, print the line's rank fields, run no GPU work (launcher test)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # --gpus N without a launcher: start N ranks as a child process (before anything touches the GPU) and exit
+        # with its code, so the command cannot silently measure one rank
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU "
+                 f"(torch.distributed.run --nproc-per-node {args.gpus}) or pass --gpus {world}")
     if os.environ.get("HLGS_BENCH_MEM"):
         _mem_watchdog()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # HLGS_DIST_BACKEND=gloo with more ranks than GPUs rehearses the multi-rank path on a one-GPU box (ranks share
     # the card); the driver's N-GPU runs use the default, RCCL ("nccl"), one rank per GPU.
     backend = os.environ.get("HLGS_DIST_BACKEND", "nccl")
+    if args.dry_run:
+        return dry_run(world, rank, backend, args)
     gpu = local % max(1, torch.cuda.device_count()) if world > 1 else 0
     if world > 1:
         torch.cuda.set_device(gpu)
