@@ -6,6 +6,7 @@
 // Re-entrancy: no device memory is allocated here and no scratch is static; every buffer is passed
 // in.  The only process-wide state is the opt-in stage-timing instrumentation used by bench.py.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <stdio.h>
 #include <string.h>
@@ -16,15 +17,24 @@
 #include "hlgs_internal.h"
 
 namespace hlgs {
-int g_entry_packing = 1;  // hlgs_set_entry_packing
-int g_drop_empty = 1;     // hlgs_set_drop_empty
-extern uint32_t g_plan_polls;  // hlgs_set_plan_polls (raster_fwd.hip)
-bool pack_entries(int P) { return g_entry_packing && P < (1 << (32 - kEntryShift)); }
-bool drop_empty(int P) { return g_drop_empty && pack_entries(P); }
+// The process-wide test switches, read once per frame (frame_opts) and never inside one.
+static std::atomic<int> g_entry_packing{1};       // hlgs_set_entry_packing
+static std::atomic<int> g_drop_empty{1};          // hlgs_set_drop_empty
+static std::atomic<uint32_t> g_plan_polls{kPlanPolls};  // hlgs_set_plan_polls
+bool pack_entries(int P) { return g_entry_packing.load(std::memory_order_relaxed) && P < (1 << (32 - kEntryShift)); }
+bool drop_empty(int P) { return g_drop_empty.load(std::memory_order_relaxed) && pack_entries(P); }
+FrameOpts frame_opts(int P)
+{
+    FrameOpts o;
+    o.pack = pack_entries(P) ? 1 : 0;
+    o.drop = o.pack && g_drop_empty.load(std::memory_order_relaxed) ? 1 : 0;
+    o.polls = g_plan_polls.load(std::memory_order_relaxed);
+    return o;
+}
 void launch_preprocess(const hlgs_raster_args& a, const Geom& g, int* radii, uint32_t* tile_count, int gx, int gy,
                        const ZeroJob& z,
                        hipStream_t s);
-void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s);
+void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, uint32_t flags, hipStream_t s);
 void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s,
                  bool fused);
 bool lds_binning(int P, int gx, int gy);
@@ -94,7 +104,7 @@ static T* take(char*& p, size_t count)
     return r;
 }
 
-Geom carve_geom(void* base, int P, size_t* total)
+Geom carve_geom(void* base, int P, size_t* total, const FrameOpts& o)
 {
     char* p = static_cast<char*>(base);
     Geom g;
@@ -108,8 +118,9 @@ Geom carve_geom(void* base, int P, size_t* total)
     g.splat = take<float4>(p, 4 * (size_t)P);
     g.sh_jac = take<float>(p, 9 * (size_t)P);
     g.qmask = take<uint32_t>(p, (size_t)P);
-    g.pack = pack_entries(P) ? 1 : 0;
-    g.drop = drop_empty(P) ? 1 : 0;
+    g.pack = o.pack;
+    g.drop = o.drop;
+    g.polls = o.polls;
     g.scan_tmp = take<uint32_t>(p, scan_scratch_elems(P));
     if (total) *total = (size_t)(p - static_cast<char*>(base));
     return g;
@@ -279,9 +290,9 @@ size_t hlgs_backward_scratch_size(int P, int R)
 
 static void* aligned(const void* p) { return (void*)align_up((size_t)p); }
 
-void hlgs_set_entry_packing(int on) { g_entry_packing = on ? 1 : 0; }
-void hlgs_set_drop_empty(int on) { g_drop_empty = on ? 1 : 0; }
-void hlgs_set_plan_polls(unsigned polls) { g_plan_polls = polls; }
+void hlgs_set_entry_packing(int on) { g_entry_packing.store(on ? 1 : 0, std::memory_order_relaxed); }
+void hlgs_set_drop_empty(int on) { g_drop_empty.store(on ? 1 : 0, std::memory_order_relaxed); }
+void hlgs_set_plan_polls(unsigned polls) { g_plan_polls.store(polls, std::memory_order_relaxed); }
 int hlgs_point_list_entry_shift(int P) { return pack_entries(P) ? kEntryShift : 0; }
 int hlgs_point_list_drops_empty(int P) { return drop_empty(P) ? 1 : 0; }
 
@@ -289,6 +300,11 @@ size_t hlgs_binning_point_list_offset(int R)
 {
     Bin b = carve_bin(nullptr, R < 0 ? 0 : R, nullptr);
     return (size_t)b.point_list;
+}
+size_t hlgs_image_misc_offset(int W, int H)
+{
+    Img im = carve_img(nullptr, W, H, nullptr);
+    return (size_t)im.misc;
 }
 size_t hlgs_geom_splat_offset(int P)
 {
@@ -302,14 +318,20 @@ size_t hlgs_image_ranges_offset(int W, int H)
 }
 
 namespace hlgs {
+static bool pack_entries_fit(int P) { return P < (1 << (32 - kEntryShift)); }
+static void set_frame_flags(hlgs_frame_info* info, const FrameOpts& o)
+{
+    info->entry_shift = o.pack ? kEntryShift : 0;
+    info->drops_empty = o.drop;
+}
 // Phase 1: preprocess, tile counts, scans, tile ranges (misc = R, longest list, record slots).  With LDS-histogram
 // binning the preprocess also clears tile_count and `seen`, and one k_plan block does both scans and the ranges and
 // mirrors misc into `host` (pinned, may be null); otherwise the generic path runs device-wide scans.
-static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int* radii, int* seen, uint32_t* host,
-                          uint32_t seq, hipStream_t s, bool fused = true)
+static int prepare_launch(const hlgs_raster_args* a, const FrameOpts& o, void* geom, void* img, int* radii, int* seen,
+                          uint32_t* host, uint32_t seq, hipStream_t s, bool fused = true)
 {
     const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16, T = gx * gy;
-    Geom g = carve_geom(aligned(geom), a->P, nullptr);
+    Geom g = carve_geom(aligned(geom), a->P, nullptr, o);
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     hipGetLastError();
     const bool lds_bins = lds_binning(a->P, gx, gy);
@@ -340,7 +362,7 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
     stage_mark(s, ST_SCAN, false);
     stage_mark(s, ST_RANGES, true);
     scan_inclusive_u32(im.tile_count, im.tile_cursor, (size_t)T, im.scan_tmp, s);
-    launch_tile_ranges(im, T, g.point_offsets, a->P, s);
+    launch_tile_ranges(im, T, g.point_offsets, a->P, o.flags(), s);
     stage_mark(s, ST_RANGES, false);
     if ((rc = check_stage(s, a->debug, "scan"))) return rc;
     if (host) HLGS_TRY_HIP(hipMemcpyAsync(host, im.misc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -350,11 +372,11 @@ static int prepare_launch(const hlgs_raster_args* a, void* geom, void* img, int*
 // The binning plan again with the two launches that need no inter-block wait (k_tile_offsets + k_plan), for a frame
 // whose fused plan reported a timed-out look-back (k_tile_offsets_plan: R = ~0u).  The preprocess outputs are intact;
 // the count kernel rewrites the histogram rows the failed plan had partly turned into offsets.
-static int replan_launch(const hlgs_raster_args* a, void* geom, void* img, const int* radii, uint32_t* host,
-                         uint32_t seq, hipStream_t s)
+static int replan_launch(const hlgs_raster_args* a, const FrameOpts& o, void* geom, void* img, const int* radii,
+                         uint32_t* host, uint32_t seq, hipStream_t s)
 {
     const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16;
-    Geom g = carve_geom(aligned(geom), a->P, nullptr);
+    Geom g = carve_geom(aligned(geom), a->P, nullptr, o);
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     hipGetLastError();
     launch_count_tiles(a->P, radii, g, im, gx, gy, a->variant == HLGS_VARIANT_ALT, s, bin_histogram(im, a->P, gx, gy),
@@ -363,11 +385,12 @@ static int replan_launch(const hlgs_raster_args* a, void* geom, void* img, const
     return check_stage(s, a->debug, "re-plan");
 }
 
-static int render_launch(const hlgs_raster_args* a, const int* radii, void* geom, void* img, void* binning, int R_carve,
-                         uint32_t max_count, float* out_color, float* out_invdepth, int* seen, hipStream_t s, Guard gd)
+static int render_launch(const hlgs_raster_args* a, const FrameOpts& o, const int* radii, void* geom, void* img,
+                         void* binning, int R_carve, uint32_t max_count, float* out_color, float* out_invdepth, int* seen,
+                         hipStream_t s, Guard gd)
 {
     const int gx = (a->W + 15) / 16, gy = (a->H + 15) / 16;
-    Geom g = carve_geom(aligned(geom), a->P, nullptr);
+    Geom g = carve_geom(aligned(geom), a->P, nullptr, o);
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     Bin b = carve_bin(aligned(binning), R_carve, nullptr);
     hipGetLastError();
@@ -445,15 +468,17 @@ int hlgs_rasterize_forward_prepare(const hlgs_raster_args* a, void* geom, void* 
     info->max_tile_count = 0;
     info->rendered = 0;
     info->num_binned = 0;
+    const FrameOpts o = frame_opts(a->P);  // the frame's options, handed to _render through *info
+    set_frame_flags(info, o);
     if (a->P == 0) return HLGS_OK;
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = prepare_launch(a, geom, img, radii, nullptr, nullptr, 0u, s))) return rc;
+    if ((rc = prepare_launch(a, o, geom, img, radii, nullptr, nullptr, 0u, s))) return rc;
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     uint32_t misc[3];
     HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
     HLGS_TRY_HIP(hipStreamSynchronize(s));
     if (misc[0] == ~0u) {  // the fused plan's look-back timed out: plan again without inter-block waits
-        if ((rc = replan_launch(a, geom, img, radii, nullptr, 0u, s))) return rc;
+        if ((rc = replan_launch(a, o, geom, img, radii, nullptr, 0u, s))) return rc;
         HLGS_TRY_HIP(hipMemcpyAsync(misc, im.misc, sizeof(misc), hipMemcpyDeviceToHost, s));
         HLGS_TRY_HIP(hipStreamSynchronize(s));
         if (misc[0] == ~0u) return fail(HLGS_ERR_DEVICE, "the binning plan failed twice");
@@ -474,7 +499,13 @@ int hlgs_rasterize_forward_render(const hlgs_raster_args* a, const int* radii, v
     if (a->P == 0) return HLGS_OK;
     // rasterizer_impl.cu:332-333: the hierarchy rasterizer's output stays 0; the alt rasterizer blends anyway (bg)
     if (R == 0 && a->variant != HLGS_VARIANT_ALT) return HLGS_OK;
-    return render_launch(a, radii, geom, img, binning, R, (uint32_t)info->max_tile_count, out_color, out_invdepth,
+    FrameOpts o = frame_opts(a->P);  // the options _prepare ran with (info), not the switches' state now
+    o.pack = info->entry_shift == kEntryShift ? 1 : 0;
+    o.drop = info->drops_empty ? 1 : 0;
+    if ((info->entry_shift != 0 && info->entry_shift != kEntryShift) || (o.pack && !pack_entries_fit(a->P)) ||
+        (o.drop && !o.pack))
+        return fail(HLGS_ERR_ARG, "hlgs_frame_info does not come from hlgs_rasterize_forward_prepare of this frame");
+    return render_launch(a, o, radii, geom, img, binning, R, (uint32_t)info->max_tile_count, out_color, out_invdepth,
                          seen, (hipStream_t)stream, Guard{nullptr, 0u, 0u});
 }
 
@@ -488,6 +519,8 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     info->max_tile_count = 0;
     info->rendered = 0;
     info->num_binned = 0;
+    const FrameOpts o = frame_opts(a->P);  // read once: every launch of this frame uses these
+    set_frame_flags(info, o);
     hipStream_t s = (hipStream_t)stream;
     hipGetLastError();
     const size_t HW = (size_t)a->W * a->H;
@@ -502,7 +535,7 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     if ((rc = readback_for(s, &rb))) return rc;
     if (++rb->seq == 0u) rb->seq = 1u;
     const uint32_t seq = rb->seq;
-    if ((rc = prepare_launch(a, geom, img, radii, seen, rb->host, seq, s))) return rc;
+    if ((rc = prepare_launch(a, o, geom, img, radii, seen, rb->host, seq, s))) return rc;
     Img im = carve_img(aligned(img), a->W, a->H, nullptr);
     // the LDS-binning plan (k_plan) mirrors its words with the sequence number; the generic path copies them
     const bool polled = lds_binning(a->P, (a->W + 15) / 16, (a->H + 15) / 16);
@@ -513,7 +546,7 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     const bool spec = capR > 0;
     // the queued sorts are the ones the previous frame's longest list needed
     const uint32_t cap_n = rb->last_maxc <= (uint32_t)kWaveSortCap ? (uint32_t)kWaveSortCap : (uint32_t)kSortCap;
-    if (spec && (rc = render_launch(a, radii, geom, img, binning, capR, cap_n, out_color, out_invdepth, seen, s,
+    if (spec && (rc = render_launch(a, o, radii, geom, img, binning, capR, cap_n, out_color, out_invdepth, seen, s,
                                     Guard{im.misc, (uint32_t)capR, cap_n})))
         return rc;
     uint32_t words[3];
@@ -528,7 +561,7 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
         // The fused plan's look-back timed out (k_tile_offsets_plan): the speculative render exited at once (R exceeds
         // every capacity); plan again with the two launches that need no inter-block wait, then render.
         if (++rb->seq == 0u) rb->seq = 1u;
-        if ((rc = replan_launch(a, geom, img, radii, rb->host, rb->seq, s))) return rc;
+        if ((rc = replan_launch(a, o, geom, img, radii, rb->host, rb->seq, s))) return rc;
         if ((rc = wait_plan_words(rb->host, rb->seq, s, words))) return rc;
         if (words[0] == ~0u) return fail(HLGS_ERR_DEVICE, "the binning plan failed twice");
         replanned = true;
@@ -546,7 +579,7 @@ int hlgs_rasterize_forward(const hlgs_raster_args* a, void* geom, void* img, int
     }
     if (R > (uint32_t)capR) return HLGS_OK;  // caller allocates hlgs_binning_buffer_size(R), calls _render
     if (!spec || maxc > cap_n || replanned) {
-        if ((rc = render_launch(a, radii, geom, img, binning, capR, maxc, out_color, out_invdepth, seen, s,
+        if ((rc = render_launch(a, o, radii, geom, img, binning, capR, maxc, out_color, out_invdepth, seen, s,
                                 Guard{nullptr, 0u, 0u})))
             return rc;
     }

@@ -13,7 +13,7 @@ constexpr int kSortCap = 4096;      // largest per-tile list sorted in one LDS p
 constexpr int kWaveSortCap = 1024;  // longest per-tile list sorted in registers by one wave
 constexpr size_t kAlign = 256;
 
-// Gaussians per binning block: 4,096 or 2,048 chosen per launch (raster_fwd.hip bin_gauss); threads = Gaussians / 4
+// Gaussians per binning block: 4,096 or 1,024 chosen per launch (raster_fwd.hip bin_gauss), on 1,024 threads
 constexpr int kBinMaxTiles = 16384; // tile grids up to this use LDS histograms (2 x 64 KiB)
 
 // The blend backward splits each tile's list into up to kBwdSplits + 1 chunks of bwd_chunk_len(count) entries (a
@@ -49,8 +49,9 @@ struct Geom {
     float4* splat;            // P x 4: the blend kernels' per-Gaussian record (see SplatRec)
     uint32_t* qmask;          // P: footprint quadrant masks of the first rect tiles (rect_quad_masks), written by the
                               // preprocess for the visible Gaussians when pack_entries; read by the key scatter
-    int pack;                 // pack_entries(P) of the frame this buffer is carved for
-    int drop;                 // drop_empty(P): instances whose quadrant mask is 0 are not binned
+    int pack;                 // FrameOpts::pack of the frame this buffer is carved for (0 when carved without options)
+    int drop;                 // FrameOpts::drop: instances whose quadrant mask is 0 are not binned
+    uint32_t polls;           // FrameOpts::polls: bound on each look-back poll of the fused plan
     float* sh_jac;            // P x 9: d colour / d view direction (dRGBdx, dRGBdy, dRGBdz), written by k_preprocess_sh
                               // for the visible Gaussians when sh_jac_written(); the SH backward then reads no SH rows
     uint32_t* scan_tmp;
@@ -72,12 +73,14 @@ bool lds_binning(int P, int gx, int gy);
 // 8x8 quadrant q of the tile (quad_mask), decided once by the key scatter so that the blends read it instead of
 // testing the footprint in every quadrant wave.  Otherwise the entry is idx and the blends test it themselves.
 // The low bits do not change the sort order: within a tile the (depth, idx) pairs are already distinct.
-// pack_entries(P) is decided on the host (capi.hip; hlgs_set_entry_packing turns it off for tests) and reaches the
-// kernels as Geom::pack / their pack argument.
+// pack_entries(P) is decided on the host (capi.hip; hlgs_set_entry_packing turns it off for tests), once per frame
+// (FrameOpts), and reaches the kernels as Geom::pack / their flags argument.
 constexpr int kEntryShift = 4;
-constexpr int kMiscPack = 3;  // Img::misc word holding the frame's pack_entries(P)
+constexpr int kMiscPack = 3;  // Img::misc word holding the frame's FrameOpts::pack
+constexpr int kMiscDrop = 4;  // Img::misc word holding the frame's FrameOpts::drop
 constexpr int kMiscFail = 5;  // Img::misc word: a block of the fused plan timed out in its look-back (k_tile_offsets_plan)
 constexpr int kMiscDone = 6;  // Img::misc word: blocks of the fused plan done with their ranges
+constexpr uint32_t kPlanPolls = 1u << 20;  // default bound on each look-back poll of the fused plan (~0.1 s)
 // drop_empty(P): with packed entries, an instance whose quadrant mask is 0 (its footprint reaches none of the tile's
 // four 8x8 quadrants, so no pixel of the tile blends it) is not binned: the tile lists, the sort and the blends' staging
 // skip it.  Its record slot stays (point_offsets and num_rendered are unchanged) and is never written; k_gauss_bwd
@@ -88,13 +91,23 @@ constexpr int kMiscDone = 6;  // Img::misc word: blocks of the fused plan done w
 // waits until all three carry it and the kernel needs no system-scope release (a write-back of the whole L2).
 bool pack_entries(int P);
 bool drop_empty(int P);
+// The frame's binning options, read once from the process-wide test switches (atomics, hlgs_set_entry_packing /
+// hlgs_set_drop_empty / hlgs_set_plan_polls) when the frame starts; nothing inside a frame reads the switches again,
+// so a thread that flips one while another renders changes only later frames.  The plan kernels write pack and drop
+// into Img::misc[kMiscPack], [kMiscDrop] and the host reports them in hlgs_frame_info (entry_shift, drops_empty).
+struct FrameOpts {
+    int pack = 0, drop = 0;
+    uint32_t polls = 0;
+    uint32_t flags() const { return (uint32_t)pack | (uint32_t)drop << 1; }  // the plan kernels' flags argument
+};
+FrameOpts frame_opts(int P);
 // Does the forward's preprocess (k_preprocess_sh2) leave Geom::sh_jac for the SH backward?  Same condition as its launch.
 inline bool sh_jac_written(const hlgs_raster_args& a)
 {
     const int gx = (a.W + 15) / 16, gy = (a.H + 15) / 16;
     return !a.indices && !a.colors_precomp && a.shs && a.M > 0 && a.M <= 16 && lds_binning(a.P, gx, gy);
 }
-Geom carve_geom(void* base, int P, size_t* total);
+Geom carve_geom(void* base, int P, size_t* total, const FrameOpts& o = FrameOpts());
 
 // Per-pixel / per-tile state (ImageState, rasterizer_impl.h:47-54) plus binning counters.
 struct Img {
@@ -104,7 +117,7 @@ struct Img {
     uint32_t* tile_count;  // T
     uint32_t* tile_cursor; // T
     uint32_t* misc;        // 16: [0] = binned instances, [1] = longest per-tile list, [2] = record slots (point_offsets[P-1]),
-                           // [kMiscPack] = the frame's pack_entries(P), read by the backward (not the process-wide switch),
+                           // [kMiscPack], [kMiscDrop] = the frame's FrameOpts (the backward reads pack here, not a switch),
                            // [kMiscFail], [kMiscDone]: the fused plan's failure and completion words
     uint32_t* scan_tmp;
     float* split_state;    // T x kBwdSplits x kSplitFloats (see bwd_chunk_len)

@@ -20,7 +20,7 @@
 // every per-pixel value -- the SSIM map, the A, B, C maps, the gradient -- is bit-identical to it; only the
 // workgroup partial sums of the loss are added in another grouping.  Round 4 staged both images with the halo in LDS
 // and ran the horizontal pass over all 18 rows of each 64 x 8 tile (2.25 horizontal passes per output) and the
-// vertical pass from LDS: 103 us forward and 85 us backward at 3 x 1080 x 1920 (tools/variants/loss_r04.hip).
+// vertical pass from LDS: 103 us forward and 85 us backward at 3 x 1080 x 1920 (loss_r04.hip, tools/variants/INDEX.md).
 // The forward writes the partial derivatives of the SSIM map with respect to the window means
 //   A = df/dmu1 (total), B = df/d E[x^2], C = df/d E[x y]
 // so that dSSIM/dx(p) = sum_q g(q) w(q - p) (A(q) + 2 x(p) B(q) + y(p) C(q)), which the backward evaluates with

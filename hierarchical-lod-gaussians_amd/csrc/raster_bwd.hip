@@ -12,8 +12,8 @@
 //
 // The measured variants of rounds 1-5 (two splats per reduction, opacity-uniform clamp branches, packed moments,
 // Newton reciprocals, tile-major chunk order, non-temporal loads and stores, the traffic-attribution builds, and round
-// 5's 4x4 sub-block lists) live outside the product source in tools/variants/ (raster_bwd_r04.hip, raster_bwd_sub4.hip),
-// built for A/B by tools/build_variant.py; DESIGN.md section 5 records each result.
+// 5's 4x4 sub-block lists) live outside the product source, in git history (tools/variants/INDEX.md: raster_bwd_r04.hip,
+// raster_bwd_sub4.hip), built for A/B by tools/build_variant.py; DESIGN.md section 5 records each result.
 #include "hlgs_internal.h"
 #include "hlgs_math.h"
 
@@ -174,8 +174,8 @@ struct BwdArgs {
 // 64-splat batch is staged in LDS; per splat, the quadrants its footprint reaches (and that still hold a pixel
 // whose n_contrib lies behind it) run bwd_pass, the ten moments are folded over the wave, and one record per
 // (tile, splat) is stored after the batch.
-// Round 5 measured 4x4 sub-block lists per 16-lane row here instead of 8x8 quadrant passes (tools/variants/
-// raster_bwd_sub4.hip): 61% of the pass lanes busy instead of 36%, but 697 against 354 us -- the per-row splat
+// Round 5 measured 4x4 sub-block lists per 16-lane row here instead of 8x8 quadrant passes (raster_bwd_sub4.hip,
+// tools/variants/INDEX.md): 61% of the pass lanes busy instead of 36%, but 697 against 354 us -- the per-row splat
 // indices put six LDS round trips and an LDS float atomic on every iteration, and the LDS became the limit (SQ_LDS_IDX_ACTIVE
 // 5.7x, SQ_WAIT_INST_LDS 256x); DESIGN.md section 5.
 constexpr int kMStride = 65;  // moment rows padded to 65 floats (see s_m below)

@@ -471,10 +471,11 @@ __global__ void __launch_bounds__(1024) k_scatter_keys_lds(int P, const int* __r
 
 // ranges[t] = [incl[t] - count[t], incl[t]); misc[0] = R, misc[1] = max count; cursor reset for the scatter.
 // misc[2] = point_offsets[P - 1]: instances over all tile rects (record slots; == misc[0] unless culled).
-// misc[3] = pack_entries(P) of this frame (kMiscPack), so the backward decodes the lists as they were written.
+// misc[kMiscPack], misc[kMiscDrop] = the frame's FrameOpts (flags = pack | drop << 1), so the backward decodes the lists
+// as they were written and a caller can read which binning the frame used.
 __global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict__ count, uint32_t* incl_and_cursor,
                                                      uint2* __restrict__ ranges, uint32_t* __restrict__ misc, int T,
-                                                     const uint32_t* __restrict__ point_offsets, int P, uint32_t pack)
+                                                     const uint32_t* __restrict__ point_offsets, int P, uint32_t flags)
 {
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t >= T) return;
@@ -484,7 +485,8 @@ __global__ void __launch_bounds__(256) k_tile_ranges(const uint32_t* __restrict_
     if (t == T - 1) {
         misc[0] = e;
         misc[2] = P > 0 ? point_offsets[P - 1] : 0u;
-        misc[kMiscPack] = pack;
+        misc[kMiscPack] = flags & 1u;
+        misc[kMiscDrop] = flags >> 1;
     }
     if (c) atomicMax(&misc[1], c);
 }
@@ -564,7 +566,7 @@ __device__ __forceinline__ void plan_host_words(uint32_t* host, uint32_t seq, ui
 __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot, int nb,
                                                const uint32_t* __restrict__ count, uint32_t* __restrict__ cursor,
                                                uint2* __restrict__ ranges, int T, uint32_t* __restrict__ misc,
-                                               uint32_t* host, uint32_t seq, uint32_t pack)
+                                               uint32_t* host, uint32_t seq, uint32_t flags)
 {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_max;
@@ -585,7 +587,8 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
         misc[0] = R;
         misc[1] = s_max;
         misc[2] = slots;
-        misc[kMiscPack] = pack;
+        misc[kMiscPack] = flags & 1u;
+        misc[kMiscDrop] = flags >> 1;
         // the host polls these words instead of putting an event (a queue barrier) here: three 64-bit words, each
         // carrying the frame's sequence number in its high half, written by single-copy-atomic stores, so the host
         // waits until all three carry it and the kernel needs no system-scope release to order them
@@ -608,12 +611,11 @@ __global__ void __launch_bounds__(1024) k_plan(uint32_t* __restrict__ block_tot,
 // any block failed (or the wait itself timed out).  The host then re-plans the frame with the two launches that need no
 // inter-block wait (k_tile_offsets + k_plan, capi.hip replan), and the render kernels queued behind the failed plan
 // exit at once (Guard: R exceeds every capacity).  hlgs_set_plan_polls lowers the bound for the tests that force it.
-constexpr uint32_t kPlanPolls = 1u << 20;
 template <int K>  // as k_tile_offsets
 __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict__ hist, int nb, int T,
                                                             uint32_t* __restrict__ tile_count, uint2* __restrict__ ranges,
                                                             uint32_t* __restrict__ block_tot, uint64_t* flags,
-                                                            uint32_t* misc, uint32_t* host, uint32_t seq, uint32_t pack,
+                                                            uint32_t* misc, uint32_t* host, uint32_t seq, uint32_t fopts,
                                                             uint32_t polls)
 {
     __shared__ uint32_t s_part[32][33];
@@ -736,7 +738,8 @@ __global__ void __launch_bounds__(1024) k_tile_offsets_plan(uint32_t* __restrict
         misc[0] = R;
         misc[1] = mx;
         misc[2] = slots;
-        misc[kMiscPack] = pack;
+        misc[kMiscPack] = fopts & 1u;
+        misc[kMiscDrop] = fopts >> 1;
         if (host) plan_host_words(host, seq, R, mx, slots);
     }
 }
@@ -1022,7 +1025,7 @@ struct FwdArgs {
 // reads hit the same L2.  Each 64-splat batch is staged in LDS; a ballot builds the wave-uniform bit
 // set of the batch's splats whose alpha >= 1/255 footprint reaches this quadrant, and only those are
 // visited (scalar find-first-set loop).  Skipped pairs are exactly the ones the reference discards.
-// Round 5 measured per-row 4x4 sub-block lists instead (tools/variants/raster_fwd_sub4.hip): a third fewer
+// Round 5 measured per-row 4x4 sub-block lists instead (raster_fwd_sub4.hip, tools/variants/INDEX.md): a third fewer
 // iterations, but 209 against 151 us -- per-lane LDS addresses and the row bookkeeping cost more VALU than the
 // iterations saved.
 // ------------------------------------------------------------------------------------------------
@@ -1219,8 +1222,11 @@ __global__ void __launch_bounds__(256) k_relocation(int P, const float* __restri
 // ------------------------------------------------------------------------------------------------
 // LDS-histogram binning with the one-block plan: tile grids up to kBinMaxTiles and up to kPlanRun * 1024 blocks of
 // bin_gauss(P) Gaussians (67M); anything larger takes the generic per-Gaussian path.
-// Gaussians per binning block: 4,096, or 1,024 when 4,096 would leave fewer than ~200 blocks for the 256 CUs
-int bin_gauss(int P) { return P >= 200 * 4096 ? 4096 : 1024; }
+// Gaussians per binning block: 4,096, or 1,024 when 4,096 would leave fewer than ~200 blocks for the 256 CUs.  The
+// switch sits at 768 blocks of 1,024 (786,432 Gaussians), the most the register runs of k_tile_offsets<24> /
+// k_tile_offsets_plan<24> hold (ceil(nb / 32) <= 24); above it 4,096 gives >= 193 blocks (at 200 x 4,096
+// the frames of 786,433-819,199 Gaussians took the serial per-row fallback).
+int bin_gauss(int P) { return P > 768 * 1024 ? 4096 : 1024; }
 
 bool lds_binning(int P, int gx, int gy)
 {
@@ -1282,8 +1288,6 @@ void launch_count_tiles(int P, const int* radii, const Geom& g, const Img& im, i
     }
 }
 
-uint32_t g_plan_polls = kPlanPolls;  // hlgs_set_plan_polls (tests)
-
 void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* host, uint32_t seq, hipStream_t s,
                  bool fused)
 {
@@ -1294,21 +1298,21 @@ void launch_plan(int P, const Geom& g, const Img& im, int gx, int gy, uint32_t* 
     if (hist && fused) {
         if (nb <= 32 * 8)
             hipLaunchKernelGGL(k_tile_offsets_plan<8>, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count,
-                               im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, g_plan_polls);
+                               im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, FrameOpts{g.pack, g.drop, 0}.flags(), g.polls);
         else
             hipLaunchKernelGGL(k_tile_offsets_plan<24>, dim3((T + 31) / 32), dim3(1024), 0, s, hist, nb, T, im.tile_count,
-                               im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, (uint32_t)g.pack, g_plan_polls);
+                               im.ranges, g.scan_tmp, plan_flags(im), im.misc, host, seq, FrameOpts{g.pack, g.drop, 0}.flags(), g.polls);
         return;
     }
     uint32_t* cursor = hist ? nullptr : im.tile_cursor;
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, g.scan_tmp, nb, im.tile_count, cursor, im.ranges, T, im.misc,
-                       host, seq, (uint32_t)g.pack);
+                       host, seq, FrameOpts{g.pack, g.drop, 0}.flags());
 }
 
-void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, hipStream_t s)
+void launch_tile_ranges(const Img& im, int T, const uint32_t* point_offsets, int P, uint32_t flags, hipStream_t s)
 {
     hipLaunchKernelGGL(k_tile_ranges, dim3((T + 255) / 256), dim3(256), 0, s, im.tile_count, im.tile_cursor,
-                       im.ranges, im.misc, T, point_offsets, P, (uint32_t)pack_entries(P));
+                       im.ranges, im.misc, T, point_offsets, P, flags);
 }
 
 void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, const Img& im, const Bin& b,
@@ -1323,15 +1327,15 @@ void launch_binning(const hlgs_raster_args& a, const int* radii, const Geom& g, 
     hipLaunchKernelGGL((k_scatter_keys_lds<BG, PK>), dim3((a.P + BG - 1) / BG), dim3(1024),                           \
                        2 * sizeof(uint32_t) * (size_t)T, s, a.P, radii, g, im.ranges, im.tile_cursor, b.keys, gx, gy, alt, \
                        gd, g.scan_tmp, bin_histogram(im, a.P, gx, gy))
-        const bool pk = pack_entries(a.P);
+        const bool pk = g.pack;
         if (bin_gauss(a.P) == 4096) { if (pk) HLGS_SCATTER(4096, true); else HLGS_SCATTER(4096, false); }
         else { if (pk) HLGS_SCATTER(1024, true); else HLGS_SCATTER(1024, false); }
 #undef HLGS_SCATTER
     } else
         hipLaunchKernelGGL(k_scatter_keys, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii, g, im.ranges,
-                           im.tile_cursor, b.keys, gx, gy, alt, gd, (int)pack_entries(a.P));
+                           im.tile_cursor, b.keys, gx, gy, alt, gd, g.pack);
     if (timing) { stage_mark(s, 3, false); stage_mark(s, 4, true); }
-    const KeySrc ks{reinterpret_cast<const uint32_t*>(b.keys), g.depths, (int)pack_entries(a.P)};
+    const KeySrc ks{reinterpret_cast<const uint32_t*>(b.keys), g.depths, g.pack};
     hipLaunchKernelGGL(k_tile_sort_wave, dim3(T), dim3(64), 0, s, im.ranges, ks, b.point_list, T, gd);
     if (max_count > (uint32_t)kWaveSortCap)
         hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, im.ranges, ks, b.keys2, b.point_list, T, gd);
@@ -1355,7 +1359,7 @@ void launch_blend_fwd(const hlgs_raster_args& a, const Geom& g, const Img& im, c
     const bool interp = a.ts != nullptr && a.kids != nullptr;
     const bool depth = out_invdepth != nullptr;
     FwdArgs A{im.ranges, b.point_list, a.W, a.H, gx, T, g.splat, im.final_T, im.n_contrib, a.bg, out_color,
-              out_invdepth, seen, im.split_state, (int)pack_entries(a.P)};
+              out_invdepth, seen, im.split_state, g.pack};
 #define HLGS_BLEND(I, Dp)                                                                                         \
     do {                                                                                                          \
         if (seen) hipLaunchKernelGGL((k_blend_fwd<I, Dp, true>), dim3(4 * T), dim3(64), 0, s, A, gd);           \

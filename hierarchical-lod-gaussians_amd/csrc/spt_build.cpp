@@ -292,7 +292,8 @@ void hlgs_spt_result_free(hlgs_spt_result* r) { delete r; }
 // that are alive (no ancestor culled or stopped), then its alive condition-false nodes, each in F* order.  Aliveness
 // is a subtree test: with the walk's binary tree numbered in preorder, a node is dead iff it lies strictly inside
 // the preorder interval of a non-expanding node.
-// Blob (int32): [0] M = entries of F*, [1] levels, [2] usable, [3] 0, [4 .. 4 + levels] the levels' first entries
+// Blob (int32): [0] M = entries of F*, [1] levels, [2] usable, [3] N (the node count it was built for: the cut kernels
+// reject a blob whose N differs), [4 .. 4 + levels] the levels' first entries
 // (the last = M), then from HLGS_CUT_ORDER_HEADER: node[M], preorder position[M], preorder end[M] (position + subtree
 // size), all in F* order.
 size_t hlgs_upper_tree_order_size(int N)  // (64 words of room past the last array: whole 64-entry runs are read)
@@ -357,6 +358,7 @@ int hlgs_upper_tree_order(int N, const int* nodes, void* order)
     o[0] = M;
     o[1] = levels;
     o[2] = 1;
+    o[3] = N;
     for (int l = 0; l <= levels; l++) o[4 + l] = lev[l];
     int* fn = o + HLGS_CUT_ORDER_HEADER;
     uint16_t* pre16 = reinterpret_cast<uint16_t*>(fn + ((2 * M + 3) & ~3));  // 16-byte aligned

@@ -350,12 +350,22 @@ void launch_upper_cut(const CutArgs& a, hipStream_t s)
 constexpr int kFlatRun = 64;  // entries per thread of k_cut_flat_place (1024 x 64 > HLGS_CUT_FLAT_MAX_ENTRIES)
 static_assert(1024 * kFlatRun > HLGS_CUT_FLAT_MAX_ENTRIES, "one 64-bit mask per thread run");
 
+// A blob the flat cut can use for these nodes: usable (word 2), built for this node count (word 3; a blob of another
+// tree would read nodes past N and leave holes in the cut), entries and levels within the kernels' limits.  The same
+// test in all three kernels (uniform); k_cut_flat_place reports a failure through count[1].
+__device__ __forceinline__ bool flat_blob_ok(const CutArgs& a, const int* order)
+{
+    const int M = order[0], nlev = order[1];
+    return order[2] == 1 && order[3] == a.N && M > 0 && M <= a.N && M <= HLGS_CUT_FLAT_MAX_ENTRIES && nlev >= 1 &&
+           nlev <= HLGS_CUT_FLAT_MAX_LEVELS;
+}
+
 __global__ void __launch_bounds__(256) k_cut_flat_eval(CutArgs a, const int* __restrict__ order,
                                                        uint8_t* __restrict__ st8, uint16_t* __restrict__ endv)
 {
     const int M = order[0];
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (!order[2] || i >= M) return;  // an unusable blob: k_cut_flat_place reports it
+    if (!flat_blob_ok(a, order) || i >= M) return;  // an unusable blob: k_cut_flat_place reports it
     const int* fn = order + HLGS_CUT_ORDER_HEADER;
     const int v = fn[i], pe = fn[M + i];
     const int st = cut_node<false>(a, v).st;
@@ -411,7 +421,7 @@ __global__ void __launch_bounds__(1024) k_cut_flat_place(CutArgs a, const int* _
     __shared__ int2 s_lev[HLGS_CUT_FLAT_MAX_LEVELS + 1];
     const int M = order[0], nlev = order[1];
     const int t = threadIdx.x;
-    if (!order[2] || M <= 0 || M > HLGS_CUT_FLAT_MAX_ENTRIES || nlev < 1 || nlev > HLGS_CUT_FLAT_MAX_LEVELS) {
+    if (!flat_blob_ok(a, order)) {
         if (t == 0) { a.count[0] = 0; a.count[1] = 1; }  // (uniform) not a blob the flat cut can use
         return;
     }
@@ -489,8 +499,7 @@ __global__ void __launch_bounds__(256) k_cut_flat_write(CutArgs a, const int* __
     __shared__ int s_ls[HLGS_CUT_FLAT_MAX_LEVELS + 1];
     __shared__ int2 s_lev[HLGS_CUT_FLAT_MAX_LEVELS + 1];
     const int M = order[0], nlev = order[1];
-    if (!order[2] || M <= 0 || M > HLGS_CUT_FLAT_MAX_ENTRIES || nlev < 1 || nlev > HLGS_CUT_FLAT_MAX_LEVELS ||
-        a.count[1])
+    if (!flat_blob_ok(a, order) || a.count[1])
         return;  // (uniform) reported by k_cut_flat_place
     const int t = threadIdx.x;
     if (t <= nlev) {

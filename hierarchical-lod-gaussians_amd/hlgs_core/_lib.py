@@ -42,7 +42,8 @@ class HierInfo(C.Structure):
 
 
 class FrameInfo(C.Structure):
-    _fields_ = [("num_rendered", _i), ("max_tile_count", _i), ("rendered", _i), ("num_binned", _i)]
+    _fields_ = [("num_rendered", _i), ("max_tile_count", _i), ("rendered", _i), ("num_binned", _i),
+                ("entry_shift", _i), ("drops_empty", _i)]
 
 
 class CacheArgs(C.Structure):
@@ -144,6 +145,7 @@ _SIGS = {
     "hlgs_set_drop_empty": (None, [_i]),
     "hlgs_set_plan_polls": (None, [C.c_uint]),
     "hlgs_image_ranges_offset": (_sz, [_i, _i]),
+    "hlgs_image_misc_offset": (_sz, [_i, _i]),
     "hlgs_geom_splat_offset": (_sz, [_i]),
     "hlgs_set_stage_timing": (None, [_i]),
     "hlgs_stage_count": (_i, []),

@@ -44,7 +44,7 @@ def _compile(src, extra):
 
 def variant_switches():
     """Compile-time switches in the product sources (`#if[n]def HLGS_...` / `#if HLGS_...`): there are none.  Measured
-    variants live outside the product source (tools/variants/, built by tools/build_variant.py), so libhlgs.so is
+    variants live outside the product source (patches under tools/variants/ or git history, built by tools/build_variant.py), so libhlgs.so is
     exactly the tested configuration and no diagnostic or parity-breaking path can be compiled into it."""
     import re
     pat = re.compile(r"^\s*#\s*(ifdef|ifndef|if|elif)\b.*\bHLGS_", re.M)

@@ -125,6 +125,10 @@ typedef struct hlgs_frame_info {
     int rendered;        /* hlgs_rasterize_forward: 1 when phase 2 ran inside the call */
     int num_binned;      /* instances actually binned into the per-tile lists (== num_rendered for the
                             hierarchy rasterizer); sizes hlgs_binning_buffer_size */
+    int entry_shift;     /* this frame's point_list entries are (index << entry_shift) | quadrant mask (0: plain
+                            indices); the switches are read once when the frame starts (hlgs_set_entry_packing) */
+    int drops_empty;     /* 1 if this frame's lists drop the instances whose quadrant mask is 0 (hlgs_set_drop_empty);
+                            _prepare sets both and _render runs with them */
 } hlgs_frame_info;
 
 /* Phase 1: preprocess + scans.  Writes radii (P), fills geom/img and *info (host).  One host
@@ -281,7 +285,8 @@ int hlgs_upper_tree_cut_views_ordered_device(int N, const int* nodes, const void
                                              int use_frustum, int use_lod, void* scratch, int* cut, int* count_device,
                                              void* stream);
 /* Host: the walk order of an upper tree (nodes: N x 6 HierarchyNode rows, host memory) into order_host
- * (hlgs_upper_tree_order_size(N) bytes).  Word 2 of the blob is 1 when the flat cut can use it: the nodes form a
+ * (hlgs_upper_tree_order_size(N) bytes).  Word 3 holds N: the flat cut refuses (count_device[1] = 1) a blob built for
+ * another node count.  Word 2 of the blob is 1 when the flat cut can use it: the nodes form a
  * tree as the reference walks it (root 0; first child, then that child's next sibling) with at most 65,535 nodes
  * on it over at most 64 levels; otherwise use the level walk (order = NULL above). */
 #define HLGS_CUT_ORDER_HEADER 80       /* words before the per-entry arrays of the order blob */
@@ -451,9 +456,12 @@ int hlgs_expand_to_target(int N, const int* nodes, int target, int* out, int cap
 /* ---- inspection (tests): byte offsets of fields inside the caller's buffers, counted from the
  * buffer's first 256-byte-aligned address ---- */
 size_t hlgs_binning_point_list_offset(int R);  /* uint32 point_list[R] */
-/* point_list entries of a P-Gaussian forward are (Gaussian index << shift) | footprint quadrant mask: the shift. */
+/* point_list entries of a P-Gaussian forward started now are (Gaussian index << shift) | footprint quadrant mask: the
+ * shift (a finished frame's own is hlgs_frame_info.entry_shift). */
 int hlgs_point_list_entry_shift(int P);
-/* 1 if a P-Gaussian forward bins no instance whose quadrant mask is 0 (packed entries, dropping on): its tile
+/* The process-wide switches below are atomics, read once when a frame starts: a frame in flight keeps the options it
+ * started with (reported in its hlgs_frame_info), so flipping a switch from another thread changes later frames only.
+ * 1 if a P-Gaussian forward started now bins no instance whose quadrant mask is 0 (packed entries, dropping on): its tile
  * lists and n_contrib then match the oracle run with drop_empty (oracle/hlgs_oracle.c rect_quad_masks).  0: every
  * instance of the reference's binning (rasterizer_impl.cu:70-115) is listed, and point_list / n_contrib are laid out as
  * the reference lays them out. */
@@ -467,6 +475,9 @@ void hlgs_set_drop_empty(int on);
  * look-back times out is re-run with the two-launch plan that needs no inter-block wait; polls = 0 forces that path. */
 void hlgs_set_plan_polls(unsigned polls);
 size_t hlgs_image_ranges_offset(int W, int H);  /* uint2 ranges[tiles] */
+/* uint32 misc[16]: [0] binned instances, [1] longest tile list, [2] record slots, [3] the frame's entry packing (1 when
+ * entry_shift != 0), [4] the frame's drops_empty -- written on the device by the frame's binning plan */
+size_t hlgs_image_misc_offset(int W, int H);
 size_t hlgs_geom_splat_offset(int P);           /* float4 splat[P][4]: x, y, conic a, b | conic c, opacity, r, g |
                                                    b, 1/depth, t, 1/kids | record base, tile x0, y0, width */
 

@@ -121,7 +121,8 @@ def test_no_cpu_fallback():
 
 def test_product_sources_have_no_variant_switches():
     """libhlgs.so is exactly the tested configuration: no `#if HLGS_...` switch (diagnostic or measured loser) in the
-    product sources -- the variants live in tools/variants/ and are built by tools/build_variant.py only."""
+    product sources -- variants are patches under tools/variants/ (or files in git history), built by
+    tools/build_variant.py only."""
     import importlib.util
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -130,3 +131,25 @@ def test_product_sources_have_no_variant_switches():
     B = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(B)
     assert B.variant_switches() == []
+
+
+def test_variants_are_patches_that_apply():
+    """tools/variants/ holds no full-file kernel copies: only patches against the product sources,
+    and each of them still applies to the current tree (so an A/B build cannot silently measure stale code)."""
+    import glob
+    import importlib.util
+    import os
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    vdir = os.path.join(root, "tools", "variants")
+    assert not glob.glob(os.path.join(vdir, "*.hip")) and not glob.glob(os.path.join(vdir, "*.cpp"))
+    spec = importlib.util.spec_from_file_location("build_variant", os.path.join(root, "tools", "build_variant.py"))
+    V = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(V)
+    for patch in sorted(glob.glob(os.path.join(vdir, "*.patch"))):
+        V.touched_files(patch)  # product sources only
+        with tempfile.TemporaryDirectory() as tree:
+            import shutil
+            shutil.copytree(os.path.join(root, V.CSRC_REL), os.path.join(tree, V.CSRC_REL))
+            shutil.copytree(os.path.join(root, "include"), os.path.join(tree, "include"))
+            V.apply_patch(patch, tree, check_only=True)

@@ -74,6 +74,7 @@ def test_flat_cut_restatement_matches_reference_walk(seed, dmul, frustum, lod):
     nodes, xyz, bounds, md2 = _upper_tree(2000 + 500 * seed, seed)
     blob = _blob(nodes)
     assert blob is not None and blob[2] == 1 and blob[0] == len(nodes)  # every node of this tree is on the walk
+    assert blob[3] == len(nodes)  # the node count it was built for (the kernels refuse another tree's blob)
     R = np.eye(3)
     ang = 0.3 * seed
     R[0, 0], R[0, 2], R[2, 0], R[2, 2] = np.cos(ang), np.sin(ang), -np.sin(ang), np.cos(ang)

@@ -91,3 +91,57 @@ def test_drop_empty_off_gives_reference_lists(P, W, H):
     assert lib.hlgs_point_list_drops_empty(P) == 1
     fr_drop = _lists_match(sc, cam, 1, True)
     assert binned(fr_drop) < binned(fr_ref)  # the default leaves the zero-mask instances out
+
+
+def test_switch_flipped_during_frames_is_per_frame():
+    """The binning switches are read once per frame (FrameOpts): a thread flips drop_empty while
+    this one renders.  Every frame's hlgs_frame_info.drops_empty must equal the drop word its own plan kernel wrote
+    (Img::misc[4]) and its binned count must be the oracle's for that setting -- never a mix of the two."""
+    import ctypes as C
+    import threading
+    from diff_gaussian_rasterization import _C
+    lib = L.load()
+    P, W, H = 20000, 256, 192
+    cam = S.make_camera(W, H)
+    sc = S.make_gaussians(P, 1, cam, seed=17)
+    want = {d: binned(O.forward(dict(sc), S.cam_numpy(cam), drop_empty=d)) for d in (False, True)}
+    assert want[True] < want[False]
+    t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
+    e = torch.empty(0, device=DEV)
+    a, keep, P_, _, _ = _C._raster_args(cam["bg"], e, e, e, e, t(sc["means3D"]), e, t(sc["opacities"]),
+                                        t(sc["scales"]), t(sc["rotations"]), 1.0, e, cam["viewmatrix"],
+                                        cam["projmatrix"], cam["tanfovx"], cam["tanfovy"], H, W, t(sc["shs"]), 1,
+                                        cam["campos"], False, False)
+    u8 = dict(dtype=torch.uint8, device=DEV)
+    geom = torch.empty((lib.hlgs_geom_buffer_size(P),), **u8)
+    img = torch.empty((lib.hlgs_image_buffer_size(W, H),), **u8)
+    binning = torch.empty((lib.hlgs_binning_buffer_size(2 * want[False]),), **u8)
+    radii = torch.empty((P,), dtype=torch.int32, device=DEV)
+    color = torch.empty((3, H, W), device=DEV)
+    stop = threading.Event()
+
+    def flip():
+        on = 0
+        while not stop.is_set():
+            lib.hlgs_set_drop_empty(on)
+            on ^= 1
+    th = threading.Thread(target=flip)
+    th.start()
+    seen_flags = set()
+    try:
+        for _ in range(60):
+            info = L.FrameInfo()
+            L.check(lib.hlgs_rasterize_forward(C.byref(a), L.ptr(geom), L.ptr(img), L.ptr(radii), L.ptr(binning),
+                                               binning.numel(), C.byref(info), L.ptr(color), None, None, L.stream()))
+            assert info.rendered == 1
+            misc = _C._field(img, lib.hlgs_image_misc_offset(W, H), 16, torch.int32).cpu().numpy()
+            assert info.entry_shift == 4 and misc[3] == 1
+            assert misc[4] == info.drops_empty, (misc[4], info.drops_empty)
+            assert info.num_binned == want[bool(info.drops_empty)], (info.num_binned, info.drops_empty)
+            seen_flags.add(info.drops_empty)
+    finally:
+        stop.set()
+        th.join()
+        lib.hlgs_set_drop_empty(1)
+    del keep
+    assert lib.hlgs_point_list_drops_empty(P) == 1

@@ -47,6 +47,30 @@ def test_upper_tree_cut_matches_reference_walk(seed, dmul, frustum, lod):
     np.testing.assert_array_equal(flat.cpu().numpy(), want)
 
 
+def test_flat_cut_refuses_another_trees_blob():
+    """A walk-order blob built for another tree: its entry count and node ids do not belong to these
+    nodes, so the flat cut reports it (count[1]) instead of placing a cut with holes or reading nodes past N."""
+    from hlgs_core import spt
+    nodes, xyz, bounds, md2 = _upper_tree(3000, 0)
+    big, *_ = _upper_tree(3500, 1)
+    cam = S.make_camera(320, 240, T=np.array([0.0, 0.0, 0.5]))
+    planes = spt.extract_frustum_planes(cam["projmatrix"])
+    t = lambda a: torch.tensor(a, device=DEV)  # noqa: E731
+    for other in (big, nodes[: len(nodes) // 2 * 2 - 1]):
+        order = spt.upper_tree_order(t(other))
+        if order is None:
+            continue
+        assert int(order[3]) == len(other) != len(nodes)
+        with pytest.raises(RuntimeError, match="order blob"):
+            spt.upper_tree_cut(t(nodes), t(xyz), t(bounds), t(md2), planes, cam["campos"], 1.0, True, True,
+                               order=order)
+    # its own blob still cuts
+    own = spt.upper_tree_order(t(nodes))
+    want = SR.upper_tree_cut(nodes, xyz, bounds, md2, planes.numpy(), cam["campos"].numpy(), 1.0, True, True)
+    got = spt.upper_tree_cut(t(nodes), t(xyz), t(bounds), t(md2), planes, cam["campos"], 1.0, True, True, order=own)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("n,frustum,lod", [(40000, False, False), (40000, True, True), (300000, False, False),
                                            (30000, False, False), (30000, True, True)])
 def test_upper_tree_cut_wide_levels(n, frustum, lod):
