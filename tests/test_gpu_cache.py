@@ -327,3 +327,35 @@ def test_occlusion_culling_matches_restatement():
         for t, (g, w) in enumerate(zip(_dev_list(cache), orc.dev)):
             np.testing.assert_array_equal(g.detach().cpu().numpy(), w, err_msg=f"tensor {t} view {step}")
     assert culled > 0  # the random storage positions put part of the upper tree off screen or behind the camera
+
+
+def test_occlusion_culling_two_views_is_union_of_per_view_radii():
+    """A batch of views (view-data parallel, DESIGN A-20): the occlusion cull keeps a coarse-cut node if ANY view's
+    render gives it a non-zero radius (the reference renders one view, so this union rule is ours).  The
+    kept set is checked against the union of the oracle's per-view radii on the same activated inputs, and the rest of
+    the step against the restatement run on that filtered union cut."""
+    from hlgs_core.spt_cache import SPTCache
+    sky = 4
+    b, storage = _scene(sky)
+    cams = _cameras()
+    cache = SPTCache(storage, b, sky, reuse_tolerance=0.9, occlusion_culling=True)
+    orc = _Oracle(b, storage, sky, 0.9, 10 ** 9)
+    only_one = 0
+    for step in range(len(cams) - 1):
+        pair = [cams[step], cams[step + 1]]
+        fpt = torch.stack([c["projmatrix"] for c in pair])
+        cp = torch.stack([c["campos"].reshape(-1)[:3] for c in pair])
+        got = cache.step(fpt, cp, views=pair)
+        occ = cache.last_occlusion
+        gid = occ["indices"].cpu().numpy()
+        sc = dict(means3D=occ["means3D"].cpu().numpy(), opacities=occ["opacities"].cpu().numpy(),
+                  scales=occ["scales"].cpu().numpy(), rotations=occ["rotations"].cpu().numpy(),
+                  shs=occ["shs"].cpu().numpy(), sh_degree=3)
+        per = [O.forward(sc, S.cam_numpy(dict(c, bg=np.zeros(3, np.float32))), do_depth=False).radii > 0
+               for c in pair] if len(gid) else [np.zeros(0, bool)] * 2
+        keep = per[0] | per[1]
+        np.testing.assert_array_equal(occ["keep"].cpu().numpy(), keep, err_msg=f"step {step}")
+        only_one += int((per[0] ^ per[1]).sum())
+        want = orc.step(pair, keep=keep)
+        np.testing.assert_array_equal(got.cpu().numpy(), want["render_indices"], err_msg=f"step {step}")
+    assert only_one > 0  # the two views disagree on some nodes, so the union rule is exercised

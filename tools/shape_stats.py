@@ -9,7 +9,9 @@ share of useful lanes is valid pairs / (64 x passes).  This counts both for a 16
   col:   four 4x16 column strips,
 from the CPU oracle's frame (float64 footprints).  Statistics only; experiment tooling, not product code.
 
-    python tools/shape_stats.py [P] [W] [H]
+    python tools/shape_stats.py [P] [W] [H] [STRIDE]
+
+STRIDE > 1 counts every STRIDE-th tile only (a sample: the ratios between the shapes are what matter).
 """
 import os
 import sys
@@ -23,7 +25,7 @@ from hlgs_core import synthetic as S  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 
-def main(P=1_000_000, W=1920, H=1080):
+def main(P=1_000_000, W=1920, H=1080, stride=1):
     cam = S.make_camera(W, H)
     sc = S.make_gaussians(P, 3, cam, seed=0)
     t0 = time.time()
@@ -34,9 +36,12 @@ def main(P=1_000_000, W=1920, H=1080):
     ids = fr.point_list[:Rb].astype(np.int64)
     tile = np.repeat(np.arange(gx * ((H + 15) // 16)), (fr.ranges[:, 1] - fr.ranges[:, 0]).astype(np.int64))
     li = np.arange(Rb) - fr.ranges[tile, 0].astype(np.int64)
+    sel = np.flatnonzero(tile % stride == 0)
+    ids, tile, li = ids[sel], tile[sel], li[sel]
+    Rb = len(sel)
     ncon = fr.n_contrib.reshape(H, W)
-    xy = fr.means2D[ids].astype(np.float64)
-    co = fr.conic_opacity[ids].astype(np.float64)
+    xy = fr.means2D[ids].astype(np.float32)
+    co = fr.conic_opacity[ids].astype(np.float32)
     thr = -np.log2(255.0 * co[:, 3])
     ly, lx = np.mgrid[0:16, 0:16]
     lx = lx.ravel()
@@ -45,7 +50,7 @@ def main(P=1_000_000, W=1920, H=1080):
     tot = {k: 0 for k in shapes}
     fwd = {k: 0 for k in shapes}
     valid_n = 0
-    CH = 100_000
+    CH = 20_000
     for s in range(0, Rb, CH):
         e = min(Rb, s + CH)
         t = tile[s:e]
@@ -66,7 +71,7 @@ def main(P=1_000_000, W=1920, H=1080):
                 bf = (foot & m).any(1)
                 tot[name] += int((bf & (li[s:e, None] < bl)).sum())
                 fwd[name] += int(bf.sum())  # the forward's waves visit every splat that reaches them (until done)
-    out = {"R_binned": Rb, "valid_pairs": valid_n}
+    out = {"R_binned_sampled": Rb, "tile_stride": stride, "valid_pairs": valid_n}
     for name in shapes:
         out[name] = {"bwd_passes": tot[name], "fwd_visits_upper": fwd[name], "lane_use": valid_n / (64 * tot[name])}
     print(out)
