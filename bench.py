@@ -477,7 +477,8 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
     not available offline), per iteration as train_post.py:323-812 orders it: SPTCache.step (coarse cut, cache
     bookkeeping, SPT cut, write-back / load through pinned host storage) -> activations -> alt rasterizer
     (antialiasing, active SH degree 1) -> L1 + D-SSIM (+ masked inverse-depth L1, train_single.py:111-118) ->
-    backward -> dense Adam.  The camera moves every step.  Median host-clock step and per-stage event medians.
+    backward -> dense Adam.  The activations (sigmoid opacity, exp scale, normalised rotation) run as one HIP pass
+    each way (hlgs_core.activations).  The camera moves every step.  Median host-clock step and per-stage event medians.
 
     world > 1: view-data parallel, one view per rank.  Each step the ranks gather every rank's view
     (gather_views), every rank's SPTCache.step computes the union cut of the batch, so all replicas hold the same
@@ -486,6 +487,7 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
     Barrier + synchronise around the timed steps, max over ranks; all-reduce time and bus bandwidth reported."""
     from alt_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from hlgs_core import synthetic as S
+    from hlgs_core.activations import activate
     from hlgs_core.loss import photometric_loss
     from hlgs_core.spt_cache import NAMES, SPTCache, gather_views
     b, storage, build_s, G = merged_two_chunk_scene(P)
@@ -534,9 +536,11 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
                                           sh_degree=sh_degree, campos=cam["campos"].to(dev), prefiltered=False,
                                           debug=False, antialiasing=True)
         means2D = torch.zeros_like(p["xyz"], requires_grad=True)
+        # get_opacity / get_scaling / get_rotation (sigmoid, exp, normalize) of every resident row in one HIP pass
+        opac, scales, rots = activate(p["opacity"], p["scaling"], p["rotation"])
         img, radii, invd = GaussianRasterizer(s)(
-            means3D=p["xyz"], means2D=means2D, dc=p["f_dc"], shs=p["f_rest"], opacities=torch.sigmoid(p["opacity"]),
-            scales=torch.exp(p["scaling"]), rotations=torch.nn.functional.normalize(p["rotation"]))
+            means3D=p["xyz"], means2D=means2D, dc=p["f_dc"], shs=p["f_rest"], opacities=opac, scales=scales,
+            rotations=rots)
         img = img.clamp(0, 1)
         e[2].record()
         loss = (photometric_loss(img, gt, 0.2, invd, mono, mask, 0.5) if depth else photometric_loss(img, gt, 0.2))[0]

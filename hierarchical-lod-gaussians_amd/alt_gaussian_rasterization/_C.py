@@ -109,9 +109,10 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dc, sh,
                                  dL_dout_invdepth, degree, campos, geomBuffer, R, binningBuffer, imageBuffer, B,
-                                 sampleBuffer, antialiasing, debug):
+                                 sampleBuffer, antialiasing, debug, *, need_cov3D=True):
     """-> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_ddc, dL_dsh, dL_dscales,
-    dL_drotations)  (rasterize_points.cu:138-232)."""
+    dL_drotations)  (rasterize_points.cu:138-232).  need_cov3D=False (the autograd wrapper without cov3D_precomp)
+    returns an empty dL_dcov3D and skips writing its rows."""
     lib = L.load()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     dev = means3D.device
@@ -123,7 +124,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     fac = dp.colour_factor(sh, dc) if M > 0 and dc is not None and dc.numel() else None
     out = dict(dmean2D=torch.empty((P, 3), **f32), dcolor=torch.empty((P, 3), **f32),
                dopacity=_dest(opacities, (P, 1), f32), dmean3D=_dest(means3D, (P, 3), f32, True),
-               dcov3D=torch.empty((P, 6), **f32),
+               dcov3D=torch.empty((P if need_cov3D else 0, 6), **f32),
                ddc=fac[2] if fac is not None else _dest(dc, (P, 1, 3), f32, True),
                dsh=fac[1] if fac is not None else _dest(sh, (P, M, 3), f32, True), dscale=_dest(scales, (P, 3), f32),
                drot=_dest(rotations, (P, 4), f32))

@@ -61,20 +61,21 @@ class _RasterizeGaussians(torch.autograd.Function):
                 cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, dc, sh,
                 grad_out_depth, rs.sh_degree, rs.campos, geom_buf, ctx.num_rendered, binning_buf, img_buf,
                 ctx.num_buckets, sample_buf, rs.antialiasing, rs.debug)
+        need_cov3D = cov3Ds_precomp.numel() > 0  # otherwise no gradient for it, and its rows are not written
         if rs.debug:
             cpu_args = cpu_deep_copy_tuple(args)
             try:
-                grads = _C.rasterize_gaussians_backward(*args)
+                grads = _C.rasterize_gaussians_backward(*args, need_cov3D=need_cov3D)
             except Exception as ex:
                 torch.save(cpu_args, "snapshot_bw.dump")
                 print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
                 raise ex
         else:
-            grads = _C.rasterize_gaussians_backward(*args)
+            grads = _C.rasterize_gaussians_backward(*args, need_cov3D=need_cov3D)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_dc, grad_sh,
          grad_scales, grad_rotations) = grads
         return (grad_means3D, grad_means2D, grad_dc, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
-                grad_rotations, grad_cov3Ds_precomp, None)
+                grad_rotations, grad_cov3Ds_precomp if need_cov3D else None, None)
 
 
 class GaussianRasterizationSettings(NamedTuple):

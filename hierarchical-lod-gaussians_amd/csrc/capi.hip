@@ -68,6 +68,10 @@ void launch_depth_l1_backward(long n, const float* inv, const float* mono, const
 void launch_upper_cut(const CutArgs& a, hipStream_t s);
 void launch_upper_cut_flat(const CutArgs& a, const int* order, hipStream_t s);
 void launch_rows(bool gather, long n, int row_bytes, const int64_t* idx, const void* src, void* dst, hipStream_t s);
+void launch_act_fwd(int64_t n, const float* op_raw, const float* sc_raw, const float* rot_raw, float* op, float* sc,
+                    float* rot, hipStream_t s);
+void launch_act_bwd(int64_t n, const float* op, const float* sc, const float* rot_raw, const float* g_op,
+                    const float* g_sc, const float* g_rot, float* d_op, float* d_sc, float* d_rot, hipStream_t s);
 void launch_morton(int P, const float* xyz, const float* mn, const float* mx, int64_t* codes, hipStream_t s);
 void launch_adam(float* param, const float* grad, float* m, float* v, const uint8_t* vis, float lr, float b1, float b2,
                  float eps, uint32_t N, uint32_t M, hipStream_t s);
@@ -610,7 +614,7 @@ int hlgs_rasterize_backward_split(const hlgs_raster_args* a, const int* radii, c
 {
     int rc = validate(a);
     if (rc) return rc;
-    if (!out || !out->dmean2D || !out->dcolor || !out->dopacity || !out->dmean3D || !out->dcov3D || !out->dscale ||
+    if (!out || !out->dmean2D || !out->dcolor || !out->dopacity || !out->dmean3D || !out->dscale ||
         !out->drot || (a->M > 0 && !out->dsh) || (a->variant == HLGS_VARIANT_ALT && !out->ddc))
         return fail(HLGS_ERR_ARG, "missing gradient output");
     hipStream_t s = (hipStream_t)stream;
@@ -622,7 +626,7 @@ int hlgs_rasterize_backward_split(const hlgs_raster_args* a, const int* radii, c
         HLGS_TRY_HIP(hipMemsetAsync(out->dcolor, 0, 12 * Pf, s));
         HLGS_TRY_HIP(hipMemsetAsync(out->dopacity, 0, 4 * Pf, s));
         HLGS_TRY_HIP(hipMemsetAsync(out->dmean3D, 0, 12 * Pf, s));
-        HLGS_TRY_HIP(hipMemsetAsync(out->dcov3D, 0, 24 * Pf, s));
+        if (out->dcov3D) HLGS_TRY_HIP(hipMemsetAsync(out->dcov3D, 0, 24 * Pf, s));
         if (out->dsh && a->M > 0) HLGS_TRY_HIP(hipMemsetAsync(out->dsh, 0, 12 * (size_t)a->M * Pf, s));
         if (out->ddc) HLGS_TRY_HIP(hipMemsetAsync(out->ddc, 0, 12 * Pf, s));
         HLGS_TRY_HIP(hipMemsetAsync(out->dscale, 0, 12 * Pf, s));
@@ -686,6 +690,38 @@ int hlgs_compute_relocation(int P, const float* opacity_old, const float* scale_
     hipGetLastError();
     launch_relocation(P, opacity_old, scale_old, N, binoms, n_max, opacity_new, scale_new, s);
     return check_stage(s, false, "compute_relocation");
+}
+
+int hlgs_activate_forward(int64_t n, const float* opacity_raw, const float* scaling_raw, const float* rotation_raw,
+                          float* opacity, float* scales, float* rotations, void* stream)
+{
+    if (n <= 0) return HLGS_OK;
+    if (!opacity_raw || !scaling_raw || !rotation_raw || !opacity || !scales || !rotations)
+        return fail(HLGS_ERR_ARG, "missing tensor");
+    if ((reinterpret_cast<uintptr_t>(rotation_raw) | reinterpret_cast<uintptr_t>(rotations)) & 15u)
+        return fail(HLGS_ERR_ARG, "rotation rows must be 16-byte aligned");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_act_fwd(n, opacity_raw, scaling_raw, rotation_raw, opacity, scales, rotations, s);
+    return check_stage(s, false, "activate_forward");
+}
+
+int hlgs_activate_backward(int64_t n, const float* opacity, const float* scales, const float* rotation_raw,
+                           const float* g_opacity, const float* g_scales, const float* g_rotations, float* d_opacity_raw,
+                           float* d_scaling_raw, float* d_rotation_raw, void* stream)
+{
+    if (n <= 0) return HLGS_OK;
+    if ((g_opacity && (!opacity || !d_opacity_raw)) || (g_scales && (!scales || !d_scaling_raw)) ||
+        (g_rotations && (!rotation_raw || !d_rotation_raw)))
+        return fail(HLGS_ERR_ARG, "missing tensor");
+    if ((reinterpret_cast<uintptr_t>(rotation_raw) | reinterpret_cast<uintptr_t>(g_rotations) |
+         reinterpret_cast<uintptr_t>(d_rotation_raw)) & 15u)
+        return fail(HLGS_ERR_ARG, "rotation rows must be 16-byte aligned");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_act_bwd(n, opacity, scales, rotation_raw, g_opacity, g_scales, g_rotations, d_opacity_raw, d_scaling_raw,
+                   d_rotation_raw, s);
+    return check_stage(s, false, "activate_backward");
 }
 
 int hlgs_adam_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const uint8_t* visible,

@@ -402,7 +402,8 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
         o.dcolor[3 * idx + 1] = s7;
         o.dcolor[3 * idx + 2] = s8;
         o.dopacity[idx] = dop_out;
-        for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = dc[i];
+        if (o.dcov3D)
+            for (int i = 0; i < 6; i++) o.dcov3D[6 * idx + i] = dc[i];
         o.dmean3D[3 * idx] = dmean.x;
         o.dmean3D[3 * idx + 1] = dmean.y;
         o.dmean3D[3 * idx + 2] = dmean.z;
@@ -424,7 +425,9 @@ __global__ void __launch_bounds__(256) k_gauss_bwd(hlgs_raster_args a, const int
         wave_rows_store<3>(o.dmean2D + 3 * (size_t)w0, r_dm2, stage, lane, nrows);
         wave_rows_store<3>(o.dcolor + 3 * (size_t)w0, r_dcol, stage, lane, nrows);
         wave_rows_store<1>(o.dopacity + (size_t)w0, r_dop, stage, lane, nrows);
-        wave_rows_store<6>(o.dcov3D + 6 * (size_t)w0, dc, stage, lane, nrows);
+        // dcov3D is an output only (the cov3D backward is fused into dscale / drot): skipped when the caller has no
+        // cov3D_precomp to return it for (NULL; 24 B per Gaussian of writes)
+        if (o.dcov3D) wave_rows_store<6>(o.dcov3D + 6 * (size_t)w0, dc, stage, lane, nrows);
         wave_rows_store<3>(o.dmean3D + 3 * (size_t)w0, r_dm3, stage, lane, nrows);
         wave_rows_store<3>(o.dscale + 3 * (size_t)w0, dscale, stage, lane, nrows);
         if (live) reinterpret_cast<float4*>(o.drot)[idx] = make_float4(dq[0], dq[1], dq[2], dq[3]);

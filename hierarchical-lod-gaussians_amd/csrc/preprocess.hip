@@ -424,16 +424,21 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
             r3 = make_float4(0.f, __int_as_float(o.x0 | (o.y0 << 16)), __int_as_float(o.x1 - o.x0), thr);
         }
     }
-    st[4 * lane] = r0;
-    st[4 * lane + 1] = r1;
-    st[4 * lane + 2] = r2;
-    st[4 * lane + 3] = r3;
+    // Word k of lane l's record goes to slot (k + l / 2) mod 4 of its 64-byte stage row: each ds_write_b128 group of 8
+    // consecutive lanes then covers all 32 banks once (unrotated, lanes 0, 2, 4, 6 all hit banks 0-3: 4-way conflicts,
+    // half of the kernel's SQ_LDS_BANK_CONFLICT cycles).  The reads stay linear (conflict-free); the global store puts
+    // each word back in place within the same record, so every wave store still covers contiguous 1 KiB.
+    const int rot = lane >> 1;
+    st[4 * lane + (rot & 3)] = r0;
+    st[4 * lane + ((rot + 1) & 3)] = r1;
+    st[4 * lane + ((rot + 2) & 3)] = r2;
+    st[4 * lane + ((rot + 3) & 3)] = r3;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's own stage writes, before its reads
     float4* rb = g.splat + 4 * (size_t)t0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int f4 = 64 * k + lane;
-        if (f4 < 4 * n_grp) rb[f4] = st[f4];
+        const int f4 = 64 * k + lane, rec = f4 >> 2;
+        if (f4 < 4 * n_grp) rb[4 * rec + (((f4 & 3) - (rec >> 1)) & 3)] = st[f4];
     }
 }
 

@@ -730,63 +730,70 @@ void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, 
 // Lane = one 16-byte chunk of the destination (aligned store).  Its four source words lie in rows r .. r_end; when
 // those rows are consecutive in the source too (src_rows[r_end] - src_rows[r] = r_end - r, which holds inside the
 // long runs of kept rows) they are one contiguous 16-byte load at 4-byte alignment, otherwise four word loads.
-__global__ void __launch_bounds__(256) k_rows_compact(RowTabs tabs, int64_t n, const int* __restrict__ src_rows)
+// Round 6: one 1-D grid over every table's chunks -- block b copies kCompactChunks consecutive chunks of one table
+// (CompactTabs::bstart, the blocks of the tables before it) -- instead of a 2-D grid of 2,048 blocks per table, in which
+// the narrow tables (opacity, 3-float rows: a few hundred blocks of work) left most of their blocks idle and the wide
+// SH tables took ~13 grid-stride chunks per thread.
+constexpr int kCompactU = 4;                      // chunks per thread, their loads issued together
+constexpr int kCompactChunks = 256 * kCompactU;   // chunks per block
+constexpr int kCompactTables = 20;                // the cache's 18 tables (a smaller kernel argument block)
+struct CompactTabs {
+    RowCopy t[kCompactTables];
+    int bstart[kCompactTables + 1];                // first block of each table; bstart[T] = the grid
+};
+__global__ void __launch_bounds__(256) k_rows_compact(CompactTabs tabs, int T, int64_t n, const int* __restrict__ src_rows)
 {
-    const RowCopy& tb = tabs.t[blockIdx.y];
+    int t = 0;  // this block's table (uniform): the last table whose first block is <= blockIdx.x
+    for (int j = 1; j < T; j++) t += (int)blockIdx.x >= tabs.bstart[j];
+    const RowCopy& tb = tabs.t[t];
     const int64_t words = tb.row_bytes >> 2;
-    if (words == 0) return;
     const uint32_t* __restrict__ src = static_cast<const uint32_t*>(tb.src);
     uint32_t* __restrict__ dst = static_cast<uint32_t*>(tb.dst);
     const int64_t total = n * words;
-    const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4, S = (int64_t)gridDim.x * 256 * 4;
-    int64_t r = w0 / words, k = w0 - r * words;
-    const int64_t dr = S / words, dk = S - dr * words;
-    // kU chunks per round: their row indices are loaded together, then their sources, then the stores -- two load
-    // rounds per kU chunks instead of two per chunk
-    constexpr int kU = 4;
-    for (int64_t w = w0; w < total; w += kU * S) {
-        int64_t rr[kU], kk[kU], re[kU];
-        int s0[kU], s1[kU];
-        {
-            int64_t r1 = r, k1 = k;
+    // chunk u of this thread: block chunk base + 256 u + thread, so a wave's lanes take consecutive chunks
+    const int64_t w0 = ((int64_t)(blockIdx.x - tabs.bstart[t]) * kCompactChunks + threadIdx.x) * 4;
+    if (w0 >= total) return;
+    int64_t rr[kCompactU], kk[kCompactU], re[kCompactU];
+    {
+        constexpr int64_t S = 256 * 4;  // words between a thread's chunks
+        const int64_t dr = S / words, dk = S - dr * words;
+        int64_t r1 = w0 / words, k1 = w0 - r1 * words;
 #pragma unroll
-            for (int u = 0; u < kU; u++) {
-                rr[u] = r1;
-                kk[u] = k1;
-                re[u] = r1 + (k1 + 3) / words;
-                r1 += dr;
-                k1 += dk;
-                while (k1 >= words) { k1 -= words; r1++; }
-            }
-            r = r1;
-            k = k1;
+        for (int u = 0; u < kCompactU; u++) {
+            rr[u] = r1;
+            kk[u] = k1;
+            re[u] = r1 + (k1 + 3) / words;
+            r1 += dr;
+            k1 += dk;
+            while (k1 >= words) { k1 -= words; r1++; }
         }
+    }
+    int s0[kCompactU], s1[kCompactU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const bool in = w + u * S < total;
-            s0[u] = in ? src_rows[rr[u]] : 0;
-            s1[u] = in ? src_rows[min(re[u], n - 1)] : 0;
-        }
-        uint4 v[kU];
-        bool fast[kU];
+    for (int u = 0; u < kCompactU; u++) {
+        const bool in = w0 + u * 1024 < total;
+        s0[u] = in ? src_rows[rr[u]] : 0;
+        s1[u] = in ? src_rows[min(re[u], n - 1)] : 0;
+    }
+    uint4 v[kCompactU];
+    bool fast[kCompactU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int64_t wu = w + u * S;
-            fast[u] = wu + 4 <= total && s1[u] - s0[u] == re[u] - rr[u];
-            if (fast[u]) v[u] = *reinterpret_cast<const uint4_a4*>(src + (int64_t)s0[u] * words + kk[u]);
-        }
+    for (int u = 0; u < kCompactU; u++) {
+        const int64_t wu = w0 + u * 1024;
+        fast[u] = wu + 4 <= total && s1[u] - s0[u] == re[u] - rr[u];
+        if (fast[u]) v[u] = *reinterpret_cast<const uint4_a4*>(src + (int64_t)s0[u] * words + kk[u]);
+    }
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int64_t wu = w + u * S;
-            if (wu >= total) continue;
-            if (fast[u]) {
-                *reinterpret_cast<uint4*>(dst + wu) = v[u];
-            } else {
-                int64_t r2 = rr[u], k2 = kk[u];
-                for (int q = 0; q < 4 && wu + q < total; q++) {
-                    dst[wu + q] = src[(int64_t)src_rows[r2] * words + k2];
-                    if (++k2 == words) { k2 = 0; r2++; }
-                }
+    for (int u = 0; u < kCompactU; u++) {
+        const int64_t wu = w0 + u * 1024;
+        if (wu >= total) continue;
+        if (fast[u]) {
+            *reinterpret_cast<uint4*>(dst + wu) = v[u];
+        } else {
+            int64_t r2 = rr[u], k2 = kk[u];
+            for (int q = 0; q < 4 && wu + q < total; q++) {
+                dst[wu + q] = src[(int64_t)src_rows[r2] * words + k2];
+                if (++k2 == words) { k2 = 0; r2++; }
             }
         }
     }
@@ -794,19 +801,22 @@ __global__ void __launch_bounds__(256) k_rows_compact(RowTabs tabs, int64_t n, c
 
 void launch_rows_multi(int T, const RowCopy* tabs, int64_t n, const int* src_rows, const int* dst_rows, hipStream_t s)
 {
-    bool compact = src_rows && !dst_rows;
+    bool compact = src_rows && !dst_rows && T <= kCompactTables;
     for (int t = 0; t < T && compact; t++)
         compact = tabs[t].device_only && (reinterpret_cast<uintptr_t>(tabs[t].dst) & 15u) == 0;
     if (compact) {
-        RowTabs rt{};
-        int64_t most = 0;
+        CompactTabs ct{};
+        int64_t blocks = 0;
         for (int t = 0; t < T; t++) {
-            rt.t[t] = tabs[t];
-            most = std::max<int64_t>(most, (n * (tabs[t].row_bytes >> 2) + 3) / 4);
+            ct.t[t] = tabs[t];
+            ct.bstart[t] = (int)blocks;
+            const int64_t chunks = (n * (tabs[t].row_bytes >> 2) + 3) / 4;
+            blocks += (chunks + kCompactChunks - 1) / kCompactChunks;
         }
-        const int64_t blocks = std::min<int64_t>((most + 255) / 256, 2048);
-        if (blocks > 0) hipLaunchKernelGGL(k_rows_compact, dim3((unsigned)blocks, T), dim3(256), 0, s, rt, n, src_rows);
-        return;
+        ct.bstart[T] = (int)blocks;
+        if (blocks > 0 && blocks < (1ll << 31))
+            hipLaunchKernelGGL(k_rows_compact, dim3((unsigned)blocks), dim3(256), 0, s, ct, T, n, src_rows);
+        if (blocks < (1ll << 31)) return;
     }
     RowTabs rt{};
     int64_t most = 0;

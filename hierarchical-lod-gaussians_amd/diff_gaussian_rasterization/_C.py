@@ -116,9 +116,10 @@ def rasterize_gaussians(bg, render_indices, parent_indices, ts, kids, means3D, c
 def rasterize_gaussians_backward(bg, render_indices, parent_indices, ts, kids, means3D, radii, colors, opacities,
                                  scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, dL_dout_invdepth, sh, degree, campos, geomBuffer, R,
-                                 binningBuffer, imageBuffer, debug):
+                                 binningBuffer, imageBuffer, debug, *, need_cov3D=True):
     """-> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)
-    (rasterize_points.cu:141-245)."""
+    (rasterize_points.cu:141-245).  need_cov3D=False (the autograd wrapper without cov3D_precomp) returns an empty
+    dL_dcov3D and skips writing its rows."""
     lib = L.load()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     a, keep, P, P_full, M = _raster_args(bg, render_indices, parent_indices, ts, kids, means3D, colors, opacities,
@@ -130,7 +131,7 @@ def rasterize_gaussians_backward(bg, render_indices, parent_indices, ts, kids, m
     fac = dp.colour_factor(sh) if M > 0 and keep["indices"] is None else None
     out = dict(dmean2D=torch.empty((P_full, 3), **f32), dcolor=torch.empty((P_full, 3), **f32),
                dopacity=_dest(opacities, (P_full, 1), f32), dmean3D=_dest(means3D, (P_full, 3), f32, True),
-               dcov3D=torch.empty((P_full, 6), **f32),
+               dcov3D=torch.empty((P_full if need_cov3D else 0, 6), **f32),
                dsh=fac[1] if fac is not None else _dest(sh, (P_full, M, 3), f32, True),
                dscale=_dest(scales, (P_full, 3), f32), drot=_dest(rotations, (P_full, 4), f32))
     g = L.Grads(**{k: L.ptr(v) for k, v in out.items()}, drgb=L.ptr(fac[0]) if fac is not None else None)

@@ -70,9 +70,12 @@ class _RasterizeGaussians(torch.autograd.Function):
         d_means2D, d_colors, d_opac, d_means3D, d_cov3D, d_sh, d_scales, d_rots = _C.rasterize_gaussians_backward(
             rs.bg, *_hierarchy(rs), means3D, radii, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
             cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_color, grad_invdepth, sh,
-            rs.sh_degree, rs.campos, geom_buf, ctx.num_rendered, binning_buf, img_buf, rs.debug)
-        # same order as the forward inputs; raster_settings gets None
-        return d_means3D, d_means2D, d_sh, d_colors, d_opac, d_scales, d_rots, d_cov3D, None
+            rs.sh_degree, rs.campos, geom_buf, ctx.num_rendered, binning_buf, img_buf, rs.debug,
+            need_cov3D=cov3Ds_precomp.numel() > 0)
+        # same order as the forward inputs; raster_settings gets None (and an empty cov3Ds_precomp no gradient: the
+        # library then skips the 24 B per Gaussian of dL/dcov3D rows nothing would read)
+        return (d_means3D, d_means2D, d_sh, d_colors, d_opac, d_scales, d_rots,
+                d_cov3D if cov3Ds_precomp.numel() > 0 else None, None)
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,

@@ -106,6 +106,8 @@ _SIGS = {
     "hlgs_copy_rows": (_i, [_i, C.POINTER(RowCopy), C.c_int64, _vp, _vp, _vp]),
     "hlgs_copy_rows_packed": (_i, [_i, C.POINTER(RowCopy), C.c_int64, _vp, _vp, _vp, C.c_int64, _i, _vp]),
     "hlgs_load_rows_packed": (_i, [_i, C.POINTER(RowCopy), C.c_int64, _vp, _vp, _vp, C.c_int64, _vp]),
+    "hlgs_activate_forward": (_i, [C.c_int64] + [_vp] * 7),
+    "hlgs_activate_backward": (_i, [C.c_int64] + [_vp] * 10),
     "hlgs_adam_step": (_i, [_i, C.POINTER(AdamTensor), C.c_int64, _i, C.c_double, C.c_double, C.c_double, _vp]),
     "hlgs_spt_build": (_i, [_i, _vp, _vp, _vp, _i, _f, _f, _i, _i, C.POINTER(_vp)]),
     "hlgs_spt_result_sizes": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),

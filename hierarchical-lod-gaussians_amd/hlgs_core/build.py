@@ -10,7 +10,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 OBJDIR = os.path.join(PKG, "build", "obj")
 LIB = os.path.join(LIBDIR, "libhlgs.so")
-SOURCES = ["scan.hip", "preprocess.hip", "raster_fwd.hip", "raster_bwd.hip", "gauss_bwd.hip", "lod.hip", "optim.hip", "loss.hip", "stream.hip", "capi.hip", "hier_io.cpp", "spt_build.cpp"]
+SOURCES = ["scan.hip", "preprocess.hip", "raster_fwd.hip", "raster_bwd.hip", "gauss_bwd.hip", "lod.hip", "optim.hip", "act.hip", "loss.hip", "stream.hip", "capi.hip", "hier_io.cpp", "spt_build.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HLGS_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-Wall",

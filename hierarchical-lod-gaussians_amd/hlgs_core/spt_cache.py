@@ -212,6 +212,7 @@ class SPTCache:
         self.wb_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
         self.wb_done = None
         self._wb_hold = None
+        self._wb_pending = None  # this step's write-back, launched when the next step starts (_flush_write_back)
         self._cut = self._cut_scratch = self._cut_count = None
         self.prev_SPT_indices = torch.empty(0, dtype=torch.int32, device=dev)
         self.prev_SPT_distances = torch.empty(0, dtype=torch.float32, device=dev)
@@ -333,6 +334,9 @@ class SPTCache:
     def step(self, full_proj_transform, camera_center, views=None):
         """views: the camera(s) of this step as dicts (W, H, tanfovx, tanfovy, viewmatrix, projmatrix, campos), needed
         only with occlusion_culling (the cull renders the cut's upper-tree Gaussians)."""
+        # the previous step's write-back crosses the host link now, beside this step's coarse cut and bookkeeping (the
+        # GPU is mostly idle there, waiting on host work); its rows are read again at the earliest by this step's load
+        self._flush_write_back()
         dm = 1.0
         while True:
             pl = self.plan(full_proj_transform, camera_center, dm, views)
@@ -354,18 +358,6 @@ class SPTCache:
         wb = pl["write_back_rows"]
         cur = torch.cuda.current_stream(self.device)
         prev_wb, prev_hold = self.wb_done, self._wb_hold
-        # write the evicted rows back to storage (:439-444, :473-474), on the write-back stream: nothing in this step
-        # reads those host rows (the rows it loads again come from their resident rows, below)
-        if wb.numel():
-            self.wb_stream.wait_stream(cur)
-            with torch.cuda.stream(self.wb_stream):
-                copy_rows_packed([d.detach() for d in dev_t], wb.numel(), wb, pl["write_back_indices"], self.host,
-                                 to_host=True)
-                self.wb_done = torch.cuda.Event()
-                self.wb_done.record(self.wb_stream)
-            # the write-back's inputs stay referenced until the next step has waited for it (then their memory
-            # may go back to this stream's allocations)
-            self._wb_hold = (dev_t, wb, pl["write_back_indices"])
         nk = pl["keep_rows"].numel()
         load = pl["load_from_disk_indices"]
         rows = nk + load.numel()
@@ -387,17 +379,45 @@ class SPTCache:
             self.resident_of[wbi] = wb
             load_rows_packed([n[nk:] for n in new_t], load.numel(), load, self.host, [d.detach() for d in dev_t],
                              self.resident_of)
-            self.resident_of[wbi] = -1
+            # index_fill_ takes the scalar as a kernel argument; `resident_of[wbi] = -1` copied a CPU scalar tensor
+            # to the device first, a synchronous copy that waited for the compaction and the load (~100 us per step)
+            self.resident_of.index_fill_(0, wbi, -1)
         else:
             load_rows_packed([n[nk:] for n in new_t], load.numel(), load, self.host)
+        # the evicted rows go back to storage (:439-444, :473-474) on the write-back stream when the next step starts
+        # (_flush_write_back).  Their values are final: these tensors are no longer trained.  A write-back reading HBM
+        # while writing over the host link slows whatever memory-bound kernel runs beside it (measured: the
+        # compaction 185 -> 280 us, the rasterizer's preprocess 73 -> 190-240 us, at 32-128 workgroups alike), so it
+        # runs where the GPU mostly waits on the host.  Nothing in this step reads those host rows (the rows it loads
+        # again came from their resident rows, above); the next step's load waits for it (wb_done).
+        if wb.numel():
+            self._wb_pending = (dev_t, wb, pl["write_back_indices"])
         k6 = len(NAMES)
         self.params = {k: new_t[i].requires_grad_(True) for i, k in enumerate(NAMES)}
         self.exp_avgs = {k: new_t[k6 + i] for i, k in enumerate(NAMES)}
         self.exp_avg_sqs = {k: new_t[2 * k6 + i] for i, k in enumerate(NAMES)}
 
+    def _flush_write_back(self):
+        """Launch the pending write-back of the last step on the write-back stream (behind everything queued on the
+        current stream so far); wb_done marks its end."""
+        if self._wb_pending is None:
+            return
+        dev_t, wb, idx = self._wb_pending
+        self._wb_pending = None
+        cur = torch.cuda.current_stream(self.device)
+        self.wb_stream.wait_stream(cur)
+        with torch.cuda.stream(self.wb_stream):
+            copy_rows_packed([d.detach() for d in dev_t], wb.numel(), wb, idx, self.host, to_host=True)
+            self.wb_done = torch.cuda.Event()
+            self.wb_done.record(self.wb_stream)
+        # the write-back's inputs stay referenced until a later step has waited for it (then their memory may go
+        # back to this stream's allocations)
+        self._wb_hold = (dev_t, wb, idx)
+
     def sync_storage(self):
         """Wait until the last write-back has landed in host storage.  Call before reading self.storage /
         self.opt_storage on the host (the reference's write-back is a synchronous .cpu() copy)."""
+        self._flush_write_back()
         if self.wb_done is not None:
             self.wb_done.synchronize()
 

@@ -98,7 +98,7 @@ typedef struct hlgs_grads {
     float* dcolor;    /* P_full x 3 */
     float* dopacity;  /* P_full */
     float* dmean3D;   /* P_full x 3 */
-    float* dcov3D;    /* P_full x 6 */
+    float* dcov3D;    /* P_full x 6, or NULL: not written (a caller without cov3D_precomp has nothing to return it for) */
     float* dsh;       /* P_full x M x 3 (may be NULL when M == 0) */
     float* dscale;    /* P_full x 3 */
     float* drot;      /* P_full x 4 */
@@ -398,6 +398,16 @@ typedef struct hlgs_adam_tensor {
 } hlgs_adam_tensor;
 int hlgs_adam_step(int T, const hlgs_adam_tensor* tensors, int64_t step, int skybox_rows, double beta1, double beta2,
                    double eps, void* stream);
+/* The activations render() reads (scene/gaussian_model.py:44-56: get_opacity = sigmoid(_opacity), get_scaling =
+ * exp(_scaling), get_rotation = normalize(_rotation), eps 1e-12) over n resident rows in one pass: opacity_raw n,
+ * scaling_raw n x 3, rotation_raw n x 4 (16-byte aligned) -> opacity, scales, rotations (same shapes). */
+int hlgs_activate_forward(int64_t n, const float* opacity_raw, const float* scaling_raw, const float* rotation_raw,
+                          float* opacity, float* scales, float* rotations, void* stream);
+/* Their gradients in one pass: d_opacity_raw = g (1 - o) o, d_scaling_raw = g s, d_rotation_raw through the norm.
+ * opacity / scales are the forward's outputs; any (g, d) pair may be NULL to skip that tensor. */
+int hlgs_activate_backward(int64_t n, const float* opacity, const float* scales, const float* rotation_raw,
+                           const float* g_opacity, const float* g_scales, const float* g_rotations, float* d_opacity_raw,
+                           float* d_scaling_raw, float* d_rotation_raw, void* stream);
 
 /* ---- photometric losses of the training step (utils/loss_utils.py:17-63, train_single.py:106-121,
  *      train_post.py:558-559 with the un-vendored fused_ssim) ---- */

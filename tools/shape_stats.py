@@ -48,6 +48,7 @@ def main(P=1_000_000, W=1920, H=1080, stride=1):
     ly = ly.ravel()
     shapes = {"quad": (lx >= 8) + 2 * (ly >= 8), "strip": ly // 4, "col": lx // 4}
     tot = {k: 0 for k in shapes}
+    sets = np.zeros(16, np.int64)  # quadrant layout: instances by visited-quadrant set (bit k = quadrant k)
     fwd = {k: 0 for k in shapes}
     valid_n = 0
     CH = 20_000
@@ -65,15 +66,25 @@ def main(P=1_000_000, W=1920, H=1080, stride=1):
         last = np.where(inside, ncon[np.minimum(py, H - 1), np.minimum(px, W - 1)], 0)
         valid_n += int((foot & (li[s:e, None] < last)).sum())
         for name, blk in shapes.items():
+            vset = np.zeros(e - s, np.int64)
             for k in range(4):
                 m = blk[None, :] == k
                 bl = np.where(m, last, 0).max(1)
                 bf = (foot & m).any(1)
-                tot[name] += int((bf & (li[s:e, None] < bl)).sum())
+                vk = bf & (li[s:e] < bl)
+                tot[name] += int(vk.sum())
+                vset |= vk.astype(np.int64) << k
+            if name == "quad":
+                sets += np.bincount(vset, minlength=16)
                 fwd[name] += int(bf.sum())  # the forward's waves visit every splat that reaches them (until done)
     out = {"R_binned_sampled": Rb, "tile_stride": stride, "valid_pairs": valid_n}
     for name in shapes:
         out[name] = {"bwd_passes": tot[name], "fwd_visits_upper": fwd[name], "lane_use": valid_n / (64 * tot[name])}
+    out["quad_visit_sets"] = {format(k, "04b")[::-1]: int(sets[k]) for k in range(16)}  # string: quadrants 0..3
+    out["quad_pairs"] = {"h01": int(sum(sets[k] for k in range(16) if k & 3 == 3)),
+                         "h23": int(sum(sets[k] for k in range(16) if k & 12 == 12)),
+                         "v02": int(sum(sets[k] for k in range(16) if k & 5 == 5)),
+                         "v13": int(sum(sets[k] for k in range(16) if k & 10 == 10))}
     print(out)
 
 
