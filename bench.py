@@ -541,9 +541,10 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
         img, radii, invd = GaussianRasterizer(s)(
             means3D=p["xyz"], means2D=means2D, dc=p["f_dc"], shs=p["f_rest"], opacities=opac, scales=scales,
             rotations=rots)
-        img = img.clamp(0, 1)
         e[2].record()
-        loss = (photometric_loss(img, gt, 0.2, invd, mono, mask, 0.5) if depth else photometric_loss(img, gt, 0.2))[0]
+        # the renderer's rendered_image.clamp(0, 1) folded into the loss kernels (clamp_image)
+        loss = (photometric_loss(img, gt, 0.2, invd, mono, mask, 0.5, clamp_image=True) if depth else
+                photometric_loss(img, gt, 0.2, clamp_image=True))[0]
         e[3].record()
         loss.backward()
         e[4].record()

@@ -57,9 +57,9 @@ void launch_relocation(int P, const float* oo, const float* so, const int* N, co
                        float* on, float* sn, hipStream_t s);
 size_t ssim_partials(int C, int H, int W);
 void launch_ssim_forward(int C, int H, int W, const float* img1, const float* img2, int valid, float* abc,
-                         float* partial, float* out, hipStream_t s);
+                         float* partial, float* out, hipStream_t s, bool clamp1);
 void launch_ssim_backward(int C, int H, int W, const float* img1, const float* img2, const float* abc,
-                          const float* coef, float* grad1, hipStream_t s);
+                          const float* coef, float* grad1, hipStream_t s, bool clamp1);
 int depth_l1_blocks(long n);
 void launch_depth_l1_forward(long n, const float* inv, const float* mono, const float* mask, float* partial,
                              float* out, hipStream_t s);
@@ -1068,27 +1068,43 @@ size_t hlgs_ssim_scratch_size(int C, int H, int W)
     return align_up(2 * sizeof(float) * ssim_partials(C, H, W)) + kAlign;
 }
 
-int hlgs_ssim_forward(int C, int H, int W, const float* img1, const float* img2, int valid, float* dmaps,
-                      void* scratch, float* out, void* stream)
+int hlgs_ssim_forward_ex(int C, int H, int W, const float* img1, const float* img2, int flags, float* dmaps,
+                         void* scratch, float* out, void* stream)
 {
+    const int valid = flags & HLGS_SSIM_VALID;
     if (C <= 0 || H <= 0 || W <= 0) return fail(HLGS_ERR_ARG, "empty image");
+    if (flags & ~(HLGS_SSIM_VALID | HLGS_SSIM_CLAMP1)) return fail(HLGS_ERR_ARG, "unknown SSIM flags");
     if (valid && (H <= 10 || W <= 10)) return fail(HLGS_ERR_ARG, "padding='valid' needs images larger than 10x10");
     if (!img1 || !img2 || !scratch || !out) return fail(HLGS_ERR_ARG, "missing tensor");
     hipStream_t s = (hipStream_t)stream;
     hipGetLastError();
-    launch_ssim_forward(C, H, W, img1, img2, valid, dmaps, static_cast<float*>(aligned(scratch)), out, s);
+    launch_ssim_forward(C, H, W, img1, img2, valid, dmaps, static_cast<float*>(aligned(scratch)), out, s,
+                        (flags & HLGS_SSIM_CLAMP1) != 0);
     return check_stage(s, false, "ssim_forward");
+}
+
+int hlgs_ssim_forward(int C, int H, int W, const float* img1, const float* img2, int valid, float* dmaps,
+                      void* scratch, float* out, void* stream)
+{
+    return hlgs_ssim_forward_ex(C, H, W, img1, img2, valid ? HLGS_SSIM_VALID : 0, dmaps, scratch, out, stream);
+}
+
+int hlgs_ssim_backward_ex(int C, int H, int W, const float* img1, const float* img2, int flags, const float* dmaps,
+                          const float* coef, float* grad_img1, void* stream)
+{
+    if (C <= 0 || H <= 0 || W <= 0) return fail(HLGS_ERR_ARG, "empty image");
+    if (flags & ~(HLGS_SSIM_VALID | HLGS_SSIM_CLAMP1)) return fail(HLGS_ERR_ARG, "unknown SSIM flags");
+    if (!img1 || !img2 || !dmaps || !coef || !grad_img1) return fail(HLGS_ERR_ARG, "missing tensor");
+    hipStream_t s = (hipStream_t)stream;
+    hipGetLastError();
+    launch_ssim_backward(C, H, W, img1, img2, dmaps, coef, grad_img1, s, (flags & HLGS_SSIM_CLAMP1) != 0);
+    return check_stage(s, false, "ssim_backward");
 }
 
 int hlgs_ssim_backward(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
                        const float* coef, float* grad_img1, void* stream)
 {
-    if (C <= 0 || H <= 0 || W <= 0) return fail(HLGS_ERR_ARG, "empty image");
-    if (!img1 || !img2 || !dmaps || !coef || !grad_img1) return fail(HLGS_ERR_ARG, "missing tensor");
-    hipStream_t s = (hipStream_t)stream;
-    hipGetLastError();
-    launch_ssim_backward(C, H, W, img1, img2, dmaps, coef, grad_img1, s);
-    return check_stage(s, false, "ssim_backward");
+    return hlgs_ssim_backward_ex(C, H, W, img1, img2, 0, dmaps, coef, grad_img1, stream);
 }
 
 size_t hlgs_depth_l1_scratch_size(int64_t n)

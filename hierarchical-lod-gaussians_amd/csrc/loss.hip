@@ -111,7 +111,11 @@ __device__ __forceinline__ void col_sums8(const float* hs_m, const Win11& win, i
 }
 
 // SSIM forward.  partial[2 * block] = (sum of the SSIM map over counted pixels, sum |x - y|).
-template <bool TRAIN>
+// CLAMP: img1 enters as clamp(img1, 0, 1) -- the rendered_image.clamp(0, 1) of the reference's renderers
+// (gaussian_renderer/__init__.py:142, 612) folded into the loss's own loads; NaN stays NaN, as torch.clamp keeps it.
+__device__ __forceinline__ float clamp01(float v) { return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
+
+template <bool TRAIN, bool CLAMP>
 __global__ void __launch_bounds__(kQThreads) k_ssim_fwd(int H, int W, const float* __restrict__ img1,
                                                         const float* __restrict__ img2, int valid, Win11 win,
                                                         float* __restrict__ abc, float* __restrict__ partial)
@@ -130,6 +134,10 @@ __global__ void __launch_bounds__(kQThreads) k_ssim_fwd(int H, int W, const floa
         float u[kQIn], v[kQIn], f[kQIn];
         load_run26(x, H, W, gy, xs, u);
         load_run26(y, H, W, gy, xs, v);
+        if (CLAMP) {
+#pragma unroll
+            for (int i = 0; i < kQIn; i++) u[i] = clamp01(u[i]);
+        }
         float* row = &hs[0][r * kQS + c0];
         row_sums16(u, win, row);
         row_sums16(v, win, row + kQRows * kQS);
@@ -164,7 +172,7 @@ __global__ void __launch_bounds__(kQThreads) k_ssim_fwd(int H, int W, const floa
             const float cc = mu1_sq + mu2_sq + kC1, d = s11 + s22 + kC2;
             const float fm = (a * b) / (cc * d);
             if (counted) s_map += fm;
-            s_l1 += fabsf(x[pid] - y[pid]);
+            s_l1 += fabsf((CLAMP ? clamp01(x[pid]) : x[pid]) - y[pid]);
             if (TRAIN) {
                 float A = 0.f, B = 0.f, C = 0.f;
                 if (counted) {
@@ -198,7 +206,9 @@ __global__ void __launch_bounds__(kQThreads) k_ssim_fwd(int H, int W, const floa
     }
 }
 
-// grad1 = coef[0] * dSSIM-map-sum/dx + coef[1] * sign(x - y)  (coefficients on the device: no host sync).
+// grad1 = coef[0] * dSSIM-map-sum/dx + coef[1] * sign(x - y)  (coefficients on the device: no host sync).  CLAMP: x is
+// clamp(img1, 0, 1) and the gradient passes only where 0 <= img1 <= 1 (torch's clamp backward; 0 elsewhere and at NaN).
+template <bool CLAMP>
 __global__ void __launch_bounds__(kQThreads) k_ssim_bwd(int H, int W, const float* __restrict__ img1,
                                                         const float* __restrict__ img2, const float* __restrict__ abc,
                                                         Win11 win, const float* __restrict__ coef,
@@ -233,11 +243,13 @@ __global__ void __launch_bounds__(kQThreads) k_ssim_bwd(int H, int W, const floa
         const int py = y0 + kQR * q + jj;
         if (py >= H) break;
         const size_t pid = (size_t)ch * HW + (size_t)py * W + px;
-        const float xv = img1[pid], yv = img2[pid];
+        const float raw = img1[pid], yv = img2[pid];
+        const float xv = CLAMP ? clamp01(raw) : raw;
         const float dssim = g[0][jj] + 2.f * xv * g[1][jj] + yv * g[2][jj];
         const float diff = xv - yv;
         const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);  // torch.abs backward: sign, 0 at 0
-        grad1[pid] = c0 * dssim + c1 * sgn;
+        const float gv = c0 * dssim + c1 * sgn;
+        grad1[pid] = !CLAMP || (raw >= 0.f && raw <= 1.f) ? gv : 0.f;
     }
 }
 
@@ -316,14 +328,15 @@ size_t ssim_partials(int C, int H, int W)
 }
 
 void launch_ssim_forward(int C, int H, int W, const float* img1, const float* img2, int valid, float* abc,
-                         float* partial, float* out, hipStream_t s)
+                         float* partial, float* out, hipStream_t s, bool clamp1)
 {
     const dim3 g = ssim_grid(C, H, W);
     const Win11 w = gauss_window();
-    if (abc)
-        hipLaunchKernelGGL(k_ssim_fwd<true>, g, dim3(kQThreads), 0, s, H, W, img1, img2, valid, w, abc, partial);
-    else
-        hipLaunchKernelGGL(k_ssim_fwd<false>, g, dim3(kQThreads), 0, s, H, W, img1, img2, valid, w, abc, partial);
+#define HLGS_SSIMF(TR, CL) hipLaunchKernelGGL((k_ssim_fwd<TR, CL>), g, dim3(kQThreads), 0, s, H, W, img1, img2, valid, w, \
+                                              abc, partial)
+    if (abc) { if (clamp1) HLGS_SSIMF(true, true); else HLGS_SSIMF(true, false); }
+    else { if (clamp1) HLGS_SSIMF(false, true); else HLGS_SSIMF(false, false); }
+#undef HLGS_SSIMF
     const double n_map = valid ? (double)C * (H - 2 * kHalo) * (W - 2 * kHalo) : (double)C * H * W;
     const double n_all = (double)C * H * W;
     hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(1024), 0, s, (int)(g.x * g.y * g.z), 2, partial, 1.0 / n_map,
@@ -331,10 +344,14 @@ void launch_ssim_forward(int C, int H, int W, const float* img1, const float* im
 }
 
 void launch_ssim_backward(int C, int H, int W, const float* img1, const float* img2, const float* abc,
-                          const float* coef, float* grad1, hipStream_t s)
+                          const float* coef, float* grad1, hipStream_t s, bool clamp1)
 {
-    hipLaunchKernelGGL(k_ssim_bwd, ssim_grid(C, H, W), dim3(kQThreads), 0, s, H, W, img1, img2, abc, gauss_window(), coef,
-                       grad1);
+    if (clamp1)
+        hipLaunchKernelGGL(k_ssim_bwd<true>, ssim_grid(C, H, W), dim3(kQThreads), 0, s, H, W, img1, img2, abc,
+                           gauss_window(), coef, grad1);
+    else
+        hipLaunchKernelGGL(k_ssim_bwd<false>, ssim_grid(C, H, W), dim3(kQThreads), 0, s, H, W, img1, img2, abc,
+                           gauss_window(), coef, grad1);
 }
 
 int depth_l1_blocks(long n) { return (int)std::min<long>(2048, (n + 255) / 256); }

@@ -117,6 +117,8 @@ _SIGS = {
     "hlgs_ssim_scratch_size": (_sz, [_i, _i, _i]),
     "hlgs_ssim_forward": (_i, [_i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "hlgs_ssim_backward": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "hlgs_ssim_forward_ex": (_i, [_i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
+    "hlgs_ssim_backward_ex": (_i, [_i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "hlgs_depth_l1_scratch_size": (_sz, [C.c_int64]),
     "hlgs_depth_l1_forward": (_i, [C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hlgs_depth_l1_backward": (_i, [C.c_int64, _vp, _vp, _vp, _vp, _vp, _vp]),

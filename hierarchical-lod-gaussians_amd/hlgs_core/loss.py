@@ -25,7 +25,7 @@ def _planes(t):
     return t, t.numel() // (H * W), H, W
 
 
-def _ssim_forward(img1, img2, valid, train):
+def _ssim_forward(img1, img2, valid, train, clamp1=False):
     lib = L.load()
     x, Cn, H, W = _planes(img1)
     y, Cy, Hy, Wy = _planes(img2.detach())
@@ -35,17 +35,18 @@ def _ssim_forward(img1, img2, valid, train):
     out = torch.empty(2, dtype=torch.float32, device=x.device)
     maps = torch.empty((Cn, 3, H, W), dtype=torch.float32, device=x.device) if train else None
     scratch = torch.empty(lib.hlgs_ssim_scratch_size(Cn, H, W), dtype=torch.uint8, device=x.device)
-    L.check(lib.hlgs_ssim_forward(Cn, H, W, L.ptr(x), L.ptr(y), int(bool(valid)), L.ptr(maps), L.ptr(scratch),
-                                  L.ptr(out), L.stream()))
+    flags = (1 if valid else 0) | (2 if clamp1 else 0)  # HLGS_SSIM_VALID, HLGS_SSIM_CLAMP1
+    L.check(lib.hlgs_ssim_forward_ex(Cn, H, W, L.ptr(x), L.ptr(y), flags, L.ptr(maps), L.ptr(scratch), L.ptr(out),
+                                     L.stream()))
     return out, x, y, maps, (Cn, H, W)
 
 
-def _ssim_backward(x, y, maps, shape, coef):
+def _ssim_backward(x, y, maps, shape, coef, clamp1=False):
     lib = L.load()
     Cn, H, W = shape
     grad = torch.empty_like(x)
-    L.check(lib.hlgs_ssim_backward(Cn, H, W, L.ptr(x), L.ptr(y), L.ptr(maps), L.ptr(coef.contiguous()), L.ptr(grad),
-                                   L.stream()))
+    L.check(lib.hlgs_ssim_backward_ex(Cn, H, W, L.ptr(x), L.ptr(y), 2 if clamp1 else 0, L.ptr(maps),
+                                      L.ptr(coef.contiguous()), L.ptr(grad), L.stream()))
     return grad
 
 
@@ -92,9 +93,10 @@ def l1_loss(network_output, gt):
 
 class _Photometric(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, image, gt, invdepth, mono, mask, lambda_dssim, depth_weight):
+    def forward(ctx, image, gt, invdepth, mono, mask, lambda_dssim, depth_weight, clamp_image):
         train = image.requires_grad or (invdepth is not None and invdepth.requires_grad)
-        out, x, y, maps, shape = _ssim_forward(image, gt, False, train)
+        out, x, y, maps, shape = _ssim_forward(image, gt, False, train, clamp_image)
+        ctx.clamp_image = clamp_image
         Ll1, ssim_v = out[1], out[0]
         loss = (1.0 - lambda_dssim) * Ll1 + lambda_dssim * (1.0 - ssim_v)
         Ld = torch.zeros((), dtype=torch.float32, device=x.device)
@@ -128,7 +130,7 @@ class _Photometric(torch.autograd.Function):
         n = Cn * H * W
         g = g.float()
         coef = torch.stack([g * (-lam / n), g * ((1.0 - lam) / n)])
-        d_img = _ssim_backward(x, y, maps, shape, coef).reshape(ishape)
+        d_img = _ssim_backward(x, y, maps, shape, coef, ctx.clamp_image).reshape(ishape)
         d_inv = None
         if ctx.dep is not None:
             lib = L.load()
@@ -138,11 +140,14 @@ class _Photometric(torch.autograd.Function):
             L.check(lib.hlgs_depth_l1_backward(inv.numel(), L.ptr(inv), L.ptr(mo), L.ptr(mk), L.ptr(c), L.ptr(d_inv),
                                                L.stream()))
             d_inv = d_inv.reshape(dshape)
-        return d_img, None, d_inv, None, None, None, None
+        return d_img, None, d_inv, None, None, None, None, None
 
 
-def photometric_loss(image, gt, lambda_dssim, invdepth=None, mono_invdepth=None, depth_mask=None, depth_weight=0.0):
+def photometric_loss(image, gt, lambda_dssim, invdepth=None, mono_invdepth=None, depth_mask=None, depth_weight=0.0,
+                     clamp_image=False):
     """-> (loss, Ll1, SSIM, Ll1depth_pure): the training loss of train_single.py:106-118 (and, without the depth
     term, train_post.py:558-559) with L1, SSIM and the depth L1 computed by two fused HIP passes; `loss` is
-    differentiable w.r.t. image and invdepth."""
-    return _Photometric.apply(image, gt, invdepth, mono_invdepth, depth_mask, float(lambda_dssim), float(depth_weight))
+    differentiable w.r.t. image and invdepth.  clamp_image=True is photometric_loss(image.clamp(0, 1), ...) -- the
+    renderers' rendered_image.clamp(0, 1) (gaussian_renderer/__init__.py:142, 612) -- folded into the same passes."""
+    return _Photometric.apply(image, gt, invdepth, mono_invdepth, depth_mask, float(lambda_dssim), float(depth_weight),
+                              bool(clamp_image))

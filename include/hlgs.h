@@ -423,6 +423,16 @@ int hlgs_ssim_forward(int C, int H, int W, const float* img1, const float* img2,
  * the upstream gradient never needs a host read. */
 int hlgs_ssim_backward(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
                        const float* coef, float* grad_img1, void* stream);
+/* The same two with flags: HLGS_SSIM_VALID (= valid above) and HLGS_SSIM_CLAMP1 -- img1 enters as clamp(img1, 0, 1),
+ * the rendered_image.clamp(0, 1) of the reference's renderers (gaussian_renderer/__init__.py:142, 612) folded into
+ * the loss: the forward reads the clamped values, the backward gradient passes only where 0 <= img1 <= 1 (torch's
+ * clamp backward), so the two clamp kernels of each direction disappear.  Pass the same flags to both. */
+#define HLGS_SSIM_VALID 1
+#define HLGS_SSIM_CLAMP1 2
+int hlgs_ssim_forward_ex(int C, int H, int W, const float* img1, const float* img2, int flags, float* dmaps,
+                         void* scratch, float* out, void* stream);
+int hlgs_ssim_backward_ex(int C, int H, int W, const float* img1, const float* img2, int flags, const float* dmaps,
+                          const float* coef, float* grad_img1, void* stream);
 /* Depth term of train_single.py:111-118: out[0] = mean |(invdepth - mono) * mask| over n values (mask may be
  * NULL); backward grad = coef[0] * sign((invdepth - mono) * mask) * mask. */
 size_t hlgs_depth_l1_scratch_size(int64_t n);

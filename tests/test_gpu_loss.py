@@ -77,3 +77,25 @@ def test_fused_ssim_is_deterministic_and_train_false_has_no_grad():
     assert abs(float(s) - vals[0]) <= 1e-6
     with pytest.raises(RuntimeError, match="train=False"):
         s.backward()
+
+
+@pytest.mark.parametrize("depth", [False, True])
+def test_photometric_clamp_image_equals_clamp_then_loss(depth):
+    """photometric_loss(img, ..., clamp_image=True) is photometric_loss(img.clamp(0, 1), ...) bit for bit -- the loss
+    and the gradient reaching img, including pixels outside [0, 1] (gradient 0 there, torch's clamp backward)."""
+    from hlgs_core.loss import photometric_loss
+    g = torch.Generator().manual_seed(7)
+    img = (torch.rand(3, 70, 90, generator=g) * 1.6 - 0.3).to("cuda")  # ~35% of the values outside [0, 1]
+    gt = torch.rand(3, 70, 90, generator=g).to("cuda")
+    inv = torch.rand(1, 70, 90, generator=g).to("cuda").requires_grad_(True) if depth else None
+    mono = torch.rand(1, 70, 90, generator=g).to("cuda") if depth else None
+    a = img.clone().requires_grad_(True)
+    b = img.clone().requires_grad_(True)
+    kw = dict(invdepth=inv, mono_invdepth=mono, depth_weight=0.5) if depth else {}
+    la = photometric_loss(a, gt, 0.2, clamp_image=True, **kw)[0]
+    lb = photometric_loss(b.clamp(0, 1), gt, 0.2, **kw)[0]
+    assert float(la) == float(lb)
+    la.backward()
+    lb.backward()
+    assert torch.equal(a.grad, b.grad)
+    assert (a.grad[(img < 0) | (img > 1)] == 0).all()
