@@ -546,6 +546,9 @@ def bench_config5(P, dev, steps=20, sh_degree=1, depth=True, W=1920, H=1080, ran
         loss = (photometric_loss(img, gt, 0.2, invd, mono, mask, 0.5, clamp_image=True) if depth else
                 photometric_loss(img, gt, 0.2, clamp_image=True))[0]
         e[3].record()
+        # the cache's write-back crosses the host link beside the backward (its blend kernel is VALU-bound) instead of
+        # beside the next step's bookkeeping
+        cache.flush_write_back()
         loss.backward()
         e[4].record()
         if ex is not None:

@@ -397,6 +397,13 @@ class SPTCache:
         self.exp_avgs = {k: new_t[k6 + i] for i, k in enumerate(NAMES)}
         self.exp_avg_sqs = {k: new_t[2 * k6 + i] for i, k in enumerate(NAMES)}
 
+    def flush_write_back(self):
+        """Launch the pending write-back of the last step() on the write-back stream, behind everything queued on the
+        current stream so far (wb_done marks its end).  Optional: the next step() (or sync_storage()) launches it
+        otherwise.  A training loop can call it where the GPU runs compute-bound work, e.g. just before
+        loss.backward(), whose blend backward is bound by VALU issue rather than by memory."""
+        self._flush_write_back()
+
     def _flush_write_back(self):
         """Launch the pending write-back of the last step on the write-back stream (behind everything queued on the
         current stream so far); wb_done marks its end."""
