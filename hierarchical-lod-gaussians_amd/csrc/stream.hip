@@ -716,10 +716,14 @@ void launch_rows_packed(int T, float* const* tabs, const int* words, int64_t n, 
         pt.res[t] = resident ? resident[t] : nullptr;
         pt.words[t] = words[t];
     }
-    constexpr int64_t kWriteBackBlocks = 128;
-    // 4 waves (rows) per block, grid-stride above.  The write-back is bound by the host link, not by waves: a
-    // small grid moves it as fast and leaves the CUs to the compaction and load running beside it (SPTCache).
-    // The load keeps the large grid: with 256 workgroups (fewer host reads in flight) it took 513 against 392 us
+    // 4 waves (rows) per block, grid-stride above.  The write-back's stores cross the host link, and while they are in
+    // flight every kernel beside it waits longer for memory -- a 4-element torch add beside it took 160 us, the
+    // rasterizer's preprocess 73 -> 190-240 us -- in proportion to how many of them are outstanding.  24 workgroups
+    // (96 waves) keep it at ~0.6 ms, inside the step it overlaps, with a small fraction of that pressure: config #5
+    // 2.30 ms per step at 128 workgroups, 2.13-2.16 at 16-24 (round 6, tools/c5_trace.sh; 8 workgroups took 1.5 ms
+    // and delayed the next step's load).  The load keeps the large grid: with 256 workgroups (fewer host reads in
+    // flight) it took 513 against 392 us.
+    constexpr int64_t kWriteBackBlocks = 24;
     const int64_t blocks = std::min<int64_t>((n + 3) / 4, to_host ? kWriteBackBlocks : 2048);
     if (blocks <= 0) return;
     if (to_host) hipLaunchKernelGGL(k_rows_packed<true>, dim3((unsigned)blocks), dim3(256), 0, s, pt, T, n, dev_rows, host_rows, host, hw, (const int*)nullptr);

@@ -213,6 +213,7 @@ class SPTCache:
         self.wb_done = None
         self._wb_hold = None
         self._wb_pending = None  # this step's write-back, launched when the next step starts (_flush_write_back)
+        self._row_shapes = self._widths = None  # per resident tensor: row shape and floats per row (fixed)
         self._cut = self._cut_scratch = self._cut_count = None
         self.prev_SPT_indices = torch.empty(0, dtype=torch.int32, device=dev)
         self.prev_SPT_distances = torch.empty(0, dtype=torch.float32, device=dev)
@@ -361,14 +362,23 @@ class SPTCache:
         nk = pl["keep_rows"].numel()
         load = pl["load_from_disk_indices"]
         rows = nk + load.numel()
-        # the eighteen new resident tensors carved from one allocation (each 256-byte aligned)
-        widths = [math.prod(d.shape[1:]) for d in dev_t]
+        # the eighteen new resident tensors carved from one allocation (each 256-byte aligned).  The compaction of the
+        # rows that stay (:446-479) is launched from the raw addresses first, and the eighteen tensor views are made
+        # while it runs: the views cost ~50 torch calls of host time, which the GPU otherwise waited through.
+        if self._row_shapes is None:
+            self._row_shapes = [tuple(d.shape[1:]) for d in dev_t]
+            self._widths = [math.prod(sh) for sh in self._row_shapes]
+        widths = self._widths
         lens = [(rows * w + 63) // 64 * 64 for w in widths]
         flat = torch.empty(sum(lens), dtype=torch.float32, device=self.device)
-        new_t = [part[:rows * w].view((rows,) + tuple(d.shape[1:]))
-                 for part, w, d in zip(flat.split(lens), widths, dev_t)]
-        # resident rows that stay, then the loaded rows (:446-479)
-        copy_rows([(d.detach(), n) for d, n in zip(dev_t, new_t)], nk, pl["keep_rows"], None)
+        if nk:
+            base, off = flat.data_ptr(), 0
+            tabs = (L.RowCopy * len(dev_t))()
+            for k, (d, w, ln) in enumerate(zip(dev_t, widths, lens)):
+                tabs[k] = L.RowCopy(d.data_ptr(), base + 4 * off, 4 * w)
+                off += ln
+            L.check(L.load().hlgs_copy_rows(len(dev_t), tabs, nk, _p(pl["keep_rows"]), None, L.stream()))
+        new_t = [part[:rows * w].view((rows,) + sh) for part, w, sh in zip(flat.split(lens), widths, self._row_shapes)]
         # rows written back above and loaded again (the upper-tree Gaussians, every step) come from their resident
         # rows, the rest over the host link once the previous step's write-back has landed
         if prev_wb is not None:
@@ -385,11 +395,12 @@ class SPTCache:
         else:
             load_rows_packed([n[nk:] for n in new_t], load.numel(), load, self.host)
         # the evicted rows go back to storage (:439-444, :473-474) on the write-back stream when the next step starts
-        # (_flush_write_back).  Their values are final: these tensors are no longer trained.  A write-back reading HBM
-        # while writing over the host link slows whatever memory-bound kernel runs beside it (measured: the
-        # compaction 185 -> 280 us, the rasterizer's preprocess 73 -> 190-240 us, at 32-128 workgroups alike), so it
-        # runs where the GPU mostly waits on the host.  Nothing in this step reads those host rows (the rows it loads
-        # again came from their resident rows, above); the next step's load waits for it (wb_done).
+        # (_flush_write_back), or earlier where the training loop calls flush_write_back().  Their values are final:
+        # these tensors are no longer trained.  A write-back writing over the host link slows whatever kernel runs
+        # beside it (at 128 workgroups: the compaction 185 -> 280 us, the rasterizer's preprocess 73 -> 190-240 us),
+        # so it runs on a small grid (csrc/stream.hip) and not beside the compaction.  Nothing in this step reads
+        # those host rows (the rows it loads again came from their resident rows, above); the next step's load waits
+        # for it (wb_done).
         if wb.numel():
             self._wb_pending = (dev_t, wb, pl["write_back_indices"])
         k6 = len(NAMES)
