@@ -307,12 +307,37 @@ __device__ __forceinline__ void sh_rows_load_contig(const float* gbase, float* l
     }
 }
 
+// Degree-3 rows (48 floats, 12 float4s) are staged unpadded, float4 q of row r at slot 12 r + (q ^ sh_swz(r)): the
+// staging stores (ds_write_b128, 8-lane groups), each lane's reads of its own row (ds_read_b128, 16-lane groups) and
+// a copy back out all hit distinct banks, where the odd 49-float stride takes four b32 stores and four b32 reads per
+// float4 with two-way store conflicts (a fifth of the kernel's LDS cycles were conflict cycles).
+__device__ __forceinline__ int sh_swz(int r) { return (r >> 2) & 3; }
+__device__ __forceinline__ void sh_rows_load_swz(const float* gbase, float* lds, int n, int lane)
+{
+    float4 v[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const int f = lane + 64 * k;
+        v[k] = f < n * 12 ? reinterpret_cast<const float4*>(gbase)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const int f = lane + 64 * k;
+        if (f < n * 12) {
+            const int r = f / 12, q = f - r * 12;
+            reinterpret_cast<float4*>(lds)[12 * r + (q ^ sh_swz(r))] = v[k];
+        }
+    }
+}
+
 template <bool ALT, int M3T, bool INTERP>  // INTERP = a.ts && a.kids, host-dispatched: its threshold bisection in
                                           // double would otherwise set the register budget (90 VGPRs against 67)
 __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom g, int* __restrict__ radii, int gx,
                                                         int gy, float fx, float fy, ZeroJob z)
 {
-    __shared__ float s_rows[64 * kShStride];  // the SH rows; after the second barrier the splat records' stage
+    constexpr bool SWZ = M3T == 48;           // degree-3 rows: unpadded, swizzled float4 slots (sh_rows_load_swz)
+    __shared__ __attribute__((aligned(16))) float s_rows[64 * (SWZ ? 48 : kShStride)];  // the SH rows; after the
+                                                                                         // second barrier the records' stage
     __shared__ float4 s_col[64];              // r, g, b, clamp bits
     __shared__ int s_need[64];
     __shared__ float s_jac[64 * 9];           // the direction Jacobians' stage
@@ -337,7 +362,8 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
         s_need[lane] = need;
     } else {
         const int n = min(64, a.P - t0);
-        sh_rows_load_contig<M3T>(a.shs + (size_t)t0 * M3, s_rows, n, lane, M3);
+        if constexpr (SWZ) sh_rows_load_swz(a.shs + (size_t)t0 * M3, s_rows, n, lane);
+        else sh_rows_load_contig<M3T>(a.shs + (size_t)t0 * M3, s_rows, n, lane, M3);
         // the colour's own inputs in the same round trip as the rows (not behind the barrier)
         if (live) {
             mean_r = mk(a.means3D[3 * t_idx], a.means3D[3 * t_idx + 1], a.means3D[3 * t_idx + 2]);
@@ -354,7 +380,20 @@ __global__ void __launch_bounds__(128) k_preprocess_sh2(hlgs_raster_args a, Geom
         if (s_need[lane]) {
             // coefficient c of this lane's row (the full index: the alt rasterizer's 0 is dc)
             const float* row = s_rows + lane * kShStride;
-            auto rowf = [&](int f) -> float { return row[f]; };
+            float rv[SWZ ? 48 : 1];  // SWZ: the lane's whole row, twelve ds_read_b128
+            if constexpr (SWZ) {
+                const float4* r4 = reinterpret_cast<const float4*>(s_rows) + 12 * lane;
+                const int sw = sh_swz(lane);
+#pragma unroll
+                for (int j = 0; j < 12; j++) {
+                    const float4 t = r4[(j & ~3) | ((j & 3) ^ sw)];
+                    rv[4 * j] = t.x; rv[4 * j + 1] = t.y; rv[4 * j + 2] = t.z; rv[4 * j + 3] = t.w;
+                }
+            }
+            auto rowf = [&](int f) -> float {
+                if constexpr (SWZ) return rv[f];
+                else return row[f];
+            };
             auto shv = [&](int c) {
                 if (ALT) return c == 0 ? dc0 : mk(rowf(3 * c - 3), rowf(3 * c - 2), rowf(3 * c - 1));
                 return mk(rowf(3 * c), rowf(3 * c + 1), rowf(3 * c + 2));
