@@ -847,9 +847,45 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
     }
 }
 
+// {a, b} = {x, x of lane l ^ PL} (in either order) for a 64-bit key, without the LDS: DPP within 16-lane rows for
+// PL = 1, 2 (quad_perm), 4 (row_ror:12 into banks 0 and 2, row_ror:4 into banks 1 and 3; row_ror:n reads lane l - n
+// of the row) and 8 (row_ror:8); permlane16 / permlane32 swaps of two copies for 16 and 32, which leave each lane its
+// own value in one register and its partner's in the other.  A compare-exchange only needs the pair's min and max, so
+// the order does not matter.  (ds_bpermute, which __shfl_xor compiles to, is an LDS round trip per 32-bit half.)
+template <int PL>
+__device__ __forceinline__ void lane_pair64(uint64_t x, uint64_t& a, uint64_t& b)
+{
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if constexpr (PL == 16 || PL == 32) {
+        const auto l = PL == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                                : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto h = PL == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                                : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        a = ((uint64_t)h[0] << 32) | l[0];
+        b = ((uint64_t)h[1] << 32) | l[1];
+    } else {
+        auto mv = [](uint32_t v) -> uint32_t {
+            if constexpr (PL == 1) return __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+            if constexpr (PL == 2) return __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+            if constexpr (PL == 8) return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+            const uint32_t t = __builtin_amdgcn_update_dpp(0u, v, 0x12C, 0xF, 0x5, false);            // row_ror:12
+            return __builtin_amdgcn_update_dpp(t, v, 0x124, 0xF, 0xA, false);                          // row_ror:4
+        };
+        a = x;
+        b = ((uint64_t)mv(hi) << 32) | mv(lo);
+    }
+}
+template <int PL>
+__device__ __forceinline__ uint64_t lane_cx64(uint64_t x, bool take_min)
+{
+    uint64_t a, b;
+    lane_pair64<PL>(x, a, b);
+    return ((a < b) == take_min) ? a : b;
+}
+
 // Per-tile sort of up to 64 * KPL keys by one wave, entirely in registers: lane l holds elements
 // l * KPL .. l * KPL + KPL - 1; bitonic stages with partner distance < KPL are compare-exchanges inside
-// a lane, longer ones exchange with lane l ^ (j / KPL).  No LDS, no barriers.
+// a lane, longer ones exchange with lane l ^ (j / KPL) (lane_pair64).  No LDS, no barriers.
 // The keys are read through ld (a KeyView: ld.entry(e), e < n, then ld.depth_bits(entry)), and each sorted key handed to
 // st(e, key).
 template <int KPL, typename LD, typename ST>
@@ -880,9 +916,15 @@ __device__ __forceinline__ void wave_sort_keys_st(LD&& ld, uint32_t n, ST&& st, 
                 for (int i = 0; i < KPL; i++) {
                     const uint32_t e = (uint32_t)lane * KPL + i;
                     const bool asc = (e & kk) == 0;
-                    const uint64_t y = __shfl_xor(v[i], pl, 64);
                     const bool take_min = lower == asc;
-                    v[i] = take_min ? (y < v[i] ? y : v[i]) : (y > v[i] ? y : v[i]);
+                    switch (pl) {  // a constant once the stages are unrolled
+                    case 1: v[i] = lane_cx64<1>(v[i], take_min); break;
+                    case 2: v[i] = lane_cx64<2>(v[i], take_min); break;
+                    case 4: v[i] = lane_cx64<4>(v[i], take_min); break;
+                    case 8: v[i] = lane_cx64<8>(v[i], take_min); break;
+                    case 16: v[i] = lane_cx64<16>(v[i], take_min); break;
+                    default: v[i] = lane_cx64<32>(v[i], take_min); break;
+                    }
                 }
             } else {
 #pragma unroll
