@@ -883,28 +883,13 @@ __device__ __forceinline__ uint64_t lane_cx64(uint64_t x, bool take_min)
     return ((a < b) == take_min) ? a : b;
 }
 
-// Per-tile sort of up to 64 * KPL keys by one wave, entirely in registers: lane l holds elements
-// l * KPL .. l * KPL + KPL - 1; bitonic stages with partner distance < KPL are compare-exchanges inside
-// a lane, longer ones exchange with lane l ^ (j / KPL) (lane_pair64).  No LDS, no barriers.
-// The keys are read through ld (a KeyView: ld.entry(e), e < n, then ld.depth_bits(entry)), and each sorted key handed to
-// st(e, key).
-template <int KPL, typename LD, typename ST>
-__device__ __forceinline__ void wave_sort_keys_st(LD&& ld, uint32_t n, ST&& st, int lane)
+// Per-tile sort of 64 * KPL keys by one wave, entirely in registers (~0 pads): afterwards lane l's slot i holds sorted
+// position l * KPL + i.  Bitonic stages with partner distance < KPL are compare-exchanges inside a lane, longer ones
+// exchange with lane l ^ (j / KPL) (lane_pair64).  No LDS, no barriers.  The keys may start in any lanes and slots.
+template <int KPL>
+__device__ __forceinline__ void wave_sort_regs(uint64_t (&v)[KPL], int lane)
 {
     constexpr uint32_t NP = 64u * KPL;
-    uint64_t v[KPL];
-    {
-        uint32_t en[KPL], dp[KPL];
-#pragma unroll
-        for (int i = 0; i < KPL; i++) en[i] = ld.entry(min((uint32_t)lane * KPL + i, n - 1));  // n >= 1
-#pragma unroll
-        for (int i = 0; i < KPL; i++) dp[i] = ld.depth_bits(en[i]);
-#pragma unroll
-        for (int i = 0; i < KPL; i++) {
-            const uint32_t e = (uint32_t)lane * KPL + i;
-            v[i] = e < n ? ((uint64_t)dp[i] << 32) | en[i] : ~0ull;
-        }
-    }
 #pragma unroll
     for (uint32_t kk = 2; kk <= NP; kk <<= 1) {
 #pragma unroll
@@ -941,41 +926,75 @@ __device__ __forceinline__ void wave_sort_keys_st(LD&& ld, uint32_t n, ST&& st, 
             }
         }
     }
+}
+// Keys l + 64 i (i < K, the ones below n) of the tile segment at base into v[i] of lane l: all of the lane's entries
+// are loaded first, then all of their depths (two rounds of independent loads, not an entry -> depth chain per key).
+// Consecutive lanes read consecutive entries.
+template <int K>
+__device__ __forceinline__ void wave_keys_load(const KeySrc& ks, uint32_t base, uint32_t n, uint64_t (&v)[K], int lane)
+{
+    uint32_t en[K], dp[K];
 #pragma unroll
-    for (int i = 0; i < KPL; i++) {
-        const uint32_t e = (uint32_t)lane * KPL + i;
-        if (e < n) st(e, v[i]);
+    for (int i = 0; i < K; i++) en[i] = ks.ents[base + min((uint32_t)lane + 64u * i, n - 1)];  // n >= 1
+#pragma unroll
+    for (int i = 0; i < K; i++) dp[i] = ks.depth_bits(en[i]);
+#pragma unroll
+    for (int i = 0; i < K; i++) v[i] = (uint32_t)lane + 64u * i < n ? ((uint64_t)dp[i] << 32) | en[i] : ~0ull;
+}
+// The first K slots of v sorted as 64 K keys (the ones from the strided load that reach m), stored by st(e, key) for e < m.
+template <int K, int KMAX, typename ST>
+__device__ __forceinline__ void wave_sort_first(const uint64_t (&v)[KMAX], uint32_t m, ST&& st, int lane)
+{
+    uint64_t w[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) w[i] = v[i];
+    wave_sort_regs<K>(w, lane);
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const uint32_t e = (uint32_t)lane * K + i;
+        if (e < m) st(e, w[i]);
     }
 }
-// ... with the entries (low words) written to out[0 .. n)
-template <int KPL, typename LD>
-__device__ __forceinline__ void wave_sort_keys(LD&& ld, uint32_t n, uint32_t* __restrict__ out, int lane)
-{
-    wave_sort_keys_st<KPL>(ld, n, [&](uint32_t e, uint64_t v) { out[e] = (uint32_t)v; }, lane);
-}
-// n <= 64 KMAX keys with the fewest keys per lane that hold them
-template <int KMAX, typename LD, typename ST>
-__device__ __forceinline__ void wave_sort_upto(LD&& ld, uint32_t n, ST&& st, int lane)
-{
-    if (n <= 64) { wave_sort_keys_st<1>(ld, n, st, lane); return; }
-    if constexpr (KMAX >= 2) if (n <= 128) { wave_sort_keys_st<2>(ld, n, st, lane); return; }
-    if constexpr (KMAX >= 4) if (n <= 256) { wave_sort_keys_st<4>(ld, n, st, lane); return; }
-    if constexpr (KMAX >= 8) if (n <= 512) { wave_sort_keys_st<8>(ld, n, st, lane); return; }
-    if constexpr (KMAX >= 16) wave_sort_keys_st<16>(ld, n, st, lane);
-}
-// n in (64 KH, 128 KH]: the first 64 KH keys sorted with KH keys per lane and the other n - 64 KH
-// with the fewest that hold them, both into LDS, then merged -- each lane finds the start of its run of ceil(n / 64)
-// outputs on the merge path (binary search) and merges the run.  A 300-key tile then costs a 256-key and a 64-key
-// register sort instead of a 512-key one (the mean configs[1] list is 258 keys).  Keys are unique, so the merge is
-// the same total order.
+// n in (64 KH, 128 KH]: the first A = 64 KH keys sorted with KH keys per lane and the other m = n - A with the fewest
+// that hold them, both into LDS, then merged -- each lane finds the start of its run of ceil(n / 64) outputs on the
+// merge path (binary search) and merges the run.  A 300-key tile then costs a 256-key and a 64-key register sort
+// instead of a 512-key one (the mean configs[1] list is 258 keys).  Both runs' keys are loaded before either is
+// sorted, so the wave waits for the entries and the depths once.  Keys are unique, so the merge is the same total order.
 template <int KH>
 __device__ __forceinline__ void wave_sort_split(const KeySrc& ks, uint32_t base, uint32_t n,
                                                 uint32_t* __restrict__ out, int lane, uint64_t* s)
 {
     constexpr uint32_t A = 64u * KH;
     const uint32_t m = n - A;  // 1 .. A
-    wave_sort_keys_st<KH>(KeyView{ks, base}, A, [&](uint32_t e, uint64_t v) { s[e] = v; }, lane);
-    wave_sort_upto<KH>(KeyView{ks, base + A}, m, [&](uint32_t e, uint64_t v) { s[A + e] = v; }, lane);
+    uint64_t va[KH], vb[KH];
+    {
+        uint32_t ea[KH], eb[KH], da[KH], db[KH];
+#pragma unroll
+        for (int i = 0; i < KH; i++) ea[i] = ks.ents[base + lane + 64u * i];
+#pragma unroll
+        for (int i = 0; i < KH; i++) eb[i] = ks.ents[base + A + min((uint32_t)lane + 64u * i, m - 1)];
+#pragma unroll
+        for (int i = 0; i < KH; i++) da[i] = ks.depth_bits(ea[i]);
+#pragma unroll
+        for (int i = 0; i < KH; i++) db[i] = ks.depth_bits(eb[i]);
+#pragma unroll
+        for (int i = 0; i < KH; i++) {
+            va[i] = ((uint64_t)da[i] << 32) | ea[i];
+            vb[i] = (uint32_t)lane + 64u * i < m ? ((uint64_t)db[i] << 32) | eb[i] : ~0ull;
+        }
+    }
+    wave_sort_regs<KH>(va, lane);
+#pragma unroll
+    for (int i = 0; i < KH; i++) s[(uint32_t)lane * KH + i] = va[i];
+    auto stb = [&](uint32_t e, uint64_t v) { s[A + e] = v; };
+    if (m <= 64) wave_sort_first<1>(vb, m, stb, lane);
+    else if constexpr (KH >= 2) {
+        if (m <= 128) wave_sort_first<2>(vb, m, stb, lane);
+        else if constexpr (KH >= 4) {
+            if (m <= 256) wave_sort_first<4>(vb, m, stb, lane);
+            else if constexpr (KH >= 8) wave_sort_first<8>(vb, m, stb, lane);
+        }
+    }
     __syncthreads();  // one wave: the LDS stores before the loads
     const uint32_t per = (n + 63u) / 64u, k0 = min(n, (uint32_t)lane * per), k1 = min(n, k0 + per);
     uint32_t lo = k0 > m ? k0 - m : 0u, hi = min(k0, A);  // A keys among the first k0 outputs
@@ -993,12 +1012,6 @@ __device__ __forceinline__ void wave_sort_split(const KeySrc& ks, uint32_t base,
         else j++;
     }
 }
-template <int KPL>
-__device__ __forceinline__ void wave_sort_tile(const KeySrc& ks, uint32_t* __restrict__ point_list, uint32_t base,
-                                               uint32_t n, int lane)
-{
-    wave_sort_keys<KPL>(KeyView{ks, base}, n, point_list + base, lane);
-}
 // Tiles of up to kWaveSortCap instances: one wave each (k_tile_sort handles the longer ones).
 __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__ ranges, KeySrc ks,
                                                        uint32_t* __restrict__ point_list, int T, Guard gd)
@@ -1010,7 +1023,12 @@ __global__ void __launch_bounds__(64) k_tile_sort_wave(const uint2* __restrict__
     const int lane = threadIdx.x;
     if (n == 0 || n > (uint32_t)kWaveSortCap) return;
     __shared__ uint64_t s_sort[kWaveSortCap + 1];  // + 1: the merge may read one past the second run
-    if (n <= 64) wave_sort_tile<1>(ks, point_list, r.x, n, lane);
+    if (n <= 64) {
+        uint64_t v[1];
+        wave_keys_load<1>(ks, r.x, n, v, lane);
+        wave_sort_regs<1>(v, lane);
+        if ((uint32_t)lane < n) point_list[r.x + lane] = (uint32_t)v[0];
+    }
     else if (n <= 128) wave_sort_split<1>(ks, r.x, n, point_list, lane, s_sort);
     else if (n <= 256) wave_sort_split<2>(ks, r.x, n, point_list, lane, s_sort);
     else if (n <= 512) wave_sort_split<4>(ks, r.x, n, point_list, lane, s_sort);
