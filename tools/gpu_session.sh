@@ -1,6 +1,4 @@
-# one GPU session of round 6: bit-exact lists + parity of the in-tree build, then rocprof A/B against the variants
+# one GPU session of round 6: rocprof A/B of the in-tree build against cost-floor variants
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_plan.py tests/test_gpu_lod.py tests/test_gpu_scale.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/sess_tests.log 2>&1
-rc=$?; echo "tests rc=$rc $(tail -1 gpurun_out/sess_tests.log)"; [ $rc -eq 0 ] || exit $rc
-VARIANTS="C sort_dpp C sort_dpp" bash tools/ab_quick.sh
+VARIANTS="C sort_nonet sort_nomerge" bash tools/ab_quick.sh
