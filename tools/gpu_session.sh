@@ -1,6 +1,6 @@
-# one GPU session of round 6: parity of the in-tree build (four splats per forward iteration), then rocprof A/B
+# one GPU session of round 6: parity of the in-tree build (split snapshots stored, not held), then rocprof A/B
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_plan.py tests/test_gpu_lod.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/sess_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_plan.py tests/test_gpu_lod.py tests/test_gpu_scale.py tests/test_gpu_alt.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/sess_tests.log 2>&1
 rc=$?; echo "tests rc=$rc $(tail -1 gpurun_out/sess_tests.log)"; [ $rc -eq 0 ] || exit $rc
-VARIANTS="C fwd2 C fwd2" bash tools/ab_quick.sh
+VARIANTS="C fwd_s0 C fwd_s0" bash tools/ab_quick.sh
