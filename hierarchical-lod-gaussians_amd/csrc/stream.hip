@@ -876,45 +876,97 @@ __device__ __forceinline__ bool is_close(float a, float b, float rtol, float ato
     return isfinite(err) && err <= allowed;
 }
 
+// A workgroup barrier that orders LDS only: global loads issued before it stay in flight (__syncthreads waits for
+// every outstanding memory operation, vmcnt(0), which would drain k_cache_lists' prefetches at each scan).
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// exclusive prefixes of two flags over the 1024-thread block in one pass (per-wave counts packed 16 + 16 bits)
+__device__ __forceinline__ void block_excl2(int fa, int fb, int* s_w, int& pa, int& pb, int& ta, int& tb)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t ba = __ballot(fa), bb = __ballot(fb), below = (1ull << lane) - 1ull;
+    lds_barrier();
+    if (lane == 0) s_w[w] = __popcll(ba) | (__popcll(bb) << 16);
+    lds_barrier();
+    int before = 0, t = 0;
+    for (int i = 0; i < 16; i++) {
+        const int c = s_w[i];
+        if (i < w) before += c;
+        t += c;
+    }
+    pa = (before & 0xffff) + __popcll(ba & below);
+    pb = (before >> 16) + __popcll(bb & below);
+    ta = t & 0xffff;
+    tb = t >> 16;
+}
+
+// Cut-entry fields k_cache_lists' first loop reads (v < 0: past the cut's end)
+struct CutEntry {
+    int v, leaf_n, fc, gid;
+    float x, y, z;
+};
+__device__ __forceinline__ CutEntry cut_entry(const CacheArgs& a, int v)
+{
+    CutEntry e{v, 1, -1, 0, 0.f, 0.f, 0.f};
+    if (v >= 0) {
+        e.leaf_n = a.nodes[6 * v + 2];
+        e.fc = a.nodes[6 * v + 3];
+        e.gid = a.nodes[6 * v + 5];
+        e.x = a.xyz[3 * v];
+        e.y = a.xyz[3 * v + 1];
+        e.z = a.xyz[3 * v + 2];
+    }
+    return e;
+}
+
+constexpr int kListsLdsSpts = 4096;  // the cut's SPT ids searched from LDS up to this many
 __global__ void __launch_bounds__(1024) k_cache_lists(CacheArgs a)
 {
 #pragma clang fp contract(off)
     __shared__ int s_w[16];
+    __shared__ int s_spt[kListsLdsSpts];
     // 1. leaves of the cut, in cut order: SPT leaves (first_child >= 0, with their camera distance) and
     //    upper-tree Gaussians to render (first_child <= 0; a leaf holding SPT 0 is in both lists, as in the
-    //    reference's two masks)
+    //    reference's two masks).  Software-pipelined: while one 1024-entry chunk is scanned and written, the next
+    //    chunk's node fields and the cut entries of the one after are in flight (one workgroup: it waits for every
+    //    load it does not overlap).
     int ns = 0, nu = 0;
     const int n_cut = a.n_cut_dev ? (a.n_cut_dev[1] ? 0 : min(a.n_cut_dev[0], a.n_cut)) : a.n_cut;
+    auto cut_at = [&](int i) -> int { return i < n_cut ? a.cut[i] : -1; };
+    CutEntry cur = cut_entry(a, cut_at(threadIdx.x));
+    int v_next = cut_at(1024 + threadIdx.x);
     for (int c0 = 0; c0 < n_cut; c0 += 1024) {
-        const int i = c0 + threadIdx.x;
-        int v = 0, fc = -1;
-        bool leaf = false;
-        if (i < n_cut) {
-            v = a.cut[i];
-            leaf = a.nodes[6 * v + 2] == 0;
-            fc = a.nodes[6 * v + 3];
-        }
-        const bool is_s = leaf && fc >= 0, is_u = leaf && fc <= 0;
-        int ts, tu;
-        const int ps = block_excl(is_s, s_w, &ts);
-        const int pu = block_excl(is_u, s_w, &tu);
+        const CutEntry nxt = cut_entry(a, v_next);
+        v_next = cut_at(c0 + 2048 + threadIdx.x);
+        const bool leaf = cur.v >= 0 && cur.leaf_n == 0;
+        const bool is_s = leaf && cur.fc >= 0, is_u = leaf && cur.fc <= 0;
+        int ps, pu, ts, tu;
+        block_excl2(is_s, is_u, s_w, ps, pu, ts, tu);
         if (is_s) {
             float d2 = INFINITY;  // nearest camera
             for (int g = 0; g < a.nviews; g++) {
-                const float dx = a.xyz[3 * v] - a.campos[3 * g], dy = a.xyz[3 * v + 1] - a.campos[3 * g + 1],
-                            dz = a.xyz[3 * v + 2] - a.campos[3 * g + 2];
+                const float dx = cur.x - a.campos[3 * g], dy = cur.y - a.campos[3 * g + 1],
+                            dz = cur.z - a.campos[3 * g + 2];
                 d2 = fminf(d2, dx * dx + dy * dy + dz * dz);
             }
-            a.spt_idx[ns + ps] = fc;
+            a.spt_idx[ns + ps] = cur.fc;
             a.spt_dist[ns + ps] = sqrtf(d2) * a.dmul;
+            if (ns + ps < kListsLdsSpts) s_spt[ns + ps] = cur.fc;
         }
-        if (is_u) a.upper[nu + pu] = a.nodes[6 * v + 5];
+        if (is_u) a.upper[nu + pu] = cur.gid;
         ns += ts;
         nu += tu;
+        cur = nxt;
     }
     __syncthreads();
     // 2. previous SPTs: torch.searchsorted (lower bound; the list is in cut order, not sorted, and the search
-    //    runs on it as it is), equal id and isclose distance -> kept, with the reference's segment bounds
+    //    runs on it as it is), equal id and isclose distance -> kept, with the reference's segment bounds.  The
+    //    search reads the LDS copy of the cut's SPT ids when they fit.
+    const bool spt_lds = ns <= kListsLdsSpts;
     int nk = 0, prefix = 0;
     for (int c0 = 0; c0 < a.m; c0 += 1024) {
         const int j = c0 + threadIdx.x;
@@ -925,10 +977,10 @@ __global__ void __launch_bounds__(1024) k_cache_lists(CacheArgs a)
             int lo = 0, hi = ns;
             while (lo < hi) {
                 const int mid = lo + ((hi - lo) >> 1);
-                if (!(a.spt_idx[mid] >= pv)) lo = mid + 1;
+                if (!((spt_lds ? s_spt[mid] : a.spt_idx[mid]) >= pv)) lo = mid + 1;
                 else hi = mid;
             }
-            keep = lo < ns && a.spt_idx[lo] == pv && is_close(a.spt_dist[lo], a.prev_dist[j], a.rtol, a.atol);
+            keep = lo < ns && (spt_lds ? s_spt[lo] : a.spt_idx[lo]) == pv && is_close(a.spt_dist[lo], a.prev_dist[j], a.rtol, a.atol);
             if (keep) {
                 start = a.prev_counts[j];
                 to = j == a.m - 1 ? a.tail_end : a.prev_counts[j + 1];
@@ -960,7 +1012,7 @@ __global__ void __launch_bounds__(1024) k_cache_lists(CacheArgs a)
         bool load = false;
         int v = 0;
         if (k < ns) {
-            v = a.spt_idx[k];
+            v = spt_lds ? s_spt[k] : a.spt_idx[k];
             load = !(v >= 0 && v < a.num_spts && a.flag[v]);
         }
         int tl;
