@@ -88,7 +88,8 @@ def main(src, dst):
         open(os.path.join(dst, "bench_line_under_rocprof.json"), "w").write(line + "\n")
         tr = os.path.join(src, "trace", "run_kernel_trace.csv")
         if os.path.exists(tr):
-            json.dump(launch_timing(tr, json.loads(line)), open(os.path.join(dst, "timing.json"), "w"), indent=1)
+            json.dump(dict(launch_timing(tr, json.loads(line)), build=build_identity()),
+                      open(os.path.join(dst, "timing.json"), "w"), indent=1)
     fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     sqp = os.path.join(src, "sq", "run_counter_collection.csv")
