@@ -1,10 +1,7 @@
-# one GPU session of round 6: config #5's write-back started from a hook on the rendered image's gradient (after the
-# loss backward) against before loss.backward(); plain step times interleaved, then the kernel trace of each
+# one GPU session of round 6: parity of the in-tree build (blend backward with the next batch's records prefetched,
+# 4 waves per SIMD), then rocprof A/B against the 5-wave build (4 VGPRs spilled) and the previous kernel
 set -u
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-for m in 1 0 1 0 1 0; do
-  HLGS_WB_HOOK=$m timeout -k 10 200 python3 tools/train_post_step.py --steps 30 > gpurun_out/wbh_$m.log 2>&1 || exit 1
-  echo "hook=$m $(grep '^{' gpurun_out/wbh_$m.log | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["stages_ms"])')"
-done
-HLGS_WB_HOOK=1 bash tools/c5_trace.sh c5h1 | grep -i "ssim\|blend_bwd\|rows_packed\|preprocess\|ms_per_step" | cut -c1-200
-HLGS_WB_HOOK=0 bash tools/c5_trace.sh c5h0 | grep -i "ssim\|blend_bwd\|rows_packed\|preprocess\|ms_per_step" | cut -c1-200
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_plan.py tests/test_gpu_lod.py tests/test_gpu_alt.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/sess_tests.log 2>&1
+rc=$?; echo "tests rc=$rc $(tail -1 gpurun_out/sess_tests.log)"; [ $rc -eq 0 ] || exit $rc
+VARIANTS="C bwd_pf5 bwd_old C bwd_pf5 bwd_old" bash tools/ab_quick.sh
