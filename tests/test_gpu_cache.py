@@ -16,14 +16,14 @@ NAMES = ("xyz", "f_dc", "opacity", "scaling", "rotation", "f_rest")
 SHAPES = {"xyz": (3,), "f_dc": (1, 3), "opacity": (1,), "scaling": (3,), "rotation": (4,), "f_rest": (15, 3)}
 
 
-def _scene(sky=4, n=6000, seed=8):
+def _scene(sky=4, n=6000, seed=8, volume=3.0, granularity=0.02, min_size=20):
     from hlgs_core import spt
     cam0 = S.make_camera(256, 192)
     h = S.make_dynamic_hierarchy(S.make_gaussians(n, 0, cam0, seed=seed), skybox_points=sky, seed=seed)
     nodes = torch.tensor(h["nodes"])
     nodes[:, 3] = torch.where(nodes[:, 2] == 2, nodes[:, 3], torch.zeros_like(nodes[:, 3]))
-    b = spt.build_hierarchical_spt(nodes, torch.tensor(h["means3D"]), torch.log(torch.tensor(h["scales"])), sky, 3.0,
-                                   0.02, 20)
+    b = spt.build_hierarchical_spt(nodes, torch.tensor(h["means3D"]), torch.log(torch.tensor(h["scales"])), sky,
+                                   volume, granularity, min_size)
     G = nodes.shape[0]
     rng = np.random.default_rng(seed)
     storage = {k: torch.tensor(rng.normal(size=(G,) + SHAPES[k]).astype(np.float32)) for k in NAMES}
@@ -124,6 +124,31 @@ def test_spt_cache_views_match_restatement(rtol, budget):
            [cache.opt_storage[k]["exp_avgs_sqs"] for k in NAMES]
     for t, (h, w) in enumerate(zip(host, orc.host)):
         np.testing.assert_array_equal(h.numpy(), w, err_msg=f"host tensor {t}")
+
+
+def test_spt_cache_many_spts_match_restatement():
+    """A cut with more SPTs (6,862) than k_cache_lists keeps in LDS (kListsLdsSpts = 4,096, csrc/stream.hip): the
+    searchsorted over the cut's SPT ids and the load test read the global list instead.  Every SPT is kept from the
+    second view on, so the search runs for all of them."""
+    from hlgs_core.spt_cache import SPTCache
+    sky = 4
+    b, storage = _scene(sky, n=120000, volume=0.1, granularity=0.005, min_size=4)
+    cams = _cameras()[:3]
+    cache = SPTCache(storage, b, sky, reuse_tolerance=0.9)
+    orc = _Oracle(b, storage, sky, 0.9, 10 ** 9)
+    for step, cam in enumerate(cams):
+        got = cache.step(cam["projmatrix"], cam["campos"])
+        want = orc.step(cam)
+        pl = cache.last_plan
+        assert len(want["SPT_indices"]) > 4096
+        for k in ("SPT_indices", "SPT_distances", "SPT_counts", "load_from_disk_indices"):
+            np.testing.assert_array_equal(pl[k].cpu().numpy(), want[k], err_msg=f"{k} view {step}")
+        np.testing.assert_array_equal(got.cpu().numpy(), want["render_indices"])
+        np.testing.assert_array_equal(pl["write_back_indices"].cpu().numpy(), want["write_back_indices"])
+        if step > 0:
+            assert want["n_kept"] == len(want["SPT_indices"])
+        for t, (g, w) in enumerate(zip(_dev_list(cache), orc.dev)):
+            np.testing.assert_array_equal(g.detach().cpu().numpy(), w, err_msg=f"tensor {t} view {step}")
 
 
 def test_copy_rows_tables_and_identity():
