@@ -798,6 +798,32 @@ struct KeyView {
     __device__ __forceinline__ uint32_t depth_bits(uint32_t ent) const { return ks.depth_bits(ent); }
 };
 
+// One pass of M consecutive bitonic substages (distances step 2^(M-1) .. step) of stage kk on group g: the 2^M keys
+// at base + t step (base = g with M zero bits inserted at step's bit), compare-exchanged in registers.
+template <int M>
+__device__ __forceinline__ void bitonic_group(uint64_t* s, uint32_t g, uint32_t step, uint32_t kk)
+{
+    const uint32_t low = step - 1u, base = ((g & ~low) << M) | (g & low);
+    uint64_t v[1 << M];
+#pragma unroll
+    for (int t = 0; t < (1 << M); t++) v[t] = s[base + (uint32_t)t * step];
+    const bool asc = (base & kk) == 0;
+#pragma unroll
+    for (int sub = 0; sub < M; sub++) {
+        const int d = 1 << (M - 1 - sub);
+#pragma unroll
+        for (int t = 0; t < (1 << M); t++) {
+            if (t & d) continue;
+            const uint64_t x = v[t], y = v[t + d];
+            const bool sw = (x > y) == asc;
+            v[t] = sw ? y : x;
+            v[t + d] = sw ? x : y;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < (1 << M); t++) s[base + (uint32_t)t * step] = v[t];
+}
+
 // One 256-thread block per tile: bitonic sort of the tile's keys in LDS.  Tiles longer than kSortCap
 // are sorted in kSortCap runs here and merged by k_merge_runs.
 __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ranges, KeySrc ks, uint64_t* runs,
@@ -829,16 +855,33 @@ __global__ void __launch_bounds__(256) k_tile_sort(const uint2* __restrict__ ran
             }
         }
         __syncthreads();
+        // Three substages per pass over the LDS (distances j, j/2, j/4): a thread loads the 8 keys those substages
+        // connect, runs the 12 compare-exchanges in registers and stores the 8 back, a third of the LDS traffic and
+        // barriers of one substage per pass.  Passes whose largest distance j is below the quarter seg = np / 4 stay
+        // inside one wave's quarter of the array (their 2j-blocks are aligned in it): each wave runs its own quarter's
+        // groups with no block barrier, its own LDS order (lgkmcnt(0)) separating the passes.
+        const uint32_t seg = np >> 2, wv = (uint32_t)(tid >> 6), ln = (uint32_t)(tid & 63);
         for (uint32_t kk = 2; kk <= np; kk <<= 1)
-            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < np / 2; i += 256) {
-                    const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
-                    const bool asc = (lo & kk) == 0;
-                    const uint64_t x = s[lo], y = s[hi];
-                    if ((x > y) == asc) { s[lo] = y; s[hi] = x; }
+            for (uint32_t j = kk >> 1; j > 0;) {
+                const int m = min(3, 32 - __clz(j));  // substages in this pass (j = 1 or 2 leaves fewer)
+                const uint32_t step = j >> (m - 1), ng = np >> m;
+                auto pass = [&](uint32_t g) {
+                    if (m == 3) bitonic_group<3>(s, g, step, kk);
+                    else if (m == 2) bitonic_group<2>(s, g, step, kk);
+                    else bitonic_group<1>(s, g, step, kk);
+                };
+                if (j >= seg) {  // block-uniform
+                    __syncthreads();
+                    for (uint32_t g = tid; g < ng; g += 256) pass(g);
+                    __syncthreads();
+                } else {
+                    const uint32_t gpw = seg >> m, g0 = wv * gpw;
+                    for (uint32_t g = g0 + ln; g < g0 + gpw; g += 64) pass(g);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
-                __syncthreads();
+                j >>= m;
             }
+        __syncthreads();
         if (big)  // sorted runs into the second key buffer (the entries of other tiles still occupy the first)
             for (uint32_t i = tid; i < n; i += 256) runs[r.x + c0 + i] = s[i];
         else

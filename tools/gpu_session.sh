@@ -1,4 +1,4 @@
-# one GPU session of round 6: parity of the in-tree build (long tiles sorted by register runs + merge paths), then
+# one GPU session of round 6: parity of the in-tree build (long-tile bitonic sort with wave-local small-distance substages), then
 # rocprof A/B on config #4's per-GPU frame (4M Gaussians) against the LDS bitonic block sort
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
