@@ -275,7 +275,7 @@ __device__ __forceinline__ bool preprocess_geom(const hlgs_raster_args& a, const
 // waves busy.  Same arithmetic, same outputs.
 // The rows arrive through registers: every lane loads consecutive float4s of the block's contiguous rows (1 KiB per
 // wave instruction) and stores them into LDS rows of odd stride (kShStride), so that each lane's own row walk hits
-// distinct banks.  (Round 5 measured LDS-DMA into a chunk-major image instead -- conflict-free b128 reads, no staging
+// distinct banks; degree-3 rows use the unpadded swizzled float4 layout of sh_rows_load_swz below instead.  (Round 5 measured LDS-DMA into a chunk-major image instead -- conflict-free b128 reads, no staging
 // registers: 115 against 97 us, because the DMA's source side then reads 16 bytes per lane at the row stride, 64 lines
 // per wave instruction instead of 8; preprocess_dma.hip, tools/variants/INDEX.md.)
 template <int M3T>
