@@ -103,6 +103,16 @@ def test_long_tile_lists_use_merge_path():
     _compare(sc, cam)
 
 
+@pytest.mark.parametrize("P", [1400, 2600, 4700, 12500])
+def test_long_tile_sort_lengths(P):
+    """Clustered splats whose centre tiles hold ~1,025-2,048, ~2,049-4,096 and > 4,096 entries (runs of 4,096 plus a
+    ragged last run): the block sort's three-substage LDS passes (bitonic_group), its wave-local passes, and the merge
+    passes of the longest lists."""
+    cam = S.make_camera(64, 64)
+    sc = S.make_gaussians(P, 0, cam, seed=P, zmin=10.0, zmax=12.0, xy_spread=0.05, sigma_px=(1.0, 2.0))
+    _compare(sc, cam)
+
+
 def test_backward_is_deterministic():
     sc, cam = _scene(3000, 3, 128, 128, seed=9)
     g = S.upstream_grads(128, 128)
